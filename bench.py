@@ -1,0 +1,326 @@
+#!/usr/bin/env python3
+"""Benchmark of the MI355X hash join: build + probe of BASELINE.json's C2 workload.
+
+One step = the whole join on device-resident synthetic input: build a table from
+10^7 unique int64 keys (hj_build_begin/append/finish: table clear + insert + duplicate
+passes) and probe it with 10^8 uniform int64 keys (probe kernel, canonical pair
+emission into preallocated output). With N > 1 ranks (one process per GPU, launched by
+torch.distributed.run) every rank holds a C2-sized shard (weak scaling) and a step also
+radix-partitions both sides and exchanges them with RCCL all-to-all first.
+
+Prints ONE JSON line (rank 0). `value` = probe rows of all ranks / step wall time
+(Mrows/s); `probe_mrows_s` = probe rows / probe-kernel time; `build_ms` = device build
+time. `roofline` prices the probe kernel (the dominant kernel) by its algorithmic bytes
+8P + 16B + 12M over its HIP-event time; `traffic` is the PMC-measured
+HBM bytes per probe launch from profiles/ (null if not measured for this config).
+`cpu_baseline` times the oracle's multithreaded Version-10 restatement (oracle/hj_oracle.c)
+on host cores over a bounded sample (rank 0, N = 1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import datafusion_parallelism_amd as dfp  # noqa: E402
+from datafusion_parallelism_amd.table import HashTable  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+PERM_MUL = 7368787
+
+CONFIGS = {
+    # BASELINE.json configs[1]: 10^8-probe x 10^7-build int64 uniform keys
+    "c2": dict(workload="C2: 10^8-probe x 10^7-build int64 inner equi-join, uniform keys",
+               build_rows=10**7, probe_rows=10**8, build_gen="perm", probe_range_mul=2),
+    # BASELINE.json configs[2]: 10^8 rows with exponential/skewed build keys
+    "c3": dict(workload="C3: 10^8-probe x 10^7-build int64, exponential build keys",
+               build_rows=10**7, probe_rows=10**8, build_gen="exp", probe_range_mul=1),
+}
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def gen_inputs(cfg, rank, world, dev):
+    """Device-resident synthetic input of this rank (generated on the GPU)."""
+    L = dfp.load()
+    B, P = cfg["build_rows"], cfg["probe_rows"]
+    s = torch.cuda.current_stream(dev).cuda_stream
+    bk = torch.empty(B, dtype=torch.int64, device=dev)
+    if cfg["build_gen"] == "perm":
+        # global permutation of [0, world*B); rank r holds rows [r*B, (r+1)*B)
+        gB = world * B
+        tmp = torch.empty(gB if world > 1 else B, dtype=torch.int64, device=dev)
+        assert L.hj_gen_perm_keys(tmp.data_ptr(), tmp.numel(), PERM_MUL, gB, s) == 0
+        bk.copy_(tmp[rank * B:(rank + 1) * B])
+        del tmp
+        krange = gB
+    else:
+        from datafusion_parallelism_amd.api_utils import make_exponential_int_array
+
+        e = make_exponential_int_array(0, B).astype(np.int64) + rank * B
+        bk.copy_(torch.from_numpy(e))
+        krange = world * B
+    pk = torch.empty(P, dtype=torch.int64, device=dev)
+    prange = cfg["probe_range_mul"] * krange
+    assert L.hj_gen_uniform_keys(pk.data_ptr(), P, 0xC0FFEE + rank * P, prange, s) == 0
+    torch.cuda.synchronize(dev)
+    return bk, pk
+
+
+class SingleGpuJoin:
+    """One step = build + probe on this GPU (no exchange)."""
+
+    def __init__(self, bk, pk, dev):
+        self.bk, self.pk, self.dev = bk, pk, dev
+        P = pk.numel()
+        self.ws = torch.empty(HashTable.workspace_bytes(P), dtype=torch.uint8, device=dev)
+        self.d_total = torch.zeros(1, dtype=torch.int64, device=dev)
+        self.cap = P
+        self._alloc()
+        self.ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+        self.probe_ms = []
+        self.build_ms = []
+        self.matches = 0
+
+    def _alloc(self):
+        self.ob = torch.empty(self.cap, dtype=torch.int64, device=self.dev)
+        self.op = torch.empty(self.cap, dtype=torch.int32, device=self.dev)
+
+    def step(self, record=True):
+        t = HashTable(1, "int64", self.dev.index or 0)
+        t.append(0, self.bk)
+        t.finish(0)  # device build; returns when the table is complete
+        s = torch.cuda.current_stream(self.dev)
+        self.ev[0].record(s)
+        t.probe_async(self.pk.data_ptr(), self.pk.numel(), self.ob.data_ptr(), self.op.data_ptr(), self.cap,
+                      self.d_total.data_ptr(), self.ws.data_ptr(), s.cuda_stream)
+        self.ev[1].record(s)
+        self.table = t
+        if record:
+            self._pending = True
+
+    def collect(self):
+        """After a synchronize: per-step timings (outside the timed region)."""
+        self.probe_ms.append(self.ev[0].elapsed_time(self.ev[1]))
+        self.build_ms.append(self.table.build_ns() / 1e6)
+        self.matches = int(self.d_total.item())
+        if self.matches > self.cap:
+            raise RuntimeError("output capacity too small")
+        self.table.close()
+
+
+def cpu_baseline(cfg, nthreads=8):
+    """Oracle's multithreaded Version-10 restatement on the host: full-size build, a
+    probe sample of 10^7 rows, probe time scaled to the full probe side."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+
+    B, P = cfg["build_rows"], cfg["probe_rows"]
+    if cfg["build_gen"] == "perm":
+        bk = oracle.perm_keys(B, PERM_MUL, B)
+    else:
+        bk = oracle.make_exponential_int_array(0, B).astype(np.int64)
+    ps = min(P, 10**7)
+    pk = oracle.uniform_keys(ps, 0xC0FFEE, cfg["probe_range_mul"] * B)
+    t0 = time.perf_counter()
+    tbl = oracle.V10Table(bk, nthreads=nthreads)
+    t1 = time.perf_counter()
+    m = tbl.probe(pk, nthreads=nthreads, emit=True)
+    t2 = time.perf_counter()
+    tbl.close()
+    build_s, probe_s = t1 - t0, (t2 - t1) * (P / ps)
+    cpu = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    cpu = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {
+        "value": round(P / (build_s + probe_s) / 1e6, 3),
+        "unit": "Mrows/s",
+        "cores": nthreads,
+        "kind": "port",
+        "sample": f"full {B}-row build + {ps} of the {P} probe rows (probe time scaled x{P // ps}); "
+                  f"C restatement of reference Version 10 (oracle/hj_oracle.c), {nthreads} threads on {cpu}, "
+                  f"host has {os.cpu_count()} logical CPUs",
+        "build_ms": round(build_s * 1e3, 3),
+        "probe_mrows_s": round(P / probe_s / 1e6, 3),
+        "pairs_in_sample": int(len(m[0])),
+    }
+
+
+def load_traffic(config_name):
+    p = os.path.join(ROOT, "profiles", f"traffic_{config_name}.json")
+    if os.path.exists(p):
+        with open(p) as f:
+            return json.load(f)
+    return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+    cfg = CONFIGS[args.config]
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
+    dev = torch.device("cuda", local_rank)
+    torch.cuda.set_device(dev)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    bk, pk = gen_inputs(cfg, rank, world, dev)
+    B, P = bk.numel(), pk.numel()
+
+    if world == 1:
+        job = SingleGpuJoin(bk, pk, dev)
+    else:
+        from datafusion_parallelism_amd.distributed import DistributedHashJoin
+
+        job = DistJob(DistributedHashJoin(), bk, pk, rank, dev)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        job.step()
+        torch.cuda.synchronize(dev)
+        job.collect()
+    job.probe_ms.clear()
+    job.build_ms.clear()
+
+    times = []
+    barrier()
+    torch.cuda.synchronize(dev)
+    t_start = time.perf_counter()
+    for _ in range(args.steps):
+        ts = time.perf_counter()
+        job.step()
+        torch.cuda.synchronize(dev)
+        times.append(time.perf_counter() - ts)
+        job.collect()  # reads events/counters of the finished step (inside the timed region)
+    torch.cuda.synchronize(dev)
+    barrier()
+    elapsed = time.perf_counter() - t_start
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    ms_per_step = elapsed / args.steps * 1e3
+    total_probe_rows = P * world
+    value = total_probe_rows / (elapsed / args.steps) / 1e6
+
+    probe_ms = float(np.median(job.probe_ms))
+    build_ms = float(np.median(job.build_ms))
+    M = job.matches
+    alg_bytes = 8 * P + 16 * B + 12 * M
+    achieved = alg_bytes / (probe_ms / 1e3) / 1e9
+    traffic = load_traffic(args.config)
+    roofline = {
+        "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+        "frac": round(achieved / HBM_PEAK_GBS, 4),
+        "traffic": (traffic or {}).get("hbm_bytes_per_launch"),
+        "kernel": "probe_kernel<long>", "alg_bytes_per_launch": alg_bytes,
+        "alg_bytes_formula": "8*P + 16*B + 12*M (SURVEY.md §8d)",
+    }
+
+    if rank == 0:
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            cpu = cpu_baseline(cfg)
+        line = {
+            "metric": "probe Mrows/s + build ms, 10^8-row int64 inner join; 1/2/4/8 GPUs",
+            "value": round(value, 3),
+            "unit": "Mrows/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "int64",
+            "data": "synthetic (device-generated seeded keys, SURVEY.md §8d generators)",
+            "config": {
+                "workload": cfg["workload"],
+                "build_rows_per_gpu": B,
+                "probe_rows_per_gpu": P,
+                "matches_per_gpu": M,
+                "parallelism": "single-gpu" if world == 1 else f"radix-a2a x{world} (RCCL)",
+            },
+            "probe_mrows_s": round(P / (probe_ms / 1e3) / 1e6, 1),
+            "probe_ms": round(probe_ms, 4),
+            "build_ms": round(build_ms, 4),
+            "step_ms_min": round(min(times) * 1e3, 4),
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+        }
+        if world > 1:
+            line["exchange_ms"] = round(float(np.median(job.exchange_ms)), 4)
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+class DistJob:
+    """One step = radix-partition + RCCL all-to-all of both sides + local build + probe."""
+
+    def __init__(self, dj, bk, pk, rank, dev):
+        self.dj, self.bk, self.pk, self.dev = dj, bk, pk, dev
+        self.bbase = rank * bk.numel()
+        self.pbase = rank * pk.numel()
+        self.probe_ms, self.build_ms, self.exchange_ms = [], [], []
+        self.matches = 0
+        self.cap = pk.numel()
+
+    def step(self):
+        t0 = time.perf_counter()
+        bk, bi, _ = self.dj.shard(self.bk, self.bbase)
+        pk, pi, _ = self.dj.shard(self.pk, self.pbase)
+        torch.cuda.synchronize(self.dev)
+        t1 = time.perf_counter()
+        self.exchange_ms.append((t1 - t0) * 1e3)
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+        from datafusion_parallelism_amd.distributed import gpu_local_join
+
+        ev[0].record()
+        b, p = gpu_local_join(bk, bi, pk, pi, self.cap)
+        ev[1].record()
+        self._ev = ev
+        self._t1 = t1
+        self.matches = b.numel()
+
+    def collect(self):
+        torch.cuda.synchronize(self.dev)
+        # local build + probe as one device interval (build is synchronous inside)
+        self.probe_ms.append(self._ev[0].elapsed_time(self._ev[1]))
+        self.build_ms.append(0.0)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,105 @@
+"""ctypes binding of the C ABI in ``include/hj.h`` (``lib/libdfp_hj.so``).
+
+torch is imported before the library is loaded: the library links the HIP runtime that
+torch ships (SONAME ``libamdhip64.so.7``), and loading torch first makes the dynamic
+linker reuse torch's copy, so the process holds a single HIP runtime.
+
+The library has no CPU fallback: every compute entry point fails with
+``HJ_ERR_NO_DEVICE`` on a machine without a GPU, and this module raises
+``ImportError`` if the library has not been built.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "libdfp_hj.so")
+
+HJ_OK, HJ_ERR_INVALID, HJ_ERR_OOM, HJ_ERR_HIP, HJ_ERR_RCCL, HJ_ERR_CAPACITY, HJ_ERR_NO_DEVICE = range(7)
+HJ_INT32, HJ_INT64 = 0, 1
+HJ_INPUT_DEVICE, HJ_BORROW, HJ_OUTPUT_HOST = 1, 2, 4
+
+STATUS_NAMES = {
+    HJ_OK: "HJ_OK", HJ_ERR_INVALID: "HJ_ERR_INVALID", HJ_ERR_OOM: "HJ_ERR_OOM", HJ_ERR_HIP: "HJ_ERR_HIP",
+    HJ_ERR_RCCL: "HJ_ERR_RCCL", HJ_ERR_CAPACITY: "HJ_ERR_CAPACITY", HJ_ERR_NO_DEVICE: "HJ_ERR_NO_DEVICE",
+}
+
+
+class HjError(RuntimeError):
+    """A non-OK hj_status (the reference's DataFusionError::Internal for HJ_ERR_INVALID)."""
+
+    def __init__(self, status: int, message: str):
+        super().__init__(f"{STATUS_NAMES.get(status, status)}: {message}")
+        self.status = status
+
+
+class HjPairs(ctypes.Structure):
+    _fields_ = [("build_idx", ctypes.POINTER(ctypes.c_uint64)), ("probe_idx", ctypes.POINTER(ctypes.c_uint32)),
+                ("count", ctypes.c_int64), ("device_resident", ctypes.c_int)]
+
+
+class HjTableStats(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int64) for n in (
+        "build_rows", "inserted_rows", "distinct_keys", "dup_keys", "dup_rows", "max_key_rows", "buckets",
+        "table_bytes", "build_ns")]
+
+
+# (name, restype, argtypes) of every entry point declared in include/hj.h
+P, I64, I32, U32, U64 = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_uint32, ctypes.c_uint64
+PP = ctypes.POINTER(ctypes.c_void_p)
+SIGNATURES = [
+    ("hj_last_error", ctypes.c_char_p, []),
+    ("hj_version", ctypes.c_char_p, []),
+    ("hj_device_count", I32, []),
+    ("hj_build_begin", I32, [I32, I32, I32, I64, PP]),
+    ("hj_build_append", I32, [P, I32, P, P, I64, P, I64, U32, P]),
+    ("hj_build_finish", I32, [P, I32]),
+    ("hj_build_partition_offset", I32, [P, I32, ctypes.POINTER(ctypes.c_int64)]),
+    ("hj_table_stats_get", I32, [P, ctypes.POINTER(HjTableStats)]),
+    ("hj_table_build_ns", I64, [P]),
+    ("hj_table_lookup", I32, [P, I64, P, I64, ctypes.POINTER(ctypes.c_int64)]),
+    ("hj_table_chain_links", I32, [P, P, I64]),
+    ("hj_table_free", None, [P]),
+    ("hj_probe", I32, [P, P, P, I64, I64, U32, P, ctypes.POINTER(HjPairs)]),
+    ("hj_pairs_free", None, [ctypes.POINTER(HjPairs)]),
+    ("hj_probe_workspace_bytes", I64, [I64]),
+    ("hj_probe_async", I32, [P, P, P, I64, I64, P, P, I64, P, P, P]),
+    ("hj_probe_async_ids", I32, [P, P, P, I64, P, I64, P, P, I64, P, P, P]),
+    ("hj_table_stream_wait", I32, [P, P]),
+    ("hj_partition_workspace_bytes", I64, [I64, I32]),
+    ("hj_radix_partition", I32, [I32, P, P, I64, P, U64, I64, I32, P, P, P, P, P]),
+    ("hj_gen_perm_keys", I32, [P, I64, I64, I64, P]),
+    ("hj_gen_uniform_keys", I32, [P, I64, U64, I64, P]),
+]
+
+_lib = None
+
+
+def load() -> ctypes.CDLL:
+    """Load the built library (raises ImportError if it was not built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"{LIB_PATH} is missing: run `python __graft_entry__.py build` "
+                          "(or datafusion-parallelism_amd/build.py). There is no CPU fallback.")
+    L = ctypes.CDLL(LIB_PATH)
+    for name, res, args in SIGNATURES:
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    _lib = L
+    return L
+
+
+def check(status: int) -> None:
+    if status != HJ_OK:
+        msg = load().hj_last_error()
+        raise HjError(status, msg.decode() if msg else "")
+
+
+def device_count() -> int:
+    return load().hj_device_count()

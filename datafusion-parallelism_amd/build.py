@@ -1,0 +1,86 @@
+"""Build the in-tree C-ABI library ``lib/libdfp_hj.so`` (gfx950 code objects).
+
+The kernels are compiled by ``hipcc --offload-arch=gfx950``; the host layer by g++.
+The library links the HIP runtime that PyTorch-ROCm ships (``torch/lib/libamdhip64.so``)
+so that a process which also uses torch for device memory, streams and
+``torch.distributed`` holds exactly one HIP/HSA runtime. (``/opt/rocm``'s runtime has
+SONAME ``libamdhip64.so.7``; torch's has none, so linking the ROCm one would load a
+second runtime next to torch's.)
+"""
+from __future__ import annotations
+
+import importlib.util
+import os
+import shutil
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, "csrc")
+LIBDIR = os.path.join(HERE, "lib")
+LIB = os.path.join(LIBDIR, "libdfp_hj.so")
+INCLUDE = os.path.join(os.path.dirname(HERE), "include")
+ARCH = "gfx950"
+
+SOURCES_HIP = ["hj_kernels.hip"]
+SOURCES_CPP = ["hj_api.cpp"]
+HEADERS = ["hj_device.h", "hj_launch.h"]
+
+
+def torch_lib_dir() -> str:
+    spec = importlib.util.find_spec("torch")
+    if spec is None or spec.origin is None:
+        raise RuntimeError("PyTorch-ROCm is required for its HIP runtime")
+    d = os.path.join(os.path.dirname(spec.origin), "lib")
+    if not os.path.exists(os.path.join(d, "libamdhip64.so")):
+        raise RuntimeError(f"no libamdhip64.so under {d}")
+    return d
+
+
+def _stale() -> bool:
+    if not os.path.exists(LIB):
+        return True
+    t = os.path.getmtime(LIB)
+    deps = [os.path.join(CSRC, f) for f in SOURCES_HIP + SOURCES_CPP + HEADERS]
+    deps += [os.path.join(INCLUDE, "hj.h"), __file__]
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def _run(cmd: list[str], verbose: bool) -> None:
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"command failed ({r.returncode}): {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    """Compile the HIP kernels + C-ABI host layer; returns the library path."""
+    if not force and not _stale():
+        return LIB
+    rocm = os.environ.get("ROCM_PATH", "/opt/rocm")
+    hipcc = shutil.which("hipcc") or os.path.join(rocm, "bin", "hipcc")
+    tlib = torch_lib_dir()
+    objdir = os.path.join(HERE, "build")
+    os.makedirs(objdir, exist_ok=True)
+    os.makedirs(LIBDIR, exist_ok=True)
+    objs = []
+    for src in SOURCES_HIP:
+        obj = os.path.join(objdir, src + ".o")
+        _run([hipcc, f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17", "-I", INCLUDE,
+              "-c", os.path.join(CSRC, src), "-o", obj], verbose)
+        objs.append(obj)
+    for src in SOURCES_CPP:
+        obj = os.path.join(objdir, src + ".o")
+        _run(["g++", "-O2", "-fPIC", "-std=c++17", "-D__HIP_PLATFORM_AMD__", "-I", INCLUDE,
+              "-I", os.path.join(rocm, "include"), "-c", os.path.join(CSRC, src), "-o", obj], verbose)
+        objs.append(obj)
+    tmp = LIB + ".tmp"
+    _run(["g++", "-shared", "-o", tmp, *objs, f"-L{tlib}", "-lamdhip64", f"-Wl,-rpath,{tlib}",
+          "-Wl,--no-undefined", "-lpthread"], verbose)
+    os.replace(tmp, LIB)
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv, verbose=True))

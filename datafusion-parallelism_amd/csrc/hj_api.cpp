@@ -1,0 +1,676 @@
+// hj_api.cpp — C-ABI host layer (include/hj.h) over the gfx950 kernels.
+//
+// Mirrors the reference's build/probe choreography:
+//   * hj_build_begin      ~ BuildImplementation::new / JoinStateInstances::new
+//                           (src/operator/build_implementation.rs:34-48,
+//                            src/operator/version10/parallel_join_execution_state.rs:377-403)
+//   * hj_build_append     ~ process_input_batch -> JoinStateInstance::add
+//                           (src/operator/version10/build_implementation.rs:60-71,
+//                            parallel_join_execution_state.rs:91-133)
+//   * hj_build_finish     ~ compact_join_map: every partition arrives, the last arriver
+//                           finalises, the others wait (InitializeLast,
+//                           src/utils/initialize_last.rs:26-43; BarrierOnce,
+//                           src/utils/barrier_once.rs:4-35)
+//   * hj_probe            ~ lookup_inner_join_probe_batch minus the Arrow take
+//                           (src/operator/probe_lookup_implementation/inner.rs:79-129)
+// Errors: HJ_ERR_INVALID carries the reference's DataFusionError::Internal texts where
+// one exists (e.g. "State already consumed for partition N",
+// src/operator/version10/build_implementation.rs:32-33).
+//
+// There is no CPU code path: without a GPU every entry point fails with
+// HJ_ERR_NO_DEVICE.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <chrono>
+#include <condition_variable>
+#include <mutex>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/hj.h"
+#include "hj_device.h"
+#include "hj_launch.h"
+
+using namespace dfp;
+
+namespace {
+
+thread_local std::string g_err;
+
+hj_status fail(hj_status st, const std::string& msg) {
+    g_err = msg;
+    return st;
+}
+
+#define HIP_TRY(expr)                                                                    \
+    do {                                                                                 \
+        hipError_t e_ = (expr);                                                          \
+        if (e_ != hipSuccess)                                                            \
+            return fail(HJ_ERR_HIP, std::string(#expr ": ") + hipGetErrorString(e_));    \
+    } while (0)
+
+struct ThreadStreams {
+    std::unordered_map<int, hipStream_t> m;
+    ~ThreadStreams() {
+        for (auto& kv : m) (void)hipStreamDestroy(kv.second);
+    }
+};
+thread_local ThreadStreams g_streams;
+
+hipStream_t thread_stream(int dev) {
+    auto it = g_streams.m.find(dev);
+    if (it != g_streams.m.end()) return it->second;
+    hipStream_t s = nullptr;
+    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return nullptr;
+    g_streams.m[dev] = s;
+    return s;
+}
+
+int device_count() {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+// true when p is device (or managed) memory visible to the current device
+bool is_device_ptr(const void* p) {
+    if (p == nullptr) return true;
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged;
+}
+
+double load_factor() {
+    const char* e = getenv("DFP_HJ_LOAD_FACTOR");
+    double lf = e ? atof(e) : 0.5;
+    if (!(lf > 0.05 && lf <= 0.95)) lf = 0.5;
+    return lf;
+}
+
+struct HostSeg {
+    const void* keys = nullptr;
+    const uint8_t* valid = nullptr;
+    int64_t voff = 0;
+    const uint64_t* ids = nullptr;
+    int64_t n = 0;
+    std::vector<void*> owned;  // device copies owned by the table
+    hipEvent_t ready = nullptr;  // borrowed device input: produced when this fires
+};
+
+}  // namespace
+
+struct hj_table {
+    int device = 0;
+    int parallelism = 1;
+    hj_key_type kt = HJ_INT64;
+    int key_bytes = 8;
+
+    std::mutex mu;
+    std::condition_variable cv;
+    std::vector<std::vector<HostSeg>> parts;
+    std::vector<char> finished;
+    int arrived = 0;
+    bool built = false;
+    hj_status build_st = HJ_OK;
+    std::string build_err;
+    bool has_ids = false, has_no_ids = false;
+
+    std::vector<int64_t> part_off;
+    int64_t total_rows = 0;
+
+    // device state
+    Bucket* tbl = nullptr;
+    uint32_t nb = 0;
+    uint32_t* dup_rows = nullptr;
+    uint64_t* row_ids = nullptr;
+    uint2* duprows = nullptr;
+    uint32_t* dupslots = nullptr;
+    DupDir* dir = nullptr;
+    uint32_t* big = nullptr;
+    BuildCounters* ctr = nullptr;
+    Segment* d_segs = nullptr;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    int64_t build_ns = 0;
+    std::vector<void*> allocs;
+};
+
+namespace {
+
+hj_status dev_alloc(hj_table* t, void** p, size_t bytes) {
+    *p = nullptr;
+    if (bytes == 0) bytes = 64;
+    hipError_t e = hipMallocAsync(p, bytes, t->stream);
+    if (e != hipSuccess) return fail(HJ_ERR_OOM, std::string("hipMallocAsync: ") + hipGetErrorString(e));
+    t->allocs.push_back(*p);
+    return HJ_OK;
+}
+
+// The device build, run once by the last partition to arrive at the barrier.
+hj_status run_build(hj_table* t) {
+    HIP_TRY(hipSetDevice(t->device));
+    // canonical numbering: partition 0's appends in order, then partition 1, ...
+    std::vector<Segment> segs;
+    t->part_off.assign(t->parallelism, 0);
+    int64_t row = 0;
+    for (int p = 0; p < t->parallelism; ++p) {
+        t->part_off[p] = row;
+        for (auto& hs : t->parts[p]) {
+            if (hs.n == 0) continue;
+            segs.push_back(Segment{hs.keys, hs.valid, hs.voff, hs.ids, hs.n, row});
+            row += hs.n;
+        }
+    }
+    t->total_rows = row;
+    for (int p = 0; p < t->parallelism; ++p)
+        for (auto& hs : t->parts[p])
+            if (hs.ready) HIP_TRY(hipStreamWaitEvent(t->stream, hs.ready, 0));
+    if (row > 0xFFFFFFF0ll)
+        return fail(HJ_ERR_INVALID, "build side exceeds 2^32-16 rows on one device; shard it");
+    if (t->has_ids && t->has_no_ids)
+        return fail(HJ_ERR_INVALID, "explicit build ids must be given for every batch or none");
+
+    const int64_t total = row;
+    double nbf = (double)total / (kSlots * load_factor());
+    uint64_t nb = (uint64_t)nbf + 1;
+    if (nb > (1ull << 29)) return fail(HJ_ERR_INVALID, "table too large");
+    t->nb = (uint32_t)nb;
+
+    HIP_TRY(hipEventRecord(t->ev0, t->stream));
+    hj_status st;
+    void* p;
+    if ((st = dev_alloc(t, &p, (size_t)(nb + 1) * sizeof(Bucket))) != HJ_OK) return st;
+    t->tbl = (Bucket*)p;
+    const int64_t half = total / 2 + 1;
+    if ((st = dev_alloc(t, &p, sizeof(uint2) * (size_t)std::max<int64_t>(total, 1))) != HJ_OK) return st;
+    t->duprows = (uint2*)p;
+    if ((st = dev_alloc(t, &p, sizeof(uint32_t) * (size_t)half)) != HJ_OK) return st;
+    t->dupslots = (uint32_t*)p;
+    if ((st = dev_alloc(t, &p, sizeof(DupDir) * (size_t)half)) != HJ_OK) return st;
+    t->dir = (DupDir*)p;
+    if ((st = dev_alloc(t, &p, sizeof(uint32_t) * (size_t)std::max<int64_t>(total, 1))) != HJ_OK) return st;
+    t->dup_rows = (uint32_t*)p;
+    if ((st = dev_alloc(t, &p, sizeof(uint32_t) * (size_t)(total / (kSmallSeg + 1) + 1))) != HJ_OK) return st;
+    t->big = (uint32_t*)p;
+    if ((st = dev_alloc(t, &p, sizeof(BuildCounters))) != HJ_OK) return st;
+    t->ctr = (BuildCounters*)p;
+    if (t->has_ids) {
+        if ((st = dev_alloc(t, &p, sizeof(uint64_t) * (size_t)std::max<int64_t>(total, 1))) != HJ_OK) return st;
+        t->row_ids = (uint64_t*)p;
+    }
+    if ((st = dev_alloc(t, &p, sizeof(Segment) * std::max<size_t>(segs.size(), 1))) != HJ_OK) return st;
+    t->d_segs = (Segment*)p;
+    if (!segs.empty())
+        HIP_TRY(hipMemcpyAsync(t->d_segs, segs.data(), sizeof(Segment) * segs.size(), hipMemcpyHostToDevice,
+                               t->stream));
+    HIP_TRY(hipMemsetAsync(t->tbl, 0, (size_t)(nb + 1) * sizeof(Bucket), t->stream));
+    HIP_TRY(hipMemsetAsync(t->ctr, 0, sizeof(BuildCounters), t->stream));
+
+    hipDeviceProp_t prop;
+    HIP_TRY(hipGetDeviceProperties(&prop, t->device));
+    const int grid = prop.multiProcessorCount * 8;
+    HIP_TRY(launch_insert(t->key_bytes, t->d_segs, (int)segs.size(), total, t->tbl, t->nb, t->row_ids,
+                          t->duprows, t->dupslots, t->ctr, grid, t->stream));
+    HIP_TRY(launch_dup_passes(t->tbl, t->nb, t->duprows, t->dupslots, t->dir, t->dup_rows, t->big, t->ctr,
+                              prop.multiProcessorCount * 4, t->stream));
+    HIP_TRY(launch_dup_big(t->tbl, t->nb, t->dir, t->dup_rows, t->big, t->ctr, t->d_segs, (int)segs.size(),
+                           total, t->key_bytes, prop.multiProcessorCount, t->stream));
+    HIP_TRY(hipEventRecord(t->ev1, t->stream));
+    BuildCounters hc;
+    HIP_TRY(hipMemcpyAsync(&hc, t->ctr, sizeof(hc), hipMemcpyDeviceToHost, t->stream));
+    HIP_TRY(hipStreamSynchronize(t->stream));
+    float ms = 0;
+    HIP_TRY(hipEventElapsedTime(&ms, t->ev0, t->ev1));
+    t->build_ns = (int64_t)(ms * 1e6);
+    if (hc.err) return fail(HJ_ERR_INVALID, "build: bucket probe exceeded table size");
+    return HJ_OK;
+}
+
+hj_status check_table(const hj_table* t) {
+    if (t == nullptr) return fail(HJ_ERR_INVALID, "null table");
+    if (!t->built) return fail(HJ_ERR_INVALID, "table is not built: every partition must call hj_build_finish");
+    if (t->build_st != HJ_OK) return fail(t->build_st, t->build_err);
+    return HJ_OK;
+}
+
+// device copy of host input (keys + validity bitmap slice)
+struct TmpInput {
+    void* keys = nullptr;
+    uint8_t* valid = nullptr;
+    int64_t voff = 0;
+    hipStream_t s = nullptr;
+    ~TmpInput() {
+        if (keys) (void)hipFreeAsync(keys, s);
+        if (valid) (void)hipFreeAsync(valid, s);
+    }
+};
+
+hj_status stage_input(int key_bytes, const void* keys, const uint8_t* valid, int64_t voff, int64_t n,
+                      uint32_t flags, hipStream_t s, TmpInput& tmp, const void** dkeys,
+                      const uint8_t** dvalid, int64_t* dvoff) {
+    if (flags & HJ_INPUT_DEVICE) {
+        if (!is_device_ptr(keys) || !is_device_ptr(valid))
+            return fail(HJ_ERR_INVALID, "HJ_INPUT_DEVICE given but a pointer is not device memory");
+        *dkeys = keys;
+        *dvalid = valid;
+        *dvoff = voff;
+        return HJ_OK;
+    }
+    tmp.s = s;
+    if (n > 0) {
+        HIP_TRY(hipMallocAsync(&tmp.keys, (size_t)n * key_bytes, s));
+        HIP_TRY(hipMemcpyAsync(tmp.keys, keys, (size_t)n * key_bytes, hipMemcpyDefault, s));
+    }
+    *dkeys = tmp.keys;
+    *dvalid = nullptr;
+    *dvoff = 0;
+    if (valid && n > 0) {
+        const int64_t b0 = voff >> 3;
+        const int64_t nbytes = ((voff & 7) + n + 7) >> 3;
+        HIP_TRY(hipMallocAsync((void**)&tmp.valid, (size_t)nbytes, s));
+        HIP_TRY(hipMemcpyAsync(tmp.valid, valid + b0, (size_t)nbytes, hipMemcpyDefault, s));
+        *dvalid = tmp.valid;
+        *dvoff = voff & 7;
+    }
+    return HJ_OK;
+}
+
+hj_status probe_impl(const hj_table* t, const void* keys, const uint8_t* valid, int64_t voff,
+                     const uint32_t* probe_ids, int64_t n, uint64_t* out_b, uint32_t* out_p, int64_t cap,
+                     int64_t* d_total, void* ws, hipStream_t s) {
+    if (n < 0 || n > 0xFFFFFFFFll) return fail(HJ_ERR_INVALID, "probe batch must have < 2^32 rows");
+    if (cap < 0) return fail(HJ_ERR_INVALID, "negative capacity");
+    const int64_t nt = probe_tiles(n);
+    HIP_TRY(hipMemsetAsync(ws, 0, (size_t)hj_probe_workspace_bytes(n), s));
+    if (nt == 0) {
+        HIP_TRY(hipMemsetAsync(d_total, 0, sizeof(int64_t), s));
+        return HJ_OK;
+    }
+    unsigned char* w = (unsigned char*)ws;
+    HIP_TRY(launch_probe(t->key_bytes, t->tbl, t->nb, t->dup_rows, t->row_ids, keys, valid, voff, probe_ids, n,
+                         out_b, out_p, cap, d_total, (unsigned long long*)(w + 16), (unsigned int*)w, s));
+    return HJ_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* hj_last_error(void) { return g_err.c_str(); }
+
+const char* hj_version(void) { return "dfp-hj 0.1 (gfx950)"; }
+
+int hj_device_count(void) { return device_count(); }
+
+hj_status hj_build_begin(int device, int parallelism, hj_key_type key_type, int64_t expected_rows,
+                         hj_table** out) {
+    (void)expected_rows;
+    if (out == nullptr) return fail(HJ_ERR_INVALID, "null out");
+    *out = nullptr;
+    if (parallelism < 1) return fail(HJ_ERR_INVALID, "parallelism must be >= 1");
+    if (key_type != HJ_INT32 && key_type != HJ_INT64) return fail(HJ_ERR_INVALID, "unsupported key type");
+    const int nd = device_count();
+    if (nd == 0) return fail(HJ_ERR_NO_DEVICE, "no GPU visible: the HIP path cannot run (no CPU fallback)");
+    if (device < 0 || device >= nd) return fail(HJ_ERR_INVALID, "bad device ordinal");
+    HIP_TRY(hipSetDevice(device));
+    hj_table* t = new hj_table();
+    t->device = device;
+    t->parallelism = parallelism;
+    t->kt = key_type;
+    t->key_bytes = key_type == HJ_INT64 ? 8 : 4;
+    t->parts.resize(parallelism);
+    t->finished.assign(parallelism, 0);
+    if (hipStreamCreateWithFlags(&t->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreate(&t->ev0) != hipSuccess || hipEventCreate(&t->ev1) != hipSuccess) {
+        delete t;
+        return fail(HJ_ERR_HIP, "stream/event creation failed");
+    }
+    // keep freed blocks in the pool: repeated builds re-use device memory
+    hipMemPool_t pool;
+    if (hipDeviceGetDefaultMemPool(&pool, device) == hipSuccess) {
+        uint64_t thr = UINT64_MAX;
+        (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &thr);
+    }
+    *out = t;
+    return HJ_OK;
+}
+
+hj_status hj_build_append(hj_table* t, int partition, const void* keys, const uint8_t* validity,
+                          int64_t validity_offset, const uint64_t* ids, int64_t n, uint32_t flags, void* stream) {
+    if (t == nullptr) return fail(HJ_ERR_INVALID, "null table");
+    if (partition < 0 || partition >= t->parallelism) return fail(HJ_ERR_INVALID, "bad partition");
+    if (n < 0 || validity_offset < 0) return fail(HJ_ERR_INVALID, "negative length/offset");
+    if (n > 0 && keys == nullptr) return fail(HJ_ERR_INVALID, "null keys");
+    {
+        std::lock_guard<std::mutex> g(t->mu);
+        if (t->finished[partition])
+            return fail(HJ_ERR_INVALID, "State already consumed for partition " + std::to_string(partition));
+        if (n > 0) { if (ids) t->has_ids = true; else t->has_no_ids = true; }
+    }
+    HIP_TRY(hipSetDevice(t->device));
+    HostSeg hs;
+    hs.n = n;
+    if (n == 0) return HJ_OK;
+    // the producer's stream: the build waits for its work (borrow) or copies in its order
+    hipStream_t s = (hipStream_t)stream;
+    if ((flags & HJ_INPUT_DEVICE) && (flags & HJ_BORROW)) {
+        if (!is_device_ptr(keys) || !is_device_ptr(validity) || !is_device_ptr(ids))
+            return fail(HJ_ERR_INVALID, "HJ_INPUT_DEVICE given but a pointer is not device memory");
+        HIP_TRY(hipEventCreateWithFlags(&hs.ready, hipEventDisableTiming));
+        HIP_TRY(hipEventRecord(hs.ready, s));
+        hs.keys = keys;
+        hs.valid = validity;
+        hs.voff = validity_offset;
+        hs.ids = ids;
+    } else {
+        if ((flags & HJ_INPUT_DEVICE) && (!is_device_ptr(keys) || !is_device_ptr(validity) || !is_device_ptr(ids)))
+            return fail(HJ_ERR_INVALID, "HJ_INPUT_DEVICE given but a pointer is not device memory");
+        void* dk = nullptr;
+        HIP_TRY(hipMalloc(&dk, (size_t)n * t->key_bytes));
+        hs.owned.push_back(dk);
+        HIP_TRY(hipMemcpyAsync(dk, keys, (size_t)n * t->key_bytes, hipMemcpyDefault, s));
+        hs.keys = dk;
+        if (validity) {
+            const int64_t b0 = validity_offset >> 3;
+            const int64_t nbytes = ((validity_offset & 7) + n + 7) >> 3;
+            void* dv = nullptr;
+            HIP_TRY(hipMalloc(&dv, (size_t)nbytes));
+            hs.owned.push_back(dv);
+            HIP_TRY(hipMemcpyAsync(dv, validity + b0, (size_t)nbytes, hipMemcpyDefault, s));
+            hs.valid = (const uint8_t*)dv;
+            hs.voff = validity_offset & 7;
+        }
+        if (ids) {
+            void* di = nullptr;
+            HIP_TRY(hipMalloc(&di, (size_t)n * 8));
+            hs.owned.push_back(di);
+            HIP_TRY(hipMemcpyAsync(di, ids, (size_t)n * 8, hipMemcpyDefault, s));
+            hs.ids = (const uint64_t*)di;
+        }
+        HIP_TRY(hipStreamSynchronize(s));
+    }
+    std::lock_guard<std::mutex> g(t->mu);
+    t->parts[partition].push_back(std::move(hs));
+    return HJ_OK;
+}
+
+hj_status hj_build_finish(hj_table* t, int partition) {
+    if (t == nullptr) return fail(HJ_ERR_INVALID, "null table");
+    if (partition < 0 || partition >= t->parallelism) return fail(HJ_ERR_INVALID, "bad partition");
+    std::unique_lock<std::mutex> g(t->mu);
+    if (t->finished[partition])
+        return fail(HJ_ERR_INVALID, "State already consumed for partition " + std::to_string(partition));
+    t->finished[partition] = 1;
+    t->arrived++;
+    if (t->arrived == t->parallelism) {
+        // last arriver finalises (InitializeLast::initialize_or_wait)
+        hj_status st = run_build(t);
+        t->build_st = st;
+        t->build_err = st == HJ_OK ? "" : g_err;
+        t->built = true;
+        t->cv.notify_all();
+    } else {
+        // a partition that never arrives would block the rest forever; like the
+        // reference's "Possible deadlock" timeouts (src/utils/parallel_compaction_batch_list.rs:56-58)
+        const char* e = getenv("DFP_HJ_BARRIER_TIMEOUT_S");
+        const double secs = e ? atof(e) : 300.0;
+        if (!t->cv.wait_for(g, std::chrono::duration<double>(secs), [t] { return t->built; }))
+            return fail(HJ_ERR_INVALID, "Possible deadlock: partition " + std::to_string(partition) +
+                                            " waited for the build barrier; every partition must call "
+                                            "hj_build_finish concurrently");
+    }
+    if (t->build_st != HJ_OK) return fail(t->build_st, t->build_err);
+    return HJ_OK;
+}
+
+hj_status hj_build_partition_offset(const hj_table* t, int partition, int64_t* out) {
+    hj_status st = check_table(t);
+    if (st != HJ_OK) return st;
+    if (partition < 0 || partition >= t->parallelism || out == nullptr) return fail(HJ_ERR_INVALID, "bad args");
+    *out = t->part_off[partition];
+    return HJ_OK;
+}
+
+hj_status hj_table_stats_get(const hj_table* t, hj_table_stats* out) {
+    hj_status st = check_table(t);
+    if (st != HJ_OK) return st;
+    if (out == nullptr) return fail(HJ_ERR_INVALID, "null out");
+    HIP_TRY(hipSetDevice(t->device));
+    hipStream_t s = thread_stream(t->device);
+    unsigned long long* d = nullptr;
+    HIP_TRY(hipMallocAsync((void**)&d, 4 * sizeof(unsigned long long), s));
+    HIP_TRY(hipMemsetAsync(d, 0, 4 * sizeof(unsigned long long), s));
+    HIP_TRY(launch_table_stats(t->tbl, t->nb, d, s));
+    unsigned long long h[4];
+    HIP_TRY(hipMemcpyAsync(h, d, sizeof(h), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipFreeAsync(d, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    out->build_rows = t->total_rows;
+    out->distinct_keys = (int64_t)h[0];
+    out->dup_keys = (int64_t)h[1];
+    out->dup_rows = (int64_t)h[2];
+    out->max_key_rows = (int64_t)h[3];
+    out->inserted_rows = (int64_t)h[0] - (int64_t)h[1] + (int64_t)h[2];
+    out->buckets = t->nb;
+    out->table_bytes = (int64_t)(t->nb + 1) * (int64_t)sizeof(Bucket);
+    out->build_ns = t->build_ns;
+    return HJ_OK;
+}
+
+int64_t hj_table_build_ns(const hj_table* t) {
+    if (t == nullptr || !t->built || t->build_st != HJ_OK) return -1;
+    return t->build_ns;
+}
+
+int64_t hj_probe_workspace_bytes(int64_t n) { return 16 + 8 * (probe_tiles(n > 0 ? n : 0) + 1); }
+
+hj_status hj_probe_async(const hj_table* t, const void* keys, const uint8_t* validity, int64_t validity_offset,
+                         int64_t n, uint64_t* out_build, uint32_t* out_probe, int64_t capacity, int64_t* d_total,
+                         void* workspace, void* stream) {
+    hj_status st = check_table(t);
+    if (st != HJ_OK) return st;
+    if (d_total == nullptr || workspace == nullptr) return fail(HJ_ERR_INVALID, "null d_total/workspace");
+    if (n > 0 && keys == nullptr) return fail(HJ_ERR_INVALID, "null keys");
+    HIP_TRY(hipSetDevice(t->device));
+    return probe_impl(t, keys, validity, validity_offset, nullptr, n, out_build, out_probe, capacity, d_total,
+                      workspace, (hipStream_t)stream /* NULL = the null stream */);
+}
+
+hj_status hj_probe_async_ids(const hj_table* t, const void* keys, const uint8_t* validity,
+                             int64_t validity_offset, const uint32_t* probe_ids, int64_t n, uint64_t* out_build,
+                             uint32_t* out_probe, int64_t capacity, int64_t* d_total, void* workspace,
+                             void* stream) {
+    hj_status st = check_table(t);
+    if (st != HJ_OK) return st;
+    if (d_total == nullptr || workspace == nullptr) return fail(HJ_ERR_INVALID, "null d_total/workspace");
+    HIP_TRY(hipSetDevice(t->device));
+    return probe_impl(t, keys, validity, validity_offset, probe_ids, n, out_build, out_probe, capacity, d_total,
+                      workspace, (hipStream_t)stream /* NULL = the null stream */);
+}
+
+hj_status hj_probe(const hj_table* t, const void* keys, const uint8_t* validity, int64_t validity_offset, int64_t n,
+                   uint32_t flags, void* stream, hj_pairs* out) {
+    hj_status st = check_table(t);
+    if (st != HJ_OK) return st;
+    if (out == nullptr) return fail(HJ_ERR_INVALID, "null out");
+    memset(out, 0, sizeof(*out));
+    if (n < 0) return fail(HJ_ERR_INVALID, "negative length");
+    if (n > 0 && keys == nullptr) return fail(HJ_ERR_INVALID, "null keys");
+    HIP_TRY(hipSetDevice(t->device));
+    hipStream_t s = (hipStream_t)stream;  // NULL = null stream
+    TmpInput tmp;
+    const void* dk;
+    const uint8_t* dv;
+    int64_t dvo;
+    if ((st = stage_input(t->key_bytes, keys, validity, validity_offset, n, flags, s, tmp, &dk, &dv, &dvo)) != HJ_OK)
+        return st;
+    void* ws = nullptr;
+    int64_t* d_total = nullptr;
+    HIP_TRY(hipMallocAsync(&ws, (size_t)hj_probe_workspace_bytes(n), s));
+    HIP_TRY(hipMallocAsync((void**)&d_total, sizeof(int64_t), s));
+    int64_t cap = std::max<int64_t>(n, 1);
+    uint64_t* ob = nullptr;
+    uint32_t* op = nullptr;
+    int64_t total = 0;
+    for (int attempt = 0; attempt < 2; ++attempt) {
+        HIP_TRY(hipMalloc((void**)&ob, (size_t)cap * 8));
+        HIP_TRY(hipMalloc((void**)&op, (size_t)cap * 4));
+        if ((st = probe_impl(t, dk, dv, dvo, nullptr, n, ob, op, cap, d_total, ws, s)) != HJ_OK) break;
+        unsigned long long err = 0;
+        HIP_TRY(hipMemcpyAsync(&total, d_total, 8, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipMemcpyAsync(&err, (char*)ws + 8, 8, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        if (err) { st = fail(HJ_ERR_HIP, "probe look-back timed out"); break; }
+        if (total <= cap) break;
+        (void)hipFree(ob);
+        (void)hipFree(op);
+        ob = nullptr;
+        op = nullptr;
+        cap = total;
+    }
+    (void)hipFreeAsync(ws, s);
+    (void)hipFreeAsync(d_total, s);
+    if (st != HJ_OK) {
+        if (ob) (void)hipFree(ob);
+        if (op) (void)hipFree(op);
+        (void)hipStreamSynchronize(s);
+        return st;
+    }
+    out->count = total;
+    if (flags & HJ_OUTPUT_HOST) {
+        out->build_idx = (uint64_t*)malloc((size_t)std::max<int64_t>(total, 1) * 8);
+        out->probe_idx = (uint32_t*)malloc((size_t)std::max<int64_t>(total, 1) * 4);
+        if (!out->build_idx || !out->probe_idx) {
+            free(out->build_idx);
+            free(out->probe_idx);
+            (void)hipFree(ob);
+            (void)hipFree(op);
+            return fail(HJ_ERR_OOM, "host allocation failed");
+        }
+        if (total > 0) {
+            HIP_TRY(hipMemcpyAsync(out->build_idx, ob, (size_t)total * 8, hipMemcpyDeviceToHost, s));
+            HIP_TRY(hipMemcpyAsync(out->probe_idx, op, (size_t)total * 4, hipMemcpyDeviceToHost, s));
+        }
+        HIP_TRY(hipStreamSynchronize(s));
+        (void)hipFree(ob);
+        (void)hipFree(op);
+        out->device_resident = 0;
+    } else {
+        HIP_TRY(hipStreamSynchronize(s));
+        out->build_idx = ob;
+        out->probe_idx = op;
+        out->device_resident = 1;
+    }
+    return HJ_OK;
+}
+
+void hj_pairs_free(hj_pairs* p) {
+    if (p == nullptr) return;
+    if (p->device_resident) {
+        if (p->build_idx) (void)hipFree(p->build_idx);
+        if (p->probe_idx) (void)hipFree(p->probe_idx);
+    } else {
+        free(p->build_idx);
+        free(p->probe_idx);
+    }
+    memset(p, 0, sizeof(*p));
+}
+
+hj_status hj_table_lookup(const hj_table* t, int64_t key, uint64_t* rows, int64_t cap, int64_t* count) {
+    hj_status st = check_table(t);
+    if (st != HJ_OK) return st;
+    if (count == nullptr || (cap > 0 && rows == nullptr)) return fail(HJ_ERR_INVALID, "bad args");
+    hj_pairs pr;
+    int32_t k32 = (int32_t)key;
+    if (t->kt == HJ_INT32 && (int64_t)k32 != key) {  // cannot be present
+        *count = 0;
+        return HJ_OK;
+    }
+    const void* kp = t->kt == HJ_INT64 ? (const void*)&key : (const void*)&k32;
+    if ((st = hj_probe(t, kp, nullptr, 0, 1, HJ_OUTPUT_HOST, thread_stream(t->device), &pr)) != HJ_OK) return st;
+    *count = pr.count;
+    for (int64_t i = 0; i < std::min<int64_t>(cap, pr.count); ++i) rows[i] = pr.build_idx[i];
+    hj_pairs_free(&pr);
+    return HJ_OK;
+}
+
+hj_status hj_table_chain_links(const hj_table* t, int64_t* prev, int64_t n) {
+    hj_status st = check_table(t);
+    if (st != HJ_OK) return st;
+    if (n != t->total_rows || (n > 0 && prev == nullptr)) return fail(HJ_ERR_INVALID, "prev must hold build_rows entries");
+    if (n == 0) return HJ_OK;
+    HIP_TRY(hipSetDevice(t->device));
+    hipStream_t s = thread_stream(t->device);
+    int64_t* d = nullptr;
+    HIP_TRY(hipMallocAsync((void**)&d, (size_t)n * 8, s));
+    HIP_TRY(launch_chain_links(t->tbl, t->nb, t->dup_rows, d, n, s));
+    HIP_TRY(hipMemcpyAsync(prev, d, (size_t)n * 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipFreeAsync(d, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    return HJ_OK;
+}
+
+hj_status hj_table_stream_wait(const hj_table* t, void* stream) {
+    hj_status st = check_table(t);
+    if (st != HJ_OK) return st;
+    HIP_TRY(hipStreamWaitEvent((hipStream_t)stream, t->ev1, 0));
+    return HJ_OK;
+}
+
+void hj_table_free(hj_table* t) {
+    if (t == nullptr) return;
+    (void)hipSetDevice(t->device);
+    for (void* p : t->allocs) (void)hipFreeAsync(p, t->stream);
+    (void)hipStreamSynchronize(t->stream);
+    for (auto& part : t->parts)
+        for (auto& hs : part)
+        {
+            for (void* p : hs.owned) (void)hipFree(p);
+            if (hs.ready) (void)hipEventDestroy(hs.ready);
+        }
+    if (t->ev0) (void)hipEventDestroy(t->ev0);
+    if (t->ev1) (void)hipEventDestroy(t->ev1);
+    if (t->stream) (void)hipStreamDestroy(t->stream);
+    delete t;
+}
+
+int64_t hj_partition_workspace_bytes(int64_t n, int nparts) { return radix_partition_workspace(n, nparts); }
+
+hj_status hj_radix_partition(hj_key_type key_type, const void* keys, const uint8_t* validity,
+                             int64_t validity_offset, const uint64_t* ids, uint64_t id_base, int64_t n, int nparts,
+                             void* out_keys, uint64_t* out_ids, int64_t* counts, void* workspace, void* stream) {
+    if (device_count() == 0) return fail(HJ_ERR_NO_DEVICE, "no GPU visible");
+    if (nparts < 1 || nparts > 64 || (nparts & (nparts - 1))) return fail(HJ_ERR_INVALID, "nparts must be a power of two <= 64");
+    if (n < 0) return fail(HJ_ERR_INVALID, "negative length");
+    if (!is_device_ptr(keys) || !is_device_ptr(validity) || !is_device_ptr(ids) || !is_device_ptr(out_keys) ||
+        !is_device_ptr(out_ids) || !is_device_ptr(counts) || !is_device_ptr(workspace))
+        return fail(HJ_ERR_INVALID, "hj_radix_partition takes device pointers");
+    HIP_TRY(launch_radix_partition(key_type == HJ_INT64 ? 8 : 4, keys, validity, validity_offset, ids, id_base, n,
+                                   nparts, out_keys, out_ids, counts, workspace, (hipStream_t)stream));
+    return HJ_OK;
+}
+
+hj_status hj_gen_perm_keys(int64_t* out, int64_t n, int64_t mul, int64_t range, void* stream) {
+    if (device_count() == 0) return fail(HJ_ERR_NO_DEVICE, "no GPU visible");
+    if (range <= 0 || n < 0) return fail(HJ_ERR_INVALID, "bad range");
+    HIP_TRY(launch_gen_perm(out, n, mul, range, (hipStream_t)stream));
+    return HJ_OK;
+}
+
+hj_status hj_gen_uniform_keys(int64_t* out, int64_t n, uint64_t seed, int64_t range, void* stream) {
+    if (device_count() == 0) return fail(HJ_ERR_NO_DEVICE, "no GPU visible");
+    if (range <= 0 || n < 0) return fail(HJ_ERR_INVALID, "bad range");
+    HIP_TRY(launch_gen_uniform(out, n, seed, range, (hipStream_t)stream));
+    return HJ_OK;
+}
+
+}  // extern "C"

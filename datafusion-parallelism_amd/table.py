@@ -1,0 +1,266 @@
+"""Thin RAII wrapper of one device hash table (``hj_table``) of the C ABI.
+
+Accepts key columns as pyarrow Int32/Int64 arrays (host, zero-copy pointers incl. the
+validity bitmap and offset), numpy int32/int64 arrays (+ optional boolean validity), or
+torch int32/int64 tensors (device tensors are passed as device pointers).
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+from typing import Any
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import HJ_BORROW, HJ_INPUT_DEVICE, HJ_INT32, HJ_INT64, HJ_OUTPUT_HOST, check
+
+try:  # pyarrow is optional for the device path
+    import pyarrow as pa
+except ImportError:  # pragma: no cover
+    pa = None
+
+
+@dataclass
+class KeyInput:
+    ptr: int
+    valid_ptr: int | None
+    voff: int
+    n: int
+    flags: int
+    key_type: int
+    keepalive: Any
+
+
+def _key_type_of_dtype(dt) -> int:
+    if dt in (np.int64, torch.int64) or str(dt) in ("int64",):
+        return HJ_INT64
+    if dt in (np.int32, torch.int32) or str(dt) in ("int32",):
+        return HJ_INT32
+    raise TypeError(f"join keys must be int32 or int64, got {dt}")
+
+
+def as_key_input(keys, valid=None) -> KeyInput:
+    """Normalise a key column into raw pointers for the C ABI."""
+    if pa is not None and isinstance(keys, pa.ChunkedArray):
+        keys = keys.combine_chunks()
+    if pa is not None and isinstance(keys, pa.Array):
+        if pa.types.is_int64(keys.type):
+            kt, isz = HJ_INT64, 8
+        elif pa.types.is_int32(keys.type):
+            kt, isz = HJ_INT32, 4
+        else:
+            raise TypeError(f"join keys must be Int32 or Int64, got {keys.type}")
+        if valid is not None:
+            raise ValueError("pyarrow arrays carry their own validity")
+        bufs = keys.buffers()
+        data = bufs[1]
+        ptr = (data.address if data is not None else 0) + keys.offset * isz
+        vptr = bufs[0].address if (bufs[0] is not None and keys.null_count > 0) else None
+        return KeyInput(ptr, vptr, keys.offset if vptr else 0, len(keys), 0, kt, keys)
+    if isinstance(keys, torch.Tensor):
+        kt = _key_type_of_dtype(keys.dtype)
+        t = keys.contiguous()
+        flags = HJ_INPUT_DEVICE if t.is_cuda else 0
+        vptr, keep_v = None, None
+        if valid is not None:
+            vb = torch.as_tensor(valid)
+            if vb.dtype == torch.bool:  # mask -> LSB bitmap
+                bits = np.packbits(vb.cpu().numpy(), bitorder="little")
+                vb = torch.from_numpy(bits)
+                if t.is_cuda:
+                    vb = vb.to(t.device)
+            keep_v = vb.contiguous()
+            vptr = keep_v.data_ptr()
+        return KeyInput(t.data_ptr(), vptr, 0, t.numel(), flags, kt, (t, keep_v))
+    a = np.ascontiguousarray(np.asarray(keys))
+    kt = _key_type_of_dtype(a.dtype)
+    vptr, keep_v = None, None
+    if valid is not None:
+        bits = np.packbits(np.asarray(valid, dtype=bool), bitorder="little")
+        keep_v = bits
+        vptr = bits.ctypes.data
+    return KeyInput(a.ctypes.data if a.size else 0, vptr, 0, a.size, 0, kt, (a, keep_v))
+
+
+def _producer_stream(keys, device: int) -> int | None:
+    """torch's current stream for device tensors (the stream that produced them)."""
+    if isinstance(keys, torch.Tensor) and keys.is_cuda:
+        return torch.cuda.current_stream(keys.device).cuda_stream or None
+    return None
+
+
+class HashTable:
+    """One shared build table for `parallelism` partitions (hj_build_begin .. finish)."""
+
+    def __init__(self, parallelism: int = 1, key_type: str | int = "int64", device: int = 0,
+                 expected_rows: int = 0):
+        self._L = _lib.load()
+        kt = key_type if isinstance(key_type, int) else (HJ_INT64 if key_type == "int64" else HJ_INT32)
+        if key_type not in ("int64", "int32", HJ_INT32, HJ_INT64):
+            raise TypeError(f"unsupported key type {key_type}")
+        self.key_type = kt
+        self.parallelism = parallelism
+        self.device = device
+        h = ctypes.c_void_p()
+        check(self._L.hj_build_begin(device, parallelism, kt, expected_rows, ctypes.byref(h)))
+        self._h = h
+        self._keep = []  # borrowed device inputs stay alive until the barrier
+
+    # -- build --------------------------------------------------------------
+    def append(self, partition: int, keys, valid=None, ids=None, borrow: bool = True) -> None:
+        ki = as_key_input(keys, valid)
+        if ki.n and ki.key_type != self.key_type:
+            raise TypeError("key type of the batch differs from the table's")
+        flags = ki.flags | (HJ_BORROW if (borrow and ki.flags & HJ_INPUT_DEVICE) else 0)
+        ids_ptr, keep_ids = None, None
+        if ids is not None:
+            if isinstance(ids, torch.Tensor):
+                keep_ids = ids.to(torch.int64).contiguous()
+                ids_ptr = keep_ids.data_ptr()
+            else:
+                keep_ids = np.ascontiguousarray(np.asarray(ids, dtype=np.uint64))
+                ids_ptr = keep_ids.ctypes.data
+        check(self._L.hj_build_append(self._h, partition, ki.ptr or None, ki.valid_ptr, ki.voff, ids_ptr, ki.n,
+                                      flags, _producer_stream(keys, self.device)))
+        if flags & HJ_BORROW:
+            self._keep.append((ki.keepalive, keep_ids))
+
+    def finish(self, partition: int) -> None:
+        check(self._L.hj_build_finish(self._h, partition))
+
+    def finish_all(self) -> None:
+        """Call the barrier for every partition concurrently (one thread each), as
+        DataFusion's executor does for the reference's partitions."""
+        import threading
+
+        errs = []
+
+        def run(p):
+            try:
+                self.finish(p)
+            except Exception as e:  # noqa: BLE001
+                errs.append(e)
+
+        ths = [threading.Thread(target=run, args=(p,)) for p in range(self.parallelism)]
+        for th in ths:
+            th.start()
+        for th in ths:
+            th.join()
+        if errs:
+            raise errs[0]
+
+    def build(self, keys, valid=None, ids=None) -> "HashTable":
+        """Single-partition convenience: append + finish."""
+        self.append(0, keys, valid, ids)
+        self.finish(0)
+        return self
+
+    def partition_offset(self, partition: int) -> int:
+        v = ctypes.c_int64()
+        check(self._L.hj_build_partition_offset(self._h, partition, ctypes.byref(v)))
+        return v.value
+
+    def build_ns(self) -> int:
+        """Device time of the build (HIP events), no device work."""
+        return self._L.hj_table_build_ns(self._h)
+
+    def stats(self) -> dict:
+        s = _lib.HjTableStats()
+        check(self._L.hj_table_stats_get(self._h, ctypes.byref(s)))
+        return {f: getattr(s, f) for f, _ in s._fields_}
+
+    # -- lookups ------------------------------------------------------------
+    def lookup(self, key: int) -> list[int]:
+        """IndexLookup::get_iter: build rows of `key`, newest first (descending)."""
+        cnt = ctypes.c_int64()
+        check(self._L.hj_table_lookup(self._h, int(key), None, 0, ctypes.byref(cnt)))
+        out = np.empty(max(cnt.value, 1), dtype=np.uint64)
+        check(self._L.hj_table_lookup(self._h, int(key), out.ctypes.data, cnt.value, ctypes.byref(cnt)))
+        return [int(x) for x in out[: cnt.value]]
+
+    def chain_links(self, nrows: int) -> np.ndarray:
+        out = np.empty(max(nrows, 1), dtype=np.int64)
+        check(self._L.hj_table_chain_links(self._h, out.ctypes.data, nrows))
+        return out[:nrows]
+
+    # -- probe --------------------------------------------------------------
+    def probe(self, keys, valid=None, device_output: bool = False):
+        """Synchronous probe; returns (build_idx uint64, probe_idx uint32) in canonical
+        order as numpy arrays, or as torch device tensors (int64, int32) with
+        device_output=True (then keys must be a device tensor)."""
+        if device_output:
+            return self._probe_device(keys, valid)
+        ki = as_key_input(keys, valid)
+        if ki.n and ki.key_type != self.key_type:
+            raise TypeError("probe key type differs from the build key type")
+        pr = _lib.HjPairs()
+        flags = ki.flags | HJ_OUTPUT_HOST
+        check(self._L.hj_probe(self._h, ki.ptr or None, ki.valid_ptr, ki.voff, ki.n, flags,
+                               _producer_stream(keys, self.device), ctypes.byref(pr)))
+        try:
+            n = pr.count
+            b = np.ctypeslib.as_array(pr.build_idx, shape=(n,)).copy() if n else np.empty(0, np.uint64)
+            p = np.ctypeslib.as_array(pr.probe_idx, shape=(n,)).copy() if n else np.empty(0, np.uint32)
+            return b, p
+        finally:
+            self._L.hj_pairs_free(ctypes.byref(pr))
+
+    def _probe_device(self, keys: torch.Tensor, valid=None):
+        if not (isinstance(keys, torch.Tensor) and keys.is_cuda):
+            raise TypeError("device_output=True takes a device tensor of keys")
+        ki = as_key_input(keys, valid)
+        if ki.n and ki.key_type != self.key_type:
+            raise TypeError("probe key type differs from the build key type")
+        dev = keys.device
+        ws = torch.empty(self.workspace_bytes(ki.n), dtype=torch.uint8, device=dev)
+        d_total = torch.zeros(1, dtype=torch.int64, device=dev)
+        cap = max(ki.n, 1)
+        stream = torch.cuda.current_stream(dev).cuda_stream
+        for _ in range(2):
+            ob = torch.empty(cap, dtype=torch.int64, device=dev)
+            op = torch.empty(cap, dtype=torch.int32, device=dev)
+            self.probe_async(ki.ptr, ki.n, ob.data_ptr(), op.data_ptr(), cap, d_total.data_ptr(), ws.data_ptr(),
+                             stream, ki.valid_ptr, ki.voff)
+            total = int(d_total.item())
+            if int(ws[8:16].view(torch.int64).item()) != 0:
+                raise _lib.HjError(_lib.HJ_ERR_HIP, "probe look-back timed out")
+            if total <= cap:
+                return ob[:total], op[:total]
+            cap = total
+        raise RuntimeError("unreachable")
+
+    def probe_async(self, keys_ptr: int, n: int, out_build_ptr: int, out_probe_ptr: int, capacity: int,
+                    d_total_ptr: int, workspace_ptr: int, stream: int = 0, valid_ptr: int | None = None,
+                    voff: int = 0, probe_ids_ptr: int | None = None) -> None:
+        """hj_probe_async(_ids) on raw device pointers (no sync, no allocation)."""
+        if probe_ids_ptr is None:
+            check(self._L.hj_probe_async(self._h, keys_ptr, valid_ptr, voff, n, out_build_ptr, out_probe_ptr,
+                                         capacity, d_total_ptr, workspace_ptr, stream or None))
+        else:
+            check(self._L.hj_probe_async_ids(self._h, keys_ptr, valid_ptr, voff, probe_ids_ptr, n, out_build_ptr,
+                                             out_probe_ptr, capacity, d_total_ptr, workspace_ptr, stream or None))
+
+    @staticmethod
+    def workspace_bytes(n: int) -> int:
+        return _lib.load().hj_probe_workspace_bytes(n)
+
+    # -- lifetime -----------------------------------------------------------
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            self._L.hj_table_free(self._h)
+            self._h = None
+            self._keep.clear()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

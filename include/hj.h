@@ -1,0 +1,199 @@
+/*
+ * hj.h — C ABI of the MI355X-native parallel hash join (build + inner probe).
+ *
+ * This is the drop-in boundary for the hot path of jamesfer/datafusion-parallelism
+ * (paths below are relative to that repository). Every entry point names the
+ * reference interface it replaces. Plain pointers and sizes only; no torch or HIP
+ * types appear here (a stream is an opaque `void*` that is a hipStream_t, NULL =
+ * the null stream).
+ *
+ * Semantics (canonical parity contract):
+ *   * build_row_idx  = position of the row in the concatenation of all appended
+ *                      build rows in (partition 0 appends in order, partition 1, ...)
+ *                      order; or the caller's explicit id when `ids` is given.
+ *   * probe_row_idx  = position of the row inside the probe call (the reference's
+ *                      per-batch u32 index, src/shared/shared.rs:32-41).
+ *   * pair order     = probe ascending, then build index DESCENDING within a probe
+ *                      row (the reference's newest-first chain order at parallelism 1,
+ *                      src/utils/concurrent_self_hash_join_map.rs:223-249).
+ *   * null keys never match (src/shared/datafusion_private.rs:18-38 with
+ *     null_equals_null = false, src/operator/probe_lookup_implementation/inner.rs:101-108).
+ *   * pairs are those of get_matching_indices + equal_rows_arr
+ *     (src/shared/shared.rs:29-47, src/shared/datafusion_private.rs:40-80): exact key
+ *     equality, independent of the hash function.
+ */
+#ifndef DFP_HJ_H
+#define DFP_HJ_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum hj_status {
+    HJ_OK = 0,
+    HJ_ERR_INVALID = 1,   /* bad argument / state (DataFusionError::Internal) */
+    HJ_ERR_OOM = 2,       /* device allocation failed */
+    HJ_ERR_HIP = 3,       /* HIP runtime error */
+    HJ_ERR_RCCL = 4,      /* reserved for the multi-GPU exchange */
+    HJ_ERR_CAPACITY = 5,  /* output buffer too small; *count holds the size needed */
+    HJ_ERR_NO_DEVICE = 6  /* no GPU: the HIP path cannot run (there is no CPU fallback) */
+} hj_status;
+
+typedef enum hj_key_type { HJ_INT32 = 0, HJ_INT64 = 1 } hj_key_type;
+
+/* flags for hj_build_append / hj_probe */
+enum {
+    HJ_INPUT_DEVICE = 1u << 0, /* pointers are device memory (else host memory, copied) */
+    HJ_BORROW = 1u << 1,       /* device input is not copied: caller keeps it alive until
+                                  hj_build_finish returns on every partition */
+    HJ_OUTPUT_HOST = 1u << 2   /* hj_probe: return pairs in host memory (else device) */
+};
+
+typedef struct hj_table hj_table; /* opaque, device resident */
+
+/* Match pairs of one probe call (ProbeBuildIndices, src/shared/shared.rs:24-27).
+ * Owned by the library; release with hj_pairs_free. */
+typedef struct hj_pairs {
+    uint64_t* build_idx;   /* UInt64 build indices (length count) */
+    uint32_t* probe_idx;   /* UInt32 probe indices (length count) */
+    int64_t count;
+    int device_resident;   /* 1: pointers are device memory; 0: host memory */
+} hj_pairs;
+
+/* Build statistics, filled by hj_table_stats after the build barrier. */
+typedef struct hj_table_stats {
+    int64_t build_rows;     /* rows appended (incl. null rows) */
+    int64_t inserted_rows;  /* non-null rows inserted */
+    int64_t distinct_keys;  /* occupied slots */
+    int64_t dup_keys;       /* keys with > 1 row */
+    int64_t dup_rows;       /* rows belonging to keys with > 1 row */
+    int64_t max_key_rows;   /* largest chain length */
+    int64_t buckets;        /* 64-byte buckets of 4 slots */
+    int64_t table_bytes;    /* device bytes of the slot table */
+    int64_t build_ns;       /* device time of the last build (HIP events) */
+} hj_table_stats;
+
+/* ---- library ------------------------------------------------------------ */
+
+/* Last error text of the calling thread ("" if none). */
+const char* hj_last_error(void);
+/* Version string; "gfx950" code object target is baked in. */
+const char* hj_version(void);
+/* Number of visible GPUs (0 on a machine without one). */
+int hj_device_count(void);
+
+/* ---- build: replaces BuildImplementation::new / build_side
+ *      (src/operator/build_implementation.rs:34-48, 50-112) and the v10 insert
+ *      path (src/operator/version10/parallel_join_execution_state.rs:91-133,
+ *      src/operator/version10/new_map_3/fixed_table.rs:560-672). ----------------- */
+
+/* Create a table for `parallelism` build partitions on GPU `device`.
+ * `expected_rows` sizes the staging (a hint; 0 is fine). */
+hj_status hj_build_begin(int device, int parallelism, hj_key_type key_type,
+                         int64_t expected_rows, hj_table** out);
+
+/* Append one build batch of partition `partition` (one RecordBatch's key column).
+ * keys: int32/int64 values; validity: Arrow LSB bitmap (NULL = all valid) starting at
+ * bit `validity_offset`; ids: optional explicit build ids (NULL = canonical numbering).
+ * stream: the stream on which device input is produced (NULL = the null stream); the
+ * build waits for the work enqueued on it up to this call.
+ * Thread-safe: one caller per partition, partitions concurrently
+ * (JoinStateInstance::add, version10/parallel_join_execution_state.rs:91-133). */
+hj_status hj_build_append(hj_table* t, int partition, const void* keys,
+                          const uint8_t* validity, int64_t validity_offset,
+                          const uint64_t* ids, int64_t n, uint32_t flags, void* stream);
+
+/* Barrier: every one of the `parallelism` partitions calls this once. The last
+ * arriver runs the device build (InitializeLast::initialize_or_wait,
+ * src/utils/initialize_last.rs:26-43); the others block until it is done. After it
+ * returns the table is read-only and may be probed concurrently. */
+hj_status hj_build_finish(hj_table* t, int partition);
+
+/* Canonical id of partition `partition`'s first row (valid after the barrier). */
+hj_status hj_build_partition_offset(const hj_table* t, int partition, int64_t* out);
+
+hj_status hj_table_stats_get(const hj_table* t, hj_table_stats* out);
+
+/* Device time of the build (HIP events around clear + insert + duplicate passes), ns;
+ * -1 if the table is not built. Cheap: no device work. */
+int64_t hj_table_build_ns(const hj_table* t);
+
+/* IndexLookup::get_iter (src/utils/index_lookup.rs:1-6,
+ * src/operator/version10/lookup_implementation_3.rs:46-59): build rows of `key` in
+ * chain order (newest first = descending). Writes up to `cap` rows, *count = total. */
+hj_status hj_table_lookup(const hj_table* t, int64_t key, uint64_t* rows, int64_t cap,
+                          int64_t* count);
+
+/* Chain links in canonical form: prev[i] = next older build row with the same key as
+ * row i, or -1 (the reference's overflow buffer at parallelism 1, minus 1;
+ * src/operator/version10/parallel_join_execution_state.rs:91-133). Host array of
+ * build_rows entries. */
+hj_status hj_table_chain_links(const hj_table* t, int64_t* prev, int64_t n);
+
+void hj_table_free(hj_table* t);
+
+/* ---- probe: replaces get_matching_indices + equal_rows_arr inside
+ *      lookup_inner_join_probe_batch (src/operator/probe_lookup_implementation/
+ *      inner.rs:79-129, src/shared/shared.rs:29-47,
+ *      src/shared/datafusion_private.rs:40-80). -------------------------------- */
+
+/* Synchronous, reentrant probe of a finished table, run on `stream` (NULL = the null
+ * stream; device input must be ready in that stream's order). Pairs are library-owned. */
+hj_status hj_probe(const hj_table* t, const void* keys, const uint8_t* validity,
+                   int64_t validity_offset, int64_t n, uint32_t flags, void* stream,
+                   hj_pairs* out);
+
+void hj_pairs_free(hj_pairs* p);
+
+/* Asynchronous probe into caller buffers (device memory), on `stream`.
+ * Writes min(total, capacity) pairs and the total to *d_total (device int64).
+ * `workspace` (device, hj_probe_workspace_bytes(n) bytes) must not be shared by
+ * concurrent calls; its bytes 8..15 (uint64) are non-zero after the call if a bounded
+ * spin gave up (results invalid). No host synchronisation, no allocation. */
+int64_t hj_probe_workspace_bytes(int64_t n);
+hj_status hj_probe_async(const hj_table* t, const void* keys, const uint8_t* validity,
+                         int64_t validity_offset, int64_t n, uint64_t* out_build,
+                         uint32_t* out_probe, int64_t capacity, int64_t* d_total,
+                         void* workspace, void* stream);
+
+/* As hj_probe_async, but probe_idx of a match is probe_ids[row] instead of row
+ * (rows received through the multi-GPU exchange carry their global ids). */
+hj_status hj_probe_async_ids(const hj_table* t, const void* keys, const uint8_t* validity,
+                             int64_t validity_offset, const uint32_t* probe_ids, int64_t n,
+                             uint64_t* out_build, uint32_t* out_probe, int64_t capacity,
+                             int64_t* d_total, void* workspace, void* stream);
+
+/* Makes `stream` wait for the build of `t` (for probes on other streams). */
+hj_status hj_table_stream_wait(const hj_table* t, void* stream);
+
+/* ---- radix partitioning for the multi-GPU exchange (new; the reference's nearest
+ *      relative is the shard function of
+ *      src/utils/partitioned_concurrent_self_hash_join_map.rs:13-16). ------------ */
+
+/* Partition n rows into `nparts` (power of two) by hash bits:
+ * out_keys/out_ids are grouped by destination; counts[nparts] (device int64) receives
+ * the rows per destination. ids may be NULL (then id = id_base + i). Null rows are
+ * dropped. Device pointers, asynchronous on `stream`; `workspace` of
+ * hj_partition_workspace_bytes(n, nparts) bytes. */
+int64_t hj_partition_workspace_bytes(int64_t n, int nparts);
+hj_status hj_radix_partition(hj_key_type key_type, const void* keys,
+                             const uint8_t* validity, int64_t validity_offset,
+                             const uint64_t* ids, uint64_t id_base, int64_t n, int nparts,
+                             void* out_keys, uint64_t* out_ids, int64_t* counts,
+                             void* workspace, void* stream);
+
+/* ---- synthetic generators of SURVEY.md §8(d) on the device (bench inputs) ----- */
+/* out[i] = (i * mul) mod range  (unique build keys when gcd(mul, range) = 1);
+ * requires n * mul < 2^64 */
+hj_status hj_gen_perm_keys(int64_t* out, int64_t n, int64_t mul, int64_t range,
+                           void* stream);
+/* out[i] = splitmix64(seed + i) mod range */
+hj_status hj_gen_uniform_keys(int64_t* out, int64_t n, uint64_t seed, int64_t range,
+                              void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DFP_HJ_H */

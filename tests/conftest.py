@@ -1,0 +1,34 @@
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (runs the gfx950 kernels)")
+
+
+@pytest.fixture(scope="session")
+def oracle_mod():
+    import oracle
+
+    oracle.build()
+    return oracle
+
+
+@pytest.fixture(scope="session")
+def dfp():
+    # (re)build the in-tree library if a source is newer than it (no-op otherwise)
+    sys.path.insert(0, os.path.join(ROOT, "datafusion-parallelism_amd"))
+    import build as hipbuild
+
+    sys.path.pop(0)
+    hipbuild.build()
+    import datafusion_parallelism_amd as m
+
+    m.load()
+    return m

@@ -1,0 +1,100 @@
+"""CPU, world_size 2 (gloo): the multi-GPU exchange logic of
+datafusion_parallelism_amd.distributed — counts all-to-all, uneven-split row exchange,
+global build/probe ids — joined per rank by the oracle (test-local stand-ins for the
+HIP partition / local-join kernels, which need a GPU). Global pairs gathered from both
+ranks must equal the single-process oracle join after canonical ordering."""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _mix64(k: np.ndarray) -> np.ndarray:
+    with np.errstate(over="ignore"):
+        k = k.astype(np.uint64)
+        k ^= k >> np.uint64(33)
+        k *= np.uint64(0xFF51AFD7ED558CCD)
+        k ^= k >> np.uint64(33)
+        k *= np.uint64(0xC4CEB9FE1A85EC53)
+        k ^= k >> np.uint64(33)
+        return k
+
+
+def cpu_partition(keys, ids, id_base, nparts):
+    """Stable multi-split by the low hash bits (the semantics of hj_radix_partition)."""
+    k = keys.numpy()
+    i = np.arange(len(k), dtype=np.int64) + id_base if ids is None else ids.numpy()
+    dest = (_mix64(k) & np.uint64(nparts - 1)).astype(np.int64)
+    order = np.argsort(dest, kind="stable")
+    counts = np.bincount(dest, minlength=nparts)
+    return torch.from_numpy(k[order].copy()), torch.from_numpy(i[order].copy()), torch.from_numpy(counts)
+
+
+def oracle_local_join(bk, bi, pk, pi, cap=None):
+    import oracle
+
+    b, p = oracle.inner_join(bk.numpy(), pk.numpy())
+    return torch.from_numpy(bi.numpy()[b.astype(np.int64)]), torch.from_numpy(pi.numpy()[p.astype(np.int64)])
+
+
+def _worker(rank, world, port, bks, pks, q):
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from datafusion_parallelism_amd.distributed import DistributedHashJoin
+
+    dj = DistributedHashJoin(partition_fn=cpu_partition, local_join_fn=oracle_local_join)
+    bbase = sum(len(x) for x in bks[:rank])
+    pbase = sum(len(x) for x in pks[:rank])
+    b, p = dj.run(torch.from_numpy(bks[rank]), bbase, torch.from_numpy(pks[rank]), pbase)
+    # every rank's local output is already canonical for its key subset
+    pl = p.numpy().astype(np.int64)
+    bl = b.numpy().astype(np.int64)
+    same = pl[1:] == pl[:-1]
+    ok = bool(np.all(pl[1:] >= pl[:-1]) and np.all(bl[1:][same] < bl[:-1][same]))
+    sizes = [None] * world
+    dist.all_gather_object(sizes, (bl.tolist(), pl.tolist(), ok))
+    if rank == 0:
+        q.put(sizes)
+    dist.destroy_process_group()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+@pytest.mark.parametrize("world", [2])
+def test_distributed_exchange_matches_single_join(oracle_mod, world):
+    rng = np.random.default_rng(9)
+    bk = rng.integers(0, 3000, 9000).astype(np.int64)
+    pk = rng.integers(0, 5000, 14000).astype(np.int64)
+    bks = [bk[:4000], bk[4000:]]
+    pks = [pk[:9000], pk[9000:]]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, bks, pks, q)) for r in range(world)]
+    for pr in procs:
+        pr.start()
+    res = q.get(timeout=240)
+    for pr in procs:
+        pr.join(timeout=60)
+        assert pr.exitcode == 0
+    allb = np.concatenate([np.array(r[0], np.int64) for r in res]).astype(np.uint64)
+    allp = np.concatenate([np.array(r[1], np.int64) for r in res]).astype(np.uint32)
+    assert all(r[2] for r in res), "per-rank output not in canonical order"
+    cb, cp = oracle_mod.canonical_pairs(allb, allp)
+    ob, op = oracle_mod.inner_join(bk, pk)
+    assert np.array_equal(cb, ob) and np.array_equal(cp.astype(np.uint32), op)

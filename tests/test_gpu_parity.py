@@ -1,0 +1,250 @@
+"""GPU parity: the gfx950 build + probe through the C ABI against the oracle
+(reference semantics restated in oracle/hj_oracle.c) — bit-exact pairs in canonical
+order (probe ascending, build descending) — and against the reference's own KATs.
+
+Run on an MI355X: ``pytest -m gpu``.
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+I64_MIN = np.iinfo(np.int64).min
+
+
+def gpu_join(dfp, bkeys, pkeys, bvalid=None, pvalid=None, key_type="int64", device_input=True, parts=None):
+    """Build (optionally split into `parts` partitions) and probe on the GPU."""
+    bk = np.asarray(bkeys)
+    pk = np.asarray(pkeys)
+    nparts = 1 if parts is None else len(parts) - 1
+    with dfp.HashTable(nparts, key_type, 0) as t:
+        for p in range(nparts):
+            lo, hi = (0, len(bk)) if parts is None else (parts[p], parts[p + 1])
+            keys = torch.from_numpy(bk[lo:hi].copy()).cuda() if device_input else bk[lo:hi]
+            t.append(p, keys, None if bvalid is None else np.asarray(bvalid)[lo:hi])
+        t.finish_all()
+        keys = torch.from_numpy(pk.copy()).cuda() if device_input else pk
+        b, pp = t.probe(keys, pvalid)
+        return b, pp, t.stats()
+
+
+def assert_same(b, p, ob, op):
+    assert len(b) == len(ob), f"count {len(b)} != oracle {len(ob)}"
+    assert np.array_equal(np.asarray(p, np.uint32), op), "probe indices differ"
+    assert np.array_equal(np.asarray(b, np.uint64), ob), "build indices differ"
+
+
+# ---- reference KATs -----------------------------------------------------------
+
+def test_v10_build_lookup_kat(dfp):
+    """src/operator/version10/build_implementation.rs:98-178: batches [1,2,3],[2,4,5],
+    [1,6,7]; id -> rows (reversed chain order in the reference test)."""
+    with dfp.HashTable(1, "int32", 0) as t:
+        for batch in ([1, 2, 3], [2, 4, 5], [1, 6, 7]):
+            t.append(0, np.array(batch, dtype=np.int32))
+        t.finish(0)
+        expected = {1: [0, 6], 2: [1, 3], 3: [2], 4: [4], 5: [5], 6: [7], 7: [8]}
+        for k, rows in expected.items():
+            got = t.lookup(k)
+            assert list(reversed(got)) == rows, (k, got)
+        assert t.lookup(999) == []
+
+
+def test_fixed_table_insert_previous_kat(dfp):
+    """fixed_table.rs:1411-1419: insert returns the previous value:
+    (1,1)->None, (1,2)->1, (4023,4)->None, (1,5)->2, (4023,6)->4. Rows inserted in
+    that order; chain_links gives each row's previous row with the same key."""
+    keys = np.array([1, 1, 4023, 1, 4023], dtype=np.int64)
+    values = [1, 2, 4, 5, 6]
+    with dfp.HashTable(1, "int64", 0) as t:
+        t.build(keys)
+        prev = t.chain_links(len(keys))
+    got = [None if prev[i] < 0 else values[prev[i]] for i in range(len(keys))]
+    assert got == [None, 1, None, 2, 4]
+
+
+def test_zero_and_extreme_keys(dfp, oracle_mod):
+    """fixed_table.rs:1399-1409 (zero hash storable) + the sentinel-colliding key."""
+    bk = np.array([0, I64_MIN, np.iinfo(np.int64).max, -1, 0, I64_MIN], dtype=np.int64)
+    pk = np.array([I64_MIN, 0, 5, -1, np.iinfo(np.int64).max, I64_MIN], dtype=np.int64)
+    b, p, _ = gpu_join(dfp, bk, pk)
+    ob, op = oracle_mod.inner_join(bk, pk)
+    assert_same(b, p, ob, op)
+
+
+def test_inner_join_with_nulls_kat(dfp, oracle_mod):
+    """src/lib.rs:149-193: [1,2,NULL] join [NULL,2,3] -> only 2."""
+    b, p, _ = gpu_join(dfp, np.array([1, 2, 0], np.int32), np.array([0, 2, 3], np.int32),
+                       [True, True, False], [False, True, True], key_type="int32")
+    assert list(b) == [1] and list(p) == [1]
+
+
+def test_inner_join_without_matches_kat(dfp):
+    """src/lib.rs:210-246: no matching keys -> 0 rows."""
+    b, p, _ = gpu_join(dfp, np.array([1, 2, 0], np.int32), np.array([0, 4, 5], np.int32),
+                       [True, True, False], [False, True, True], key_type="int32")
+    assert len(b) == 0
+
+
+def test_chain_order_across_partitions_kat(dfp):
+    """src/utils/concurrent_self_hash_join_map.rs:321-373: rows of one key appended by
+    two partitions; the chain lists every row newest first. Canonical numbering puts
+    partition 0's rows first, so the chain is the descending list of all rows."""
+    with dfp.HashTable(2, "int64", 0) as t:
+        t.append(0, np.array([1, 7, 1, 1], np.int64))
+        t.append(1, np.array([1, 1, 3, 1], np.int64))
+        t.finish_all()
+        assert t.partition_offset(1) == 4
+        assert t.lookup(1) == [7, 5, 4, 3, 2, 0]
+
+
+# ---- randomized parity vs the oracle -------------------------------------------
+
+@pytest.mark.parametrize("nb,np_,krange,null_frac,key_type", [
+    (0, 100, 10, 0.0, "int64"),
+    (100, 0, 10, 0.0, "int64"),
+    (1, 1, 1, 0.0, "int64"),
+    (1000, 4095, 700, 0.0, "int64"),
+    (4096, 4096, 3000, 0.1, "int64"),
+    (5000, 4097, 10000, 0.2, "int32"),
+    (100003, 300007, 60000, 0.05, "int64"),
+    (50000, 123457, 20000, 0.0, "int32"),
+    (200000, 1000000, 400000, 0.01, "int64"),
+])
+def test_random_parity(dfp, oracle_mod, nb, np_, krange, null_frac, key_type):
+    rng = np.random.default_rng(nb * 31 + np_)
+    dt = np.int64 if key_type == "int64" else np.int32
+    bk = rng.integers(-krange // 2, krange, nb).astype(dt)
+    pk = rng.integers(-krange // 2, krange, np_).astype(dt)
+    bv = rng.random(nb) >= null_frac if null_frac else None
+    pv = rng.random(np_) >= null_frac if null_frac else None
+    b, p, _ = gpu_join(dfp, bk, pk, bv, pv, key_type=key_type)
+    ob, op = oracle_mod.inner_join(bk, pk, bv, pv)
+    assert_same(b, p, ob, op)
+
+
+def test_host_input_parity(dfp, oracle_mod):
+    rng = np.random.default_rng(5)
+    bk = rng.integers(0, 3000, 10000).astype(np.int64)
+    pk = rng.integers(0, 6000, 20000).astype(np.int64)
+    b, p, _ = gpu_join(dfp, bk, pk, device_input=False)
+    ob, op = oracle_mod.inner_join(bk, pk)
+    assert_same(b, p, ob, op)
+
+
+def test_multi_partition_canonical_numbering(dfp, oracle_mod):
+    rng = np.random.default_rng(11)
+    bk = rng.integers(0, 5000, 30000).astype(np.int64)
+    pk = rng.integers(0, 9000, 40000).astype(np.int64)
+    parts = [0, 7000, 7000, 19000, 30000]  # includes an empty partition
+    b, p, _ = gpu_join(dfp, bk, pk, parts=parts)
+    ob, op = oracle_mod.inner_join(bk, pk)
+    assert_same(b, p, ob, op)
+
+
+@pytest.mark.parametrize("dups", [17, 300, 5000, 70000])
+def test_heavy_duplicates(dfp, oracle_mod, dups):
+    """Segments > 16 rows (LDS sort) and > 4096 rows (ordered rescan)."""
+    rng = np.random.default_rng(dups)
+    hot = np.full(dups, 42, np.int64)
+    other = rng.integers(0, 1000, 20000).astype(np.int64)
+    bk = np.concatenate([other[:10000], hot, other[10000:]])
+    rng.shuffle(bk)
+    pk = np.array([42, 1, 42, 999, 5000, 42], np.int64)
+    b, p, st = gpu_join(dfp, bk, pk)
+    ob, op = oracle_mod.inner_join(bk, pk)
+    assert_same(b, p, ob, op)
+    assert st["max_key_rows"] >= dups
+
+
+def test_chain_links_match_reference_semantics(dfp):
+    """Each valid row's link is the next older valid row with the same key (the
+    reference's overflow chain at parallelism 1 with exact keys); nulls never chain."""
+    rng = np.random.default_rng(3)
+    bk = rng.integers(0, 2000, 20000).astype(np.int64)
+    bv = rng.random(len(bk)) > 0.1
+    with dfp.HashTable(1, "int64", 0) as t:
+        t.build(torch.from_numpy(bk).cuda(), bv)
+        prev = t.chain_links(len(bk))
+    last = {}
+    want = np.full(len(bk), -1, np.int64)
+    for i, (k, v) in enumerate(zip(bk.tolist(), bv.tolist())):
+        if v:
+            want[i] = last.get(k, -1)
+            last[k] = i
+    assert np.array_equal(prev, want)
+
+
+def test_exponential_keys_parity(dfp, oracle_mod):
+    """benches/exponential_distribution.rs key distribution (src/api_utils.rs:15-23)."""
+    bk = oracle_mod.make_exponential_int_array(0, 200000).astype(np.int64)
+    pk = oracle_mod.uniform_keys(500000, 0xC0FFEE, 200000)
+    b, p, st = gpu_join(dfp, bk, pk)
+    ob, op = oracle_mod.inner_join(bk, pk)
+    assert_same(b, p, ob, op)
+    assert st["dup_keys"] > 0
+
+
+def test_stats(dfp):
+    bk = np.array([5, 5, 5, 6, 7, 7], np.int64)
+    with dfp.HashTable(1, "int64", 0) as t:
+        t.build(bk, np.array([1, 1, 1, 1, 1, 0], bool))
+        s = t.stats()
+    assert s["build_rows"] == 6 and s["inserted_rows"] == 5
+    assert s["distinct_keys"] == 3 and s["dup_keys"] == 1 and s["dup_rows"] == 3 and s["max_key_rows"] == 3
+
+
+# ---- full-size properties (BASELINE configs) -------------------------------------
+
+def test_c2_full_size_properties(dfp, oracle_mod):
+    """C2 (10^7 unique build keys x 10^8 uniform probe keys over 2*10^7): every probe key
+    < 10^7 matches exactly once, at build row k * inv(7368787) mod 10^7; check count,
+    order and a sample of values against the closed form."""
+    B, P, R = 10**7, 10**8, 2 * 10**7
+    dev = torch.device("cuda", 0)
+    lib = dfp.load()
+    bk = torch.empty(B, dtype=torch.int64, device=dev)
+    pk = torch.empty(P, dtype=torch.int64, device=dev)
+    s = torch.cuda.current_stream().cuda_stream
+    assert lib.hj_gen_perm_keys(bk.data_ptr(), B, 7368787, B, s) == 0
+    assert lib.hj_gen_uniform_keys(pk.data_ptr(), P, 0xC0FFEE, R, s) == 0
+    with dfp.HashTable(1, "int64", 0) as t:
+        t.build(bk)
+        b, p = t.probe(pk, device_output=True)
+    expected = int((pk < B).sum().item())
+    assert b.numel() == expected
+    # probe indices strictly ascending (unique build keys -> at most one match per row)
+    assert bool((p[1:] > p[:-1]).all().item())
+    # every emitted pair has equal keys
+    assert bool((bk[b] == pk[p.long()]).all().item())
+    inv = pow(7368787, -1, B)
+    sample = torch.randint(0, b.numel(), (10000,), device=dev)
+    keys = pk[p[sample].long()].cpu().numpy().astype(object)
+    want = np.array([(int(k) * inv) % B for k in keys], dtype=np.int64)
+    assert np.array_equal(b[sample].cpu().numpy(), want)
+
+
+def test_c3_full_size_digest(dfp, oracle_mod):
+    """C3 (10^7 exponential build keys x 10^8 uniform probe keys): the pair count and
+    per-probe-row match counts against the closed form multiplicity of each key."""
+    B, P = 10**7, 10**8
+    bk_np = oracle_mod.make_exponential_int_array(0, B).astype(np.int64)
+    mult = np.bincount(bk_np, minlength=B)
+    dev = torch.device("cuda", 0)
+    lib = dfp.load()
+    pk = torch.empty(P, dtype=torch.int64, device=dev)
+    assert lib.hj_gen_uniform_keys(pk.data_ptr(), P, 0xC0FFEE, B, torch.cuda.current_stream().cuda_stream) == 0
+    with dfp.HashTable(1, "int64", 0) as t:
+        t.build(torch.from_numpy(bk_np).cuda())
+        st = t.stats()
+        b, p = t.probe(pk, device_output=True)
+    assert st["distinct_keys"] == 6602610 and st["max_key_rows"] == 6
+    expected = int(torch.from_numpy(mult).cuda()[pk].sum().item())
+    assert b.numel() == expected
+    assert bool((torch.from_numpy(bk_np).cuda()[b] == pk[p.long()]).all().item())
+    # canonical order: probe ascending, build strictly descending within a probe row
+    pl = p.long()
+    assert bool((pl[1:] >= pl[:-1]).all().item())
+    same = pl[1:] == pl[:-1]
+    assert bool((b[1:][same] < b[:-1][same]).all().item())
