@@ -72,6 +72,33 @@ hipStream_t thread_stream(int dev) {
     return s;
 }
 
+// Tables reuse build streams and events (creating them costs ~0.1 ms per table).
+struct BuildResources {
+    hipStream_t stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+};
+std::mutex g_pool_mu;
+std::unordered_map<int, std::vector<BuildResources>> g_pool;
+
+bool acquire_resources(int dev, BuildResources* r) {
+    {
+        std::lock_guard<std::mutex> g(g_pool_mu);
+        auto& v = g_pool[dev];
+        if (!v.empty()) {
+            *r = v.back();
+            v.pop_back();
+            return true;
+        }
+    }
+    return hipStreamCreateWithFlags(&r->stream, hipStreamNonBlocking) == hipSuccess &&
+           hipEventCreate(&r->ev0) == hipSuccess && hipEventCreate(&r->ev1) == hipSuccess;
+}
+
+void release_resources(int dev, const BuildResources& r) {
+    std::lock_guard<std::mutex> g(g_pool_mu);
+    g_pool[dev].push_back(r);
+}
+
 int device_count() {
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess) return 0;
@@ -102,7 +129,7 @@ struct HostSeg {
     int64_t voff = 0;
     const uint64_t* ids = nullptr;
     int64_t n = 0;
-    std::vector<void*> owned;  // device copies owned by the table
+    std::vector<void*> owned;    // device copies owned by the table
     hipEvent_t ready = nullptr;  // borrowed device input: produced when this fires
 };
 
@@ -129,29 +156,115 @@ struct hj_table {
 
     // device state
     Bucket* tbl = nullptr;
-    uint32_t nb = 0;
+    uint32_t nb = 0, clog2 = 10, nchunks = 0;
     uint32_t* dup_rows = nullptr;
     uint64_t* row_ids = nullptr;
-    uint2* duprows = nullptr;
-    uint32_t* dupslots = nullptr;
-    DupDir* dir = nullptr;
-    uint32_t* big = nullptr;
-    BuildCounters* ctr = nullptr;
-    Segment* d_segs = nullptr;
-    hipStream_t stream = nullptr;
-    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    BuildResources res;
     int64_t build_ns = 0;
-    std::vector<void*> allocs;
+    std::vector<void*> allocs;   // live for the table's lifetime
+    std::vector<void*> scratch;  // build-only, released when the build completes
 };
 
 namespace {
 
-hj_status dev_alloc(hj_table* t, void** p, size_t bytes) {
+hj_status dev_alloc(hj_table* t, std::vector<void*>& list, void** p, size_t bytes) {
     *p = nullptr;
     if (bytes == 0) bytes = 64;
-    hipError_t e = hipMallocAsync(p, bytes, t->stream);
+    hipError_t e = hipMallocAsync(p, (bytes + 255) & ~(size_t)255, t->res.stream);
     if (e != hipSuccess) return fail(HJ_ERR_OOM, std::string("hipMallocAsync: ") + hipGetErrorString(e));
-    t->allocs.push_back(*p);
+    list.push_back(*p);
+    return HJ_OK;
+}
+
+void free_list(hj_table* t, std::vector<void*>& list) {
+    for (void* p : list) (void)hipFreeAsync(p, t->res.stream);
+    list.clear();
+}
+
+hipDeviceProp_t* device_props(int dev) {
+    static std::mutex mu;
+    static std::unordered_map<int, hipDeviceProp_t> cache;
+    std::lock_guard<std::mutex> g(mu);
+    auto it = cache.find(dev);
+    if (it == cache.end()) {
+        hipDeviceProp_t p;
+        if (hipGetDeviceProperties(&p, dev) != hipSuccess) return nullptr;
+        it = cache.emplace(dev, p).first;
+    }
+    return &it->second;
+}
+
+// One device build attempt at load factor lf; sets *retry when a chunk overflowed.
+hj_status build_attempt(hj_table* t, const std::vector<Segment>& segs, double lf, bool* retry) {
+    *retry = false;
+    const int64_t total = t->total_rows;
+    // geometry: 5-slot buckets, chunks of 2^clog2 buckets (one workgroup builds one)
+    const double want = (double)total / (kSlots * lf);
+    uint32_t clog2 = 10;
+    uint64_t nchunks = (uint64_t)(want / (1u << clog2)) + 1;
+    if (nchunks > (uint64_t)kMaxChunks) {
+        clog2 = 11;
+        nchunks = (uint64_t)(want / (1u << clog2)) + 1;
+    }
+    if (nchunks > (uint64_t)kMaxChunks)
+        return fail(HJ_ERR_INVALID, "build side too large for one device table; shard it (hj_radix_partition)");
+    t->clog2 = clog2;
+    t->nchunks = (uint32_t)nchunks;
+    t->nb = (uint32_t)(nchunks << clog2);
+    const int64_t ntiles = build_tiles(total);
+    const int64_t hlen = (int64_t)(nchunks + 1) * ntiles;
+
+    hj_status st;
+    void* p;
+    if ((st = dev_alloc(t, t->allocs, &p, (size_t)(t->nb + 1) * sizeof(Bucket))) != HJ_OK) return st;
+    t->tbl = (Bucket*)p;
+    if ((st = dev_alloc(t, t->allocs, &p, sizeof(uint32_t) * (size_t)(2 * total + 2))) != HJ_OK) return st;
+    t->dup_rows = (uint32_t*)p;
+    if (t->has_ids) {
+        if ((st = dev_alloc(t, t->allocs, &p, sizeof(uint64_t) * (size_t)std::max<int64_t>(total, 1))) != HJ_OK)
+            return st;
+        t->row_ids = (uint64_t*)p;
+    }
+    Segment* d_segs;
+    uint32_t *hist, *srows;
+    unsigned long long* skeys;
+    BigSeg* big;
+    BuildCounters* ctr;
+    void* scan;
+    if ((st = dev_alloc(t, t->scratch, &p, sizeof(Segment) * std::max<size_t>(segs.size(), 1))) != HJ_OK) return st;
+    d_segs = (Segment*)p;
+    if ((st = dev_alloc(t, t->scratch, &p, sizeof(uint32_t) * (size_t)std::max<int64_t>(hlen, 1))) != HJ_OK) return st;
+    hist = (uint32_t*)p;
+    if ((st = dev_alloc(t, t->scratch, &p, (size_t)scan_scratch_bytes(hlen))) != HJ_OK) return st;
+    scan = p;
+    if ((st = dev_alloc(t, t->scratch, &p, 8 * (size_t)std::max<int64_t>(total, 1))) != HJ_OK) return st;
+    skeys = (unsigned long long*)p;
+    if ((st = dev_alloc(t, t->scratch, &p, 4 * (size_t)std::max<int64_t>(total, 1))) != HJ_OK) return st;
+    srows = (uint32_t*)p;
+    if ((st = dev_alloc(t, t->scratch, &p, sizeof(BigSeg) * (size_t)(total / (kSmallSeg + 1) + 2))) != HJ_OK)
+        return st;
+    big = (BigSeg*)p;
+    if ((st = dev_alloc(t, t->scratch, &p, sizeof(BuildCounters))) != HJ_OK) return st;
+    ctr = (BuildCounters*)p;
+
+    hipStream_t s = t->res.stream;
+    if (!segs.empty())
+        HIP_TRY(hipMemcpyAsync(d_segs, segs.data(), sizeof(Segment) * segs.size(), hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemsetAsync(ctr, 0, sizeof(BuildCounters), s));
+    if (total == 0) HIP_TRY(hipMemsetAsync(t->tbl, 0, (size_t)(t->nb + 1) * sizeof(Bucket), s));
+    hipDeviceProp_t* prop = device_props(t->device);
+    const int cus = prop ? prop->multiProcessorCount : 256;
+    HIP_TRY(launch_build(t->key_bytes, d_segs, (int)segs.size(), total, t->nb, t->clog2, t->nchunks, hist, ntiles,
+                         scan, skeys, srows, t->row_ids, t->tbl, t->dup_rows, big, ctr, cus, s));
+    BuildCounters hc;
+    HIP_TRY(hipMemcpyAsync(&hc, ctr, sizeof(hc), hipMemcpyDeviceToHost, s));
+    free_list(t, t->scratch);
+    HIP_TRY(hipStreamSynchronize(s));
+    if (hc.err) {
+        *retry = true;
+        free_list(t, t->allocs);
+        t->row_ids = nullptr;
+    }
     return HJ_OK;
 }
 
@@ -171,67 +284,31 @@ hj_status run_build(hj_table* t) {
         }
     }
     t->total_rows = row;
-    for (int p = 0; p < t->parallelism; ++p)
-        for (auto& hs : t->parts[p])
-            if (hs.ready) HIP_TRY(hipStreamWaitEvent(t->stream, hs.ready, 0));
-    if (row > 0xFFFFFFF0ll)
-        return fail(HJ_ERR_INVALID, "build side exceeds 2^32-16 rows on one device; shard it");
+    if (row > 0x7FFFFFF0ll) return fail(HJ_ERR_INVALID, "build side exceeds 2^31-16 rows on one device; shard it");
     if (t->has_ids && t->has_no_ids)
         return fail(HJ_ERR_INVALID, "explicit build ids must be given for every batch or none");
-
-    const int64_t total = row;
-    double nbf = (double)total / (kSlots * load_factor());
-    uint64_t nb = (uint64_t)nbf + 1;
-    if (nb > (1ull << 29)) return fail(HJ_ERR_INVALID, "table too large");
-    t->nb = (uint32_t)nb;
-
-    HIP_TRY(hipEventRecord(t->ev0, t->stream));
-    hj_status st;
-    void* p;
-    if ((st = dev_alloc(t, &p, (size_t)(nb + 1) * sizeof(Bucket))) != HJ_OK) return st;
-    t->tbl = (Bucket*)p;
-    const int64_t half = total / 2 + 1;
-    if ((st = dev_alloc(t, &p, sizeof(uint2) * (size_t)std::max<int64_t>(total, 1))) != HJ_OK) return st;
-    t->duprows = (uint2*)p;
-    if ((st = dev_alloc(t, &p, sizeof(uint32_t) * (size_t)half)) != HJ_OK) return st;
-    t->dupslots = (uint32_t*)p;
-    if ((st = dev_alloc(t, &p, sizeof(DupDir) * (size_t)half)) != HJ_OK) return st;
-    t->dir = (DupDir*)p;
-    if ((st = dev_alloc(t, &p, sizeof(uint32_t) * (size_t)std::max<int64_t>(total, 1))) != HJ_OK) return st;
-    t->dup_rows = (uint32_t*)p;
-    if ((st = dev_alloc(t, &p, sizeof(uint32_t) * (size_t)(total / (kSmallSeg + 1) + 1))) != HJ_OK) return st;
-    t->big = (uint32_t*)p;
-    if ((st = dev_alloc(t, &p, sizeof(BuildCounters))) != HJ_OK) return st;
-    t->ctr = (BuildCounters*)p;
-    if (t->has_ids) {
-        if ((st = dev_alloc(t, &p, sizeof(uint64_t) * (size_t)std::max<int64_t>(total, 1))) != HJ_OK) return st;
-        t->row_ids = (uint64_t*)p;
+    hipStream_t s = t->res.stream;
+    // wait for the producers of borrowed device input
+    for (int p = 0; p < t->parallelism; ++p)
+        for (auto& hs : t->parts[p])
+            if (hs.ready) HIP_TRY(hipStreamWaitEvent(s, hs.ready, 0));
+    HIP_TRY(hipEventRecord(t->res.ev0, s));
+    double lf = load_factor();
+    for (int attempt = 0;; ++attempt) {
+        bool retry = false;
+        hj_status st = build_attempt(t, segs, lf, &retry);
+        if (st != HJ_OK) return st;
+        if (!retry) break;
+        // a chunk overflowed (adversarial key distribution): halve the load and rebuild
+        if (attempt >= 4) return fail(HJ_ERR_INVALID, "build: a table chunk overflowed at every load factor");
+        lf *= 0.5;
+        HIP_TRY(hipEventRecord(t->res.ev0, s));
     }
-    if ((st = dev_alloc(t, &p, sizeof(Segment) * std::max<size_t>(segs.size(), 1))) != HJ_OK) return st;
-    t->d_segs = (Segment*)p;
-    if (!segs.empty())
-        HIP_TRY(hipMemcpyAsync(t->d_segs, segs.data(), sizeof(Segment) * segs.size(), hipMemcpyHostToDevice,
-                               t->stream));
-    HIP_TRY(hipMemsetAsync(t->tbl, 0, (size_t)(nb + 1) * sizeof(Bucket), t->stream));
-    HIP_TRY(hipMemsetAsync(t->ctr, 0, sizeof(BuildCounters), t->stream));
-
-    hipDeviceProp_t prop;
-    HIP_TRY(hipGetDeviceProperties(&prop, t->device));
-    const int grid = prop.multiProcessorCount * 8;
-    HIP_TRY(launch_insert(t->key_bytes, t->d_segs, (int)segs.size(), total, t->tbl, t->nb, t->row_ids,
-                          t->duprows, t->dupslots, t->ctr, grid, t->stream));
-    HIP_TRY(launch_dup_passes(t->tbl, t->nb, t->duprows, t->dupslots, t->dir, t->dup_rows, t->big, t->ctr,
-                              prop.multiProcessorCount * 4, t->stream));
-    HIP_TRY(launch_dup_big(t->tbl, t->nb, t->dir, t->dup_rows, t->big, t->ctr, t->d_segs, (int)segs.size(),
-                           total, t->key_bytes, prop.multiProcessorCount, t->stream));
-    HIP_TRY(hipEventRecord(t->ev1, t->stream));
-    BuildCounters hc;
-    HIP_TRY(hipMemcpyAsync(&hc, t->ctr, sizeof(hc), hipMemcpyDeviceToHost, t->stream));
-    HIP_TRY(hipStreamSynchronize(t->stream));
+    HIP_TRY(hipEventRecord(t->res.ev1, s));
+    HIP_TRY(hipEventSynchronize(t->res.ev1));
     float ms = 0;
-    HIP_TRY(hipEventElapsedTime(&ms, t->ev0, t->ev1));
+    HIP_TRY(hipEventElapsedTime(&ms, t->res.ev0, t->res.ev1));
     t->build_ns = (int64_t)(ms * 1e6);
-    if (hc.err) return fail(HJ_ERR_INVALID, "build: bucket probe exceeded table size");
     return HJ_OK;
 }
 
@@ -242,11 +319,12 @@ hj_status check_table(const hj_table* t) {
     return HJ_OK;
 }
 
+TableView view_of(const hj_table* t) { return TableView{t->tbl, t->dup_rows, t->row_ids, t->nb, t->clog2}; }
+
 // device copy of host input (keys + validity bitmap slice)
 struct TmpInput {
     void* keys = nullptr;
     uint8_t* valid = nullptr;
-    int64_t voff = 0;
     hipStream_t s = nullptr;
     ~TmpInput() {
         if (keys) (void)hipFreeAsync(keys, s);
@@ -254,9 +332,8 @@ struct TmpInput {
     }
 };
 
-hj_status stage_input(int key_bytes, const void* keys, const uint8_t* valid, int64_t voff, int64_t n,
-                      uint32_t flags, hipStream_t s, TmpInput& tmp, const void** dkeys,
-                      const uint8_t** dvalid, int64_t* dvoff) {
+hj_status stage_input(int key_bytes, const void* keys, const uint8_t* valid, int64_t voff, int64_t n, uint32_t flags,
+                      hipStream_t s, TmpInput& tmp, const void** dkeys, const uint8_t** dvalid, int64_t* dvoff) {
     if (flags & HJ_INPUT_DEVICE) {
         if (!is_device_ptr(keys) || !is_device_ptr(valid))
             return fail(HJ_ERR_INVALID, "HJ_INPUT_DEVICE given but a pointer is not device memory");
@@ -289,15 +366,9 @@ hj_status probe_impl(const hj_table* t, const void* keys, const uint8_t* valid, 
                      int64_t* d_total, void* ws, hipStream_t s) {
     if (n < 0 || n > 0xFFFFFFFFll) return fail(HJ_ERR_INVALID, "probe batch must have < 2^32 rows");
     if (cap < 0) return fail(HJ_ERR_INVALID, "negative capacity");
-    const int64_t nt = probe_tiles(n);
-    HIP_TRY(hipMemsetAsync(ws, 0, (size_t)hj_probe_workspace_bytes(n), s));
-    if (nt == 0) {
-        HIP_TRY(hipMemsetAsync(d_total, 0, sizeof(int64_t), s));
-        return HJ_OK;
-    }
-    unsigned char* w = (unsigned char*)ws;
-    HIP_TRY(launch_probe(t->key_bytes, t->tbl, t->nb, t->dup_rows, t->row_ids, keys, valid, voff, probe_ids, n,
-                         out_b, out_p, cap, d_total, (unsigned long long*)(w + 16), (unsigned int*)w, s));
+    HIP_TRY(hipMemsetAsync((char*)ws + 8, 0, 8, s));  // error word (reserved)
+    HIP_TRY(launch_probe(t->key_bytes, view_of(t), keys, valid, voff, probe_ids, n, out_b, out_p, cap, d_total, ws,
+                         s));
     return HJ_OK;
 }
 
@@ -307,12 +378,11 @@ extern "C" {
 
 const char* hj_last_error(void) { return g_err.c_str(); }
 
-const char* hj_version(void) { return "dfp-hj 0.1 (gfx950)"; }
+const char* hj_version(void) { return "dfp-hj 0.2 (gfx950)"; }
 
 int hj_device_count(void) { return device_count(); }
 
-hj_status hj_build_begin(int device, int parallelism, hj_key_type key_type, int64_t expected_rows,
-                         hj_table** out) {
+hj_status hj_build_begin(int device, int parallelism, hj_key_type key_type, int64_t expected_rows, hj_table** out) {
     (void)expected_rows;
     if (out == nullptr) return fail(HJ_ERR_INVALID, "null out");
     *out = nullptr;
@@ -329,17 +399,20 @@ hj_status hj_build_begin(int device, int parallelism, hj_key_type key_type, int6
     t->key_bytes = key_type == HJ_INT64 ? 8 : 4;
     t->parts.resize(parallelism);
     t->finished.assign(parallelism, 0);
-    if (hipStreamCreateWithFlags(&t->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreate(&t->ev0) != hipSuccess || hipEventCreate(&t->ev1) != hipSuccess) {
+    if (!acquire_resources(device, &t->res)) {
         delete t;
         return fail(HJ_ERR_HIP, "stream/event creation failed");
     }
     // keep freed blocks in the pool: repeated builds re-use device memory
-    hipMemPool_t pool;
-    if (hipDeviceGetDefaultMemPool(&pool, device) == hipSuccess) {
-        uint64_t thr = UINT64_MAX;
-        (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &thr);
-    }
+    static std::once_flag pool_once[64];
+    if (device < 64)
+        std::call_once(pool_once[device], [device] {
+            hipMemPool_t pool;
+            if (hipDeviceGetDefaultMemPool(&pool, device) == hipSuccess) {
+                uint64_t thr = UINT64_MAX;
+                (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &thr);
+            }
+        });
     *out = t;
     return HJ_OK;
 }
@@ -354,7 +427,10 @@ hj_status hj_build_append(hj_table* t, int partition, const void* keys, const ui
         std::lock_guard<std::mutex> g(t->mu);
         if (t->finished[partition])
             return fail(HJ_ERR_INVALID, "State already consumed for partition " + std::to_string(partition));
-        if (n > 0) { if (ids) t->has_ids = true; else t->has_no_ids = true; }
+        if (n > 0) {
+            if (ids) t->has_ids = true;
+            else t->has_no_ids = true;
+        }
     }
     HIP_TRY(hipSetDevice(t->device));
     HostSeg hs;
@@ -362,9 +438,10 @@ hj_status hj_build_append(hj_table* t, int partition, const void* keys, const ui
     if (n == 0) return HJ_OK;
     // the producer's stream: the build waits for its work (borrow) or copies in its order
     hipStream_t s = (hipStream_t)stream;
-    if ((flags & HJ_INPUT_DEVICE) && (flags & HJ_BORROW)) {
-        if (!is_device_ptr(keys) || !is_device_ptr(validity) || !is_device_ptr(ids))
-            return fail(HJ_ERR_INVALID, "HJ_INPUT_DEVICE given but a pointer is not device memory");
+    const bool dev_in = (flags & HJ_INPUT_DEVICE) != 0;
+    if (dev_in && (!is_device_ptr(keys) || !is_device_ptr(validity) || !is_device_ptr(ids)))
+        return fail(HJ_ERR_INVALID, "HJ_INPUT_DEVICE given but a pointer is not device memory");
+    if (dev_in && (flags & HJ_BORROW)) {
         HIP_TRY(hipEventCreateWithFlags(&hs.ready, hipEventDisableTiming));
         HIP_TRY(hipEventRecord(hs.ready, s));
         hs.keys = keys;
@@ -372,8 +449,6 @@ hj_status hj_build_append(hj_table* t, int partition, const void* keys, const ui
         hs.voff = validity_offset;
         hs.ids = ids;
     } else {
-        if ((flags & HJ_INPUT_DEVICE) && (!is_device_ptr(keys) || !is_device_ptr(validity) || !is_device_ptr(ids)))
-            return fail(HJ_ERR_INVALID, "HJ_INPUT_DEVICE given but a pointer is not device memory");
         void* dk = nullptr;
         HIP_TRY(hipMalloc(&dk, (size_t)n * t->key_bytes));
         hs.owned.push_back(dk);
@@ -449,7 +524,7 @@ hj_status hj_table_stats_get(const hj_table* t, hj_table_stats* out) {
     unsigned long long* d = nullptr;
     HIP_TRY(hipMallocAsync((void**)&d, 4 * sizeof(unsigned long long), s));
     HIP_TRY(hipMemsetAsync(d, 0, 4 * sizeof(unsigned long long), s));
-    HIP_TRY(launch_table_stats(t->tbl, t->nb, d, s));
+    HIP_TRY(launch_table_stats(view_of(t), d, s));
     unsigned long long h[4];
     HIP_TRY(hipMemcpyAsync(h, d, sizeof(h), hipMemcpyDeviceToHost, s));
     HIP_TRY(hipFreeAsync(d, s));
@@ -471,7 +546,7 @@ int64_t hj_table_build_ns(const hj_table* t) {
     return t->build_ns;
 }
 
-int64_t hj_probe_workspace_bytes(int64_t n) { return 16 + 8 * (probe_tiles(n > 0 ? n : 0) + 1); }
+int64_t hj_probe_workspace_bytes(int64_t n) { return probe_workspace(n); }
 
 hj_status hj_probe_async(const hj_table* t, const void* keys, const uint8_t* validity, int64_t validity_offset,
                          int64_t n, uint64_t* out_build, uint32_t* out_probe, int64_t capacity, int64_t* d_total,
@@ -485,10 +560,9 @@ hj_status hj_probe_async(const hj_table* t, const void* keys, const uint8_t* val
                       workspace, (hipStream_t)stream /* NULL = the null stream */);
 }
 
-hj_status hj_probe_async_ids(const hj_table* t, const void* keys, const uint8_t* validity,
-                             int64_t validity_offset, const uint32_t* probe_ids, int64_t n, uint64_t* out_build,
-                             uint32_t* out_probe, int64_t capacity, int64_t* d_total, void* workspace,
-                             void* stream) {
+hj_status hj_probe_async_ids(const hj_table* t, const void* keys, const uint8_t* validity, int64_t validity_offset,
+                             const uint32_t* probe_ids, int64_t n, uint64_t* out_build, uint32_t* out_probe,
+                             int64_t capacity, int64_t* d_total, void* workspace, void* stream) {
     hj_status st = check_table(t);
     if (st != HJ_OK) return st;
     if (d_total == nullptr || workspace == nullptr) return fail(HJ_ERR_INVALID, "null d_total/workspace");
@@ -525,11 +599,8 @@ hj_status hj_probe(const hj_table* t, const void* keys, const uint8_t* validity,
         HIP_TRY(hipMalloc((void**)&ob, (size_t)cap * 8));
         HIP_TRY(hipMalloc((void**)&op, (size_t)cap * 4));
         if ((st = probe_impl(t, dk, dv, dvo, nullptr, n, ob, op, cap, d_total, ws, s)) != HJ_OK) break;
-        unsigned long long err = 0;
         HIP_TRY(hipMemcpyAsync(&total, d_total, 8, hipMemcpyDeviceToHost, s));
-        HIP_TRY(hipMemcpyAsync(&err, (char*)ws + 8, 8, hipMemcpyDeviceToHost, s));
         HIP_TRY(hipStreamSynchronize(s));
-        if (err) { st = fail(HJ_ERR_HIP, "probe look-back timed out"); break; }
         if (total <= cap) break;
         (void)hipFree(ob);
         (void)hipFree(op);
@@ -606,13 +677,14 @@ hj_status hj_table_lookup(const hj_table* t, int64_t key, uint64_t* rows, int64_
 hj_status hj_table_chain_links(const hj_table* t, int64_t* prev, int64_t n) {
     hj_status st = check_table(t);
     if (st != HJ_OK) return st;
-    if (n != t->total_rows || (n > 0 && prev == nullptr)) return fail(HJ_ERR_INVALID, "prev must hold build_rows entries");
+    if (n != t->total_rows || (n > 0 && prev == nullptr))
+        return fail(HJ_ERR_INVALID, "prev must hold build_rows entries");
     if (n == 0) return HJ_OK;
     HIP_TRY(hipSetDevice(t->device));
     hipStream_t s = thread_stream(t->device);
     int64_t* d = nullptr;
     HIP_TRY(hipMallocAsync((void**)&d, (size_t)n * 8, s));
-    HIP_TRY(launch_chain_links(t->tbl, t->nb, t->dup_rows, d, n, s));
+    HIP_TRY(launch_chain_links(view_of(t), d, n, s));
     HIP_TRY(hipMemcpyAsync(prev, d, (size_t)n * 8, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipFreeAsync(d, s));
     HIP_TRY(hipStreamSynchronize(s));
@@ -622,34 +694,33 @@ hj_status hj_table_chain_links(const hj_table* t, int64_t* prev, int64_t n) {
 hj_status hj_table_stream_wait(const hj_table* t, void* stream) {
     hj_status st = check_table(t);
     if (st != HJ_OK) return st;
-    HIP_TRY(hipStreamWaitEvent((hipStream_t)stream, t->ev1, 0));
+    HIP_TRY(hipStreamWaitEvent((hipStream_t)stream, t->res.ev1, 0));
     return HJ_OK;
 }
 
 void hj_table_free(hj_table* t) {
     if (t == nullptr) return;
     (void)hipSetDevice(t->device);
-    for (void* p : t->allocs) (void)hipFreeAsync(p, t->stream);
-    (void)hipStreamSynchronize(t->stream);
+    // stream-ordered frees on the (pooled) build stream; no host synchronisation
+    free_list(t, t->allocs);
+    free_list(t, t->scratch);
     for (auto& part : t->parts)
-        for (auto& hs : part)
-        {
+        for (auto& hs : part) {
             for (void* p : hs.owned) (void)hipFree(p);
             if (hs.ready) (void)hipEventDestroy(hs.ready);
         }
-    if (t->ev0) (void)hipEventDestroy(t->ev0);
-    if (t->ev1) (void)hipEventDestroy(t->ev1);
-    if (t->stream) (void)hipStreamDestroy(t->stream);
+    release_resources(t->device, t->res);
     delete t;
 }
 
 int64_t hj_partition_workspace_bytes(int64_t n, int nparts) { return radix_partition_workspace(n, nparts); }
 
-hj_status hj_radix_partition(hj_key_type key_type, const void* keys, const uint8_t* validity,
-                             int64_t validity_offset, const uint64_t* ids, uint64_t id_base, int64_t n, int nparts,
-                             void* out_keys, uint64_t* out_ids, int64_t* counts, void* workspace, void* stream) {
+hj_status hj_radix_partition(hj_key_type key_type, const void* keys, const uint8_t* validity, int64_t validity_offset,
+                             const uint64_t* ids, uint64_t id_base, int64_t n, int nparts, void* out_keys,
+                             uint64_t* out_ids, int64_t* counts, void* workspace, void* stream) {
     if (device_count() == 0) return fail(HJ_ERR_NO_DEVICE, "no GPU visible");
-    if (nparts < 1 || nparts > 64 || (nparts & (nparts - 1))) return fail(HJ_ERR_INVALID, "nparts must be a power of two <= 64");
+    if (nparts < 1 || nparts > 64 || (nparts & (nparts - 1)))
+        return fail(HJ_ERR_INVALID, "nparts must be a power of two <= 64");
     if (n < 0) return fail(HJ_ERR_INVALID, "negative length");
     if (!is_device_ptr(keys) || !is_device_ptr(validity) || !is_device_ptr(ids) || !is_device_ptr(out_keys) ||
         !is_device_ptr(out_ids) || !is_device_ptr(counts) || !is_device_ptr(workspace))

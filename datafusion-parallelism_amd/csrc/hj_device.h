@@ -2,35 +2,39 @@
 // C-ABI host layer (hj_api.cpp).
 //
 // Slot table in HBM:
-//   Bucket[nbuckets + 1], 64-byte aligned, one 64-byte line per bucket:
-//     uint64 key[4]   stored key = key ^ 2^63, 0 = empty slot
-//     uint2  pay[4]   .x = rows with this key, .y = row (x == 1) or dup_rows start (x > 1)
-//   Bucket[nbuckets] is the side bucket: slot 0 holds the key INT64_MIN, whose stored
-//   form collides with "empty".
-//   dup_rows[]      u32 build rows of every key with > 1 row, one segment per key,
-//                   sorted descending (= the reference's newest-first chain order).
-//   row_ids[]       optional u64 explicit build ids (multi-GPU exchange).
+//   Bucket[nb + 1], one 64-byte line each, nb = nchunks << clog2:
+//     uint64 key[5]   stored key = key ^ 2^63, 0 = empty slot
+//     uint32 ref[5]   bit 31 clear: the key's only build row
+//                     bit 31 set:   offset of its duplicate segment in dup_rows
+//     uint32 meta     (side bucket only: rows of the key INT64_MIN)
+//   A key's probe sequence stays inside its chunk of 2^clog2 buckets (linear probing
+//   modulo the chunk), so one workgroup can build a whole chunk in LDS.
+//   Bucket[nb] is the side bucket for INT64_MIN, whose stored form collides with
+//   "empty": ref[0] + meta = row count.
+//   dup_rows[]: per duplicated key a segment [count, row_0 > row_1 > ... ] — rows sorted
+//   descending = the reference's newest-first chain order at parallelism 1.
+//   row_ids[]: optional u64 explicit build ids (multi-GPU exchange).
 //
 // The reference's v10 table (src/operator/version10/new_map_3/fixed_table.rs:114-140)
-// stores (hash|bit63, row+1) slots with a separate u8 tag array and an overflow chain
-// array; this layout instead keeps the exact key in the slot (so the probe needs no
-// second gather for equal_rows_arr, src/shared/datafusion_private.rs:40-80) and
-// replaces pointer-chasing chains with one contiguous sorted segment per key.
+// stores (hash|bit63, row+1) slots, a separate u8 tag array and an overflow chain array;
+// this layout keeps the exact key in the slot (the equality re-check of equal_rows_arr,
+// src/shared/datafusion_private.rs:40-80, needs no second gather) and replaces pointer
+// chasing with one contiguous sorted segment per duplicated key.
 #pragma once
 #include <stdint.h>
 
 namespace dfp {
 
 constexpr uint64_t kSign = 0x8000000000000000ull;
-constexpr int kSlots = 4;
-constexpr int kProbeThreads = 256;
-constexpr int kRowsPerThread = 4;
-constexpr int kProbeTile = kProbeThreads * kRowsPerThread;  // 1024 probe rows per tile
+constexpr int kSlots = 5;
+constexpr unsigned kDupFlag = 0x80000000u;
+constexpr unsigned kMiss = 0xFFFFFFFFu;
 constexpr int kSmallSeg = 16;  // dup segments up to this size are sorted by one thread
 
 struct alignas(64) Bucket {
     unsigned long long key[kSlots];
-    unsigned int pay[kSlots][2];
+    unsigned int ref[kSlots];
+    unsigned int meta;
 };
 static_assert(sizeof(Bucket) == 64, "bucket must be one 64-byte line");
 
@@ -46,18 +50,17 @@ struct Segment {
 
 // Device-side build counters (zeroed before every build).
 struct BuildCounters {
-    unsigned long long n_dupslots;   // keys with > 1 row
-    unsigned long long n_duprows;    // 2nd..nth rows of such keys
+    unsigned long long n_valid;      // non-null rows (scan total)
     unsigned long long dup_used;     // dup_rows entries allocated
     unsigned long long n_big;        // segments > kSmallSeg
-    unsigned long long inserted;     // non-null rows inserted
-    unsigned long long distinct;     // occupied slots
-    unsigned long long max_key_rows; // longest segment
-    unsigned long long err;          // != 0: bounded spin gave up / overflow
+    unsigned long long err;          // bit 0: chunk full; bit 1: chunk dup-directory full
 };
 
-struct DupDir {
-    unsigned int start, n, fill, slot;
+// a duplicate segment too large for one thread to sort
+struct BigSeg {
+    unsigned long long key;
+    unsigned int off;
+    unsigned int pad;
 };
 
 __host__ __device__ inline uint64_t mix64(uint64_t k) {
@@ -71,11 +74,20 @@ __host__ __device__ inline uint64_t mix64(uint64_t k) {
     return k;
 }
 
-// bucket index from the high 32 hash bits (multiply-shift range reduction);
-// radix partitioning for the multi-GPU exchange uses the LOW bits, so a shard's keys
-// still spread over its whole table.
+// home bucket from the high 32 hash bits (multiply-shift range reduction); radix
+// partitioning for the multi-GPU exchange uses the LOW bits, so a shard's keys still
+// spread over its whole table.
 __host__ __device__ inline uint32_t bucket_of(uint64_t h, uint32_t nbuckets) {
     return (uint32_t)(((h >> 32) * (uint64_t)nbuckets) >> 32);
 }
+
+// Table geometry handed to the kernels.
+struct TableView {
+    const struct Bucket* tbl;
+    const uint32_t* dup_rows;
+    const uint64_t* row_ids;
+    uint32_t nb;      // buckets (excl. side bucket) = nchunks << clog2
+    uint32_t clog2;   // log2 buckets per chunk
+};
 
 }  // namespace dfp

@@ -1,28 +1,33 @@
 // hj_kernels.hip — hand-written gfx950 (CDNA4) kernels of the parallel hash join.
 //
 // Hot path:
-//   insert_kernel   build: concurrent open-addressing insert with 64-bit atomicCAS on
-//                   the key word and a 32-bit atomicAdd row count per slot. Replaces
-//                   Inner::insert_atomically (src/operator/version10/new_map_3/
-//                   fixed_table.rs:560-672) driven by JoinStateInstance::add
-//                   (src/operator/version10/parallel_join_execution_state.rs:91-133).
-//   dup_* kernels   build: turn the rows of duplicated keys into one contiguous segment
-//                   per key, sorted descending (the reference's chain order newest ->
-//                   oldest at parallelism 1, src/utils/concurrent_self_hash_join_map.rs:
-//                   83-124,223-249), replacing the overflow chain array.
-//   probe_kernel    probe: hash lookup + exact key compare + ordered pair emission in one
-//                   pass (single-pass decoupled look-back over 4096-row tiles). Replaces
-//                   get_matching_indices (src/shared/shared.rs:29-47), the chain walk
-//                   (src/operator/version10/lookup_implementation_3.rs:22-59) and
-//                   equal_rows_arr (src/shared/datafusion_private.rs:40-80).
+//   build   (replaces Inner::insert_atomically, src/operator/version10/new_map_3/
+//            fixed_table.rs:560-672, driven by JoinStateInstance::add,
+//            src/operator/version10/parallel_join_execution_state.rs:91-133, and the
+//            overflow-chain compaction of the same file, 135-315)
+//     build_hist_kernel     rows per (table chunk, row tile), LDS histogram
+//     scan_*_kernel         exclusive scan of the histogram (reduce-then-scan)
+//     build_scatter_kernel  partition (key, row) by chunk (stable per tile offsets)
+//     chunk_build_kernel    one workgroup per 2^clog2-bucket chunk: insert with LDS
+//                           64-bit CAS + LDS counts, lay out duplicate segments, write
+//                           the finished chunk out with coalesced 16-byte stores
+//     dup_sort_big_kernel   order large duplicate segments (LDS bitonic / ordered rescan)
+//   probe   (replaces get_matching_indices, src/shared/shared.rs:29-47, the chain walk,
+//            src/operator/version10/lookup_implementation_3.rs:22-59, and
+//            equal_rows_arr, src/shared/datafusion_private.rs:40-80)
+//     probe_lookup_kernel   per probe row: hash, one 64-byte bucket line (exact key
+//                           compare, so no separate equality gather), 4-byte match ref,
+//                           per-tile match count
+//     probe_scan_kernel     tile counts -> output offsets, total
+//     probe_emit_kernel     ordered (probe asc, build desc) pair emission per tile
 //
-// Design rules followed (cdna_hip_programming.md): wave64 ballots/shuffles, 16-byte
-// vector loads for streamed keys, no same-address atomics in the hot loops (the
-// single-word atomic rate is ~88/us, MI355X_MICROARCH.md "dequeue"), inter-workgroup
-// hand-off only through 8-byte agent-scope {flag,value} granules (Guideline 16, R2),
-// bounded spins.
+// No same-address global atomics on the hot loops (a single word sustains ~88
+// atomics/us, MI355X_MICROARCH.md "dequeue"), no inter-workgroup hand-offs inside a
+// launch: kernels communicate only through kernel boundaries.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
+
 #include "hj_device.h"
 #include "hj_launch.h"
 
@@ -42,201 +47,189 @@ __device__ __forceinline__ int64_t ld_key(const void* keys, int64_t i) {
     return (int64_t)(reinterpret_cast<const K*>(keys)[i]);
 }
 
-__device__ __forceinline__ unsigned long long wave_incl_scan(unsigned long long v) {
+__device__ __forceinline__ int64_t seg_key(const Segment& sg, int64_t i, int key_bytes) {
+    return key_bytes == 8 ? ld_key<int64_t>(sg.keys, i) : ld_key<int32_t>(sg.keys, i);
+}
+
+__device__ __forceinline__ int find_seg(const Segment* segs, int nseg, int64_t r) {
+    int lo = 0, hi = nseg - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (segs[mid].row_base <= r) lo = mid; else hi = mid - 1;
+    }
+    return lo;
+}
+
+template <typename T>
+__device__ __forceinline__ T wave_incl_scan(T v) {
     const int lane = threadIdx.x & 63;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
-        unsigned long long t = __shfl_up(v, (unsigned)d, 64);
+        T t = __shfl_up(v, (unsigned)d, 64);
         if (lane >= d) v += t;
     }
     return v;
 }
 
-__device__ __forceinline__ unsigned long long wave_sum(unsigned long long v) {
+template <typename T>
+__device__ __forceinline__ T wave_sum(T v) {
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
     return v;
 }
 
-__device__ __forceinline__ unsigned long long ld_agent(const unsigned long long* p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+// chunk of a key: the probe sequence of a key never leaves it
+__device__ __forceinline__ uint32_t home_bucket(int64_t key, uint32_t nb) {
+    return bucket_of(mix64((uint64_t)key), nb);
 }
-__device__ __forceinline__ void st_agent(unsigned long long* p, unsigned long long v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+
+// exclusive block scan of one value per thread (blockDim.x <= 1024), returns the
+// exclusive prefix, *total = block total. Uses s_w[blockDim.x / 64].
+template <typename T>
+__device__ __forceinline__ T block_excl_scan(T v, T* s_w, T* total) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    const T incl = wave_incl_scan(v);
+    if (lane == 63) s_w[wave] = incl;
+    __syncthreads();
+    T off = 0, tot = 0;
+    for (int w = 0; w < nw; ++w) {
+        const T x = s_w[w];
+        if (w < wave) off += x;
+        tot += x;
+    }
+    __syncthreads();
+    *total = tot;
+    return off + incl - v;
 }
 
 // ---------------------------------------------------------------------------
-// build: insert
+// build 1: histogram of rows per (chunk, tile); chunk nchunks = side key INT64_MIN
 // ---------------------------------------------------------------------------
-constexpr int kInsThreads = 256;
-constexpr int kDupBuf = 2048;  // LDS staging of dup entries per block (16 KB + 8 KB)
+constexpr int kHistThreads = 512;
 
 template <typename K>
-__global__ void __launch_bounds__(kInsThreads)
-insert_kernel(const Segment* __restrict__ segs, int nseg, int64_t total, Bucket* tbl,
-              uint32_t nb, uint64_t* __restrict__ row_ids, uint2* __restrict__ duprows,
-              uint32_t* __restrict__ dupslots, BuildCounters* ctr) {
-    __shared__ uint2 s_rows[kDupBuf];
-    __shared__ uint32_t s_slots[kDupBuf];
-    __shared__ unsigned s_nrows, s_nslots;
-    __shared__ unsigned long long s_base_r, s_base_s;
-    if (threadIdx.x == 0) { s_nrows = 0; s_nslots = 0; }
+__global__ void __launch_bounds__(kHistThreads)
+build_hist_kernel(const Segment* __restrict__ segs, int nseg, int64_t total, uint32_t nb, uint32_t clog2,
+                  uint32_t nchunks, uint32_t* __restrict__ hist, int64_t ntiles) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t s_h[];
+    const uint32_t nbins = nchunks + 1;
+    for (uint32_t c = threadIdx.x; c < nbins; c += kHistThreads) s_h[c] = 0;
     __syncthreads();
-
-    auto flush = [&]() {
-        // one global reservation per block and flush, never per row
-        if (threadIdx.x == 0) {
-            if (s_nrows) s_base_r = atomicAdd(&ctr->n_duprows, (unsigned long long)s_nrows);
-            if (s_nslots) s_base_s = atomicAdd(&ctr->n_dupslots, (unsigned long long)s_nslots);
-        }
-        __syncthreads();
-        for (unsigned k = threadIdx.x; k < s_nrows; k += kInsThreads) duprows[s_base_r + k] = s_rows[k];
-        for (unsigned k = threadIdx.x; k < s_nslots; k += kInsThreads) dupslots[s_base_s + k] = s_slots[k];
-        __syncthreads();
-        if (threadIdx.x == 0) { s_nrows = 0; s_nslots = 0; }
-        __syncthreads();
-    };
-
-    const int64_t stride = (int64_t)gridDim.x * kInsThreads;
-    for (int64_t base = (int64_t)blockIdx.x * kInsThreads; base < total; base += stride) {
-        const int64_t r = base + threadIdx.x;
-        if (r < total) {
-            int lo = 0, hi = nseg - 1;
-            while (lo < hi) {
-                const int mid = (lo + hi + 1) >> 1;
-                if (segs[mid].row_base <= r) lo = mid; else hi = mid - 1;
-            }
-            const Segment sg = segs[lo];
-            const int64_t i = r - sg.row_base;
-            if (sg.ids != nullptr) row_ids[r] = sg.ids[i];
-            if (bit_valid(sg.valid, sg.voff, i)) {
-                const int64_t key = ld_key<K>(sg.keys, i);
-                const unsigned long long skey = (unsigned long long)key ^ kSign;
-                Bucket* B;
-                int j = 0;
-                bool ok = true;
-                if (skey == 0) {
-                    B = tbl + nb;  // side bucket for INT64_MIN
-                } else {
-                    uint32_t b = bucket_of(mix64((uint64_t)key), nb);
-                    for (uint32_t probes = 0;; ++probes) {
-                        B = tbl + b;
-                        const ulonglong2* kp = reinterpret_cast<const ulonglong2*>(B->key);
-                        const ulonglong2 k01 = kp[0], k23 = kp[1];
-                        unsigned long long k[4] = {k01.x, k01.y, k23.x, k23.y};
-                        bool done = false;
-#pragma unroll
-                        for (int jj = 0; jj < kSlots; ++jj) {
-                            if (done) continue;
-                            unsigned long long kk = k[jj];
-                            if (kk == 0) kk = atomicCAS(&B->key[jj], 0ull, skey);  // claim
-                            if (kk == 0 || kk == skey) { done = true; j = jj; }
-                        }
-                        if (done) break;
-                        b = (b + 1 == nb) ? 0 : b + 1;  // linear probing over buckets
-                        if (probes > nb) { ok = false; atomicOr(&ctr->err, 1ull); break; }
-                    }
-                }
-                if (ok) {
-                    const uint32_t slot = (uint32_t)((B - tbl) * kSlots + j);
-                    const unsigned c = atomicAdd(&B->pay[j][0], 1u);
-                    if (c == 0) {
-                        B->pay[j][1] = (uint32_t)r;
-                    } else {
-                        const unsigned e = atomicAdd(&s_nrows, 1u);
-                        s_rows[e] = make_uint2(slot, (uint32_t)r);
-                        if (c == 1) s_slots[atomicAdd(&s_nslots, 1u)] = slot;
-                    }
-                }
-            }
-        }
-        __syncthreads();
-        if (s_nrows > kDupBuf - kInsThreads || s_nslots > kDupBuf - kInsThreads) flush();
+    const int64_t r0 = (int64_t)blockIdx.x * kBuildTile;
+    const int64_t r1 = min<int64_t>(total, r0 + kBuildTile);
+    int si = find_seg(segs, nseg, r0);
+    for (int64_t r = r0 + threadIdx.x; r < r1; r += kHistThreads) {
+        while (si + 1 < nseg && segs[si + 1].row_base <= r) ++si;
+        const Segment& sg = segs[si];
+        const int64_t i = r - sg.row_base;
+        if (!bit_valid(sg.valid, sg.voff, i)) continue;
+        const int64_t key = ld_key<K>(sg.keys, i);
+        const uint32_t c = ((uint64_t)key ^ kSign) == 0 ? nchunks : (home_bucket(key, nb) >> clog2);
+        atomicAdd(&s_h[c], 1u);
     }
     __syncthreads();
-    if (s_nrows || s_nslots) flush();
+    for (uint32_t c = threadIdx.x; c < nbins; c += kHistThreads) hist[(int64_t)c * ntiles + blockIdx.x] = s_h[c];
 }
 
 // ---------------------------------------------------------------------------
-// build: duplicate-key segments
+// exclusive scan of u32 (reduce-then-scan, three launches, no inter-block hand-off)
 // ---------------------------------------------------------------------------
-constexpr int kDupThreads = 256;
-constexpr int kDupPerThread = 16;
-constexpr int kDupChunk = kDupThreads * kDupPerThread;  // dupslots per block reservation
+constexpr int kScanThreads = 256;
+constexpr int kScanPerThread = 16;
+constexpr int kScanSeg = kScanThreads * kScanPerThread;
 
-__device__ __forceinline__ Bucket* slot_bucket(Bucket* tbl, uint32_t slot, int& j) {
-    j = (int)(slot & (kSlots - 1));
-    return tbl + (slot / kSlots);
+__global__ void __launch_bounds__(kScanThreads)
+scan_reduce_kernel(const uint32_t* __restrict__ a, int64_t len, unsigned long long* __restrict__ bsum) {
+    __shared__ unsigned long long s_w[kScanThreads / 64];
+    const int64_t base = (int64_t)blockIdx.x * kScanSeg + (int64_t)threadIdx.x * kScanPerThread;
+    unsigned long long s = 0;
+#pragma unroll
+    for (int k = 0; k < kScanPerThread; ++k)
+        if (base + k < len) s += a[base + k];
+    unsigned long long tot;
+    block_excl_scan<unsigned long long>(s, s_w, &tot);
+    if (threadIdx.x == 0) bsum[blockIdx.x] = tot;
 }
 
-// pass A: per duplicated key, reserve its dup_rows segment (one atomic per 4096 keys),
-// seed it with the first-arrived row, and park the dir index in the slot.
-__global__ void __launch_bounds__(kDupThreads)
-dup_alloc_kernel(Bucket* tbl, const uint32_t* __restrict__ dupslots, DupDir* dir,
-                 uint32_t* dup_rows, BuildCounters* ctr) {
-    __shared__ unsigned long long s_wave[kDupThreads / 64];
-    __shared__ unsigned long long s_base;
-    const unsigned long long nds = ctr->n_dupslots;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    for (unsigned long long c0 = (unsigned long long)blockIdx.x * kDupChunk; c0 < nds;
-         c0 += (unsigned long long)gridDim.x * kDupChunk) {
-        unsigned n[kDupPerThread];
-        unsigned long long mine = 0;
-#pragma unroll
-        for (int q = 0; q < kDupPerThread; ++q) {
-            const unsigned long long d = c0 + (unsigned long long)threadIdx.x * kDupPerThread + q;
-            n[q] = 0;
-            if (d < nds) {
-                int j;
-                Bucket* B = slot_bucket(tbl, dupslots[d], j);
-                n[q] = B->pay[j][0];
-            }
-            mine += n[q];
+// single block: exclusive scan of nblk block sums; bsum[nblk] = grand total
+__global__ void __launch_bounds__(1024)
+scan_top_kernel(unsigned long long* bsum, int64_t nblk, unsigned long long* total_out) {
+    __shared__ unsigned long long s_w[16];
+    const int64_t per = (nblk + 1023) / 1024;
+    const int64_t b0 = (int64_t)threadIdx.x * per;
+    unsigned long long s = 0;
+    for (int64_t k = 0; k < per; ++k)
+        if (b0 + k < nblk) s += bsum[b0 + k];
+    unsigned long long tot;
+    unsigned long long off = block_excl_scan<unsigned long long>(s, s_w, &tot);
+    for (int64_t k = 0; k < per; ++k) {
+        if (b0 + k < nblk) {
+            const unsigned long long x = bsum[b0 + k];
+            bsum[b0 + k] = off;
+            off += x;
         }
-        const unsigned long long incl = wave_incl_scan(mine);
-        if (lane == 63) s_wave[wave] = incl;
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            unsigned long long tot = 0;
-            for (int w = 0; w < kDupThreads / 64; ++w) tot += s_wave[w];
-            s_base = tot ? atomicAdd(&ctr->dup_used, tot) : 0;
-        }
-        __syncthreads();
-        unsigned long long off = s_base + incl - mine;
-        for (int w = 0; w < wave; ++w) off += s_wave[w];
-#pragma unroll
-        for (int q = 0; q < kDupPerThread; ++q) {
-            const unsigned long long d = c0 + (unsigned long long)threadIdx.x * kDupPerThread + q;
-            if (d < nds) {
-                const uint32_t slot = dupslots[d];
-                int j;
-                Bucket* B = slot_bucket(tbl, slot, j);
-                const uint32_t first = B->pay[j][1];
-                dir[d] = DupDir{(unsigned)off, n[q], 1u, slot};
-                dup_rows[off] = first;
-                B->pay[j][1] = (uint32_t)d;
-                off += n[q];
-            }
-        }
-        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        bsum[nblk] = tot;
+        if (total_out) *total_out = tot;
     }
 }
 
-// pass B: scatter the 2nd..nth rows of every duplicated key into its segment.
-__global__ void __launch_bounds__(kDupThreads)
-dup_scatter_kernel(const Bucket* tbl, const uint2* __restrict__ duprows, DupDir* dir,
-                   uint32_t* dup_rows, const BuildCounters* ctr) {
-    const unsigned long long ndr = ctr->n_duprows;
-    for (unsigned long long e = (unsigned long long)blockIdx.x * kDupThreads + threadIdx.x; e < ndr;
-         e += (unsigned long long)gridDim.x * kDupThreads) {
-        const uint2 sr = duprows[e];
-        const uint32_t d = tbl[sr.x / kSlots].pay[sr.x & (kSlots - 1)][1];
-        const unsigned pos = atomicAdd(&dir[d].fill, 1u);
-        dup_rows[dir[d].start + pos] = sr.y;
+__global__ void __launch_bounds__(kScanThreads)
+scan_down_kernel(uint32_t* __restrict__ a, int64_t len, const unsigned long long* __restrict__ bsum) {
+    __shared__ unsigned long long s_w[kScanThreads / 64];
+    const int64_t base = (int64_t)blockIdx.x * kScanSeg + (int64_t)threadIdx.x * kScanPerThread;
+    uint32_t v[kScanPerThread];
+    unsigned long long s = 0;
+#pragma unroll
+    for (int k = 0; k < kScanPerThread; ++k) {
+        v[k] = (base + k < len) ? a[base + k] : 0u;
+        s += v[k];
+    }
+    unsigned long long tot;
+    unsigned long long off = bsum[blockIdx.x] + block_excl_scan<unsigned long long>(s, s_w, &tot);
+#pragma unroll
+    for (int k = 0; k < kScanPerThread; ++k) {
+        if (base + k < len) a[base + k] = (uint32_t)off;
+        off += v[k];
     }
 }
 
-// in-register bitonic sort of 16 u32, descending (compile-time indices: no scratch)
+// ---------------------------------------------------------------------------
+// build 2: scatter (key, row) into chunk order (positions from the scanned histogram)
+// ---------------------------------------------------------------------------
+template <typename K>
+__global__ void __launch_bounds__(kHistThreads)
+build_scatter_kernel(const Segment* __restrict__ segs, int nseg, int64_t total, uint32_t nb, uint32_t clog2,
+                     uint32_t nchunks, const uint32_t* __restrict__ hist, int64_t ntiles,
+                     unsigned long long* __restrict__ skeys, uint32_t* __restrict__ srows,
+                     uint64_t* __restrict__ row_ids) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t s_cur[];
+    const uint32_t nbins = nchunks + 1;
+    for (uint32_t c = threadIdx.x; c < nbins; c += kHistThreads) s_cur[c] = hist[(int64_t)c * ntiles + blockIdx.x];
+    __syncthreads();
+    const int64_t r0 = (int64_t)blockIdx.x * kBuildTile;
+    const int64_t r1 = min<int64_t>(total, r0 + kBuildTile);
+    int si = find_seg(segs, nseg, r0);
+    for (int64_t r = r0 + threadIdx.x; r < r1; r += kHistThreads) {
+        while (si + 1 < nseg && segs[si + 1].row_base <= r) ++si;
+        const Segment& sg = segs[si];
+        const int64_t i = r - sg.row_base;
+        if (sg.ids != nullptr) row_ids[r] = sg.ids[i];
+        if (!bit_valid(sg.valid, sg.voff, i)) continue;
+        const int64_t key = ld_key<K>(sg.keys, i);
+        const uint32_t c = ((uint64_t)key ^ kSign) == 0 ? nchunks : (home_bucket(key, nb) >> clog2);
+        const uint32_t pos = atomicAdd(&s_cur[c], 1u);  // order inside a chunk is canonicalised later
+        skeys[pos] = (unsigned long long)key;
+        srows[pos] = (uint32_t)r;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// build 3: one workgroup per chunk builds the chunk's buckets in LDS
+// ---------------------------------------------------------------------------
+constexpr int kChunkThreads = 1024;
+
 __device__ __forceinline__ void sort16_desc(uint32_t (&v)[16]) {
 #pragma unroll
     for (int k = 2; k <= 16; k <<= 1) {
@@ -257,53 +250,194 @@ __device__ __forceinline__ void sort16_desc(uint32_t (&v)[16]) {
     }
 }
 
-// pass C: sort small segments (<= 16 rows) in registers, queue larger ones.
-__global__ void __launch_bounds__(kDupThreads)
-dup_sort_small_kernel(Bucket* tbl, const DupDir* __restrict__ dir, uint32_t* dup_rows,
-                      uint32_t* big, BuildCounters* ctr) {
-    const unsigned long long nds = ctr->n_dupslots;
-    for (unsigned long long d = (unsigned long long)blockIdx.x * kDupThreads + threadIdx.x; d < nds;
-         d += (unsigned long long)gridDim.x * kDupThreads) {
-        const DupDir e = dir[d];
-        if (e.n <= (unsigned)kSmallSeg) {
+// LDS slot of `key` inside the chunk image (insert = claim an empty slot with CAS)
+template <bool INSERT>
+__device__ __forceinline__ int chunk_slot(Bucket* img, uint32_t cmask, uint32_t i0, unsigned long long sk) {
+    uint32_t i = i0;
+    for (uint32_t probes = 0; probes <= cmask; ++probes) {
+        Bucket& B = img[i];
+#pragma unroll
+        for (int j = 0; j < kSlots; ++j) {
+            unsigned long long kk = B.key[j];
+            if (INSERT && kk == 0) kk = atomicCAS(&B.key[j], 0ull, sk);
+            if (kk == sk || (INSERT && kk == 0)) return (int)(i * kSlots + j);
+            if (!INSERT && kk == 0) return -1;
+        }
+        i = (i + 1) & cmask;
+    }
+    return -1;
+}
+
+__global__ void __launch_bounds__(kChunkThreads)
+chunk_build_kernel(uint32_t nb, uint32_t clog2, uint32_t nchunks, const uint32_t* __restrict__ hist,
+                   int64_t ntiles, const unsigned long long* __restrict__ skeys,
+                   const uint32_t* __restrict__ srows, Bucket* __restrict__ tbl, uint32_t* __restrict__ dup_rows,
+                   BigSeg* __restrict__ big, BuildCounters* ctr, uint32_t dupcap) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const uint32_t CB = 1u << clog2, cmask = CB - 1;
+    Bucket* img = reinterpret_cast<Bucket*>(smem);
+    uint32_t* d_off = reinterpret_cast<uint32_t*>(smem + (size_t)CB * sizeof(Bucket));
+    uint32_t* d_cur = d_off + dupcap;
+    uint32_t* d_cnt = d_cur + dupcap;
+    __shared__ unsigned s_ndup;
+    __shared__ unsigned long long s_w[kChunkThreads / 64];
+    __shared__ unsigned long long s_base;
+
+    const uint32_t c = blockIdx.x;
+    const bool side = (c == nchunks);
+    const uint32_t start = hist[(int64_t)c * ntiles];
+    const uint32_t end = side ? (uint32_t)ctr->n_valid : hist[(int64_t)(c + 1) * ntiles];
+    const uint32_t nimg = side ? 1u : CB;
+
+    // zero the chunk image
+    {
+        uint4* p = reinterpret_cast<uint4*>(img);
+        for (uint32_t k = threadIdx.x; k < nimg * 4; k += kChunkThreads) p[k] = make_uint4(0, 0, 0, 0);
+        if (threadIdx.x == 0) s_ndup = 0;
+    }
+    __syncthreads();
+
+    // pass A: claim slots (LDS CAS), count rows per slot in ref[] (LDS atomics)
+    for (uint32_t r = start + threadIdx.x; r < end; r += kChunkThreads) {
+        const unsigned long long sk = skeys[r] ^ kSign;
+        int slot;
+        if (side) {
+            slot = 0;
+        } else {
+            const uint32_t i0 = home_bucket((int64_t)(sk ^ kSign), nb) & cmask;
+            slot = chunk_slot<true>(img, cmask, i0, sk);
+            if (slot < 0) { atomicOr(&ctr->err, 1ull); continue; }  // chunk full
+        }
+        atomicAdd(&img[slot / kSlots].ref[slot % kSlots], 1u);
+    }
+    __syncthreads();
+
+    // pass B: directory of duplicated keys (count > 1)
+    for (uint32_t sl = threadIdx.x; sl < nimg * kSlots; sl += kChunkThreads) {
+        unsigned& ref = img[sl / kSlots].ref[sl % kSlots];
+        const unsigned cnt = ref;
+        if (cnt > 1) {
+            const unsigned li = atomicAdd(&s_ndup, 1u);
+            if (li < dupcap) {
+                d_cnt[li] = cnt;
+                d_cur[li] = 0;
+                ref = kDupFlag | li;
+            } else {
+                atomicOr(&ctr->err, 2ull);  // dup directory full: the host retries at half load
+            }
+        }
+    }
+    __syncthreads();
+    const unsigned ndup = min(s_ndup, dupcap);
+    // segment offsets: exclusive scan of (count + 1) over the directory, one global
+    // reservation per chunk
+    {
+        unsigned long long carry = 0;
+        for (unsigned b = 0; b < ndup; b += kChunkThreads) {
+            const unsigned li = b + threadIdx.x;
+            const unsigned long long v = li < ndup ? (unsigned long long)d_cnt[li] + 1 : 0;
+            unsigned long long tot;
+            const unsigned long long ex = block_excl_scan<unsigned long long>(v, s_w, &tot);
+            if (li < ndup) d_off[li] = (uint32_t)(carry + ex);
+            carry += tot;
+        }
+        if (threadIdx.x == 0) s_base = carry ? atomicAdd(&ctr->dup_used, carry) : 0;
+        __syncthreads();
+        for (unsigned li = threadIdx.x; li < ndup; li += kChunkThreads) {
+            d_off[li] += (uint32_t)s_base;
+            dup_rows[d_off[li]] = d_cnt[li];  // segment header = row count
+        }
+    }
+    __syncthreads();
+
+    // pass C: place rows: single-row keys keep their row in ref, duplicated keys append
+    // to their segment (unordered here, sorted in pass D)
+    for (uint32_t r = start + threadIdx.x; r < end; r += kChunkThreads) {
+        const unsigned long long sk = skeys[r] ^ kSign;
+        int slot = 0;
+        if (!side) {
+            const uint32_t i0 = home_bucket((int64_t)(sk ^ kSign), nb) & cmask;
+            slot = chunk_slot<false>(img, cmask, i0, sk);
+            if (slot < 0) continue;
+        }
+        unsigned& ref = img[slot / kSlots].ref[slot % kSlots];
+        const unsigned rv = ref;
+        const uint32_t row = srows[r];
+        if (rv & kDupFlag) {
+            const unsigned li = rv & ~kDupFlag;
+            const unsigned k = atomicAdd(&d_cur[li], 1u);
+            dup_rows[d_off[li] + 1 + k] = row;
+        } else if (rv == 1) {
+            ref = row;  // the key's only row (rv == count == 1)
+        }
+    }
+    __syncthreads();
+
+    // pass D: canonical order inside segments (descending rows), final refs
+    for (unsigned li = threadIdx.x; li < ndup; li += kChunkThreads) {
+        const unsigned n = d_cnt[li], off = d_off[li];
+        if (n <= (unsigned)kSmallSeg) {
             uint32_t v[16];
 #pragma unroll
-            for (int i = 0; i < 16; ++i) v[i] = (i < (int)e.n) ? dup_rows[e.start + i] : 0u;
+            for (int i = 0; i < 16; ++i) v[i] = (i < (int)n) ? dup_rows[off + 1 + i] : 0u;
             sort16_desc(v);
 #pragma unroll
             for (int i = 0; i < 16; ++i)
-                if (i < (int)e.n) dup_rows[e.start + i] = v[i];
-            int j;
-            Bucket* B = slot_bucket(tbl, e.slot, j);
-            B->pay[j][1] = e.start;
-        } else {
-            big[atomicAdd(&ctr->n_big, 1ull)] = (uint32_t)d;  // rare: keys with > 16 rows
+                if (i < (int)n) dup_rows[off + 1 + i] = v[i];
         }
+    }
+    for (uint32_t sl = threadIdx.x; sl < nimg * kSlots; sl += kChunkThreads) {
+        Bucket& B = img[sl / kSlots];
+        unsigned& ref = B.ref[sl % kSlots];
+        if (ref & kDupFlag) {
+            const unsigned li = ref & ~kDupFlag;
+            if (d_cnt[li] > (unsigned)kSmallSeg) {
+                const unsigned bi = (unsigned)atomicAdd(&ctr->n_big, 1ull);  // rare: > 16 rows
+                big[bi] = BigSeg{side ? kSign : (B.key[sl % kSlots] ^ kSign), d_off[li], 0u};
+            }
+            ref = kDupFlag | d_off[li];
+        }
+    }
+    __syncthreads();
+
+    // pass E: write the finished chunk (coalesced 16-byte stores)
+    if (side) {
+        if (threadIdx.x == 0) {
+            Bucket& S = tbl[nb];
+            for (int j = 0; j < kSlots; ++j) { S.key[j] = 0; S.ref[j] = 0; }
+            S.ref[0] = img[0].ref[0];
+            S.meta = end - start;
+        }
+    } else {
+        const uint4* src = reinterpret_cast<const uint4*>(img);
+        uint4* dst = reinterpret_cast<uint4*>(tbl + ((size_t)c << clog2));
+        for (uint32_t k = threadIdx.x; k < CB * 4; k += kChunkThreads) dst[k] = src[k];
     }
 }
 
+// ---------------------------------------------------------------------------
+// build 4: large duplicate segments (> 16 rows; rare). <= 4096 rows: bitonic sort in
+// LDS. Larger: rebuild the segment by an ordered scan of the build input (stream
+// compaction of the rows equal to the key; deterministic, no scratch).
+// ---------------------------------------------------------------------------
 constexpr int kBigThreads = 256;
 constexpr int kBigLds = 4096;
 
-// pass D: one workgroup per large segment. <= 4096 rows: bitonic sort in LDS.
-// Larger: rebuild the segment by an ordered scan of the whole build input (stream
-// compaction of rows equal to the key; deterministic, no scratch).
 __global__ void __launch_bounds__(kBigThreads)
-dup_sort_big_kernel(Bucket* tbl, uint32_t nb, const DupDir* __restrict__ dir,
-                    uint32_t* dup_rows, const uint32_t* __restrict__ big,
-                    const BuildCounters* ctr, const Segment* __restrict__ segs, int nseg,
-                    int64_t total, int key_bytes) {
+dup_sort_big_kernel(uint32_t* dup_rows, const BigSeg* __restrict__ big, const BuildCounters* ctr,
+                    const Segment* __restrict__ segs, int nseg, int64_t total, int key_bytes) {
     __shared__ uint32_t s_v[kBigLds];
     __shared__ unsigned s_wave[kBigThreads / 64];
     const unsigned long long nbig = ctr->n_big;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     for (unsigned long long bi = blockIdx.x; bi < nbig; bi += gridDim.x) {
-        const DupDir e = dir[big[bi]];
-        if (e.n <= (unsigned)kBigLds) {
+        const BigSeg e = big[bi];
+        const uint32_t n = dup_rows[e.off];
+        uint32_t* rows = dup_rows + e.off + 1;
+        if (n <= (unsigned)kBigLds) {
             unsigned N = 1;
-            while (N < e.n) N <<= 1;
-            for (unsigned i = threadIdx.x; i < N; i += kBigThreads)
-                s_v[i] = (i < e.n) ? dup_rows[e.start + i] : 0u;
+            while (N < n) N <<= 1;
+            for (unsigned i = threadIdx.x; i < N; i += kBigThreads) s_v[i] = (i < n) ? rows[i] : 0u;
             __syncthreads();
             for (unsigned k = 2; k <= N; k <<= 1) {
                 for (unsigned jj = k >> 1; jj > 0; jj >>= 1) {
@@ -318,30 +452,19 @@ dup_sort_big_kernel(Bucket* tbl, uint32_t nb, const DupDir* __restrict__ dir,
                     __syncthreads();
                 }
             }
-            for (unsigned i = threadIdx.x; i < e.n; i += kBigThreads) dup_rows[e.start + i] = s_v[i];
+            for (unsigned i = threadIdx.x; i < n; i += kBigThreads) rows[i] = s_v[i];
         } else {
-            int j;
-            Bucket* B = slot_bucket(tbl, e.slot, j);
-            const bool side = (B == tbl + nb);
-            const unsigned long long skey = side ? 0ull : B->key[j];
-            const int64_t key = (int64_t)(skey ^ kSign);
+            const int64_t key = (int64_t)e.key;
             unsigned long long done = 0;  // rows placed so far (ascending row order)
+            int si = 0;
             for (int64_t base = 0; base < total; base += kBigThreads) {
                 const int64_t r = base + threadIdx.x;
                 bool hit = false;
                 if (r < total) {
-                    int lo = 0, hi = nseg - 1;
-                    while (lo < hi) {
-                        const int mid = (lo + hi + 1) >> 1;
-                        if (segs[mid].row_base <= r) lo = mid; else hi = mid - 1;
-                    }
-                    const Segment sg = segs[lo];
+                    while (si + 1 < nseg && segs[si + 1].row_base <= r) ++si;
+                    const Segment& sg = segs[si];
                     const int64_t i = r - sg.row_base;
-                    if (bit_valid(sg.valid, sg.voff, i)) {
-                        const int64_t k = key_bytes == 8 ? ld_key<int64_t>(sg.keys, i)
-                                                         : ld_key<int32_t>(sg.keys, i);
-                        hit = (k == key);
-                    }
+                    if (bit_valid(sg.valid, sg.voff, i)) hit = (seg_key(sg, i, key_bytes) == key);
                 }
                 const unsigned long long m = __ballot(hit);
                 const unsigned below = __popcll(m & ((1ull << lane) - 1));
@@ -354,16 +477,11 @@ dup_sort_big_kernel(Bucket* tbl, uint32_t nb, const DupDir* __restrict__ dir,
                 }
                 if (hit) {
                     const unsigned long long rank = done + woff + below;  // ascending rank
-                    dup_rows[e.start + (e.n - 1 - rank)] = (uint32_t)r;  // descending layout
+                    rows[n - 1 - rank] = (uint32_t)r;                    // descending layout
                 }
                 done += tot;
                 __syncthreads();
             }
-        }
-        if (threadIdx.x == 0) {
-            int j;
-            Bucket* B = slot_bucket(tbl, e.slot, j);
-            B->pay[j][1] = e.start;
         }
         __syncthreads();
     }
@@ -372,18 +490,19 @@ dup_sort_big_kernel(Bucket* tbl, uint32_t nb, const DupDir* __restrict__ dir,
 // ---------------------------------------------------------------------------
 // probe
 // ---------------------------------------------------------------------------
-constexpr int kGroups = 4;                    // 4 groups x 1024 rows = 4096-row tile
-constexpr int kTile = kProbeTile * kGroups;
-constexpr unsigned long long kFlagA = 1ull << 62, kFlagP = 2ull << 62, kValMask = (1ull << 62) - 1;
+constexpr int kProbeThreads = 256;
+constexpr int kGroups = 4;                                 // 4 groups x 1024 rows
+constexpr int kProbeTile = kProbeThreads * 4 * kGroups;   // 4096 probe rows per tile
+
+typedef long long v2i64 __attribute__((ext_vector_type(2)));
 
 template <typename K>
-__device__ __forceinline__ void load4(const void* keys, int64_t row0, int64_t n, bool vec,
-                                      int64_t (&k)[4]) {
+__device__ __forceinline__ void load4(const void* keys, int64_t row0, int64_t n, bool vec, int64_t (&k)[4]) {
     const K* kp = reinterpret_cast<const K*>(keys);
     if (vec && row0 + 4 <= n) {
         if constexpr (sizeof(K) == 8) {
-            const longlong2* p = reinterpret_cast<const longlong2*>(kp + row0);
-            const longlong2 a = p[0], b = p[1];
+            const v2i64* p = reinterpret_cast<const v2i64*>(kp + row0);
+            const v2i64 a = p[0], b = p[1];
             k[0] = a.x; k[1] = a.y; k[2] = b.x; k[3] = b.y;
         } else {
             const int4 a = *reinterpret_cast<const int4*>(kp + row0);
@@ -395,168 +514,160 @@ __device__ __forceinline__ void load4(const void* keys, int64_t row0, int64_t n,
     }
 }
 
-template <typename K>
+// count of build rows behind a match ref
+__device__ __forceinline__ uint32_t ref_count(const uint32_t* dup_rows, uint32_t ref) {
+    if (ref == kMiss) return 0;
+    return (ref & kDupFlag) ? dup_rows[ref & ~kDupFlag] : 1u;
+}
+
+// One bucket line: ref of `sk` if present, else kMiss; *more = the line is full and does
+// not hold the key (look at the next bucket of the chunk). Slots fill in order and are
+// never freed, so an empty slot ends a key's probe sequence. Branch-free.
+__device__ __forceinline__ uint32_t scan_line(const uint4& a0, const uint4& a1, const uint4& a2, const uint4& a3,
+                                              unsigned long long sk, bool* more) {
+    const unsigned long long k0 = ((unsigned long long)a0.y << 32) | a0.x;
+    const unsigned long long k1 = ((unsigned long long)a0.w << 32) | a0.z;
+    const unsigned long long k2 = ((unsigned long long)a1.y << 32) | a1.x;
+    const unsigned long long k3 = ((unsigned long long)a1.w << 32) | a1.z;
+    const unsigned long long k4 = ((unsigned long long)a2.y << 32) | a2.x;
+    const bool e0 = k0 == sk, e1 = k1 == sk, e2 = k2 == sk, e3 = k3 == sk, e4 = k4 == sk;
+    const bool z = (k0 == 0) | (k1 == 0) | (k2 == 0) | (k3 == 0) | (k4 == 0);
+    uint32_t ref = e4 ? a3.z : kMiss;
+    ref = e3 ? a3.y : ref;
+    ref = e2 ? a3.x : ref;
+    ref = e1 ? a2.w : ref;
+    ref = e0 ? a2.z : ref;
+    *more = (ref == kMiss) & !z;
+    return ref;
+}
+
+template <typename K, bool HAS_VALID>
 __global__ void __launch_bounds__(kProbeThreads)
-probe_kernel(const Bucket* __restrict__ tbl, uint32_t nb, const uint32_t* __restrict__ dup_rows,
-             const uint64_t* __restrict__ row_ids, const void* __restrict__ keys,
-             const uint8_t* __restrict__ valid, int64_t voff,
-             const uint32_t* __restrict__ probe_ids, int64_t n, uint64_t* __restrict__ out_b,
-             uint32_t* __restrict__ out_p, int64_t cap, int64_t* d_total,
-             unsigned long long* status, unsigned int* ticket, int64_t ntiles, bool vec) {
-    __shared__ unsigned s_tile;
-    __shared__ unsigned long long s_wtot[kGroups][kProbeThreads / 64];
-    __shared__ unsigned long long s_excl;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-
-    // dynamic tile id in dispatch order: every predecessor tile is already running,
-    // so the look-back below cannot wait on a workgroup that is not resident.
-    if (threadIdx.x == 0) s_tile = atomicAdd(ticket, 1u);
-    __syncthreads();
-    const int64_t tile = s_tile;
-    const int64_t tile_row0 = tile * kTile;
-
-    uint32_t cnt[kGroups][4];
-    uint32_t rv[kGroups][4];
-    unsigned long long gsum[kGroups];
-
+probe_lookup_kernel(TableView tv, const void* __restrict__ keys, const uint8_t* __restrict__ valid, int64_t voff,
+                    int64_t n, bool vec, uint32_t* __restrict__ info, unsigned long long* __restrict__ tcnt) {
+    __shared__ unsigned long long s_w[kProbeThreads / 64];
+    const Bucket* __restrict__ tbl = tv.tbl;
+    const uint32_t cmask = (1u << tv.clog2) - 1;
+    unsigned long long tsum = 0;
+    const int64_t tile0 = (int64_t)blockIdx.x * kProbeTile;
 #pragma unroll
     for (int g = 0; g < kGroups; ++g) {
-        const int64_t row0 = tile_row0 + (int64_t)g * kProbeTile + (int64_t)threadIdx.x * 4;
+        const int64_t row0 = tile0 + (int64_t)g * (kProbeThreads * 4) + (int64_t)threadIdx.x * 4;
+        if (row0 >= n) break;
         int64_t k[4];
         load4<K>(keys, row0, n, vec, k);
         bool in[4];
-        uint32_t b[4];
         unsigned long long sk[4];
+        uint32_t b[4];
+        uint4 L0[4], L1[4], L2[4], L3[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-            in[q] = (row0 + q < n) && bit_valid(valid, voff, row0 + q);
+            in[q] = (row0 + q < n) && (!HAS_VALID || bit_valid(valid, voff, row0 + q));
             sk[q] = (unsigned long long)k[q] ^ kSign;
-            b[q] = bucket_of(mix64((uint64_t)k[q]), nb);
-            cnt[g][q] = 0;
-            rv[g][q] = 0;
+            b[q] = (in[q] && sk[q] != 0) ? home_bucket(k[q], tv.nb) : tv.nb;
         }
-        // issue the first bucket load of all four rows before any compare (MLP)
-        ulonglong2 k01[4], k23[4];
+        // issue the 64-byte bucket line of all four rows before any compare (MLP)
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-            const ulonglong2* kp = reinterpret_cast<const ulonglong2*>(tbl[b[q]].key);
-            if (in[q] && sk[q] != 0) { k01[q] = kp[0]; k23[q] = kp[1]; }
-            else { k01[q] = make_ulonglong2(0, 0); k23[q] = make_ulonglong2(0, 0); }
+            const uint4* p = reinterpret_cast<const uint4*>(tbl + b[q]);
+            L0[q] = p[0]; L1[q] = p[1]; L2[q] = p[2]; L3[q] = p[3];
         }
-        unsigned long long tsum = 0;
+        uint32_t ref[4];
+        bool more[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-            if (!in[q]) continue;
-            if (sk[q] == 0) {  // INT64_MIN lives in the side bucket
-                const uint2 p = *reinterpret_cast<const uint2*>(tbl[nb].pay[0]);
-                cnt[g][q] = p.x; rv[g][q] = p.y;
-            } else {
-                uint32_t bb = b[q];
-                unsigned long long kk[4] = {k01[q].x, k01[q].y, k23[q].x, k23[q].y};
-                for (uint32_t probes = 0; probes <= nb; ++probes) {
-                    int hitj = -1;
-                    bool empty = false;
-#pragma unroll
-                    for (int jj = 0; jj < kSlots; ++jj) {
-                        if (hitj < 0 && !empty) {
-                            if (kk[jj] == sk[q]) hitj = jj;
-                            else if (kk[jj] == 0) empty = true;
-                        }
-                    }
-                    if (hitj >= 0) {
-                        const uint2 p = *reinterpret_cast<const uint2*>(tbl[bb].pay[hitj]);
-                        cnt[g][q] = p.x; rv[g][q] = p.y;
-                        break;
-                    }
-                    if (empty) break;
-                    bb = (bb + 1 == nb) ? 0 : bb + 1;  // bucket overflow (rare)
-                    const ulonglong2* kp = reinterpret_cast<const ulonglong2*>(tbl[bb].key);
-                    const ulonglong2 a = kp[0], c = kp[1];
-                    kk[0] = a.x; kk[1] = a.y; kk[2] = c.x; kk[3] = c.y;
-                }
+            ref[q] = scan_line(L0[q], L1[q], L2[q], L3[q], sk[q], &more[q]);
+            if (sk[q] == 0) {  // INT64_MIN: the side bucket (ref[0] = word 10, meta = word 15)
+                ref[q] = L3[q].w ? L2[q].z : kMiss;
+                more[q] = false;
             }
-            tsum += cnt[g][q];
+            if (!in[q]) { ref[q] = kMiss; more[q] = false; }
         }
-        gsum[g] = tsum;
+        // rare: the home line is full and does not hold the key
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            uint32_t bb = b[q];
+            for (uint32_t probes = 0; more[q] && probes < cmask; ++probes) {
+                bb = (bb & ~cmask) | ((bb + 1) & cmask);
+                const uint4* p = reinterpret_cast<const uint4*>(tbl + bb);
+                ref[q] = scan_line(p[0], p[1], p[2], p[3], sk[q], &more[q]);
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) tsum += ref_count(tv.dup_rows, ref[q]);
+        if (vec && row0 + 4 <= n) {
+            *reinterpret_cast<uint4*>(info + row0) = make_uint4(ref[0], ref[1], ref[2], ref[3]);
+        } else {
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                if (row0 + q < n) info[row0 + q] = ref[q];
+        }
     }
+    unsigned long long tot;
+    block_excl_scan<unsigned long long>(tsum, s_w, &tot);
+    if (threadIdx.x == 0) tcnt[blockIdx.x] = tot;
+}
 
-    // block scan of the per-thread match counts, ordered (group, thread)
-    unsigned long long gincl[kGroups];
+template <typename K, bool HAS_ROW_IDS, bool HAS_PROBE_IDS>
+__global__ void __launch_bounds__(kProbeThreads)
+probe_emit_kernel(TableView tv, const uint32_t* __restrict__ info, const uint32_t* __restrict__ probe_ids,
+                  int64_t n, const unsigned long long* __restrict__ toff, uint64_t* __restrict__ out_b,
+                  uint32_t* __restrict__ out_p, int64_t cap) {
+    __shared__ unsigned long long s_w[kGroups][kProbeThreads / 64];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int64_t tile0 = (int64_t)blockIdx.x * kProbeTile;
+    uint32_t ref[kGroups][4];
+    uint32_t cnt[kGroups][4];
+    unsigned long long gsum[kGroups], gincl[kGroups];
 #pragma unroll
     for (int g = 0; g < kGroups; ++g) {
-        gincl[g] = wave_incl_scan(gsum[g]);
-        if (lane == 63) s_wtot[g][wave] = gincl[g];
-    }
-    __syncthreads();
-    unsigned long long agg = 0;
-#pragma unroll
-    for (int g = 0; g < kGroups; ++g)
-        for (int w = 0; w < kProbeThreads / 64; ++w) agg += s_wtot[g][w];
-
-    // decoupled look-back (one wave); status words are single 8-byte agent-scope
-    // granules {flag:2, value:62}
-    if (wave == 0) {
-        unsigned long long excl = 0;
-        if (tile == 0) {
-            if (lane == 0) st_agent(&status[0], kFlagP | agg);
+        const int64_t row0 = tile0 + (int64_t)g * (kProbeThreads * 4) + (int64_t)threadIdx.x * 4;
+        if (row0 + 4 <= n) {
+            const uint4 v = *reinterpret_cast<const uint4*>(info + row0);
+            ref[g][0] = v.x; ref[g][1] = v.y; ref[g][2] = v.z; ref[g][3] = v.w;
         } else {
-            if (lane == 0) st_agent(&status[tile], kFlagA | agg);
-            int64_t pred = tile - 1;
-            unsigned spins = 0;
-            while (true) {
-                const int64_t idx = pred - lane;
-                const unsigned long long v = idx >= 0 ? ld_agent(&status[idx]) : kFlagP;
-                const unsigned long long f = v >> 62;
-                const unsigned long long pm = __ballot(f == 2);
-                const unsigned long long xm = __ballot(f == 0);
-                const int firstP = pm ? (__ffsll((long long)pm) - 1) : 64;
-                const unsigned long long need = firstP >= 63 ? ~0ull : ((2ull << firstP) - 1);
-                if (xm & need) {
-                    if (++spins > (1u << 26)) {  // bounded: never hang the GPU
-                        if (lane == 0) st_agent(reinterpret_cast<unsigned long long*>(ticket) + 1, 1ull);
-                        break;
-                    }
-                    __builtin_amdgcn_s_sleep(1);
-                    continue;
-                }
-                excl += wave_sum(lane <= firstP ? (v & kValMask) : 0ull);
-                if (firstP < 64) break;
-                pred -= 64;
-            }
-            if (lane == 0) st_agent(&status[tile], kFlagP | (excl + agg));
+#pragma unroll
+            for (int q = 0; q < 4; ++q) ref[g][q] = (row0 + q < n) ? info[row0 + q] : kMiss;
         }
-        if (lane == 0) {
-            s_excl = excl;
-            if (tile == ntiles - 1) *d_total = (int64_t)(excl + agg);
+        unsigned long long s = 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            cnt[g][q] = ref_count(tv.dup_rows, ref[g][q]);
+            s += cnt[g][q];
         }
+        gsum[g] = s;
+        gincl[g] = wave_incl_scan<unsigned long long>(s);
+        if (lane == 63) s_w[g][wave] = gincl[g];
     }
     __syncthreads();
-
-    // ordered emission: probe ascending, build descending within a probe row
-    unsigned long long gbase = s_excl;
+    unsigned long long gbase = toff[blockIdx.x];
 #pragma unroll
     for (int g = 0; g < kGroups; ++g) {
         unsigned long long pos = gbase + gincl[g] - gsum[g];
-        for (int w = 0; w < wave; ++w) pos += s_wtot[g][w];
-        for (int w = 0; w < kProbeThreads / 64; ++w) gbase += s_wtot[g][w];
-        const int64_t row0 = (int64_t)g * kProbeTile + (int64_t)threadIdx.x * 4;
+        for (int w = 0; w < kProbeThreads / 64; ++w) {
+            if (w < wave) pos += s_w[g][w];
+            gbase += s_w[g][w];
+        }
+        const int64_t row0 = tile0 + (int64_t)g * (kProbeThreads * 4) + (int64_t)threadIdx.x * 4;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const uint32_t c = cnt[g][q];
             if (c == 0) continue;
-            const int64_t prow = tile_row0 + row0 + q;
-            const uint32_t pidx = probe_ids ? probe_ids[prow] : (uint32_t)prow;
+            const int64_t prow = row0 + q;
+            const uint32_t pidx = HAS_PROBE_IDS ? probe_ids[prow] : (uint32_t)prow;
+            const uint32_t r = ref[g][q];
             if (c == 1) {
                 if (pos < (unsigned long long)cap) {
-                    const uint32_t br = rv[g][q];
-                    out_b[pos] = row_ids ? row_ids[br] : (uint64_t)br;
+                    const uint32_t br = (r & kDupFlag) ? tv.dup_rows[(r & ~kDupFlag) + 1] : r;
+                    out_b[pos] = HAS_ROW_IDS ? tv.row_ids[br] : (uint64_t)br;
                     out_p[pos] = pidx;
                 }
             } else {
+                const uint32_t* seg = tv.dup_rows + (r & ~kDupFlag) + 1;
                 for (uint32_t t = 0; t < c; ++t) {
                     if (pos + t < (unsigned long long)cap) {
-                        const uint32_t br = dup_rows[rv[g][q] + t];
-                        out_b[pos + t] = row_ids ? row_ids[br] : (uint64_t)br;
+                        const uint32_t br = seg[t];
+                        out_b[pos + t] = HAS_ROW_IDS ? tv.row_ids[br] : (uint64_t)br;
                         out_p[pos + t] = pidx;
                     }
                 }
@@ -569,18 +680,34 @@ probe_kernel(const Bucket* __restrict__ tbl, uint32_t nb, const uint32_t* __rest
 // ---------------------------------------------------------------------------
 // table queries (not on the hot path)
 // ---------------------------------------------------------------------------
-__global__ void table_stats_kernel(const Bucket* tbl, uint32_t nb, unsigned long long* out) {
+__global__ void table_stats_kernel(TableView tv, unsigned long long* out) {
     unsigned long long distinct = 0, dupk = 0, dupr = 0, mx = 0;
-    for (uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s < (uint64_t)(nb + 1) * kSlots;
-         s += (uint64_t)gridDim.x * blockDim.x) {
-        const unsigned c = tbl[s / kSlots].pay[s % kSlots][0];
-        if (c) { distinct++; if (c > 1) { dupk++; dupr += c; } if (c > mx) mx = c; }
+    const uint64_t nslots = (uint64_t)tv.nb * kSlots;
+    for (uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s <= nslots; s += (uint64_t)gridDim.x * blockDim.x) {
+        uint32_t c = 0;
+        if (s == nslots) {  // side bucket
+            c = tv.tbl[tv.nb].meta;
+        } else if (tv.tbl[s / kSlots].key[s % kSlots] != 0) {
+            c = ref_count(tv.dup_rows, tv.tbl[s / kSlots].ref[s % kSlots]);
+        }
+        if (c) {
+            distinct++;
+            if (c > 1) { dupk++; dupr += c; }
+            if (c > mx) mx = c;
+        }
     }
-    distinct = wave_sum(distinct); dupk = wave_sum(dupk); dupr = wave_sum(dupr);
+    distinct = wave_sum(distinct);
+    dupk = wave_sum(dupk);
+    dupr = wave_sum(dupr);
 #pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) { unsigned long long o = __shfl_xor(mx, d, 64); mx = o > mx ? o : mx; }
+    for (int d = 32; d >= 1; d >>= 1) {
+        const unsigned long long o = __shfl_xor(mx, d, 64);
+        mx = o > mx ? o : mx;
+    }
     if ((threadIdx.x & 63) == 0) {
-        atomicAdd(&out[0], distinct); atomicAdd(&out[1], dupk); atomicAdd(&out[2], dupr);
+        atomicAdd(&out[0], distinct);
+        atomicAdd(&out[1], dupk);
+        atomicAdd(&out[2], dupr);
         atomicMax(&out[3], mx);
     }
 }
@@ -590,15 +717,21 @@ __global__ void chain_fill_kernel(int64_t* prev, int64_t n) {
         prev[i] = -1;
 }
 
-__global__ void chain_links_kernel(const Bucket* tbl, uint32_t nb, const uint32_t* dup_rows,
-                                   int64_t* prev) {
-    for (uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s < (uint64_t)(nb + 1) * kSlots;
-         s += (uint64_t)gridDim.x * blockDim.x) {
-        const unsigned c = tbl[s / kSlots].pay[s % kSlots][0];
-        if (c > 1) {
-            const unsigned st = tbl[s / kSlots].pay[s % kSlots][1];
-            for (unsigned t = 0; t + 1 < c; ++t) prev[dup_rows[st + t]] = dup_rows[st + t + 1];
+__global__ void chain_links_kernel(TableView tv, int64_t* prev) {
+    const uint64_t nslots = (uint64_t)tv.nb * kSlots;
+    for (uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s <= nslots; s += (uint64_t)gridDim.x * blockDim.x) {
+        uint32_t ref;
+        if (s == nslots) {
+            if (tv.tbl[tv.nb].meta < 2) continue;
+            ref = tv.tbl[tv.nb].ref[0];
+        } else {
+            if (tv.tbl[s / kSlots].key[s % kSlots] == 0) continue;
+            ref = tv.tbl[s / kSlots].ref[s % kSlots];
         }
+        if (!(ref & kDupFlag)) continue;
+        const uint32_t* seg = tv.dup_rows + (ref & ~kDupFlag);
+        const uint32_t c = seg[0];
+        for (uint32_t t = 0; t + 1 < c; ++t) prev[seg[1 + t]] = seg[2 + t];
     }
 }
 
@@ -610,16 +743,16 @@ constexpr int kPartChunk = 4096;  // rows per block
 constexpr int kMaxParts = 64;
 
 template <typename K>
-__device__ __forceinline__ int part_of(const void* keys, const uint8_t* valid, int64_t voff,
-                                       int64_t i, int64_t n, int mask) {
+__device__ __forceinline__ int part_of(const void* keys, const uint8_t* valid, int64_t voff, int64_t i, int64_t n,
+                                       int mask) {
     if (i >= n || !bit_valid(valid, voff, i)) return -1;
     return (int)(mix64((uint64_t)ld_key<K>(keys, i)) & (uint64_t)mask);
 }
 
 template <typename K>
 __global__ void __launch_bounds__(kPartThreads)
-part_hist_kernel(const void* keys, const uint8_t* valid, int64_t voff, int64_t n, int nparts,
-                 unsigned long long* hist, int64_t nblocks) {
+part_hist_kernel(const void* keys, const uint8_t* valid, int64_t voff, int64_t n, int nparts, uint32_t* hist,
+                 int64_t nblocks) {
     __shared__ unsigned s_h[kMaxParts];
     for (int p = threadIdx.x; p < nparts; p += kPartThreads) s_h[p] = 0;
     __syncthreads();
@@ -632,40 +765,20 @@ part_hist_kernel(const void* keys, const uint8_t* valid, int64_t voff, int64_t n
     for (int p = threadIdx.x; p < nparts; p += kPartThreads) hist[(int64_t)p * nblocks + blockIdx.x] = s_h[p];
 }
 
-// single-block exclusive scan over hist (partition-major), totals to counts[]
-__global__ void __launch_bounds__(1024)
-part_scan_kernel(unsigned long long* hist, int64_t len, int64_t nblocks, int nparts, int64_t* counts) {
-    __shared__ unsigned long long s_w[16];
-    __shared__ unsigned long long s_carry;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    if (threadIdx.x == 0) s_carry = 0;
-    __syncthreads();
-    for (int64_t base = 0; base < len; base += 1024) {
-        const int64_t i = base + threadIdx.x;
-        const unsigned long long v = i < len ? hist[i] : 0;
-        const unsigned long long incl = wave_incl_scan(v);
-        if (lane == 63) s_w[wave] = incl;
-        __syncthreads();
-        unsigned long long off = s_carry;
-        for (int w = 0; w < wave; ++w) off += s_w[w];
-        if (i < len) hist[i] = off + incl - v;
-        __syncthreads();
-        if (threadIdx.x == 0) for (int w = 0; w < 16; ++w) s_carry += s_w[w];
-        __syncthreads();
-    }
-    // counts[p] = start(p+1) - start(p)
-    for (int p = threadIdx.x; p < nparts; p += 1024) {
+__global__ void part_counts_kernel(const uint32_t* hist, int64_t nblocks, int nparts, const unsigned long long* total,
+                                   int64_t* counts) {
+    const int p = threadIdx.x;
+    if (p < nparts) {
         const unsigned long long st = hist[(int64_t)p * nblocks];
-        const unsigned long long en = (p + 1 < nparts) ? hist[(int64_t)(p + 1) * nblocks] : s_carry;
+        const unsigned long long en = (p + 1 < nparts) ? hist[(int64_t)(p + 1) * nblocks] : *total;
         counts[p] = (int64_t)(en - st);
     }
 }
 
 template <typename K>
 __global__ void __launch_bounds__(kPartThreads)
-part_scatter_kernel(const void* keys, const uint8_t* valid, int64_t voff, const uint64_t* ids,
-                    uint64_t id_base, int64_t n, int nparts, const unsigned long long* hist,
-                    int64_t nblocks, K* out_keys, uint64_t* out_ids) {
+part_scatter_kernel(const void* keys, const uint8_t* valid, int64_t voff, const uint64_t* ids, uint64_t id_base,
+                    int64_t n, int nparts, const uint32_t* hist, int64_t nblocks, K* out_keys, uint64_t* out_ids) {
     __shared__ unsigned long long s_off[kMaxParts];
     __shared__ unsigned s_wc[kPartThreads / 64][kMaxParts];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -727,97 +840,137 @@ __global__ void gen_uniform_kernel(int64_t* out, int64_t n, uint64_t seed, int64
 // ---------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------
-hipError_t launch_insert(int key_bytes, const Segment* d_segs, int nseg, int64_t total,
-                         Bucket* tbl, uint32_t nbuckets, uint64_t* row_ids, uint2* duprows,
-                         uint32_t* dupslots, BuildCounters* ctr, int grid, hipStream_t s) {
-    if (total <= 0) return hipSuccess;
-    int64_t need = (total + kInsThreads - 1) / kInsThreads;
-    const int g = (int)(need < grid ? need : grid);
-    if (key_bytes == 8)
-        insert_kernel<int64_t><<<g, kInsThreads, 0, s>>>(d_segs, nseg, total, tbl, nbuckets, row_ids,
-                                                         duprows, dupslots, ctr);
-    else
-        insert_kernel<int32_t><<<g, kInsThreads, 0, s>>>(d_segs, nseg, total, tbl, nbuckets, row_ids,
-                                                         duprows, dupslots, ctr);
+int64_t build_tiles(int64_t total) { return (total + kBuildTile - 1) / kBuildTile; }
+
+int64_t scan_scratch_bytes(int64_t len) { return 8 * ((len + kScanSeg - 1) / kScanSeg + 2); }
+
+static hipError_t launch_scan_u32(uint32_t* a, int64_t len, unsigned long long* bsum, unsigned long long* total,
+                                  hipStream_t s) {
+    const int64_t nblk = (len + kScanSeg - 1) / kScanSeg;
+    if (nblk == 0) return hipSuccess;
+    scan_reduce_kernel<<<(unsigned)nblk, kScanThreads, 0, s>>>(a, len, bsum);
+    scan_top_kernel<<<1, 1024, 0, s>>>(bsum, nblk, total);
+    scan_down_kernel<<<(unsigned)nblk, kScanThreads, 0, s>>>(a, len, bsum);
     return hipGetLastError();
 }
 
-hipError_t launch_dup_passes(Bucket* tbl, uint32_t nbuckets, const uint2* duprows,
-                             const uint32_t* dupslots, DupDir* dir, uint32_t* dup_rows,
-                             uint32_t* big, BuildCounters* ctr, int grid, hipStream_t s) {
-    // fixed grids that read their trip counts from device counters: no host sync
-    dup_alloc_kernel<<<grid, kDupThreads, 0, s>>>(tbl, dupslots, dir, dup_rows, ctr);
-    dup_scatter_kernel<<<grid, kDupThreads, 0, s>>>(tbl, duprows, dir, dup_rows, ctr);
-    dup_sort_small_kernel<<<grid, kDupThreads, 0, s>>>(tbl, dir, dup_rows, big, ctr);
+hipError_t launch_build(int key_bytes, const Segment* d_segs, int nseg, int64_t total, uint32_t nb, uint32_t clog2,
+                        uint32_t nchunks, uint32_t* hist, int64_t ntiles, void* scan_scratch,
+                        unsigned long long* skeys, uint32_t* srows, uint64_t* row_ids, Bucket* tbl,
+                        uint32_t* dup_rows, BigSeg* big, BuildCounters* ctr, int big_grid, hipStream_t s) {
+    const size_t hist_lds = sizeof(uint32_t) * (nchunks + 1);
+    const int64_t hlen = (int64_t)(nchunks + 1) * ntiles;
+    if (ntiles > 0) {
+        if (key_bytes == 8)
+            build_hist_kernel<int64_t><<<(unsigned)ntiles, kHistThreads, hist_lds, s>>>(d_segs, nseg, total, nb, clog2,
+                                                                                      nchunks, hist, ntiles);
+        else
+            build_hist_kernel<int32_t><<<(unsigned)ntiles, kHistThreads, hist_lds, s>>>(d_segs, nseg, total, nb, clog2,
+                                                                                      nchunks, hist, ntiles);
+        hipError_t e = launch_scan_u32(hist, hlen, (unsigned long long*)scan_scratch, &ctr->n_valid, s);
+        if (e != hipSuccess) return e;
+        if (key_bytes == 8)
+            build_scatter_kernel<int64_t><<<(unsigned)ntiles, kHistThreads, hist_lds, s>>>(
+                d_segs, nseg, total, nb, clog2, nchunks, hist, ntiles, skeys, srows, row_ids);
+        else
+            build_scatter_kernel<int32_t><<<(unsigned)ntiles, kHistThreads, hist_lds, s>>>(
+                d_segs, nseg, total, nb, clog2, nchunks, hist, ntiles, skeys, srows, row_ids);
+    }
+    // chunk build: LDS = bucket image + dup directory (3 u32 per entry)
+    const uint32_t CB = 1u << clog2;
+    const size_t img = (size_t)CB * sizeof(Bucket);
+    const size_t lds_cap = 160 * 1024 - 2048;  // leave room for the static LDS
+    uint32_t dupcap = (uint32_t)std::min<size_t>((size_t)CB * kSlots, (lds_cap - img) / 12);
+    const size_t lds = img + (size_t)dupcap * 12;
+    hipError_t e = hipFuncSetAttribute((const void*)chunk_build_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)lds);
+    if (e != hipSuccess) return e;
+    if (ntiles > 0) {
+        chunk_build_kernel<<<nchunks + 1, kChunkThreads, lds, s>>>(nb, clog2, nchunks, hist, ntiles, skeys, srows, tbl,
+                                                                   dup_rows, big, ctr, dupcap);
+        dup_sort_big_kernel<<<big_grid, kBigThreads, 0, s>>>(dup_rows, big, ctr, d_segs, nseg, total, key_bytes);
+    }
     return hipGetLastError();
 }
 
-hipError_t launch_dup_big(Bucket* tbl, uint32_t nbuckets, const DupDir* dir, uint32_t* dup_rows,
-                          const uint32_t* big, const BuildCounters* ctr, const Segment* segs,
-                          int nseg, int64_t total, int key_bytes, int grid, hipStream_t s) {
-    dup_sort_big_kernel<<<grid, kBigThreads, 0, s>>>(tbl, nbuckets, dir, dup_rows, big, ctr, segs, nseg,
-                                                     total, key_bytes);
-    return hipGetLastError();
+int64_t probe_tiles(int64_t n) { return (n + kProbeTile - 1) / kProbeTile; }
+
+int64_t probe_workspace(int64_t n) {
+    const int64_t nt = probe_tiles(n > 0 ? n : 0);
+    return 16 + 8 * (nt + 2) + 16 + 4 * (n > 0 ? n : 0) + 16;
 }
 
-int64_t probe_tiles(int64_t n) { return (n + kTile - 1) / kTile; }
-
-hipError_t launch_probe(int key_bytes, const Bucket* tbl, uint32_t nbuckets,
-                        const uint32_t* dup_rows, const uint64_t* row_ids, const void* keys,
-                        const uint8_t* valid, int64_t voff, const uint32_t* probe_ids, int64_t n,
-                        uint64_t* out_b, uint32_t* out_p, int64_t cap, int64_t* d_total,
-                        unsigned long long* status, unsigned int* ticket, hipStream_t s) {
+hipError_t launch_probe(int key_bytes, const TableView& tv, const void* keys, const uint8_t* valid, int64_t voff,
+                        const uint32_t* probe_ids, int64_t n, uint64_t* out_b, uint32_t* out_p, int64_t cap,
+                        int64_t* d_total, void* workspace, hipStream_t s) {
     const int64_t nt = probe_tiles(n);
-    if (nt == 0) return hipSuccess;
+    unsigned char* w = (unsigned char*)workspace;
+    unsigned long long* tcnt = (unsigned long long*)(w + 16);
+    uint32_t* info = (uint32_t*)(((uintptr_t)(tcnt + nt + 2) + 15) & ~(uintptr_t)15);
+    if (nt == 0) return hipMemsetAsync(d_total, 0, sizeof(int64_t), s);
     const bool vec = (reinterpret_cast<uintptr_t>(keys) & 15) == 0;
-    if (key_bytes == 8)
-        probe_kernel<int64_t><<<(unsigned)nt, kProbeThreads, 0, s>>>(tbl, nbuckets, dup_rows, row_ids, keys,
-                                                                    valid, voff, probe_ids, n, out_b, out_p,
-                                                                    cap, d_total, status, ticket, nt, vec);
-    else
-        probe_kernel<int32_t><<<(unsigned)nt, kProbeThreads, 0, s>>>(tbl, nbuckets, dup_rows, row_ids, keys,
-                                                                    valid, voff, probe_ids, n, out_b, out_p,
-                                                                    cap, d_total, status, ticket, nt, vec);
+#define DFP_LOOKUP(KT, HV) \
+    probe_lookup_kernel<KT, HV><<<(unsigned)nt, kProbeThreads, 0, s>>>(tv, keys, valid, voff, n, vec, info, tcnt)
+    if (key_bytes == 8) {
+        if (valid) DFP_LOOKUP(int64_t, true); else DFP_LOOKUP(int64_t, false);
+    } else {
+        if (valid) DFP_LOOKUP(int32_t, true); else DFP_LOOKUP(int32_t, false);
+    }
+#undef DFP_LOOKUP
+    scan_top_kernel<<<1, 1024, 0, s>>>(tcnt, nt, (unsigned long long*)d_total);
+#define DFP_EMIT(RI, PI) \
+    probe_emit_kernel<int64_t, RI, PI><<<(unsigned)nt, kProbeThreads, 0, s>>>(tv, info, probe_ids, n, tcnt, out_b, out_p, cap)
+    const bool ri = tv.row_ids != nullptr, pi = probe_ids != nullptr;
+    if (ri && pi) DFP_EMIT(true, true);
+    else if (ri) DFP_EMIT(true, false);
+    else if (pi) DFP_EMIT(false, true);
+    else DFP_EMIT(false, false);
+#undef DFP_EMIT
     return hipGetLastError();
 }
 
-hipError_t launch_table_stats(const Bucket* tbl, uint32_t nbuckets, unsigned long long* out,
-                              hipStream_t s) {
-    table_stats_kernel<<<1024, 256, 0, s>>>(tbl, nbuckets, out);
+hipError_t launch_table_stats(const TableView& tv, unsigned long long* out, hipStream_t s) {
+    table_stats_kernel<<<1024, 256, 0, s>>>(tv, out);
     return hipGetLastError();
 }
 
-hipError_t launch_chain_links(const Bucket* tbl, uint32_t nbuckets, const uint32_t* dup_rows,
-                              int64_t* prev, int64_t nrows, hipStream_t s) {
+hipError_t launch_chain_links(const TableView& tv, int64_t* prev, int64_t nrows, hipStream_t s) {
     chain_fill_kernel<<<1024, 256, 0, s>>>(prev, nrows);
-    chain_links_kernel<<<1024, 256, 0, s>>>(tbl, nbuckets, dup_rows, prev);
+    chain_links_kernel<<<1024, 256, 0, s>>>(tv, prev);
     return hipGetLastError();
 }
 
 int64_t radix_partition_workspace(int64_t n, int nparts) {
     const int64_t nblocks = (n + kPartChunk - 1) / kPartChunk;
-    return (nblocks * nparts + 1) * 8;
+    const int64_t hlen = nblocks * nparts;
+    return 4 * (hlen + 4) + scan_scratch_bytes(hlen) + 16;
 }
 
-hipError_t launch_radix_partition(int key_bytes, const void* keys, const uint8_t* valid,
-                                  int64_t voff, const uint64_t* ids, uint64_t id_base, int64_t n,
-                                  int nparts, void* out_keys, uint64_t* out_ids, int64_t* counts,
-                                  void* workspace, hipStream_t s) {
+hipError_t launch_radix_partition(int key_bytes, const void* keys, const uint8_t* valid, int64_t voff,
+                                  const uint64_t* ids, uint64_t id_base, int64_t n, int nparts, void* out_keys,
+                                  uint64_t* out_ids, int64_t* counts, void* workspace, hipStream_t s) {
     if (nparts < 1 || nparts > kMaxParts || (nparts & (nparts - 1))) return hipErrorInvalidValue;
     const int64_t nblocks = (n + kPartChunk - 1) / kPartChunk;
     if (nblocks == 0) return hipMemsetAsync(counts, 0, sizeof(int64_t) * nparts, s);
-    unsigned long long* hist = reinterpret_cast<unsigned long long*>(workspace);
-    if (key_bytes == 8) {
+    const int64_t hlen = nblocks * nparts;
+    uint32_t* hist = reinterpret_cast<uint32_t*>(workspace);
+    unsigned long long* scratch =
+        reinterpret_cast<unsigned long long*>(((uintptr_t)(hist + hlen + 4) + 15) & ~(uintptr_t)15);
+    const int64_t nsb = (hlen + kScanSeg - 1) / kScanSeg;
+    unsigned long long* total = scratch + nsb;  // scan_top writes bsum[nblk] = grand total
+    if (key_bytes == 8)
         part_hist_kernel<int64_t><<<(unsigned)nblocks, kPartThreads, 0, s>>>(keys, valid, voff, n, nparts, hist, nblocks);
-        part_scan_kernel<<<1, 1024, 0, s>>>(hist, nblocks * nparts, nblocks, nparts, counts);
+    else
+        part_hist_kernel<int32_t><<<(unsigned)nblocks, kPartThreads, 0, s>>>(keys, valid, voff, n, nparts, hist, nblocks);
+    hipError_t e = launch_scan_u32(hist, hlen, scratch, nullptr, s);
+    if (e != hipSuccess) return e;
+    part_counts_kernel<<<1, 64, 0, s>>>(hist, nblocks, nparts, total, counts);
+    if (key_bytes == 8)
         part_scatter_kernel<int64_t><<<(unsigned)nblocks, kPartThreads, 0, s>>>(
             keys, valid, voff, ids, id_base, n, nparts, hist, nblocks, (int64_t*)out_keys, out_ids);
-    } else {
-        part_hist_kernel<int32_t><<<(unsigned)nblocks, kPartThreads, 0, s>>>(keys, valid, voff, n, nparts, hist, nblocks);
-        part_scan_kernel<<<1, 1024, 0, s>>>(hist, nblocks * nparts, nblocks, nparts, counts);
+    else
         part_scatter_kernel<int32_t><<<(unsigned)nblocks, kPartThreads, 0, s>>>(
             keys, valid, voff, ids, id_base, n, nparts, hist, nblocks, (int32_t*)out_keys, out_ids);
-    }
     return hipGetLastError();
 }
 

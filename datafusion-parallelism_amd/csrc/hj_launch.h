@@ -1,6 +1,6 @@
 // hj_launch.h — host-callable launchers of the gfx950 kernels (implemented in
 // hj_kernels.hip). Every launcher is asynchronous on `stream` and returns the
-// hipError_t of the launch.
+// hipError_t of its launches.
 #pragma once
 #include <hip/hip_runtime.h>
 #include "hj_device.h"
@@ -8,34 +8,33 @@
 namespace dfp {
 
 // ---- build ---------------------------------------------------------------
-hipError_t launch_insert(int key_bytes, const Segment* d_segs, int nseg, int64_t total,
-                         Bucket* tbl, uint32_t nbuckets, uint64_t* row_ids,
-                         uint2* duprows, uint32_t* dupslots, BuildCounters* ctr,
-                         int grid, hipStream_t s);
-hipError_t launch_dup_passes(Bucket* tbl, uint32_t nbuckets, const uint2* duprows,
-                             const uint32_t* dupslots, DupDir* dir, uint32_t* dup_rows,
-                             uint32_t* big, BuildCounters* ctr, int grid, hipStream_t s);
+constexpr int kBuildTile = 8192;     // build rows per histogram/scatter block
+constexpr int kMaxChunks = 16383;    // + side partition -> LDS histogram <= 64 KB
 
-hipError_t launch_dup_big(Bucket* tbl, uint32_t nbuckets, const DupDir* dir, uint32_t* dup_rows,
-                          const uint32_t* big, const BuildCounters* ctr, const Segment* segs,
-                          int nseg, int64_t total, int key_bytes, int grid, hipStream_t s);
+int64_t build_tiles(int64_t total);
+// bytes of the scan scratch for a histogram of `len` u32
+int64_t scan_scratch_bytes(int64_t len);
+
+hipError_t launch_build(int key_bytes, const Segment* d_segs, int nseg, int64_t total,
+                        uint32_t nb, uint32_t clog2, uint32_t nchunks, uint32_t* hist,
+                        int64_t ntiles, void* scan_scratch, unsigned long long* skeys,
+                        uint32_t* srows, uint64_t* row_ids, Bucket* tbl, uint32_t* dup_rows,
+                        BigSeg* big, BuildCounters* ctr, int big_grid, hipStream_t s);
 
 // ---- probe ---------------------------------------------------------------
 int64_t probe_tiles(int64_t n);
-hipError_t launch_probe(int key_bytes, const Bucket* tbl, uint32_t nbuckets,
-                        const uint32_t* dup_rows, const uint64_t* row_ids,
-                        const void* keys, const uint8_t* valid, int64_t voff,
-                        const uint32_t* probe_ids, int64_t n, uint64_t* out_b,
-                        uint32_t* out_p, int64_t cap, int64_t* d_total,
-                        unsigned long long* status, unsigned int* ticket,
+int64_t probe_workspace(int64_t n);
+// workspace: [0,8) unused, [8,16) error word, then tile counts/offsets, then per-row refs
+hipError_t launch_probe(int key_bytes, const TableView& tv, const void* keys, const uint8_t* valid,
+                        int64_t voff, const uint32_t* probe_ids, int64_t n, uint64_t* out_b,
+                        uint32_t* out_p, int64_t cap, int64_t* d_total, void* workspace,
                         hipStream_t s);
 
 // ---- table queries -------------------------------------------------------
-hipError_t launch_table_stats(const Bucket* tbl, uint32_t nbuckets,
+hipError_t launch_table_stats(const TableView& tv,
                               unsigned long long* out /* [4]: distinct, dupkeys, duprows, maxrows */,
                               hipStream_t s);
-hipError_t launch_chain_links(const Bucket* tbl, uint32_t nbuckets, const uint32_t* dup_rows,
-                              int64_t* prev, int64_t nrows, hipStream_t s);
+hipError_t launch_chain_links(const TableView& tv, int64_t* prev, int64_t nrows, hipStream_t s);
 
 // ---- multi-GPU radix partition -------------------------------------------
 hipError_t launch_radix_partition(int key_bytes, const void* keys, const uint8_t* valid,
