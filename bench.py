@@ -179,6 +179,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--force-dist", action="store_true",
+                    help="use the radix-exchange path even with one rank (testing)")
     args = ap.parse_args()
     cfg = CONFIGS[args.config]
 
@@ -189,13 +191,14 @@ def main():
         log(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
     dev = torch.device("cuda", local_rank)
     torch.cuda.set_device(dev)
-    if world > 1:
+    if world > 1 or args.force_dist:
         dist.init_process_group("nccl", device_id=dev)
 
     bk, pk = gen_inputs(cfg, rank, world, dev)
     B, P = bk.numel(), pk.numel()
 
-    if world == 1:
+    use_dist = world > 1 or args.force_dist
+    if not use_dist:
         job = SingleGpuJoin(bk, pk, dev)
     else:
         from datafusion_parallelism_amd.distributed import DistributedHashJoin
@@ -203,7 +206,7 @@ def main():
         job = DistJob(DistributedHashJoin(), bk, pk, rank, dev)
 
     def barrier():
-        if world > 1:
+        if use_dist:
             dist.barrier()
 
     for _ in range(args.warmup):
@@ -226,7 +229,7 @@ def main():
     torch.cuda.synchronize(dev)
     barrier()
     elapsed = time.perf_counter() - t_start
-    if world > 1:
+    if use_dist:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
@@ -271,7 +274,7 @@ def main():
                 "build_rows_per_gpu": B,
                 "probe_rows_per_gpu": P,
                 "matches_per_gpu": M,
-                "parallelism": "single-gpu" if world == 1 else f"radix-a2a x{world} (RCCL)",
+                "parallelism": "single-gpu" if not use_dist else f"radix-a2a x{world} (RCCL)",
             },
             "probe_mrows_s": round(P / (probe_ms / 1e3) / 1e6, 1),
             "probe_ms": round(probe_ms, 4),
@@ -280,10 +283,10 @@ def main():
             "roofline": roofline,
             "cpu_baseline": cpu,
         }
-        if world > 1:
+        if use_dist:
             line["exchange_ms"] = round(float(np.median(job.exchange_ms)), 4)
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if use_dist:
         dist.destroy_process_group()
 
 

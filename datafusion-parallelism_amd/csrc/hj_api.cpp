@@ -99,6 +99,68 @@ void release_resources(int dev, const BuildResources& r) {
     g_pool[dev].push_back(r);
 }
 
+// Caching device allocator: tables come and go per query, and hipMallocAsync/
+// hipFreeAsync cost ~0.1 ms per call on ROCm; blocks are kept per (device, size class)
+// and handed out again. A block is only reused after its table was freed, and the
+// caller frees a table only after every stream that probed it has been synchronised
+// (hj_table_free contract).
+struct DevCache {
+    std::mutex mu;
+    std::unordered_map<uint64_t, std::vector<void*>> bins;  // key = device << 48 | size class
+    size_t cached_bytes = 0;
+};
+DevCache g_cache;
+
+size_t size_class(size_t bytes) {
+    if (bytes <= 4096) return 4096;
+    if (bytes <= (1u << 20)) {  // powers of two below 1 MiB
+        size_t c = 4096;
+        while (c < bytes) c <<= 1;
+        return c;
+    }
+    const size_t step = bytes <= (256u << 20) ? (2u << 20) : (32u << 20);
+    return (bytes + step - 1) / step * step;
+}
+
+void* cache_alloc(int dev, size_t bytes, hipError_t* err) {
+    const size_t c = size_class(bytes);
+    const uint64_t key = ((uint64_t)dev << 48) | c;
+    {
+        std::lock_guard<std::mutex> g(g_cache.mu);
+        auto it = g_cache.bins.find(key);
+        if (it != g_cache.bins.end() && !it->second.empty()) {
+            void* p = it->second.back();
+            it->second.pop_back();
+            g_cache.cached_bytes -= c;
+            *err = hipSuccess;
+            return p;
+        }
+    }
+    void* p = nullptr;
+    *err = hipMalloc(&p, c);
+    if (*err != hipSuccess) {
+        (void)hipGetLastError();
+        // release every cached block of this device and retry once
+        std::lock_guard<std::mutex> g(g_cache.mu);
+        for (auto& kv : g_cache.bins) {
+            if ((int)(kv.first >> 48) != dev) continue;
+            for (void* q : kv.second) (void)hipFree(q);
+            g_cache.cached_bytes -= (kv.first & ((1ull << 48) - 1)) * kv.second.size();
+            kv.second.clear();
+        }
+        *err = hipMalloc(&p, c);
+    }
+    return *err == hipSuccess ? p : nullptr;
+}
+
+void cache_free(int dev, void* p, size_t bytes) {
+    if (p == nullptr) return;
+    const size_t c = size_class(bytes);
+    std::lock_guard<std::mutex> g(g_cache.mu);
+    g_cache.bins[((uint64_t)dev << 48) | c].push_back(p);
+    g_cache.cached_bytes += c;
+}
+
 int device_count() {
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess) return 0;
@@ -161,23 +223,24 @@ struct hj_table {
     uint64_t* row_ids = nullptr;
     BuildResources res;
     int64_t build_ns = 0;
-    std::vector<void*> allocs;   // live for the table's lifetime
-    std::vector<void*> scratch;  // build-only, released when the build completes
+    std::vector<std::pair<void*, size_t>> allocs;   // live for the table's lifetime
+    std::vector<std::pair<void*, size_t>> scratch;  // build-only, released after the build
 };
 
 namespace {
 
-hj_status dev_alloc(hj_table* t, std::vector<void*>& list, void** p, size_t bytes) {
-    *p = nullptr;
+hj_status dev_alloc(hj_table* t, std::vector<std::pair<void*, size_t>>& list, void** p, size_t bytes) {
     if (bytes == 0) bytes = 64;
-    hipError_t e = hipMallocAsync(p, (bytes + 255) & ~(size_t)255, t->res.stream);
-    if (e != hipSuccess) return fail(HJ_ERR_OOM, std::string("hipMallocAsync: ") + hipGetErrorString(e));
-    list.push_back(*p);
+    hipError_t e;
+    *p = cache_alloc(t->device, bytes, &e);
+    if (*p == nullptr) return fail(HJ_ERR_OOM, std::string("device allocation: ") + hipGetErrorString(e));
+    list.emplace_back(*p, bytes);
     return HJ_OK;
 }
 
-void free_list(hj_table* t, std::vector<void*>& list) {
-    for (void* p : list) (void)hipFreeAsync(p, t->res.stream);
+// only once no queued work uses the blocks any more
+void free_list(hj_table* t, std::vector<std::pair<void*, size_t>>& list) {
+    for (auto& pb : list) cache_free(t->device, pb.first, pb.second);
     list.clear();
 }
 
@@ -258,8 +321,8 @@ hj_status build_attempt(hj_table* t, const std::vector<Segment>& segs, double lf
                          scan, skeys, srows, t->row_ids, t->tbl, t->dup_rows, big, ctr, cus, s));
     BuildCounters hc;
     HIP_TRY(hipMemcpyAsync(&hc, ctr, sizeof(hc), hipMemcpyDeviceToHost, s));
-    free_list(t, t->scratch);
     HIP_TRY(hipStreamSynchronize(s));
+    free_list(t, t->scratch);  // the build has completed: scratch blocks are idle
     if (hc.err) {
         *retry = true;
         free_list(t, t->allocs);

@@ -28,6 +28,8 @@
 #include <stdint.h>
 #include <stdlib.h>
 
+#include <algorithm>
+
 #include "hj_device.h"
 #include "hj_launch.h"
 
@@ -608,21 +610,42 @@ probe_lookup_kernel(TableView tv, const void* __restrict__ keys, const uint8_t* 
     if (threadIdx.x == 0) tcnt[blockIdx.x] = tot;
 }
 
-template <typename K, bool HAS_ROW_IDS, bool HAS_PROBE_IDS>
+// SORTED: `info` holds each tile's refs in the tile's partition-sorted order (the
+// partitioned probe) and perm[row] is the row's position in that order; the tile's refs
+// are staged through LDS (one coalesced 16 KB load) and read back in row order.
+template <bool SORTED, bool HAS_ROW_IDS, bool HAS_PROBE_IDS>
 __global__ void __launch_bounds__(kProbeThreads)
-probe_emit_kernel(TableView tv, const uint32_t* __restrict__ info, const uint32_t* __restrict__ probe_ids,
-                  int64_t n, const unsigned long long* __restrict__ toff, uint64_t* __restrict__ out_b,
-                  uint32_t* __restrict__ out_p, int64_t cap) {
+probe_emit_kernel(TableView tv, const uint32_t* __restrict__ info, const uint16_t* __restrict__ perm,
+                  const uint32_t* __restrict__ probe_ids, int64_t n, const unsigned long long* __restrict__ toff,
+                  uint64_t* __restrict__ out_b, uint32_t* __restrict__ out_p, int64_t cap) {
     __shared__ unsigned long long s_w[kGroups][kProbeThreads / 64];
+    __shared__ __attribute__((aligned(16))) uint32_t s_info[SORTED ? kProbeTile : 1];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int64_t tile0 = (int64_t)blockIdx.x * kProbeTile;
     uint32_t ref[kGroups][4];
     uint32_t cnt[kGroups][4];
     unsigned long long gsum[kGroups], gincl[kGroups];
+    if constexpr (SORTED) {
+        const int64_t rows = min<int64_t>(kProbeTile, n - tile0);
+        for (int64_t i = threadIdx.x * 4; i < rows; i += kProbeThreads * 4) {
+            if (i + 4 <= rows) *reinterpret_cast<uint4*>(s_info + i) = *reinterpret_cast<const uint4*>(info + tile0 + i);
+            else for (int64_t k = i; k < rows; ++k) s_info[k] = info[tile0 + k];
+        }
+        __syncthreads();
+    }
 #pragma unroll
     for (int g = 0; g < kGroups; ++g) {
         const int64_t row0 = tile0 + (int64_t)g * (kProbeThreads * 4) + (int64_t)threadIdx.x * 4;
-        if (row0 + 4 <= n) {
+        if constexpr (SORTED) {
+            if (row0 + 4 <= n) {
+                const uint2 pv = *reinterpret_cast<const uint2*>(perm + row0);
+                ref[g][0] = s_info[pv.x & 0xFFFF]; ref[g][1] = s_info[pv.x >> 16];
+                ref[g][2] = s_info[pv.y & 0xFFFF]; ref[g][3] = s_info[pv.y >> 16];
+            } else {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) ref[g][q] = (row0 + q < n) ? s_info[perm[row0 + q]] : kMiss;
+            }
+        } else if (row0 + 4 <= n) {
             const uint4 v = *reinterpret_cast<const uint4*>(info + row0);
             ref[g][0] = v.x; ref[g][1] = v.y; ref[g][2] = v.z; ref[g][3] = v.w;
         } else {
@@ -675,6 +698,208 @@ probe_emit_kernel(TableView tv, const uint32_t* __restrict__ info, const uint32_
             pos += c;
         }
     }
+}
+
+// ---------------------------------------------------------------------------
+// partitioned probe (tables much larger than L2): the table is cut into pieces of
+// `cpp` chunks (~2 MB); probe rows are grouped by piece inside each 4096-row tile, and
+// the lookups of one piece run on one XCD so that its L2 holds the piece.
+// ---------------------------------------------------------------------------
+constexpr int kMaxPieces = 255;  // + 1 direct bin (nulls, INT64_MIN) <= 256 bins
+
+struct PieceGeom {
+    uint32_t cpp;     // chunks per piece
+    uint32_t npiece;  // pieces (bin npiece = rows that need no table lookup)
+};
+
+// P1: per tile, counting sort of the rows by piece in LDS; writes the tile's keys in
+// sorted order, perm[row] = sorted position, the tile's bin offsets, and resolves the
+// direct bin (nulls -> miss, INT64_MIN -> side bucket) on the spot.
+template <typename K, bool HAS_VALID>
+__global__ void __launch_bounds__(kProbeThreads)
+pp_partition_kernel(TableView tv, PieceGeom pg, const void* __restrict__ keys, const uint8_t* __restrict__ valid,
+                    int64_t voff, int64_t n, bool vec, unsigned long long* __restrict__ skeys,
+                    uint16_t* __restrict__ perm, uint16_t* __restrict__ toff, uint32_t* __restrict__ info,
+                    uint32_t* __restrict__ cnt2) {
+    __shared__ __attribute__((aligned(16))) unsigned long long s_keys[kProbeTile];
+    __shared__ unsigned s_bin[kMaxPieces + 2];
+    __shared__ unsigned s_cur[kMaxPieces + 2];
+    __shared__ unsigned s_direct;
+    const int64_t tile = blockIdx.x;
+    const int64_t tile0 = tile * kProbeTile;
+    const uint32_t nbins = pg.npiece + 1;
+    for (uint32_t b = threadIdx.x; b < nbins; b += kProbeThreads) s_bin[b] = 0;
+    if (threadIdx.x == 0) s_direct = 0;
+    __syncthreads();
+    int64_t k[kGroups][4];
+    uint32_t bin[kGroups][4];
+#pragma unroll
+    for (int g = 0; g < kGroups; ++g) {
+        const int64_t row0 = tile0 + (int64_t)g * (kProbeThreads * 4) + (int64_t)threadIdx.x * 4;
+        load4<K>(keys, row0, n, vec, k[g]);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const bool in = row0 + q < n;
+            const bool ok = in && (!HAS_VALID || bit_valid(valid, voff, row0 + q));
+            const unsigned long long sk = (unsigned long long)k[g][q] ^ kSign;
+            bin[g][q] = (!in) ? 0xFFFFFFFFu
+                        : (ok && sk != 0) ? ((home_bucket(k[g][q], tv.nb) >> tv.clog2) / pg.cpp) : pg.npiece;
+            if (in && !ok) k[g][q] = 0, bin[g][q] |= 0x80000000u;  // null: no lookup, ref = miss
+            if (in) atomicAdd(&s_bin[bin[g][q] & 0x7FFFFFFF], 1u);
+        }
+    }
+    __syncthreads();
+    // exclusive scan of the bins (<= 256) by wave 0
+    if (threadIdx.x < 64) {
+        unsigned carry = 0;
+        for (uint32_t b0 = 0; b0 < nbins; b0 += 64) {
+            const uint32_t b = b0 + threadIdx.x;
+            const unsigned v = b < nbins ? s_bin[b] : 0u;
+            const unsigned incl = wave_incl_scan<unsigned>(v);
+            if (b < nbins) s_cur[b] = carry + incl - v;
+            carry += __shfl(incl, 63, 64);
+        }
+        if (threadIdx.x == 0) s_cur[nbins] = carry;
+    }
+    __syncthreads();
+    for (uint32_t b = threadIdx.x; b <= nbins; b += kProbeThreads) toff[tile * (kMaxPieces + 2) + b] = (uint16_t)s_cur[b];
+    __syncthreads();
+    uint32_t direct_cnt = 0;
+#pragma unroll
+    for (int g = 0; g < kGroups; ++g) {
+        const int64_t row0 = tile0 + (int64_t)g * (kProbeThreads * 4) + (int64_t)threadIdx.x * 4;
+        uint32_t pos[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            pos[q] = 0;
+            if (row0 + q < n) {
+                const uint32_t b = bin[g][q] & 0x7FFFFFFF;
+                pos[q] = atomicAdd(&s_cur[b], 1u);
+                s_keys[pos[q]] = (unsigned long long)k[g][q];
+                if (b == pg.npiece) {  // direct bin: resolve now
+                    uint32_t ref = kMiss;
+                    if (!(bin[g][q] & 0x80000000u)) {  // INT64_MIN (not null)
+                        const Bucket& S = tv.tbl[tv.nb];
+                        ref = S.meta ? S.ref[0] : kMiss;
+                    }
+                    info[tile0 + pos[q]] = ref;
+                    direct_cnt += ref_count(tv.dup_rows, ref);
+                }
+            }
+        }
+        if (row0 + 4 <= n) {
+            *reinterpret_cast<uint2*>(perm + row0) = make_uint2(pos[0] | (pos[1] << 16), pos[2] | (pos[3] << 16));
+        } else {
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                if (row0 + q < n) perm[row0 + q] = (uint16_t)pos[q];
+        }
+    }
+    if (direct_cnt) atomicAdd(&s_direct, direct_cnt);
+    __syncthreads();
+    const int64_t rows = min<int64_t>(kProbeTile, n - tile0);
+    for (int64_t i = threadIdx.x * 2; i < rows; i += kProbeThreads * 2) {
+        if (i + 2 <= rows) *reinterpret_cast<ulonglong2*>(skeys + tile0 + i) = *reinterpret_cast<const ulonglong2*>(s_keys + i);
+        else skeys[tile0 + i] = s_keys[i];
+    }
+    if (threadIdx.x == 0) cnt2[tile * (kMaxPieces + 1) + pg.npiece] = s_direct;
+}
+
+// P2: lookups of piece p on XCD p % 8 (blocks b with b % 8 == p % 8 — the observed
+// round-robin placement; a speed heuristic only, never needed for correctness). For
+// each piece every wave of the XCD takes a contiguous range of tiles, so the XCD's
+// waves move through the pieces together and the current piece stays in its L2. A
+// wave flattens the piece's runs of 64 tiles over its 64 lanes (wave scan of the run
+// lengths, owner lane by binary search over shuffles) and keeps 4 lookups per lane in
+// flight; refs go to the rows' sorted positions, match counts to cnt2[tile][piece].
+constexpr int kP2Unroll = 4;
+
+__global__ void __launch_bounds__(kProbeThreads)
+pp_lookup_kernel(TableView tv, PieceGeom pg, int64_t n, int64_t ntiles, const unsigned long long* __restrict__ skeys,
+                 const uint16_t* __restrict__ toff, uint32_t* __restrict__ info, uint32_t* __restrict__ cnt2) {
+    __shared__ unsigned s_cnt[kProbeThreads / 64][64];
+    const Bucket* __restrict__ tbl = tv.tbl;
+    const uint32_t cmask = (1u << tv.clog2) - 1;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t xcd = blockIdx.x & 7;
+    const uint32_t wpx = (gridDim.x >> 3) * (kProbeThreads / 64);                   // waves per XCD
+    const uint32_t wid = (blockIdx.x >> 3) * (kProbeThreads / 64) + (uint32_t)wave;  // wave index in XCD
+    const int64_t tb = ntiles * wid / wpx, te = ntiles * (wid + 1) / wpx;
+    for (uint32_t p = xcd; p < pg.npiece; p += 8) {
+        for (int64_t tc = tb; tc < te; tc += 64) {
+            const int64_t t = tc + lane;
+            const bool have = t < te;
+            uint32_t st = 0, len = 0;
+            if (have) {
+                const uint16_t* to = toff + t * (kMaxPieces + 2);
+                st = to[p];
+                len = to[p + 1] - st;
+            }
+            const uint32_t incl = wave_incl_scan<uint32_t>(len);
+            const uint32_t excl = incl - len;
+            const uint32_t R = __shfl(incl, 63, 64);
+            s_cnt[wave][lane] = 0;
+            __builtin_amdgcn_wave_barrier();
+            for (uint32_t r0 = 0; r0 < R; r0 += 64 * kP2Unroll) {
+                unsigned long long sk[kP2Unroll];
+                int64_t row[kP2Unroll];
+                uint32_t own[kP2Unroll], b0[kP2Unroll];
+                uint4 a0[kP2Unroll], a1[kP2Unroll], a2[kP2Unroll], a3[kP2Unroll];
+#pragma unroll
+                for (int u = 0; u < kP2Unroll; ++u) {
+                    const uint32_t r = r0 + u * 64 + lane;
+                    // owner lane j = number of lanes whose inclusive end is <= r
+                    uint32_t j = 0;
+#pragma unroll
+                    for (uint32_t step = 32; step >= 1; step >>= 1) {
+                        const uint32_t e = __shfl(incl, (int)(j + step - 1), 64);
+                        if (e <= r) j += step;
+                    }
+                    j = j > 63 ? 63 : j;
+                    own[u] = j;
+                    const uint32_t sj = __shfl(st, (int)j, 64), xj = __shfl(excl, (int)j, 64);
+                    row[u] = (tc + j) * kProbeTile + sj + (r - xj);
+                    sk[u] = (r < R) ? (__builtin_nontemporal_load(skeys + row[u]) ^ kSign) : 0;
+                }
+#pragma unroll
+                for (int u = 0; u < kP2Unroll; ++u) {
+                    b0[u] = home_bucket((int64_t)(sk[u] ^ kSign), tv.nb);
+                    const uint4* lp = reinterpret_cast<const uint4*>(tbl + b0[u]);
+                    a0[u] = lp[0]; a1[u] = lp[1]; a2[u] = lp[2]; a3[u] = lp[3];
+                }
+#pragma unroll
+                for (int u = 0; u < kP2Unroll; ++u) {
+                    const uint32_t r = r0 + u * 64 + lane;
+                    if (r >= R) continue;
+                    bool more;
+                    uint32_t ref = scan_line(a0[u], a1[u], a2[u], a3[u], sk[u], &more);
+                    uint32_t bb = b0[u];
+                    for (uint32_t probes = 0; more && probes < cmask; ++probes) {
+                        bb = (bb & ~cmask) | ((bb + 1) & cmask);
+                        const uint4* q = reinterpret_cast<const uint4*>(tbl + bb);
+                        ref = scan_line(q[0], q[1], q[2], q[3], sk[u], &more);
+                    }
+                    __builtin_nontemporal_store(ref, info + row[u]);
+                    const uint32_t c = ref_count(tv.dup_rows, ref);
+                    if (c) atomicAdd(&s_cnt[wave][own[u]], c);
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            if (have) cnt2[t * (kMaxPieces + 1) + p] = s_cnt[wave][lane];
+            __builtin_amdgcn_wave_barrier();
+        }
+    }
+}
+
+// per-tile match totals of the partitioned probe
+__global__ void pp_count_kernel(const uint32_t* __restrict__ cnt2, uint32_t nbins, int64_t ntiles,
+                                unsigned long long* __restrict__ tcnt) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= ntiles) return;
+    unsigned long long s = 0;
+    for (uint32_t b = 0; b < nbins; ++b) s += cnt2[t * (kMaxPieces + 1) + b];
+    tcnt[t] = s;
 }
 
 // ---------------------------------------------------------------------------
@@ -895,36 +1120,127 @@ hipError_t launch_build(int key_bytes, const Segment* d_segs, int nseg, int64_t 
 
 int64_t probe_tiles(int64_t n) { return (n + kProbeTile - 1) / kProbeTile; }
 
-int64_t probe_workspace(int64_t n) {
+// workspace layout (all regions 256-byte aligned):
+//   [0,16) header (bytes 8..15: error word) | tcnt u64[nt+2] | cnt2 u32[nt][256] |
+//   toff u16[nt][257] | skeys u64[nt*4096] | perm u16[n] | info u32[nt*4096]
+namespace {
+struct ProbeWs {
+    unsigned long long* tcnt;
+    uint32_t* cnt2;
+    uint16_t* toff;
+    unsigned long long* skeys;
+    uint16_t* perm;
+    uint32_t* info;
+    int64_t bytes;
+};
+inline uintptr_t al256(uintptr_t x) { return (x + 255) & ~(uintptr_t)255; }
+ProbeWs probe_ws_layout(void* base, int64_t n) {
     const int64_t nt = probe_tiles(n > 0 ? n : 0);
-    return 16 + 8 * (nt + 2) + 16 + 4 * (n > 0 ? n : 0) + 16;
+    const int64_t rows = nt * kProbeTile;
+    ProbeWs w;
+    uintptr_t p = (uintptr_t)base + 256;
+    w.tcnt = (unsigned long long*)p; p = al256(p + 8 * (nt + 2));
+    w.cnt2 = (uint32_t*)p;           p = al256(p + 4 * nt * (kMaxPieces + 1));
+    w.toff = (uint16_t*)p;           p = al256(p + 2 * nt * (kMaxPieces + 2));
+    w.skeys = (unsigned long long*)p; p = al256(p + 8 * rows);
+    w.perm = (uint16_t*)p;           p = al256(p + 2 * rows);
+    w.info = (uint32_t*)p;           p = al256(p + 4 * rows);
+    w.bytes = (int64_t)(p - (uintptr_t)base) + 256;  // + slack for an unaligned base
+    return w;
 }
+
+int probe_mode() {  // 0 auto, 1 direct, 2 partitioned
+    static const int m = [] {
+        const char* e = getenv("DFP_HJ_PROBE_MODE");
+        if (!e) return 0;
+        if (e[0] == 'd') return 1;
+        if (e[0] == 'p') return 2;
+        return 0;
+    }();
+    return m;
+}
+}  // namespace
+
+int64_t probe_workspace(int64_t n) { return probe_ws_layout(nullptr, n).bytes; }
 
 hipError_t launch_probe(int key_bytes, const TableView& tv, const void* keys, const uint8_t* valid, int64_t voff,
                         const uint32_t* probe_ids, int64_t n, uint64_t* out_b, uint32_t* out_p, int64_t cap,
                         int64_t* d_total, void* workspace, hipStream_t s) {
     const int64_t nt = probe_tiles(n);
-    unsigned char* w = (unsigned char*)workspace;
-    unsigned long long* tcnt = (unsigned long long*)(w + 16);
-    uint32_t* info = (uint32_t*)(((uintptr_t)(tcnt + nt + 2) + 15) & ~(uintptr_t)15);
     if (nt == 0) return hipMemsetAsync(d_total, 0, sizeof(int64_t), s);
+    // align the layout on the workspace base
+    ProbeWs w = probe_ws_layout((void*)(((uintptr_t)workspace + 255) & ~(uintptr_t)255), n);
     const bool vec = (reinterpret_cast<uintptr_t>(keys) & 15) == 0;
-#define DFP_LOOKUP(KT, HV) \
-    probe_lookup_kernel<KT, HV><<<(unsigned)nt, kProbeThreads, 0, s>>>(tv, keys, valid, voff, n, vec, info, tcnt)
-    if (key_bytes == 8) {
-        if (valid) DFP_LOOKUP(int64_t, true); else DFP_LOOKUP(int64_t, false);
+    // The partitioned probe (pieces L2-resident per XCD) is opt-in: measured on MI355X
+    // it lifts the L2 hit rate of the lookups from ~19% to ~73% but per-lane scattered
+    // line accesses stay bound by the L2 request rate, and its two extra passes cost
+    // more than it saves at C2 (profiles/r01_*). DESIGN.md §5.
+    const int mode = probe_mode();
+    const bool part = mode == 2;
+    if (part) {
+        const uint32_t chunk_bytes = (1u << tv.clog2) * (uint32_t)sizeof(Bucket);
+        const uint32_t nchunks = tv.nb >> tv.clog2;
+        PieceGeom pg;
+        static const uint32_t piece_bytes = [] {
+            const char* e = getenv("DFP_HJ_PIECE_KB");
+            const long kb = e ? atol(e) : 2048;
+            return (uint32_t)std::max<long>(64, kb) << 10;
+        }();
+        pg.cpp = std::max<uint32_t>(1, piece_bytes / chunk_bytes);
+        pg.npiece = (nchunks + pg.cpp - 1) / pg.cpp;
+        if (pg.npiece > (uint32_t)kMaxPieces) {
+            pg.cpp = (nchunks + kMaxPieces - 1) / kMaxPieces;
+            pg.npiece = (nchunks + pg.cpp - 1) / pg.cpp;
+        }
+#define DFP_PART(KT, HV)                                                                                         \
+    pp_partition_kernel<KT, HV><<<(unsigned)nt, kProbeThreads, 0, s>>>(tv, pg, keys, valid, voff, n, vec, w.skeys, \
+                                                                       w.perm, w.toff, w.info, w.cnt2)
+        if (key_bytes == 8) {
+            if (valid) DFP_PART(int64_t, true); else DFP_PART(int64_t, false);
+        } else {
+            if (valid) DFP_PART(int32_t, true); else DFP_PART(int32_t, false);
+        }
+#undef DFP_PART
+        // one resident wave set: every block must be running at once for the XCD
+        // grouping (blockIdx % 8) and the lockstep over pieces to hold
+        static const int pp_grid = [] {
+            int dev = 0, per_cu = 0;
+            hipDeviceProp_t prop;
+            if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&prop, dev) != hipSuccess) return 1024;
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, pp_lookup_kernel, kProbeThreads, 0) !=
+                    hipSuccess || per_cu < 1)
+                per_cu = 1;
+            const int g = per_cu * prop.multiProcessorCount;
+            return std::max(8, g & ~7);
+        }();
+        pp_lookup_kernel<<<pp_grid, kProbeThreads, 0, s>>>(tv, pg, n, nt, w.skeys, w.toff, w.info, w.cnt2);
+        pp_count_kernel<<<(unsigned)((nt + 255) / 256), 256, 0, s>>>(w.cnt2, pg.npiece + 1, nt, w.tcnt);
     } else {
-        if (valid) DFP_LOOKUP(int32_t, true); else DFP_LOOKUP(int32_t, false);
-    }
+#define DFP_LOOKUP(KT, HV) \
+    probe_lookup_kernel<KT, HV><<<(unsigned)nt, kProbeThreads, 0, s>>>(tv, keys, valid, voff, n, vec, w.info, w.tcnt)
+        if (key_bytes == 8) {
+            if (valid) DFP_LOOKUP(int64_t, true); else DFP_LOOKUP(int64_t, false);
+        } else {
+            if (valid) DFP_LOOKUP(int32_t, true); else DFP_LOOKUP(int32_t, false);
+        }
 #undef DFP_LOOKUP
-    scan_top_kernel<<<1, 1024, 0, s>>>(tcnt, nt, (unsigned long long*)d_total);
-#define DFP_EMIT(RI, PI) \
-    probe_emit_kernel<int64_t, RI, PI><<<(unsigned)nt, kProbeThreads, 0, s>>>(tv, info, probe_ids, n, tcnt, out_b, out_p, cap)
+    }
+    scan_top_kernel<<<1, 1024, 0, s>>>(w.tcnt, nt, (unsigned long long*)d_total);
+#define DFP_EMIT(SO, RI, PI)                                                                                          \
+    probe_emit_kernel<SO, RI, PI><<<(unsigned)nt, kProbeThreads, 0, s>>>(tv, w.info, w.perm, probe_ids, n, w.tcnt, \
+                                                                        out_b, out_p, cap)
     const bool ri = tv.row_ids != nullptr, pi = probe_ids != nullptr;
-    if (ri && pi) DFP_EMIT(true, true);
-    else if (ri) DFP_EMIT(true, false);
-    else if (pi) DFP_EMIT(false, true);
-    else DFP_EMIT(false, false);
+    if (part) {
+        if (ri && pi) DFP_EMIT(true, true, true);
+        else if (ri) DFP_EMIT(true, true, false);
+        else if (pi) DFP_EMIT(true, false, true);
+        else DFP_EMIT(true, false, false);
+    } else {
+        if (ri && pi) DFP_EMIT(false, true, true);
+        else if (ri) DFP_EMIT(false, true, false);
+        else if (pi) DFP_EMIT(false, false, true);
+        else DFP_EMIT(false, false, false);
+    }
 #undef DFP_EMIT
     return hipGetLastError();
 }

@@ -1,0 +1,30 @@
+"""Diagnostic: one build + 5 probes of a C2-shaped join (B from argv, P = 10^8), for
+per-kernel profiling with rocprofv3."""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+import datafusion_parallelism_amd as dfp  # noqa: E402
+from datafusion_parallelism_amd.table import HashTable  # noqa: E402
+
+B = int(float(sys.argv[1])) if len(sys.argv) > 1 else 10**7
+P = int(float(sys.argv[2])) if len(sys.argv) > 2 else 10**8
+L = dfp.load()
+dev = torch.device("cuda", 0)
+bk = torch.empty(B, dtype=torch.int64, device=dev)
+pk = torch.empty(P, dtype=torch.int64, device=dev)
+assert L.hj_gen_perm_keys(bk.data_ptr(), B, 7368787, B, None) == 0
+assert L.hj_gen_uniform_keys(pk.data_ptr(), P, 0xC0FFEE, 2 * B, None) == 0
+ob = torch.empty(P, dtype=torch.int64, device=dev)
+op = torch.empty(P, dtype=torch.int32, device=dev)
+ws = torch.empty(HashTable.workspace_bytes(P), dtype=torch.uint8, device=dev)
+dt = torch.zeros(1, dtype=torch.int64, device=dev)
+t = HashTable(1, "int64", 0)
+t.build(bk)
+for _ in range(5):
+    t.probe_async(pk.data_ptr(), P, ob.data_ptr(), op.data_ptr(), P, dt.data_ptr(), ws.data_ptr(), 0)
+torch.cuda.synchronize()
+print("matches", int(dt.item()))
+t.close()
