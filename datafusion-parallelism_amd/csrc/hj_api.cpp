@@ -611,6 +611,13 @@ int64_t hj_table_build_ns(const hj_table* t) {
 
 int64_t hj_probe_workspace_bytes(int64_t n) { return probe_workspace(n); }
 
+int hj_set_probe_mode(int mode) {
+    if (mode < 0 || mode > 2) return -1;
+    const int old = get_probe_mode();
+    set_probe_mode(mode);
+    return old;
+}
+
 hj_status hj_probe_async(const hj_table* t, const void* keys, const uint8_t* validity, int64_t validity_offset,
                          int64_t n, uint64_t* out_build, uint32_t* out_probe, int64_t capacity, int64_t* d_total,
                          void* workspace, void* stream) {

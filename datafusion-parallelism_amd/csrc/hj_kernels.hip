@@ -29,6 +29,7 @@
 #include <stdlib.h>
 
 #include <algorithm>
+#include <atomic>
 
 #include "hj_device.h"
 #include "hj_launch.h"
@@ -1149,17 +1150,26 @@ ProbeWs probe_ws_layout(void* base, int64_t n) {
     return w;
 }
 
-int probe_mode() {  // 0 auto, 1 direct, 2 partitioned
-    static const int m = [] {
-        const char* e = getenv("DFP_HJ_PROBE_MODE");
-        if (!e) return 0;
-        if (e[0] == 'd') return 1;
-        if (e[0] == 'p') return 2;
-        return 0;
-    }();
+int env_probe_mode() {  // 0 auto, 1 direct, 2 partitioned
+    const char* e = getenv("DFP_HJ_PROBE_MODE");
+    if (!e) return 0;
+    if (e[0] == 'd') return 1;
+    if (e[0] == 'p') return 2;
+    return 0;
+}
+std::atomic<int> g_probe_mode{-1};
+int probe_mode() {
+    int m = g_probe_mode.load(std::memory_order_relaxed);
+    if (m < 0) {
+        m = env_probe_mode();
+        g_probe_mode.store(m, std::memory_order_relaxed);
+    }
     return m;
 }
 }  // namespace
+
+void set_probe_mode(int mode) { g_probe_mode.store(mode < 0 || mode > 2 ? 0 : mode, std::memory_order_relaxed); }
+int get_probe_mode() { return probe_mode(); }
 
 int64_t probe_workspace(int64_t n) { return probe_ws_layout(nullptr, n).bytes; }
 

@@ -22,6 +22,9 @@ hipError_t launch_build(int key_bytes, const Segment* d_segs, int nseg, int64_t 
                         BigSeg* big, BuildCounters* ctr, int big_grid, hipStream_t s);
 
 // ---- probe ---------------------------------------------------------------
+// 0 auto (= direct), 1 direct, 2 partitioned (L2-resident pieces per XCD)
+void set_probe_mode(int mode);
+int get_probe_mode();
 int64_t probe_tiles(int64_t n);
 int64_t probe_workspace(int64_t n);
 // workspace: [0,8) unused, [8,16) error word, then tile counts/offsets, then per-row refs

@@ -165,6 +165,12 @@ hj_status hj_probe_async_ids(const hj_table* t, const void* keys, const uint8_t*
                              uint64_t* out_build, uint32_t* out_probe, int64_t capacity,
                              int64_t* d_total, void* workspace, void* stream);
 
+/* Probe strategy for later probes of this process: 0 auto (= direct), 1 direct
+ * (lookup per row in row order), 2 partitioned (rows grouped by table piece inside each
+ * tile, pieces looked up L2-resident per XCD). Results are identical; returns the
+ * previous mode, -1 for a bad value. Also settable with DFP_HJ_PROBE_MODE. */
+int hj_set_probe_mode(int mode);
+
 /* Makes `stream` wait for the build of `t` (for probes on other streams). */
 hj_status hj_table_stream_wait(const hj_table* t, void* stream);
 

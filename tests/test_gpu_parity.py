@@ -13,6 +13,15 @@ pytestmark = pytest.mark.gpu
 I64_MIN = np.iinfo(np.int64).min
 
 
+@pytest.fixture(params=["direct", "partitioned"])
+def probe_mode(request, dfp):
+    """Run a test under both probe strategies (identical results required)."""
+    L = dfp.load()
+    old = L.hj_set_probe_mode(1 if request.param == "direct" else 2)
+    yield request.param
+    L.hj_set_probe_mode(old)
+
+
 def gpu_join(dfp, bkeys, pkeys, bvalid=None, pvalid=None, key_type="int64", device_input=True, parts=None):
     """Build (optionally split into `parts` partitions) and probe on the GPU."""
     bk = np.asarray(bkeys)
@@ -64,7 +73,7 @@ def test_fixed_table_insert_previous_kat(dfp):
     assert got == [None, 1, None, 2, 4]
 
 
-def test_zero_and_extreme_keys(dfp, oracle_mod):
+def test_zero_and_extreme_keys(dfp, oracle_mod, probe_mode):
     """fixed_table.rs:1399-1409 (zero hash storable) + the sentinel-colliding key."""
     bk = np.array([0, I64_MIN, np.iinfo(np.int64).max, -1, 0, I64_MIN], dtype=np.int64)
     pk = np.array([I64_MIN, 0, 5, -1, np.iinfo(np.int64).max, I64_MIN], dtype=np.int64)
@@ -112,7 +121,7 @@ def test_chain_order_across_partitions_kat(dfp):
     (50000, 123457, 20000, 0.0, "int32"),
     (200000, 1000000, 400000, 0.01, "int64"),
 ])
-def test_random_parity(dfp, oracle_mod, nb, np_, krange, null_frac, key_type):
+def test_random_parity(dfp, oracle_mod, probe_mode, nb, np_, krange, null_frac, key_type):
     rng = np.random.default_rng(nb * 31 + np_)
     dt = np.int64 if key_type == "int64" else np.int32
     bk = rng.integers(-krange // 2, krange, nb).astype(dt)
@@ -133,7 +142,7 @@ def test_host_input_parity(dfp, oracle_mod):
     assert_same(b, p, ob, op)
 
 
-def test_multi_partition_canonical_numbering(dfp, oracle_mod):
+def test_multi_partition_canonical_numbering(dfp, oracle_mod, probe_mode):
     rng = np.random.default_rng(11)
     bk = rng.integers(0, 5000, 30000).astype(np.int64)
     pk = rng.integers(0, 9000, 40000).astype(np.int64)
@@ -144,7 +153,7 @@ def test_multi_partition_canonical_numbering(dfp, oracle_mod):
 
 
 @pytest.mark.parametrize("dups", [17, 300, 5000, 70000])
-def test_heavy_duplicates(dfp, oracle_mod, dups):
+def test_heavy_duplicates(dfp, oracle_mod, probe_mode, dups):
     """Segments > 16 rows (LDS sort) and > 4096 rows (ordered rescan)."""
     rng = np.random.default_rng(dups)
     hot = np.full(dups, 42, np.int64)
@@ -176,7 +185,7 @@ def test_chain_links_match_reference_semantics(dfp):
     assert np.array_equal(prev, want)
 
 
-def test_exponential_keys_parity(dfp, oracle_mod):
+def test_exponential_keys_parity(dfp, oracle_mod, probe_mode):
     """benches/exponential_distribution.rs key distribution (src/api_utils.rs:15-23)."""
     bk = oracle_mod.make_exponential_int_array(0, 200000).astype(np.int64)
     pk = oracle_mod.uniform_keys(500000, 0xC0FFEE, 200000)
