@@ -108,7 +108,7 @@ __device__ __forceinline__ T block_excl_scan(T v, T* s_w, T* total) {
 // ---------------------------------------------------------------------------
 // build 1: histogram of rows per (chunk, tile); chunk nchunks = side key INT64_MIN
 // ---------------------------------------------------------------------------
-constexpr int kHistThreads = 512;
+constexpr int kHistThreads = 1024;
 
 template <typename K>
 __global__ void __launch_bounds__(kHistThreads)
@@ -1105,7 +1105,10 @@ hipError_t launch_build(int key_bytes, const Segment* d_segs, int nseg, int64_t 
     // chunk build: LDS = bucket image + dup directory (3 u32 per entry)
     const uint32_t CB = 1u << clog2;
     const size_t img = (size_t)CB * sizeof(Bucket);
-    const size_t lds_cap = 160 * 1024 - 2048;  // leave room for the static LDS
+    // two workgroups per CU when the image is 64 KB (the duplicate directory takes the
+    // rest; a chunk with more duplicated keys than that makes the host rebuild at half
+    // load), one for 128 KB images
+    const size_t lds_cap = (CB <= 1024 ? 80 * 1024 : 160 * 1024) - 2048;
     uint32_t dupcap = (uint32_t)std::min<size_t>((size_t)CB * kSlots, (lds_cap - img) / 12);
     const size_t lds = img + (size_t)dupcap * 12;
     hipError_t e = hipFuncSetAttribute((const void*)chunk_build_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,

@@ -8,7 +8,7 @@
 namespace dfp {
 
 // ---- build ---------------------------------------------------------------
-constexpr int kBuildTile = 8192;     // build rows per histogram/scatter block
+constexpr int kBuildTile = 32768;    // build rows per histogram/scatter block
 constexpr int kMaxChunks = 16383;    // + side partition -> LDS histogram <= 64 KB
 
 int64_t build_tiles(int64_t total);
