@@ -243,13 +243,19 @@ def main():
     M = job.matches
     alg_bytes = 8 * P + 16 * B + 12 * M
     achieved = alg_bytes / (probe_ms / 1e3) / 1e9
-    traffic = load_traffic(args.config)
+    traffic = load_traffic(args.config) if not use_dist else None
     roofline = {
         "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
         "frac": round(achieved / HBM_PEAK_GBS, 4),
         "traffic": (traffic or {}).get("hbm_bytes_per_launch"),
-        "kernel": "probe_kernel<long>", "alg_bytes_per_launch": alg_bytes,
+        "traffic_lower": ((traffic or {}).get("probe_phase") or {}).get("hbm_bytes_lower"),
+        "kernel": "probe (probe_lookup_kernel + tile-count scan + probe_emit_kernel, one hj_probe_async)",
+        "alg_bytes_per_launch": alg_bytes,
         "alg_bytes_formula": "8*P + 16*B + 12*M (SURVEY.md §8d)",
+        # the lookup is one random 64-B bucket read per probe row; DESIGN.md §4 prices it
+        # against the measured random-line ceiling (profiles/r01_ubench_gather.txt)
+        "random_lines_per_s": round(P / (probe_ms / 1e3) / 1e9, 2),
+        "random_lines_unit": "G/s",
     }
 
     if rank == 0:

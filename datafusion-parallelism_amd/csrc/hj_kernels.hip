@@ -135,14 +135,15 @@ build_hist_kernel(const Segment* __restrict__ segs, int nseg, int64_t total, uin
 }
 
 // ---------------------------------------------------------------------------
-// exclusive scan of u32 (reduce-then-scan, three launches, no inter-block hand-off)
+// exclusive scan of u32 / u64 (reduce-then-scan, three launches, no inter-block hand-off)
 // ---------------------------------------------------------------------------
 constexpr int kScanThreads = 256;
 constexpr int kScanPerThread = 16;
 constexpr int kScanSeg = kScanThreads * kScanPerThread;
 
+template <typename T>
 __global__ void __launch_bounds__(kScanThreads)
-scan_reduce_kernel(const uint32_t* __restrict__ a, int64_t len, unsigned long long* __restrict__ bsum) {
+scan_reduce_kernel(const T* __restrict__ a, int64_t len, unsigned long long* __restrict__ bsum) {
     __shared__ unsigned long long s_w[kScanThreads / 64];
     const int64_t base = (int64_t)blockIdx.x * kScanSeg + (int64_t)threadIdx.x * kScanPerThread;
     unsigned long long s = 0;
@@ -178,22 +179,23 @@ scan_top_kernel(unsigned long long* bsum, int64_t nblk, unsigned long long* tota
     }
 }
 
+template <typename T>
 __global__ void __launch_bounds__(kScanThreads)
-scan_down_kernel(uint32_t* __restrict__ a, int64_t len, const unsigned long long* __restrict__ bsum) {
+scan_down_kernel(T* __restrict__ a, int64_t len, const unsigned long long* __restrict__ bsum) {
     __shared__ unsigned long long s_w[kScanThreads / 64];
     const int64_t base = (int64_t)blockIdx.x * kScanSeg + (int64_t)threadIdx.x * kScanPerThread;
-    uint32_t v[kScanPerThread];
+    T v[kScanPerThread];
     unsigned long long s = 0;
 #pragma unroll
     for (int k = 0; k < kScanPerThread; ++k) {
-        v[k] = (base + k < len) ? a[base + k] : 0u;
+        v[k] = (base + k < len) ? a[base + k] : (T)0;
         s += v[k];
     }
     unsigned long long tot;
     unsigned long long off = bsum[blockIdx.x] + block_excl_scan<unsigned long long>(s, s_w, &tot);
 #pragma unroll
     for (int k = 0; k < kScanPerThread; ++k) {
-        if (base + k < len) a[base + k] = (uint32_t)off;
+        if (base + k < len) a[base + k] = (T)off;
         off += v[k];
     }
 }
@@ -1070,13 +1072,16 @@ int64_t build_tiles(int64_t total) { return (total + kBuildTile - 1) / kBuildTil
 
 int64_t scan_scratch_bytes(int64_t len) { return 8 * ((len + kScanSeg - 1) / kScanSeg + 2); }
 
-static hipError_t launch_scan_u32(uint32_t* a, int64_t len, unsigned long long* bsum, unsigned long long* total,
-                                  hipStream_t s) {
+// in-place exclusive scan of a[0, len); bsum needs scan_scratch_bytes(len); the grand
+// total goes to a[len] only through *total (if non-null)
+template <typename T>
+static hipError_t launch_scan(T* a, int64_t len, unsigned long long* bsum, unsigned long long* total,
+                              hipStream_t s) {
     const int64_t nblk = (len + kScanSeg - 1) / kScanSeg;
     if (nblk == 0) return hipSuccess;
-    scan_reduce_kernel<<<(unsigned)nblk, kScanThreads, 0, s>>>(a, len, bsum);
+    scan_reduce_kernel<T><<<(unsigned)nblk, kScanThreads, 0, s>>>(a, len, bsum);
     scan_top_kernel<<<1, 1024, 0, s>>>(bsum, nblk, total);
-    scan_down_kernel<<<(unsigned)nblk, kScanThreads, 0, s>>>(a, len, bsum);
+    scan_down_kernel<T><<<(unsigned)nblk, kScanThreads, 0, s>>>(a, len, bsum);
     return hipGetLastError();
 }
 
@@ -1093,7 +1098,7 @@ hipError_t launch_build(int key_bytes, const Segment* d_segs, int nseg, int64_t 
         else
             build_hist_kernel<int32_t><<<(unsigned)ntiles, kHistThreads, hist_lds, s>>>(d_segs, nseg, total, nb, clog2,
                                                                                       nchunks, hist, ntiles);
-        hipError_t e = launch_scan_u32(hist, hlen, (unsigned long long*)scan_scratch, &ctr->n_valid, s);
+        hipError_t e = launch_scan(hist, hlen, (unsigned long long*)scan_scratch, &ctr->n_valid, s);
         if (e != hipSuccess) return e;
         if (key_bytes == 8)
             build_scatter_kernel<int64_t><<<(unsigned)ntiles, kHistThreads, hist_lds, s>>>(
@@ -1125,11 +1130,12 @@ hipError_t launch_build(int key_bytes, const Segment* d_segs, int nseg, int64_t 
 int64_t probe_tiles(int64_t n) { return (n + kProbeTile - 1) / kProbeTile; }
 
 // workspace layout (all regions 256-byte aligned):
-//   [0,16) header (bytes 8..15: error word) | tcnt u64[nt+2] | cnt2 u32[nt][256] |
+//   [0,16) header (bytes 8..15: error word) | tcnt u64[nt+2] | bsum (scan scratch) | cnt2 u32[nt][256] |
 //   toff u16[nt][257] | skeys u64[nt*4096] | perm u16[n] | info u32[nt*4096]
 namespace {
 struct ProbeWs {
     unsigned long long* tcnt;
+    unsigned long long* bsum;
     uint32_t* cnt2;
     uint16_t* toff;
     unsigned long long* skeys;
@@ -1144,6 +1150,7 @@ ProbeWs probe_ws_layout(void* base, int64_t n) {
     ProbeWs w;
     uintptr_t p = (uintptr_t)base + 256;
     w.tcnt = (unsigned long long*)p; p = al256(p + 8 * (nt + 2));
+    w.bsum = (unsigned long long*)p; p = al256(p + scan_scratch_bytes(nt));
     w.cnt2 = (uint32_t*)p;           p = al256(p + 4 * nt * (kMaxPieces + 1));
     w.toff = (uint16_t*)p;           p = al256(p + 2 * nt * (kMaxPieces + 2));
     w.skeys = (unsigned long long*)p; p = al256(p + 8 * rows);
@@ -1238,7 +1245,10 @@ hipError_t launch_probe(int key_bytes, const TableView& tv, const void* keys, co
         }
 #undef DFP_LOOKUP
     }
-    scan_top_kernel<<<1, 1024, 0, s>>>(w.tcnt, nt, (unsigned long long*)d_total);
+    {
+        hipError_t e = launch_scan<unsigned long long>(w.tcnt, nt, w.bsum, (unsigned long long*)d_total, s);
+        if (e != hipSuccess) return e;
+    }
 #define DFP_EMIT(SO, RI, PI)                                                                                          \
     probe_emit_kernel<SO, RI, PI><<<(unsigned)nt, kProbeThreads, 0, s>>>(tv, w.info, w.perm, probe_ids, n, w.tcnt, \
                                                                         out_b, out_p, cap)
@@ -1291,7 +1301,7 @@ hipError_t launch_radix_partition(int key_bytes, const void* keys, const uint8_t
         part_hist_kernel<int64_t><<<(unsigned)nblocks, kPartThreads, 0, s>>>(keys, valid, voff, n, nparts, hist, nblocks);
     else
         part_hist_kernel<int32_t><<<(unsigned)nblocks, kPartThreads, 0, s>>>(keys, valid, voff, n, nparts, hist, nblocks);
-    hipError_t e = launch_scan_u32(hist, hlen, scratch, nullptr, s);
+    hipError_t e = launch_scan(hist, hlen, scratch, nullptr, s);
     if (e != hipSuccess) return e;
     part_counts_kernel<<<1, 64, 0, s>>>(hist, nblocks, nparts, total, counts);
     if (key_bytes == 8)

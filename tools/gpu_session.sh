@@ -1,0 +1,39 @@
+#!/bin/bash
+# One GPU-box session: parity tests, the bench line, its rocprofv3 kernel-trace summary,
+# and HBM traffic counters (FETCH_SIZE and WRITE_SIZE in separate passes, MI355X_MICROARCH.md
+# "rocprofv3 PMC slots"), plus the gather microbenchmark under FETCH_SIZE to calibrate what
+# the counter reports for random 16-/64-byte line accesses.
+# usage: tools/gpu_session.sh TAG [tests|bench|prof|pmc|cal ...]   (default: all)
+set -o pipefail
+TAG=${1:-r01}; shift
+STEPS=${*:-tests bench prof pmc}
+export TMPDIR=/tmp
+O=gpurun_out/$TAG
+mkdir -p $O
+run() { echo "== $*" >&2; "$@"; }
+for s in $STEPS; do
+  case $s in
+    tests)
+      run timeout -k 10 900 python3 -m pytest tests -m gpu -x -q --timeout 300 > $O/tests.log 2>&1 || { tail -30 $O/tests.log; exit 1; }
+      tail -3 $O/tests.log ;;
+    bench)
+      run timeout -k 10 400 python3 bench.py > $O/bench.json 2> $O/bench.err || { tail -30 $O/bench.err; exit 1; }
+      cat $O/bench.json ;;
+    prof)
+      run timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/kt -o bench --output-format csv \
+        -- python3 bench.py > $O/prof_bench.json 2> $O/prof_bench.err || { tail -30 $O/prof_bench.err; exit 1; }
+      cat $O/prof_bench.json ;;
+    pmc)
+      for c in FETCH_SIZE WRITE_SIZE; do
+        run timeout -k 10 400 rocprofv3 --pmc $c -d $O/pmc_$c -o pmc --output-format csv \
+          -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline > $O/pmc_$c.json 2> $O/pmc_$c.err \
+          || { tail -30 $O/pmc_$c.err; exit 1; }
+      done ;;
+    cal)
+      run timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE -d $O/cal -o cal --output-format csv \
+        -- tools/ubench_gather > $O/cal.log 2> $O/cal.err || { tail -30 $O/cal.err; exit 1; }
+      cat $O/cal.log ;;
+    *) echo "unknown step $s"; exit 2 ;;
+  esac
+done
+echo "session $TAG done"

@@ -1,0 +1,83 @@
+#!/usr/bin/env python3
+"""Summarise rocprofv3 PMC passes (FETCH_SIZE, WRITE_SIZE; separate runs of
+`bench.py --steps 3 --warmup 1 --no-cpu-baseline`) into profiles/traffic_<config>.json.
+
+Units: both counters are KiB (WRITE_SIZE reproduces known write volumes exactly, e.g.
+gen_uniform_kernel's 800 MB). gfx950 correction (MI355X_MICROARCH.md, HBM section):
+FETCH_SIZE = TCC_EA0_RDREQ x 64 B and reports 1/2 of the bytes of wide streaming reads,
+so streamed bytes are FETCH_SIZE x 2. For random 64-byte bucket reads the calibration
+run (`ubench_gather` under --pmc FETCH_SIZE, profiles/r01_fetch_calibration.json)
+shows one RDREQ per random access; whether that request moves 64 or 128 bytes is not
+calibrated, so both bounds are reported and `hbm_bytes_per_launch` uses the doubled
+(upper) figure that the guide prescribes.
+
+usage: traffic_summary.py OUTDIR CONFIG   (OUTDIR holds pmc_FETCH_SIZE/ pmc_WRITE_SIZE/)
+"""
+import collections
+import csv
+import json
+import os
+import sys
+
+PROBE_KERNELS = ("probe_lookup_kernel", "probe_emit_kernel", "scan_reduce_kernel<unsigned long long>",
+                 "scan_down_kernel<unsigned long long>", "pp_partition_kernel", "pp_lookup_kernel",
+                 "pp_count_kernel")
+BUILD_KERNELS = ("build_hist_kernel", "scan_reduce_kernel<unsigned int>", "scan_down_kernel<unsigned int>",
+                 "build_scatter_kernel", "chunk_build_kernel", "dup_sort_big_kernel")
+
+
+def per_kernel(path):
+    d = collections.defaultdict(list)
+    for r in csv.DictReader(open(path)):
+        d[r["Kernel_Name"]].append(float(r["Counter_Value"]) * 1024.0)
+    return {k: sum(v) / len(v) for k, v in d.items()}, {k: len(v) for k, v in d.items()}
+
+
+def short(name):
+    return name.split("(")[0].replace("void ", "").replace("dfp::", "")
+
+
+def main():
+    out, cfg = sys.argv[1], sys.argv[2]
+    fetch, nf = per_kernel(os.path.join(out, "pmc_FETCH_SIZE", "pmc_counter_collection.csv"))
+    write, _ = per_kernel(os.path.join(out, "pmc_WRITE_SIZE", "pmc_counter_collection.csv"))
+    kernels = {}
+    for k in fetch:
+        kernels[short(k)] = {
+            "launches": nf[k],
+            "fetch_size_bytes_raw": round(fetch[k]),
+            "fetch_bytes_corrected_x2": round(2 * fetch[k]),
+            "write_size_bytes": round(write.get(k, 0.0)),
+        }
+
+    def phase(names):
+        sel = [v for k, v in kernels.items() if any(k.startswith(n) or n in k for n in names)]
+        raw = sum(v["fetch_size_bytes_raw"] for v in sel)
+        w = sum(v["write_size_bytes"] for v in sel)
+        return {"fetch_raw": raw, "fetch_x2": 2 * raw, "write": w,
+                "hbm_bytes_upper": 2 * raw + w, "hbm_bytes_lower": raw + w}
+
+    probe = phase(PROBE_KERNELS)
+    build = phase(BUILD_KERNELS)
+    res = {
+        "config": cfg,
+        "source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes) of "
+                  "`bench.py --steps 3 --warmup 1 --no-cpu-baseline`; per-launch averages",
+        "unit": "bytes",
+        "hbm_bytes_per_launch": probe["hbm_bytes_upper"],
+        "probe_phase": probe,
+        "build_phase": build,
+        "kernels": kernels,
+        "note": "probe phase = probe_lookup + tile-count scan + probe_emit (one hj_probe_async). "
+                "Upper = 2 x FETCH_SIZE + WRITE_SIZE (guide's gfx950 correction applied to all reads); "
+                "lower = FETCH_SIZE + WRITE_SIZE (random 64-B bucket reads counted at 64 B each).",
+    }
+    path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles",
+                        f"traffic_{cfg}.json")
+    with open(path, "w") as f:
+        json.dump(res, f, indent=1)
+    print(json.dumps({"probe": probe, "build": build}, indent=1))
+
+
+if __name__ == "__main__":
+    main()
