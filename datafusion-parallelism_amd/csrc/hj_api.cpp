@@ -178,10 +178,14 @@ bool is_device_ptr(const void* p) {
     return a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged;
 }
 
+// Slots per key. 0.35 measured best for the C2 probe on MI355X (fused probe 2048 us vs
+// 2150 us at 0.5, build unchanged; profiles/r01_load_factor.txt): fewer full buckets,
+// so fewer second bucket lines on the miss path. Override with DFP_HJ_LOAD_FACTOR.
+constexpr double kDefaultLoadFactor = 0.35;
 double load_factor() {
     const char* e = getenv("DFP_HJ_LOAD_FACTOR");
-    double lf = e ? atof(e) : 0.5;
-    if (!(lf > 0.05 && lf <= 0.95)) lf = 0.5;
+    double lf = e ? atof(e) : kDefaultLoadFactor;
+    if (!(lf > 0.05 && lf <= 0.95)) lf = kDefaultLoadFactor;
     return lf;
 }
 
@@ -429,7 +433,8 @@ hj_status probe_impl(const hj_table* t, const void* keys, const uint8_t* valid, 
                      int64_t* d_total, void* ws, hipStream_t s) {
     if (n < 0 || n > 0xFFFFFFFFll) return fail(HJ_ERR_INVALID, "probe batch must have < 2^32 rows");
     if (cap < 0) return fail(HJ_ERR_INVALID, "negative capacity");
-    HIP_TRY(hipMemsetAsync((char*)ws + 8, 0, 8, s));  // error word (reserved)
+    if (reinterpret_cast<uintptr_t>(ws) & 7) return fail(HJ_ERR_INVALID, "workspace must be 8-byte aligned");
+    HIP_TRY(hipMemsetAsync((char*)ws + 8, 0, 8, s));  // error word
     HIP_TRY(launch_probe(t->key_bytes, view_of(t), keys, valid, voff, probe_ids, n, out_b, out_p, cap, d_total, ws,
                          s));
     return HJ_OK;
@@ -612,7 +617,7 @@ int64_t hj_table_build_ns(const hj_table* t) {
 int64_t hj_probe_workspace_bytes(int64_t n) { return probe_workspace(n); }
 
 int hj_set_probe_mode(int mode) {
-    if (mode < 0 || mode > 2) return -1;
+    if (mode < 0 || mode > 3) return -1;
     const int old = get_probe_mode();
     set_probe_mode(mode);
     return old;
@@ -669,8 +674,14 @@ hj_status hj_probe(const hj_table* t, const void* keys, const uint8_t* validity,
         HIP_TRY(hipMalloc((void**)&ob, (size_t)cap * 8));
         HIP_TRY(hipMalloc((void**)&op, (size_t)cap * 4));
         if ((st = probe_impl(t, dk, dv, dvo, nullptr, n, ob, op, cap, d_total, ws, s)) != HJ_OK) break;
+        uint64_t werr = 0;
         HIP_TRY(hipMemcpyAsync(&total, d_total, 8, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipMemcpyAsync(&werr, (char*)ws + 8, 8, hipMemcpyDeviceToHost, s));
         HIP_TRY(hipStreamSynchronize(s));
+        if (werr != 0) {
+            st = fail(HJ_ERR_HIP, "probe: tile look-back gave up (results invalid)");
+            break;
+        }
         if (total <= cap) break;
         (void)hipFree(ob);
         (void)hipFree(op);

@@ -6,7 +6,9 @@
 //     uint64 key[5]   stored key = key ^ 2^63, 0 = empty slot
 //     uint32 ref[5]   bit 31 clear: the key's only build row
 //                     bit 31 set:   offset of its duplicate segment in dup_rows
-//     uint32 meta     (side bucket only: rows of the key INT64_MIN)
+//     uint32 meta     bit 0: an insert passed this bucket full (a lookup that misses
+//                     here continues to the next bucket only if set);
+//                     side bucket: rows of the key INT64_MIN
 //   A key's probe sequence stays inside its chunk of 2^clog2 buckets (linear probing
 //   modulo the chunk), so one workgroup can build a whole chunk in LDS.
 //   Bucket[nb] is the side bucket for INT64_MIN, whose stored form collides with

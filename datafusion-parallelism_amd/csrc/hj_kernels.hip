@@ -15,15 +15,16 @@
 //   probe   (replaces get_matching_indices, src/shared/shared.rs:29-47, the chain walk,
 //            src/operator/version10/lookup_implementation_3.rs:22-59, and
 //            equal_rows_arr, src/shared/datafusion_private.rs:40-80)
-//     probe_lookup_kernel   per probe row: hash, one 64-byte bucket line (exact key
-//                           compare, so no separate equality gather), 4-byte match ref,
-//                           per-tile match count
-//     probe_scan_kernel     tile counts -> output offsets, total
-//     probe_emit_kernel     ordered (probe asc, build desc) pair emission per tile
+//     probe_fused_kernel    (default) per probe row: hash, one 64-byte bucket line
+//                           (exact key compare, so no separate equality gather); the
+//                           tile's output offset by decoupled look-back; ordered
+//                           (probe asc, build desc) pair emission
+//     probe_lookup_kernel + scan + probe_emit_kernel: the same in two passes (4-byte
+//                           ref per row in between); partitioned variant pp_*
 //
 // No same-address global atomics on the hot loops (a single word sustains ~88
-// atomics/us, MI355X_MICROARCH.md "dequeue"), no inter-workgroup hand-offs inside a
-// launch: kernels communicate only through kernel boundaries.
+// atomics/us, MI355X_MICROARCH.md "dequeue"). The one inter-workgroup hand-off is the
+// fused probe's look-back (per-tile flags, each written by its own tile).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdlib.h>
@@ -268,6 +269,9 @@ __device__ __forceinline__ int chunk_slot(Bucket* img, uint32_t cmask, uint32_t 
             if (kk == sk || (INSERT && kk == 0)) return (int)(i * kSlots + j);
             if (!INSERT && kk == 0) return -1;
         }
+        // passing a full bucket: mark it, so that a lookup missing in a full bucket
+        // without the mark can stop there (meta bit 0 = "a probe sequence continues")
+        if (INSERT) atomicOr(&B.meta, 1u);
         i = (i + 1) & cmask;
     }
     return -1;
@@ -501,13 +505,20 @@ constexpr int kProbeTile = kProbeThreads * 4 * kGroups;   // 4096 probe rows per
 
 typedef long long v2i64 __attribute__((ext_vector_type(2)));
 
-template <typename K>
+template <typename K, bool NT = false>
 __device__ __forceinline__ void load4(const void* keys, int64_t row0, int64_t n, bool vec, int64_t (&k)[4]) {
     const K* kp = reinterpret_cast<const K*>(keys);
     if (vec && row0 + 4 <= n) {
         if constexpr (sizeof(K) == 8) {
             const v2i64* p = reinterpret_cast<const v2i64*>(kp + row0);
-            const v2i64 a = p[0], b = p[1];
+            v2i64 a, b;
+            if constexpr (NT) {
+                a = __builtin_nontemporal_load(p);
+                b = __builtin_nontemporal_load(p + 1);
+            } else {
+                a = p[0];
+                b = p[1];
+            }
             k[0] = a.x; k[1] = a.y; k[2] = b.x; k[3] = b.y;
         } else {
             const int4 a = *reinterpret_cast<const int4*>(kp + row0);
@@ -525,9 +536,10 @@ __device__ __forceinline__ uint32_t ref_count(const uint32_t* dup_rows, uint32_t
     return (ref & kDupFlag) ? dup_rows[ref & ~kDupFlag] : 1u;
 }
 
-// One bucket line: ref of `sk` if present, else kMiss; *more = the line is full and does
-// not hold the key (look at the next bucket of the chunk). Slots fill in order and are
-// never freed, so an empty slot ends a key's probe sequence. Branch-free.
+// One bucket line: ref of `sk` if present, else kMiss; *more = the line is full, does
+// not hold the key, and some insert passed it (meta bit 0): look at the next bucket of
+// the chunk. Slots fill in order and are never freed, so an empty slot ends a key's probe
+// sequence, and so does a full bucket that no insert ever passed. Branch-free.
 __device__ __forceinline__ uint32_t scan_line(const uint4& a0, const uint4& a1, const uint4& a2, const uint4& a3,
                                               unsigned long long sk, bool* more) {
     const unsigned long long k0 = ((unsigned long long)a0.y << 32) | a0.x;
@@ -542,8 +554,55 @@ __device__ __forceinline__ uint32_t scan_line(const uint4& a0, const uint4& a1, 
     ref = e2 ? a3.x : ref;
     ref = e1 ? a2.w : ref;
     ref = e0 ? a2.z : ref;
-    *more = (ref == kMiss) & !z;
+    *more = (ref == kMiss) & !z & ((a3.w & 1u) != 0);
     return ref;
+}
+
+// Refs of the four probe rows row0..row0+3 (kMiss: no match, null, or past n).
+template <typename K, bool HAS_VALID, bool NT = false>
+__device__ __forceinline__ void lookup4(const TableView& tv, const void* __restrict__ keys,
+                                        const uint8_t* __restrict__ valid, int64_t voff, int64_t n, bool vec,
+                                        int64_t row0, uint32_t (&ref)[4]) {
+    const Bucket* __restrict__ tbl = tv.tbl;
+    const uint32_t cmask = (1u << tv.clog2) - 1;
+    int64_t k[4];
+    load4<K, NT>(keys, row0, n, vec, k);
+    bool in[4];
+    unsigned long long sk[4];
+    uint32_t b[4];
+    uint4 L0[4], L1[4], L2[4], L3[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        in[q] = (row0 + q < n) && (!HAS_VALID || bit_valid(valid, voff, row0 + q));
+        sk[q] = (unsigned long long)k[q] ^ kSign;
+        b[q] = (in[q] && sk[q] != 0) ? home_bucket(k[q], tv.nb) : tv.nb;
+    }
+    // issue the 64-byte bucket line of all four rows before any compare (MLP)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const uint4* p = reinterpret_cast<const uint4*>(tbl + b[q]);
+        L0[q] = p[0]; L1[q] = p[1]; L2[q] = p[2]; L3[q] = p[3];
+    }
+    bool more[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        ref[q] = scan_line(L0[q], L1[q], L2[q], L3[q], sk[q], &more[q]);
+        if (sk[q] == 0) {  // INT64_MIN: the side bucket (ref[0] = word 10, meta = word 15)
+            ref[q] = L3[q].w ? L2[q].z : kMiss;
+            more[q] = false;
+        }
+        if (!in[q]) { ref[q] = kMiss; more[q] = false; }
+    }
+    // rare: the home line is full and does not hold the key
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        uint32_t bb = b[q];
+        for (uint32_t probes = 0; more[q] && probes < cmask; ++probes) {
+            bb = (bb & ~cmask) | ((bb + 1) & cmask);
+            const uint4* p = reinterpret_cast<const uint4*>(tbl + bb);
+            ref[q] = scan_line(p[0], p[1], p[2], p[3], sk[q], &more[q]);
+        }
+    }
 }
 
 template <typename K, bool HAS_VALID>
@@ -551,53 +610,14 @@ __global__ void __launch_bounds__(kProbeThreads)
 probe_lookup_kernel(TableView tv, const void* __restrict__ keys, const uint8_t* __restrict__ valid, int64_t voff,
                     int64_t n, bool vec, uint32_t* __restrict__ info, unsigned long long* __restrict__ tcnt) {
     __shared__ unsigned long long s_w[kProbeThreads / 64];
-    const Bucket* __restrict__ tbl = tv.tbl;
-    const uint32_t cmask = (1u << tv.clog2) - 1;
     unsigned long long tsum = 0;
     const int64_t tile0 = (int64_t)blockIdx.x * kProbeTile;
 #pragma unroll
     for (int g = 0; g < kGroups; ++g) {
         const int64_t row0 = tile0 + (int64_t)g * (kProbeThreads * 4) + (int64_t)threadIdx.x * 4;
         if (row0 >= n) break;
-        int64_t k[4];
-        load4<K>(keys, row0, n, vec, k);
-        bool in[4];
-        unsigned long long sk[4];
-        uint32_t b[4];
-        uint4 L0[4], L1[4], L2[4], L3[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            in[q] = (row0 + q < n) && (!HAS_VALID || bit_valid(valid, voff, row0 + q));
-            sk[q] = (unsigned long long)k[q] ^ kSign;
-            b[q] = (in[q] && sk[q] != 0) ? home_bucket(k[q], tv.nb) : tv.nb;
-        }
-        // issue the 64-byte bucket line of all four rows before any compare (MLP)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const uint4* p = reinterpret_cast<const uint4*>(tbl + b[q]);
-            L0[q] = p[0]; L1[q] = p[1]; L2[q] = p[2]; L3[q] = p[3];
-        }
         uint32_t ref[4];
-        bool more[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            ref[q] = scan_line(L0[q], L1[q], L2[q], L3[q], sk[q], &more[q]);
-            if (sk[q] == 0) {  // INT64_MIN: the side bucket (ref[0] = word 10, meta = word 15)
-                ref[q] = L3[q].w ? L2[q].z : kMiss;
-                more[q] = false;
-            }
-            if (!in[q]) { ref[q] = kMiss; more[q] = false; }
-        }
-        // rare: the home line is full and does not hold the key
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            uint32_t bb = b[q];
-            for (uint32_t probes = 0; more[q] && probes < cmask; ++probes) {
-                bb = (bb & ~cmask) | ((bb + 1) & cmask);
-                const uint4* p = reinterpret_cast<const uint4*>(tbl + bb);
-                ref[q] = scan_line(p[0], p[1], p[2], p[3], sk[q], &more[q]);
-            }
-        }
+        lookup4<K, HAS_VALID>(tv, keys, valid, voff, n, vec, row0, ref);
 #pragma unroll
         for (int q = 0; q < 4; ++q) tsum += ref_count(tv.dup_rows, ref[q]);
         if (vec && row0 + 4 <= n) {
@@ -611,6 +631,215 @@ probe_lookup_kernel(TableView tv, const void* __restrict__ keys, const uint8_t* 
     unsigned long long tot;
     block_excl_scan<unsigned long long>(tsum, s_w, &tot);
     if (threadIdx.x == 0) tcnt[blockIdx.x] = tot;
+}
+
+// Writes the pairs of four probe rows starting at output position `pos` (canonical:
+// rows ascending, each row's build rows descending = the order of its dup segment).
+template <bool HAS_ROW_IDS, bool HAS_PROBE_IDS>
+__device__ __forceinline__ void emit4(const TableView& tv, const uint32_t* __restrict__ probe_ids, int64_t row0,
+                                      const uint32_t (&ref)[4], const uint32_t (&cnt)[4], unsigned long long pos,
+                                      uint64_t* __restrict__ out_b, uint32_t* __restrict__ out_p, int64_t cap) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const uint32_t c = cnt[q];
+        if (c == 0) continue;
+        const int64_t prow = row0 + q;
+        const uint32_t pidx = HAS_PROBE_IDS ? probe_ids[prow] : (uint32_t)prow;
+        const uint32_t r = ref[q];
+        if (c == 1) {
+            if (pos < (unsigned long long)cap) {
+                const uint32_t br = (r & kDupFlag) ? tv.dup_rows[(r & ~kDupFlag) + 1] : r;
+                out_b[pos] = HAS_ROW_IDS ? tv.row_ids[br] : (uint64_t)br;
+                out_p[pos] = pidx;
+            }
+        } else {
+            const uint32_t* seg = tv.dup_rows + (r & ~kDupFlag) + 1;
+            for (uint32_t t = 0; t < c; ++t) {
+                if (pos + t < (unsigned long long)cap) {
+                    const uint32_t br = seg[t];
+                    out_b[pos + t] = HAS_ROW_IDS ? tv.row_ids[br] : (uint64_t)br;
+                    out_p[pos + t] = pidx;
+                }
+            }
+        }
+        pos += c;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// fused probe (default): lookup + ordered emission in one launch. A tile's output
+// offset comes from a decoupled look-back over the per-tile flags in blockIdx order:
+// flag = status (2 bits: 1 aggregate, 2 inclusive prefix) | 62-bit value. Workgroups
+// are dispatched in blockIdx order on every XCD, so the lowest unfinished tile is
+// always resident and the look-back makes progress; the spin is still bounded and a
+// give-up raises the workspace error word instead of hanging. No ticket atomics: the
+// flags are written once each, by their own tile.
+// ---------------------------------------------------------------------------
+constexpr unsigned long long kFlagAgg = 1ull << 62;
+constexpr unsigned long long kFlagIncl = 2ull << 62;
+constexpr unsigned long long kFlagVal = (1ull << 62) - 1;
+constexpr unsigned kLookbackSpinLimit = 1u << 22;
+constexpr int kStage = 2048;          // pairs per LDS emission window (16 KB + the 16 KB s_ref)
+constexpr int kStageMaxWindows = 8;   // beyond this a group's pairs are stored directly
+
+__device__ __forceinline__ unsigned long long flag_load(const unsigned long long* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void flag_store(unsigned long long* p, unsigned long long v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// wave 0 of tile t: exclusive prefix of the tile counts before t (t > 0)
+__device__ unsigned long long lookback(unsigned long long* flags, int64_t t, unsigned long long* err) {
+    const int lane = threadIdx.x & 63;
+    unsigned long long excl = 0;
+    int64_t j = t - 1;
+    unsigned spins = 0;
+    while (true) {
+        const int64_t idx = j - lane;
+        const unsigned long long f = idx >= 0 ? flag_load(flags + idx) : kFlagIncl;
+        const unsigned long long st = f >> 62;
+        const unsigned long long incl_mask = __ballot(st == 2);
+        const unsigned long long zero_mask = __ballot(st == 0);
+        const int first = incl_mask ? __ffsll((long long)incl_mask) - 1 : 63;
+        const unsigned long long need = (2ull << first) - 1;  // lanes 0..first (first = 63: all)
+        if (zero_mask & need) {
+            if (++spins > kLookbackSpinLimit) {  // never expected: report, do not hang
+                if (lane == 0) atomicOr(err, 1ull);
+                return excl;
+            }
+            __builtin_amdgcn_s_sleep(1);
+            continue;
+        }
+        excl += wave_sum<unsigned long long>(lane <= first ? (f & kFlagVal) : 0ull);
+        if (incl_mask) return excl;
+        j -= 64;
+    }
+}
+
+template <typename K, bool HAS_VALID, bool HAS_ROW_IDS, bool HAS_PROBE_IDS>
+__global__ void __launch_bounds__(kProbeThreads)
+probe_fused_kernel(TableView tv, const void* __restrict__ keys, const uint8_t* __restrict__ valid, int64_t voff,
+                   const uint32_t* __restrict__ probe_ids, int64_t n, bool vec, unsigned long long* flags,
+                   unsigned long long* err, uint64_t* __restrict__ out_b, uint32_t* __restrict__ out_p,
+                   int64_t cap, int64_t* __restrict__ d_total, int nt) {
+    // the tile's refs wait in LDS across the look-back (registers stay free for the
+    // lookups' line loads: occupancy is what keeps enough random reads in flight)
+    __shared__ __attribute__((aligned(16))) uint32_t s_ref[kProbeTile];
+    __shared__ uint64_t s_b[kStage];
+    __shared__ unsigned long long s_w[kGroups][kProbeThreads / 64];
+    __shared__ unsigned long long s_excl;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int64_t tile0 = (int64_t)blockIdx.x * kProbeTile;
+#pragma unroll
+    for (int g = 0; g < kGroups; ++g) {
+        const int64_t row0 = tile0 + (int64_t)g * (kProbeThreads * 4) + (int64_t)threadIdx.x * 4;
+        uint32_t ref[4] = {kMiss, kMiss, kMiss, kMiss};
+        if (row0 < n) {
+            if (nt & 1) lookup4<K, HAS_VALID, true>(tv, keys, valid, voff, n, vec, row0, ref);
+            else lookup4<K, HAS_VALID, false>(tv, keys, valid, voff, n, vec, row0, ref);
+        }
+        *reinterpret_cast<uint4*>(s_ref + g * (kProbeThreads * 4) + threadIdx.x * 4) =
+            make_uint4(ref[0], ref[1], ref[2], ref[3]);
+        unsigned long long s = 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) s += ref_count(tv.dup_rows, ref[q]);
+        const unsigned long long ws = wave_sum<unsigned long long>(s);
+        if (lane == 0) s_w[g][wave] = ws;
+    }
+    __syncthreads();
+    if (wave == 0) {
+        unsigned long long tile_total = 0;
+#pragma unroll
+        for (int g = 0; g < kGroups; ++g)
+            for (int w = 0; w < kProbeThreads / 64; ++w) tile_total += s_w[g][w];
+        unsigned long long excl = 0;
+        if (blockIdx.x == 0) {
+            if (lane == 0) flag_store(flags, kFlagIncl | tile_total);
+        } else {
+            if (lane == 0) flag_store(flags + blockIdx.x, kFlagAgg | tile_total);
+            excl = lookback(flags, blockIdx.x, err);
+            if (lane == 0) flag_store(flags + blockIdx.x, kFlagIncl | (excl + tile_total));
+        }
+        if (lane == 0) {
+            s_excl = excl;
+            if (blockIdx.x == gridDim.x - 1) *d_total = (int64_t)(excl + tile_total);
+        }
+    }
+    __syncthreads();
+    // emission, staged through LDS per group of 1024 rows: each thread drops its pairs
+    // into the window [w0, w0 + kStage) of the group's output, then the block copies the
+    // window out contiguously (whole lines, no partial-line stores left to merge in an
+    // L2 that the random bucket reads keep evicting). Groups with more than
+    // kStageMaxWindows windows of output (heavy duplicates) store directly.
+    uint32_t ref[kGroups][4];
+#pragma unroll
+    for (int g = 0; g < kGroups; ++g) {
+        const uint4 r4 = *reinterpret_cast<const uint4*>(s_ref + g * (kProbeThreads * 4) + threadIdx.x * 4);
+        ref[g][0] = r4.x; ref[g][1] = r4.y; ref[g][2] = r4.z; ref[g][3] = r4.w;
+    }
+    __syncthreads();  // s_ref is reused as the probe-index half of the staging window
+    uint32_t* s_p = s_ref;
+    unsigned long long gbase = s_excl;
+#pragma unroll
+    for (int g = 0; g < kGroups; ++g) {
+        const int64_t row0 = tile0 + (int64_t)g * (kProbeThreads * 4) + (int64_t)threadIdx.x * 4;
+        uint32_t cnt[4];
+        unsigned long long c_sum = 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            cnt[q] = ref_count(tv.dup_rows, ref[g][q]);
+            c_sum += cnt[q];
+        }
+        unsigned long long lpos = wave_incl_scan<unsigned long long>(c_sum) - c_sum;  // inside the group
+        unsigned long long gt = 0;
+        for (int w = 0; w < kProbeThreads / 64; ++w) {
+            if (w < wave) lpos += s_w[g][w];
+            gt += s_w[g][w];
+        }
+        if (gt > (unsigned long long)kStage * kStageMaxWindows) {
+            if (row0 < n)
+                emit4<HAS_ROW_IDS, HAS_PROBE_IDS>(tv, probe_ids, row0, ref[g], cnt, gbase + lpos, out_b, out_p, cap);
+        } else {
+            for (unsigned long long w0 = 0; w0 < gt; w0 += kStage) {
+                const unsigned long long w1 = w0 + kStage;
+                unsigned long long p = lpos;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const uint32_t c = cnt[q];
+                    const unsigned long long a = p > w0 ? p : w0;
+                    const unsigned long long b = (p + c) < w1 ? (p + c) : w1;
+                    if (a < b) {
+                        const uint32_t r = ref[g][q];
+                        const uint32_t pidx = HAS_PROBE_IDS ? probe_ids[row0 + q] : (uint32_t)(row0 + q);
+                        const uint32_t* seg = (r & kDupFlag) ? tv.dup_rows + (r & ~kDupFlag) + 1 : nullptr;
+                        for (unsigned long long t = a; t < b; ++t) {
+                            const uint32_t br = seg ? seg[t - p] : r;
+                            s_b[t - w0] = HAS_ROW_IDS ? tv.row_ids[br] : (uint64_t)br;
+                            s_p[t - w0] = pidx;
+                        }
+                    }
+                    p += c;
+                }
+                __syncthreads();
+                const unsigned long long len = (gt - w0) < (unsigned long long)kStage ? (gt - w0) : kStage;
+                const unsigned long long o = gbase + w0;
+                for (unsigned i = threadIdx.x; i < len; i += kProbeThreads) {
+                    if (o + i < (unsigned long long)cap) {
+                        if (nt & 2) {
+                            __builtin_nontemporal_store(s_b[i], out_b + o + i);
+                            __builtin_nontemporal_store(s_p[i], out_p + o + i);
+                        } else {
+                            out_b[o + i] = s_b[i];
+                            out_p[o + i] = s_p[i];
+                        }
+                    }
+                }
+                __syncthreads();
+            }
+        }
+        gbase += gt;
+    }
 }
 
 // SORTED: `info` holds each tile's refs in the tile's partition-sorted order (the
@@ -675,31 +904,7 @@ probe_emit_kernel(TableView tv, const uint32_t* __restrict__ info, const uint16_
             gbase += s_w[g][w];
         }
         const int64_t row0 = tile0 + (int64_t)g * (kProbeThreads * 4) + (int64_t)threadIdx.x * 4;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const uint32_t c = cnt[g][q];
-            if (c == 0) continue;
-            const int64_t prow = row0 + q;
-            const uint32_t pidx = HAS_PROBE_IDS ? probe_ids[prow] : (uint32_t)prow;
-            const uint32_t r = ref[g][q];
-            if (c == 1) {
-                if (pos < (unsigned long long)cap) {
-                    const uint32_t br = (r & kDupFlag) ? tv.dup_rows[(r & ~kDupFlag) + 1] : r;
-                    out_b[pos] = HAS_ROW_IDS ? tv.row_ids[br] : (uint64_t)br;
-                    out_p[pos] = pidx;
-                }
-            } else {
-                const uint32_t* seg = tv.dup_rows + (r & ~kDupFlag) + 1;
-                for (uint32_t t = 0; t < c; ++t) {
-                    if (pos + t < (unsigned long long)cap) {
-                        const uint32_t br = seg[t];
-                        out_b[pos + t] = HAS_ROW_IDS ? tv.row_ids[br] : (uint64_t)br;
-                        out_p[pos + t] = pidx;
-                    }
-                }
-            }
-            pos += c;
-        }
+        emit4<HAS_ROW_IDS, HAS_PROBE_IDS>(tv, probe_ids, row0, ref[g], cnt[g], pos, out_b, out_p, cap);
     }
 }
 
@@ -1160,11 +1365,12 @@ ProbeWs probe_ws_layout(void* base, int64_t n) {
     return w;
 }
 
-int env_probe_mode() {  // 0 auto, 1 direct, 2 partitioned
+int env_probe_mode() {  // 0 auto, 1 two-pass direct, 2 partitioned, 3 fused
     const char* e = getenv("DFP_HJ_PROBE_MODE");
     if (!e) return 0;
-    if (e[0] == 'd') return 1;
+    if (e[0] == 'd' || e[0] == 't') return 1;
     if (e[0] == 'p') return 2;
+    if (e[0] == 'f') return 3;
     return 0;
 }
 std::atomic<int> g_probe_mode{-1};
@@ -1178,7 +1384,7 @@ int probe_mode() {
 }
 }  // namespace
 
-void set_probe_mode(int mode) { g_probe_mode.store(mode < 0 || mode > 2 ? 0 : mode, std::memory_order_relaxed); }
+void set_probe_mode(int mode) { g_probe_mode.store(mode < 0 || mode > 3 ? 0 : mode, std::memory_order_relaxed); }
 int get_probe_mode() { return probe_mode(); }
 
 int64_t probe_workspace(int64_t n) { return probe_ws_layout(nullptr, n).bytes; }
@@ -1197,6 +1403,36 @@ hipError_t launch_probe(int key_bytes, const TableView& tv, const void* keys, co
     // more than it saves at C2 (profiles/r01_*). DESIGN.md §5.
     const int mode = probe_mode();
     const bool part = mode == 2;
+    if (mode == 0 || mode == 3) {
+        static const int fused_nt = [] {  // 1: keys nontemporal, 2: pair stores nontemporal
+            const char* e = getenv("DFP_HJ_NT");
+            return e ? atoi(e) : 0;
+        }();
+        // fused lookup + emission; tile flags live in the tile-count region
+        hipError_t e = hipMemsetAsync(w.tcnt, 0, sizeof(unsigned long long) * nt, s);
+        if (e != hipSuccess) return e;
+        unsigned long long* err = reinterpret_cast<unsigned long long*>((char*)workspace + 8);
+        const bool ri = tv.row_ids != nullptr, pi = probe_ids != nullptr;
+#define DFP_FUSED(KT, HV, RI, PI)                                                                             \
+    probe_fused_kernel<KT, HV, RI, PI><<<(unsigned)nt, kProbeThreads, 0, s>>>(tv, keys, valid, voff, probe_ids, n, \
+                                                                             vec, w.tcnt, err, out_b, out_p, cap, \
+                                                                             d_total, fused_nt)
+#define DFP_FUSED_K(KT, HV)                              \
+    do {                                                 \
+        if (ri && pi) DFP_FUSED(KT, HV, true, true);     \
+        else if (ri) DFP_FUSED(KT, HV, true, false);     \
+        else if (pi) DFP_FUSED(KT, HV, false, true);     \
+        else DFP_FUSED(KT, HV, false, false);            \
+    } while (0)
+        if (key_bytes == 8) {
+            if (valid) DFP_FUSED_K(int64_t, true); else DFP_FUSED_K(int64_t, false);
+        } else {
+            if (valid) DFP_FUSED_K(int32_t, true); else DFP_FUSED_K(int32_t, false);
+        }
+#undef DFP_FUSED_K
+#undef DFP_FUSED
+        return hipGetLastError();
+    }
     if (part) {
         const uint32_t chunk_bytes = (1u << tv.clog2) * (uint32_t)sizeof(Bucket);
         const uint32_t nchunks = tv.nb >> tv.clog2;

@@ -149,9 +149,10 @@ void hj_pairs_free(hj_pairs* p);
 
 /* Asynchronous probe into caller buffers (device memory), on `stream`.
  * Writes min(total, capacity) pairs and the total to *d_total (device int64).
- * `workspace` (device, hj_probe_workspace_bytes(n) bytes) must not be shared by
- * concurrent calls; its bytes 8..15 (uint64) are non-zero after the call if a bounded
- * spin gave up (results invalid). No host synchronisation, no allocation. */
+ * `workspace` (device, 8-byte aligned, hj_probe_workspace_bytes(n) bytes) must not be
+ * shared by concurrent calls; its bytes 8..15 (uint64) are non-zero after the call if
+ * the fused probe's bounded look-back spin gave up (results invalid; never observed).
+ * No host synchronisation, no allocation. */
 int64_t hj_probe_workspace_bytes(int64_t n);
 hj_status hj_probe_async(const hj_table* t, const void* keys, const uint8_t* validity,
                          int64_t validity_offset, int64_t n, uint64_t* out_build,
@@ -165,10 +166,12 @@ hj_status hj_probe_async_ids(const hj_table* t, const void* keys, const uint8_t*
                              uint64_t* out_build, uint32_t* out_probe, int64_t capacity,
                              int64_t* d_total, void* workspace, void* stream);
 
-/* Probe strategy for later probes of this process: 0 auto (= direct), 1 direct
- * (lookup per row in row order), 2 partitioned (rows grouped by table piece inside each
- * tile, pieces looked up L2-resident per XCD). Results are identical; returns the
- * previous mode, -1 for a bad value. Also settable with DFP_HJ_PROBE_MODE. */
+/* Probe strategy for later probes of this process: 0 auto (= fused), 1 two-pass direct
+ * (lookup kernel writes a 4-byte ref per row, then ordered emission), 2 partitioned
+ * (rows grouped by table piece inside each tile, pieces looked up L2-resident per XCD),
+ * 3 fused (lookup + emission in one launch, tile offsets by decoupled look-back).
+ * Results are identical; returns the previous mode, -1 for a bad value. Also settable
+ * with DFP_HJ_PROBE_MODE=fused|two-pass|partitioned. */
 int hj_set_probe_mode(int mode);
 
 /* Makes `stream` wait for the build of `t` (for probes on other streams). */

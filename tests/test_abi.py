@@ -96,3 +96,16 @@ def test_product_path_does_not_import_the_oracle():
             if f.endswith((".py", ".cpp", ".hip", ".h")):
                 src = open(os.path.join(dirpath, f)).read()
                 assert "import oracle" not in src and "hj_oracle" not in src and "ora_" not in src, f
+
+
+def test_probe_mode_switch(dfp):
+    """hj_set_probe_mode: 0 auto (fused), 1 two-pass, 2 partitioned, 3 fused; bad -> -1.
+    No device work."""
+    from datafusion_parallelism_amd import _lib
+
+    L = _lib.load()
+    assert L.hj_set_probe_mode(4) == -1
+    assert L.hj_set_probe_mode(-1) == -1
+    old = L.hj_set_probe_mode(3)
+    assert L.hj_set_probe_mode(1) == 3
+    assert L.hj_set_probe_mode(old) == 1

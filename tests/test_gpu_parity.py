@@ -13,11 +13,14 @@ pytestmark = pytest.mark.gpu
 I64_MIN = np.iinfo(np.int64).min
 
 
-@pytest.fixture(params=["direct", "partitioned"])
+MODES = {"fused": 3, "two-pass": 1, "partitioned": 2}
+
+
+@pytest.fixture(params=list(MODES))
 def probe_mode(request, dfp):
-    """Run a test under both probe strategies (identical results required)."""
+    """Run a test under every probe strategy (identical results required)."""
     L = dfp.load()
-    old = L.hj_set_probe_mode(1 if request.param == "direct" else 2)
+    old = L.hj_set_probe_mode(MODES[request.param])
     yield request.param
     L.hj_set_probe_mode(old)
 

@@ -33,6 +33,31 @@ for s in $STEPS; do
       run timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE -d $O/cal -o cal --output-format csv \
         -- tools/ubench_gather > $O/cal.log 2> $O/cal.err || { tail -30 $O/cal.err; exit 1; }
       cat $O/cal.log ;;
+    modes)
+      # probe strategies side by side: one build + 5 probes each, kernel trace
+      for m in fused two-pass partitioned; do
+        export DFP_HJ_PROBE_MODE=$m
+        run timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/mode_$m -o m \
+          --output-format csv -- python3 tools/probe_one.py > $O/mode_$m.log 2>&1 || { tail -30 $O/mode_$m.log; exit 1; }
+        unset DFP_HJ_PROBE_MODE
+        tail -1 $O/mode_$m.log
+      done ;;
+    nt)
+      # fused probe with nontemporal key loads (1) / pair stores (2)
+      for v in 0 1 2 3; do
+        export DFP_HJ_NT=$v
+        run timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/nt_$v -o m \
+          --output-format csv -- python3 tools/probe_one.py > $O/nt_$v.log 2>&1 || { tail -30 $O/nt_$v.log; exit 1; }
+        unset DFP_HJ_NT
+      done ;;
+    lf)
+      # table load factor vs build / probe time
+      for v in ${LFS:-0.35 0.42 0.5}; do
+        export DFP_HJ_LOAD_FACTOR=$v
+        run timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/lf_$v -o m \
+          --output-format csv -- python3 tools/probe_one.py > $O/lf_$v.log 2>&1 || { tail -30 $O/lf_$v.log; exit 1; }
+        unset DFP_HJ_LOAD_FACTOR
+      done ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
