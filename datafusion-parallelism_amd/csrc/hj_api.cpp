@@ -293,8 +293,8 @@ hj_status build_attempt(hj_table* t, const std::vector<Segment>& segs, double lf
         t->row_ids = (uint64_t*)p;
     }
     Segment* d_segs;
-    uint32_t *hist, *srows;
-    unsigned long long* skeys;
+    uint32_t *hist, *hist1, *srows, *trows;
+    unsigned long long *skeys, *tkeys;
     BigSeg* big;
     BuildCounters* ctr;
     void* scan;
@@ -302,12 +302,22 @@ hj_status build_attempt(hj_table* t, const std::vector<Segment>& segs, double lf
     d_segs = (Segment*)p;
     if ((st = dev_alloc(t, t->scratch, &p, sizeof(uint32_t) * (size_t)std::max<int64_t>(hlen, 1))) != HJ_OK) return st;
     hist = (uint32_t*)p;
-    if ((st = dev_alloc(t, t->scratch, &p, (size_t)scan_scratch_bytes(hlen))) != HJ_OK) return st;
+    if ((st = dev_alloc(t, t->scratch, &p, sizeof(uint32_t) * (size_t)std::max<int64_t>(kCoarseBins * ntiles, 1))) !=
+        HJ_OK)
+        return st;
+    hist1 = (uint32_t*)p;
+    if ((st = dev_alloc(t, t->scratch, &p, (size_t)scan_scratch_bytes(std::max<int64_t>(hlen, kCoarseBins * ntiles)))) !=
+        HJ_OK)
+        return st;
     scan = p;
     if ((st = dev_alloc(t, t->scratch, &p, 8 * (size_t)std::max<int64_t>(total, 1))) != HJ_OK) return st;
     skeys = (unsigned long long*)p;
     if ((st = dev_alloc(t, t->scratch, &p, 4 * (size_t)std::max<int64_t>(total, 1))) != HJ_OK) return st;
     srows = (uint32_t*)p;
+    if ((st = dev_alloc(t, t->scratch, &p, 8 * (size_t)std::max<int64_t>(total, 1))) != HJ_OK) return st;
+    tkeys = (unsigned long long*)p;
+    if ((st = dev_alloc(t, t->scratch, &p, 4 * (size_t)std::max<int64_t>(total, 1))) != HJ_OK) return st;
+    trows = (uint32_t*)p;
     if ((st = dev_alloc(t, t->scratch, &p, sizeof(BigSeg) * (size_t)(total / (kSmallSeg + 1) + 2))) != HJ_OK)
         return st;
     big = (BigSeg*)p;
@@ -321,8 +331,8 @@ hj_status build_attempt(hj_table* t, const std::vector<Segment>& segs, double lf
     if (total == 0) HIP_TRY(hipMemsetAsync(t->tbl, 0, (size_t)(t->nb + 1) * sizeof(Bucket), s));
     hipDeviceProp_t* prop = device_props(t->device);
     const int cus = prop ? prop->multiProcessorCount : 256;
-    HIP_TRY(launch_build(t->key_bytes, d_segs, (int)segs.size(), total, t->nb, t->clog2, t->nchunks, hist, ntiles,
-                         scan, skeys, srows, t->row_ids, t->tbl, t->dup_rows, big, ctr, cus, s));
+    HIP_TRY(launch_build(t->key_bytes, d_segs, (int)segs.size(), total, t->nb, t->clog2, t->nchunks, hist, hist1,
+                         ntiles, scan, tkeys, trows, skeys, srows, t->row_ids, t->tbl, t->dup_rows, big, ctr, cus, s));
     BuildCounters hc;
     HIP_TRY(hipMemcpyAsync(&hc, ctr, sizeof(hc), hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));

@@ -5,9 +5,9 @@
 //            fixed_table.rs:560-672, driven by JoinStateInstance::add,
 //            src/operator/version10/parallel_join_execution_state.rs:91-133, and the
 //            overflow-chain compaction of the same file, 135-315)
-//     build_hist_kernel     rows per (table chunk, row tile), LDS histogram
-//     scan_*_kernel         exclusive scan of the histogram (reduce-then-scan)
-//     build_scatter_kernel  partition (key, row) by chunk (stable per tile offsets)
+//     coarse_hist/scatter   level 1: rows -> groups of 2^gshift chunks (<= 128 groups)
+//     fine_hist/scatter     level 2: group-ordered rows -> chunk order
+//     scan_*_kernel         exclusive scans of the histograms (reduce-then-scan)
 //     chunk_build_kernel    one workgroup per 2^clog2-bucket chunk: insert with LDS
 //                           64-bit CAS + LDS counts, lay out duplicate segments, write
 //                           the finished chunk out with coalesced 16-byte stores
@@ -107,32 +107,153 @@ __device__ __forceinline__ T block_excl_scan(T v, T* s_w, T* total) {
 }
 
 // ---------------------------------------------------------------------------
-// build 1: histogram of rows per (chunk, tile); chunk nchunks = side key INT64_MIN
+// build 1: rows -> chunk order in two partition levels. A 32 K-row tile spread over all
+// ~5600 chunks of a C2 table leaves ~6 rows per chunk, i.e. partial-line stores (the
+// one-level scatter wrote 4.9x its algorithmic bytes). Level 1 splits rows into <= 128
+// groups of 2^gshift consecutive chunks (~250-500 rows per group per tile); level 2 then
+// sorts the group-ordered rows by chunk, where each tile spans only a group or two, so
+// both levels write long runs.
 // ---------------------------------------------------------------------------
 constexpr int kHistThreads = 1024;
 
+__device__ __forceinline__ uint32_t chunk_of(int64_t key, uint32_t nb, uint32_t clog2, uint32_t nchunks) {
+    return ((uint64_t)key ^ kSign) == 0 ? nchunks : (home_bucket(key, nb) >> clog2);
+}
+
+// The segment descriptors of one tile's rows in LDS (per-row lookups in global memory
+// form a dependent load chain). Returns the descriptor array to use (LDS, or the
+// global one for a tile made of more than kTileSegs appends) and its count.
+constexpr int kTileSegs = 64;
+__device__ __forceinline__ const Segment* tile_segments(const Segment* __restrict__ segs, int nseg, int64_t r0,
+                                                        int64_t r1, Segment* s_seg, int* s_info, int* ns) {
+    if (threadIdx.x == 0) {
+        const int a = find_seg(segs, nseg, r0);
+        const int b = r1 > r0 ? find_seg(segs, nseg, r1 - 1) : a;
+        s_info[0] = a;
+        s_info[1] = b - a + 1;
+    }
+    __syncthreads();
+    const int a = s_info[0], cnt = s_info[1];
+    if (cnt > kTileSegs) {
+        *ns = nseg;
+        return segs;
+    }
+    for (int k = threadIdx.x; k < cnt; k += blockDim.x) s_seg[k] = segs[a + k];
+    __syncthreads();
+    *ns = cnt;
+    return s_seg;
+}
+
+// Rows base + u * kHistThreads + threadIdx.x (u < kRowBatch) of the appended build input,
+// all loads issued before any use (the tile loops are latency-bound otherwise). ok[u]:
+// row exists and is valid. With ids/row_ids, copies the explicit ids to row_ids[r].
+constexpr int kRowBatch = 8;
+template <typename K>
+__device__ __forceinline__ void load_rows(const Segment* __restrict__ segs, int nseg, int64_t base, int64_t r1,
+                                          int64_t (&key)[kRowBatch], bool (&ok)[kRowBatch],
+                                          uint64_t* __restrict__ row_ids, int64_t* rows) {
+    if (nseg == 1) {  // the whole tile inside one append: uniform pointers, loads batch up
+        const Segment sg = segs[0];
+#pragma unroll
+        for (int u = 0; u < kRowBatch; ++u) {
+            const int64_t r = base + (int64_t)u * kHistThreads + threadIdx.x;
+            if (rows) rows[u] = r;
+            ok[u] = r < r1;
+            key[u] = 0;
+            if (ok[u]) {
+                const int64_t i = r - sg.row_base;
+                if (row_ids != nullptr && sg.ids != nullptr) row_ids[r] = sg.ids[i];
+                ok[u] = bit_valid(sg.valid, sg.voff, i);
+                key[u] = ld_key<K>(sg.keys, i);
+            }
+        }
+        return;
+    }
+#pragma unroll
+    for (int u = 0; u < kRowBatch; ++u) {
+        const int64_t r = base + (int64_t)u * kHistThreads + threadIdx.x;
+        if (rows) rows[u] = r;
+        ok[u] = false;
+        key[u] = 0;
+        if (r < r1) {
+            const Segment& sg = segs[find_seg(segs, nseg, r)];  // independent per row
+            const int64_t i = r - sg.row_base;
+            if (row_ids != nullptr && sg.ids != nullptr) row_ids[r] = sg.ids[i];
+            ok[u] = bit_valid(sg.valid, sg.voff, i);
+            key[u] = ld_key<K>(sg.keys, i);
+        }
+    }
+}
+
+// level 1: rows per (group, tile); hist1[g * ntiles + tile]
 template <typename K>
 __global__ void __launch_bounds__(kHistThreads)
-build_hist_kernel(const Segment* __restrict__ segs, int nseg, int64_t total, uint32_t nb, uint32_t clog2,
-                  uint32_t nchunks, uint32_t* __restrict__ hist, int64_t ntiles) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t s_h[];
-    const uint32_t nbins = nchunks + 1;
-    for (uint32_t c = threadIdx.x; c < nbins; c += kHistThreads) s_h[c] = 0;
+coarse_hist_kernel(const Segment* __restrict__ segs, int nseg, int64_t total, uint32_t nb, uint32_t clog2,
+                   uint32_t nchunks, uint32_t gshift, uint32_t ngroups, uint32_t* __restrict__ hist1,
+                   int64_t ntiles) {
+    __shared__ uint32_t s_h[kHistThreads / 64][kCoarseBins];  // per-wave copies: fewer LDS atomic collisions
+    const int wave = threadIdx.x >> 6;
+    for (uint32_t k = threadIdx.x; k < (kHistThreads / 64) * kCoarseBins; k += kHistThreads) (&s_h[0][0])[k] = 0;
     __syncthreads();
     const int64_t r0 = (int64_t)blockIdx.x * kBuildTile;
     const int64_t r1 = min<int64_t>(total, r0 + kBuildTile);
-    int si = find_seg(segs, nseg, r0);
-    for (int64_t r = r0 + threadIdx.x; r < r1; r += kHistThreads) {
-        while (si + 1 < nseg && segs[si + 1].row_base <= r) ++si;
-        const Segment& sg = segs[si];
-        const int64_t i = r - sg.row_base;
-        if (!bit_valid(sg.valid, sg.voff, i)) continue;
-        const int64_t key = ld_key<K>(sg.keys, i);
-        const uint32_t c = ((uint64_t)key ^ kSign) == 0 ? nchunks : (home_bucket(key, nb) >> clog2);
-        atomicAdd(&s_h[c], 1u);
+    __shared__ Segment s_seg[kTileSegs];
+    __shared__ int s_info[2];
+    int tns;
+    const Segment* tsegs = tile_segments(segs, nseg, r0, r1, s_seg, s_info, &tns);
+    for (int64_t base = r0; base < r1; base += kHistThreads * kRowBatch) {
+        int64_t key[kRowBatch];
+        bool ok[kRowBatch];
+        load_rows<K>(tsegs, tns, base, r1, key, ok, nullptr, nullptr);
+#pragma unroll
+        for (int u = 0; u < kRowBatch; ++u)
+            if (ok[u]) atomicAdd(&s_h[wave][chunk_of(key[u], nb, clog2, nchunks) >> gshift], 1u);
     }
     __syncthreads();
-    for (uint32_t c = threadIdx.x; c < nbins; c += kHistThreads) hist[(int64_t)c * ntiles + blockIdx.x] = s_h[c];
+    for (uint32_t g = threadIdx.x; g < ngroups; g += kHistThreads) {
+        uint32_t v = 0;
+        for (int w = 0; w < kHistThreads / 64; ++w) v += s_h[w][g];
+        hist1[(int64_t)g * ntiles + blockIdx.x] = v;
+    }
+}
+
+// level 2: rows per (chunk, tile) over the group-ordered rows tkeys[0, n_valid); a tile
+// touches only the chunks of the groups it spans: hist2 must be zeroed beforehand
+__device__ __forceinline__ void fine_range(const unsigned long long* tkeys, int64_t r0, int64_t r1, uint32_t nb,
+                                           uint32_t clog2, uint32_t nchunks, uint32_t gshift, uint32_t* lo,
+                                           uint32_t* hi) {
+    const uint32_t g0 = chunk_of((int64_t)tkeys[r0], nb, clog2, nchunks) >> gshift;
+    const uint32_t g1 = chunk_of((int64_t)tkeys[r1 - 1], nb, clog2, nchunks) >> gshift;
+    *lo = g0 << gshift;
+    *hi = min(nchunks, ((g1 + 1) << gshift) - 1);  // inclusive
+}
+
+__global__ void __launch_bounds__(kHistThreads)
+fine_hist_kernel(const unsigned long long* __restrict__ tkeys, const BuildCounters* __restrict__ ctr, uint32_t nb,
+                 uint32_t clog2, uint32_t nchunks, uint32_t gshift, uint32_t* __restrict__ hist, int64_t ntiles) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t s_h[];
+    const int64_t nvalid = (int64_t)ctr->n_valid;
+    const int64_t r0 = (int64_t)blockIdx.x * kBuildTile;
+    const int64_t r1 = min<int64_t>(nvalid, r0 + kBuildTile);
+    if (r0 >= r1) return;
+    uint32_t lo, hi;
+    fine_range(tkeys, r0, r1, nb, clog2, nchunks, gshift, &lo, &hi);
+    for (uint32_t c = lo + threadIdx.x; c <= hi; c += kHistThreads) s_h[c - lo] = 0;
+    __syncthreads();
+    for (int64_t base = r0; base < r1; base += kHistThreads * kRowBatch) {
+        unsigned long long key[kRowBatch];
+#pragma unroll
+        for (int u = 0; u < kRowBatch; ++u) {
+            const int64_t r = base + (int64_t)u * kHistThreads + threadIdx.x;
+            key[u] = r < r1 ? tkeys[r] : 0ull;
+        }
+#pragma unroll
+        for (int u = 0; u < kRowBatch; ++u)
+            if (base + (int64_t)u * kHistThreads + threadIdx.x < r1)
+                atomicAdd(&s_h[chunk_of((int64_t)key[u], nb, clog2, nchunks) - lo], 1u);
+    }
+    __syncthreads();
+    for (uint32_t c = lo + threadIdx.x; c <= hi; c += kHistThreads) hist[(int64_t)c * ntiles + blockIdx.x] = s_h[c - lo];
 }
 
 // ---------------------------------------------------------------------------
@@ -202,32 +323,68 @@ scan_down_kernel(T* __restrict__ a, int64_t len, const unsigned long long* __res
 }
 
 // ---------------------------------------------------------------------------
-// build 2: scatter (key, row) into chunk order (positions from the scanned histogram)
+// build 2: the two scatters (positions from the scanned histograms; order inside a
+// group / chunk is canonicalised by the chunk build)
 // ---------------------------------------------------------------------------
 template <typename K>
 __global__ void __launch_bounds__(kHistThreads)
-build_scatter_kernel(const Segment* __restrict__ segs, int nseg, int64_t total, uint32_t nb, uint32_t clog2,
-                     uint32_t nchunks, const uint32_t* __restrict__ hist, int64_t ntiles,
-                     unsigned long long* __restrict__ skeys, uint32_t* __restrict__ srows,
-                     uint64_t* __restrict__ row_ids) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t s_cur[];
-    const uint32_t nbins = nchunks + 1;
-    for (uint32_t c = threadIdx.x; c < nbins; c += kHistThreads) s_cur[c] = hist[(int64_t)c * ntiles + blockIdx.x];
+coarse_scatter_kernel(const Segment* __restrict__ segs, int nseg, int64_t total, uint32_t nb, uint32_t clog2,
+                      uint32_t nchunks, uint32_t gshift, uint32_t ngroups, const uint32_t* __restrict__ hist1,
+                      int64_t ntiles, unsigned long long* __restrict__ tkeys, uint32_t* __restrict__ trows,
+                      uint64_t* __restrict__ row_ids) {
+    __shared__ uint32_t s_cur[kCoarseBins];
+    for (uint32_t g = threadIdx.x; g < ngroups; g += kHistThreads) s_cur[g] = hist1[(int64_t)g * ntiles + blockIdx.x];
     __syncthreads();
     const int64_t r0 = (int64_t)blockIdx.x * kBuildTile;
     const int64_t r1 = min<int64_t>(total, r0 + kBuildTile);
-    int si = find_seg(segs, nseg, r0);
-    for (int64_t r = r0 + threadIdx.x; r < r1; r += kHistThreads) {
-        while (si + 1 < nseg && segs[si + 1].row_base <= r) ++si;
-        const Segment& sg = segs[si];
-        const int64_t i = r - sg.row_base;
-        if (sg.ids != nullptr) row_ids[r] = sg.ids[i];
-        if (!bit_valid(sg.valid, sg.voff, i)) continue;
-        const int64_t key = ld_key<K>(sg.keys, i);
-        const uint32_t c = ((uint64_t)key ^ kSign) == 0 ? nchunks : (home_bucket(key, nb) >> clog2);
-        const uint32_t pos = atomicAdd(&s_cur[c], 1u);  // order inside a chunk is canonicalised later
-        skeys[pos] = (unsigned long long)key;
-        srows[pos] = (uint32_t)r;
+    __shared__ Segment s_seg[kTileSegs];
+    __shared__ int s_info[2];
+    int tns;
+    const Segment* tsegs = tile_segments(segs, nseg, r0, r1, s_seg, s_info, &tns);
+    for (int64_t base = r0; base < r1; base += kHistThreads * kRowBatch) {
+        int64_t key[kRowBatch], row[kRowBatch];
+        bool ok[kRowBatch];
+        load_rows<K>(tsegs, tns, base, r1, key, ok, row_ids, row);
+#pragma unroll
+        for (int u = 0; u < kRowBatch; ++u) {
+            if (!ok[u]) continue;
+            const uint32_t pos = atomicAdd(&s_cur[chunk_of(key[u], nb, clog2, nchunks) >> gshift], 1u);
+            tkeys[pos] = (unsigned long long)key[u];
+            trows[pos] = (uint32_t)row[u];
+        }
+    }
+}
+
+__global__ void __launch_bounds__(kHistThreads)
+fine_scatter_kernel(const unsigned long long* __restrict__ tkeys, const uint32_t* __restrict__ trows,
+                    const BuildCounters* __restrict__ ctr, uint32_t nb, uint32_t clog2, uint32_t nchunks,
+                    uint32_t gshift, const uint32_t* __restrict__ hist, int64_t ntiles,
+                    unsigned long long* __restrict__ skeys, uint32_t* __restrict__ srows) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t s_cur[];
+    const int64_t nvalid = (int64_t)ctr->n_valid;
+    const int64_t r0 = (int64_t)blockIdx.x * kBuildTile;
+    const int64_t r1 = min<int64_t>(nvalid, r0 + kBuildTile);
+    if (r0 >= r1) return;
+    uint32_t lo, hi;
+    fine_range(tkeys, r0, r1, nb, clog2, nchunks, gshift, &lo, &hi);
+    for (uint32_t c = lo + threadIdx.x; c <= hi; c += kHistThreads) s_cur[c - lo] = hist[(int64_t)c * ntiles + blockIdx.x];
+    __syncthreads();
+    for (int64_t base = r0; base < r1; base += kHistThreads * kRowBatch) {
+        unsigned long long key[kRowBatch];
+        uint32_t row[kRowBatch];
+#pragma unroll
+        for (int u = 0; u < kRowBatch; ++u) {
+            const int64_t r = base + (int64_t)u * kHistThreads + threadIdx.x;
+            key[u] = r < r1 ? tkeys[r] : 0ull;
+            row[u] = r < r1 ? trows[r] : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < kRowBatch; ++u) {
+            if (base + (int64_t)u * kHistThreads + threadIdx.x >= r1) continue;
+            const uint32_t pos = atomicAdd(&s_cur[chunk_of((int64_t)key[u], nb, clog2, nchunks) - lo], 1u);
+            skeys[pos] = key[u];
+            srows[pos] = row[u];
+        }
     }
 }
 
@@ -235,6 +392,7 @@ build_scatter_kernel(const Segment* __restrict__ segs, int nseg, int64_t total, 
 // build 3: one workgroup per chunk builds the chunk's buckets in LDS
 // ---------------------------------------------------------------------------
 constexpr int kChunkThreads = 1024;
+constexpr int kChunkRegRows = 4;  // rows per thread kept in registers across passes A-C
 
 __device__ __forceinline__ void sort16_desc(uint32_t (&v)[16]) {
 #pragma unroll
@@ -306,18 +464,48 @@ chunk_build_kernel(uint32_t nb, uint32_t clog2, uint32_t nchunks, const uint32_t
     }
     __syncthreads();
 
-    // pass A: claim slots (LDS CAS), count rows per slot in ref[] (LDS atomics)
-    for (uint32_t r = start + threadIdx.x; r < end; r += kChunkThreads) {
-        const unsigned long long sk = skeys[r] ^ kSign;
-        int slot;
-        if (side) {
-            slot = 0;
-        } else {
-            const uint32_t i0 = home_bucket((int64_t)(sk ^ kSign), nb) & cmask;
-            slot = chunk_slot<true>(img, cmask, i0, sk);
-            if (slot < 0) { atomicOr(&ctr->err, 1ull); continue; }  // chunk full
+    // rows of a chunk with <= kChunkThreads * kChunkRegRows rows stay in registers from
+    // pass A to pass C (key, row and claimed slot); larger chunks (duplicate-heavy
+    // keys) stream their rows twice
+    const bool in_regs = end - start <= (uint32_t)(kChunkThreads * kChunkRegRows);
+    uint32_t rrow[kChunkRegRows];
+    int rslot[kChunkRegRows];
+    if (in_regs) {
+        unsigned long long rk[kChunkRegRows];
+#pragma unroll
+        for (int u = 0; u < kChunkRegRows; ++u) {
+            const uint32_t r = start + u * kChunkThreads + threadIdx.x;
+            rk[u] = r < end ? skeys[r] : 0ull;
+            rrow[u] = r < end ? srows[r] : 0u;
         }
-        atomicAdd(&img[slot / kSlots].ref[slot % kSlots], 1u);
+        // pass A: claim slots (LDS CAS), count rows per slot in ref[] (LDS atomics)
+#pragma unroll
+        for (int u = 0; u < kChunkRegRows; ++u) {
+            rslot[u] = -1;
+            if (start + u * kChunkThreads + threadIdx.x >= end) continue;
+            const unsigned long long sk = rk[u] ^ kSign;
+            int slot = 0;
+            if (!side) {
+                slot = chunk_slot<true>(img, cmask, home_bucket((int64_t)rk[u], nb) & cmask, sk);
+                if (slot < 0) { atomicOr(&ctr->err, 1ull); continue; }  // chunk full
+            }
+            rslot[u] = slot;
+            atomicAdd(&img[slot / kSlots].ref[slot % kSlots], 1u);
+        }
+    } else {
+        // pass A (streamed)
+        for (uint32_t r = start + threadIdx.x; r < end; r += kChunkThreads) {
+            const unsigned long long sk = skeys[r] ^ kSign;
+            int slot;
+            if (side) {
+                slot = 0;
+            } else {
+                const uint32_t i0 = home_bucket((int64_t)(sk ^ kSign), nb) & cmask;
+                slot = chunk_slot<true>(img, cmask, i0, sk);
+                if (slot < 0) { atomicOr(&ctr->err, 1ull); continue; }  // chunk full
+            }
+            atomicAdd(&img[slot / kSlots].ref[slot % kSlots], 1u);
+        }
     }
     __syncthreads();
 
@@ -361,23 +549,31 @@ chunk_build_kernel(uint32_t nb, uint32_t clog2, uint32_t nchunks, const uint32_t
 
     // pass C: place rows: single-row keys keep their row in ref, duplicated keys append
     // to their segment (unordered here, sorted in pass D)
-    for (uint32_t r = start + threadIdx.x; r < end; r += kChunkThreads) {
-        const unsigned long long sk = skeys[r] ^ kSign;
-        int slot = 0;
-        if (!side) {
-            const uint32_t i0 = home_bucket((int64_t)(sk ^ kSign), nb) & cmask;
-            slot = chunk_slot<false>(img, cmask, i0, sk);
-            if (slot < 0) continue;
-        }
+    auto place = [&](int slot, uint32_t row) {
         unsigned& ref = img[slot / kSlots].ref[slot % kSlots];
         const unsigned rv = ref;
-        const uint32_t row = srows[r];
         if (rv & kDupFlag) {
             const unsigned li = rv & ~kDupFlag;
             const unsigned k = atomicAdd(&d_cur[li], 1u);
             dup_rows[d_off[li] + 1 + k] = row;
         } else if (rv == 1) {
             ref = row;  // the key's only row (rv == count == 1)
+        }
+    };
+    if (in_regs) {
+#pragma unroll
+        for (int u = 0; u < kChunkRegRows; ++u)
+            if (rslot[u] >= 0) place(rslot[u], rrow[u]);
+    } else {
+        for (uint32_t r = start + threadIdx.x; r < end; r += kChunkThreads) {
+            const unsigned long long sk = skeys[r] ^ kSign;
+            int slot = 0;
+            if (!side) {
+                const uint32_t i0 = home_bucket((int64_t)(sk ^ kSign), nb) & cmask;
+                slot = chunk_slot<false>(img, cmask, i0, sk);
+                if (slot < 0) continue;
+            }
+            place(slot, srows[r]);
         }
     }
     __syncthreads();
@@ -1290,27 +1486,46 @@ static hipError_t launch_scan(T* a, int64_t len, unsigned long long* bsum, unsig
     return hipGetLastError();
 }
 
+uint32_t coarse_shift(uint32_t nchunks) {
+    // smallest shift with (nchunks >> shift) + 1 <= kCoarseBins groups (side chunk included)
+    uint32_t sh = 0;
+    while ((nchunks >> sh) + 1 > (uint32_t)kCoarseBins) ++sh;
+    return sh;
+}
+
 hipError_t launch_build(int key_bytes, const Segment* d_segs, int nseg, int64_t total, uint32_t nb, uint32_t clog2,
-                        uint32_t nchunks, uint32_t* hist, int64_t ntiles, void* scan_scratch,
-                        unsigned long long* skeys, uint32_t* srows, uint64_t* row_ids, Bucket* tbl,
-                        uint32_t* dup_rows, BigSeg* big, BuildCounters* ctr, int big_grid, hipStream_t s) {
+                        uint32_t nchunks, uint32_t* hist, uint32_t* hist1, int64_t ntiles, void* scan_scratch,
+                        unsigned long long* tkeys, uint32_t* trows, unsigned long long* skeys, uint32_t* srows,
+                        uint64_t* row_ids, Bucket* tbl, uint32_t* dup_rows, BigSeg* big, BuildCounters* ctr,
+                        int big_grid, hipStream_t s) {
     const size_t hist_lds = sizeof(uint32_t) * (nchunks + 1);
     const int64_t hlen = (int64_t)(nchunks + 1) * ntiles;
+    const uint32_t gshift = coarse_shift(nchunks);
+    const uint32_t ngroups = (nchunks >> gshift) + 1;
     if (ntiles > 0) {
+        unsigned long long* scr = (unsigned long long*)scan_scratch;
+        // level 1: group order
         if (key_bytes == 8)
-            build_hist_kernel<int64_t><<<(unsigned)ntiles, kHistThreads, hist_lds, s>>>(d_segs, nseg, total, nb, clog2,
-                                                                                      nchunks, hist, ntiles);
+            coarse_hist_kernel<int64_t><<<(unsigned)ntiles, kHistThreads, 0, s>>>(d_segs, nseg, total, nb, clog2, nchunks,
+                                                                                 gshift, ngroups, hist1, ntiles);
         else
-            build_hist_kernel<int32_t><<<(unsigned)ntiles, kHistThreads, hist_lds, s>>>(d_segs, nseg, total, nb, clog2,
-                                                                                      nchunks, hist, ntiles);
-        hipError_t e = launch_scan(hist, hlen, (unsigned long long*)scan_scratch, &ctr->n_valid, s);
+            coarse_hist_kernel<int32_t><<<(unsigned)ntiles, kHistThreads, 0, s>>>(d_segs, nseg, total, nb, clog2, nchunks,
+                                                                                 gshift, ngroups, hist1, ntiles);
+        hipError_t e = launch_scan(hist1, (int64_t)ngroups * ntiles, scr, &ctr->n_valid, s);
         if (e != hipSuccess) return e;
         if (key_bytes == 8)
-            build_scatter_kernel<int64_t><<<(unsigned)ntiles, kHistThreads, hist_lds, s>>>(
-                d_segs, nseg, total, nb, clog2, nchunks, hist, ntiles, skeys, srows, row_ids);
+            coarse_scatter_kernel<int64_t><<<(unsigned)ntiles, kHistThreads, 0, s>>>(
+                d_segs, nseg, total, nb, clog2, nchunks, gshift, ngroups, hist1, ntiles, tkeys, trows, row_ids);
         else
-            build_scatter_kernel<int32_t><<<(unsigned)ntiles, kHistThreads, hist_lds, s>>>(
-                d_segs, nseg, total, nb, clog2, nchunks, hist, ntiles, skeys, srows, row_ids);
+            coarse_scatter_kernel<int32_t><<<(unsigned)ntiles, kHistThreads, 0, s>>>(
+                d_segs, nseg, total, nb, clog2, nchunks, gshift, ngroups, hist1, ntiles, tkeys, trows, row_ids);
+        // level 2: chunk order (tiles over the n_valid group-ordered rows)
+        if ((e = hipMemsetAsync(hist, 0, sizeof(uint32_t) * (size_t)hlen, s)) != hipSuccess) return e;
+        fine_hist_kernel<<<(unsigned)ntiles, kHistThreads, hist_lds, s>>>(tkeys, ctr, nb, clog2, nchunks, gshift, hist,
+                                                                         ntiles);
+        if ((e = launch_scan(hist, hlen, scr, &ctr->n_valid, s)) != hipSuccess) return e;
+        fine_scatter_kernel<<<(unsigned)ntiles, kHistThreads, hist_lds, s>>>(tkeys, trows, ctr, nb, clog2, nchunks,
+                                                                            gshift, hist, ntiles, skeys, srows);
     }
     // chunk build: LDS = bucket image + dup directory (3 u32 per entry)
     const uint32_t CB = 1u << clog2;

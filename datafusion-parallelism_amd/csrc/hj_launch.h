@@ -15,9 +15,15 @@ int64_t build_tiles(int64_t total);
 // bytes of the scan scratch for a histogram of `len` u32
 int64_t scan_scratch_bytes(int64_t len);
 
+constexpr int kCoarseBins = 128;     // level-1 partition groups (per-wave LDS copies)
+
+// scratch: hist u32[(nchunks + 1) * ntiles], hist1 u32[kCoarseBins * ntiles],
+// scan_scratch scan_scratch_bytes((nchunks + 1) * ntiles), tkeys/skeys u64[total],
+// trows/srows u32[total]
 hipError_t launch_build(int key_bytes, const Segment* d_segs, int nseg, int64_t total,
                         uint32_t nb, uint32_t clog2, uint32_t nchunks, uint32_t* hist,
-                        int64_t ntiles, void* scan_scratch, unsigned long long* skeys,
+                        uint32_t* hist1, int64_t ntiles, void* scan_scratch,
+                        unsigned long long* tkeys, uint32_t* trows, unsigned long long* skeys,
                         uint32_t* srows, uint64_t* row_ids, Bucket* tbl, uint32_t* dup_rows,
                         BigSeg* big, BuildCounters* ctr, int big_grid, hipStream_t s);
 
