@@ -249,7 +249,7 @@ def main():
         "frac": round(achieved / HBM_PEAK_GBS, 4),
         "traffic": (traffic or {}).get("hbm_bytes_per_launch"),
         "traffic_lower": ((traffic or {}).get("probe_phase") or {}).get("hbm_bytes_lower"),
-        "kernel": "probe (probe_lookup_kernel + tile-count scan + probe_emit_kernel, one hj_probe_async)",
+        "kernel": "probe_fused_kernel (the whole hj_probe_async: lookup + ordered pair emission)",
         "alg_bytes_per_launch": alg_bytes,
         "alg_bytes_formula": "8*P + 16*B + 12*M (SURVEY.md §8d)",
         # the lookup is one random 64-B bucket read per probe row; DESIGN.md §4 prices it

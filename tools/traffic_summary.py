@@ -19,11 +19,12 @@ import json
 import os
 import sys
 
-PROBE_KERNELS = ("probe_lookup_kernel", "probe_emit_kernel", "scan_reduce_kernel<unsigned long long>",
+PROBE_KERNELS = ("probe_fused_kernel", "probe_lookup_kernel", "probe_emit_kernel", "scan_reduce_kernel<unsigned long long>",
                  "scan_down_kernel<unsigned long long>", "pp_partition_kernel", "pp_lookup_kernel",
                  "pp_count_kernel")
-BUILD_KERNELS = ("build_hist_kernel", "scan_reduce_kernel<unsigned int>", "scan_down_kernel<unsigned int>",
-                 "build_scatter_kernel", "chunk_build_kernel", "dup_sort_big_kernel")
+BUILD_KERNELS = ("coarse_hist_kernel", "coarse_scatter_kernel", "fine_hist_kernel", "fine_scatter_kernel",
+                 "scan_reduce_kernel<unsigned int>", "scan_down_kernel<unsigned int>", "chunk_build_kernel",
+                 "dup_sort_big_kernel")
 
 
 def per_kernel(path):
@@ -68,7 +69,7 @@ def main():
         "probe_phase": probe,
         "build_phase": build,
         "kernels": kernels,
-        "note": "probe phase = probe_lookup + tile-count scan + probe_emit (one hj_probe_async). "
+        "note": "probe phase = the kernels of one hj_probe_async (default: probe_fused_kernel alone). "
                 "Upper = 2 x FETCH_SIZE + WRITE_SIZE (guide's gfx950 correction applied to all reads); "
                 "lower = FETCH_SIZE + WRITE_SIZE (random 64-B bucket reads counted at 64 B each).",
     }
