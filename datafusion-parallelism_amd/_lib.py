@@ -72,6 +72,12 @@ SIGNATURES = [
     ("hj_table_stream_wait", I32, [P, P]),
     ("hj_partition_workspace_bytes", I64, [I64, I32]),
     ("hj_radix_partition", I32, [I32, P, P, I64, P, U64, I64, I32, P, P, P, P, P]),
+    ("hj_mark_rows", I32, [P, I32, I64, P, I64, P]),
+    ("hj_select_workspace_bytes", I64, [I64]),
+    ("hj_select_rows", I32, [P, I64, I32, P, P, P, P]),
+    ("hj_gather_fixed", I32, [P, P, I64, I32, P, I32, I64, P, P, P]),
+    ("hj_gather_var_workspace_bytes", I64, [I64]),
+    ("hj_gather_var", I32, [P, I32, P, P, I64, P, I32, I64, P, P, I64, P, P, P, P]),
     ("hj_gen_perm_keys", I32, [P, I64, I64, I64, P]),
     ("hj_gen_uniform_keys", I32, [P, I64, U64, I64, P]),
 ]

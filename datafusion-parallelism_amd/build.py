@@ -22,9 +22,9 @@ LIB = os.path.join(LIBDIR, "libdfp_hj.so")
 INCLUDE = os.path.join(os.path.dirname(HERE), "include")
 ARCH = "gfx950"
 
-SOURCES_HIP = ["hj_kernels.hip"]
+SOURCES_HIP = ["hj_kernels.hip", "hj_columns.hip"]
 SOURCES_CPP = ["hj_api.cpp"]
-HEADERS = ["hj_device.h", "hj_launch.h"]
+HEADERS = ["hj_device.h", "hj_launch.h", "hj_util.h"]
 
 
 def torch_lib_dir() -> str:

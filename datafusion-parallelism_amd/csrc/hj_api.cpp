@@ -835,4 +835,69 @@ hj_status hj_gen_uniform_keys(int64_t* out, int64_t n, uint64_t seed, int64_t ra
     return HJ_OK;
 }
 
+
+// ---- join types and output materialisation (hj_columns.hip) ---------------------
+
+hj_status hj_mark_rows(const void* idx, int idx_bytes, int64_t n, uint8_t* flags, int64_t nflags, void* stream) {
+    if (device_count() == 0) return fail(HJ_ERR_NO_DEVICE, "no GPU visible");
+    if (n < 0 || nflags < 0 || (idx_bytes != 4 && idx_bytes != 8)) return fail(HJ_ERR_INVALID, "bad arguments");
+    if ((n > 0 && idx == nullptr) || (nflags > 0 && flags == nullptr))
+        return fail(HJ_ERR_INVALID, "null pointer");
+    if (!is_device_ptr(idx) || !is_device_ptr(flags)) return fail(HJ_ERR_INVALID, "hj_mark_rows takes device pointers");
+    HIP_TRY(launch_mark_rows(idx, idx_bytes, n, flags, nflags, (hipStream_t)stream));
+    return HJ_OK;
+}
+
+int64_t hj_select_workspace_bytes(int64_t n) { return select_workspace(n < 0 ? 0 : n); }
+
+hj_status hj_select_rows(const uint8_t* flags, int64_t n, int want, uint64_t* out, int64_t* d_count, void* workspace,
+                         void* stream) {
+    if (device_count() == 0) return fail(HJ_ERR_NO_DEVICE, "no GPU visible");
+    if (n < 0 || want < 0 || want > 255) return fail(HJ_ERR_INVALID, "bad arguments");
+    if (d_count == nullptr || workspace == nullptr || (n > 0 && (flags == nullptr || out == nullptr)))
+        return fail(HJ_ERR_INVALID, "null pointer");
+    if (!is_device_ptr(flags) || !is_device_ptr(out) || !is_device_ptr(d_count) || !is_device_ptr(workspace))
+        return fail(HJ_ERR_INVALID, "hj_select_rows takes device pointers");
+    HIP_TRY(launch_select_rows(flags, n, (uint8_t)want, out, d_count, workspace, (hipStream_t)stream));
+    return HJ_OK;
+}
+
+hj_status hj_gather_fixed(const void* src, const uint8_t* src_valid, int64_t src_voff, int elem_bytes, const void* idx,
+                          int idx_bytes, int64_t n, void* dst, uint8_t* dst_valid, void* stream) {
+    if (device_count() == 0) return fail(HJ_ERR_NO_DEVICE, "no GPU visible");
+    if (n < 0 || (idx_bytes != 4 && idx_bytes != 8) ||
+        !(elem_bytes == 1 || elem_bytes == 2 || elem_bytes == 4 || elem_bytes == 8 || elem_bytes == 16))
+        return fail(HJ_ERR_INVALID, "bad arguments (elem_bytes 1/2/4/8/16, idx_bytes 4/8)");
+    if (n > 0 && (idx == nullptr || dst == nullptr)) return fail(HJ_ERR_INVALID, "null pointer");
+    if (reinterpret_cast<uintptr_t>(dst_valid) & 7) return fail(HJ_ERR_INVALID, "dst_valid must be 8-byte aligned");
+    if (!is_device_ptr(src) || !is_device_ptr(src_valid) || !is_device_ptr(idx) || !is_device_ptr(dst) ||
+        !is_device_ptr(dst_valid))
+        return fail(HJ_ERR_INVALID, "hj_gather_fixed takes device pointers");
+    HIP_TRY(launch_gather_fixed(src, src_valid, src_voff, elem_bytes, idx, idx_bytes, n, dst, dst_valid,
+                                (hipStream_t)stream));
+    return HJ_OK;
+}
+
+int64_t hj_gather_var_workspace_bytes(int64_t n) { return gather_var_workspace(n < 0 ? 0 : n); }
+
+hj_status hj_gather_var(const void* offsets, int offset_bytes, const uint8_t* values, const uint8_t* src_valid,
+                        int64_t src_voff, const void* idx, int idx_bytes, int64_t n, void* out_offsets,
+                        uint8_t* out_values, int64_t values_cap, uint8_t* dst_valid, int64_t* d_values_len,
+                        void* workspace, void* stream) {
+    if (device_count() == 0) return fail(HJ_ERR_NO_DEVICE, "no GPU visible");
+    if (n < 0 || values_cap < 0 || (idx_bytes != 4 && idx_bytes != 8) || (offset_bytes != 4 && offset_bytes != 8))
+        return fail(HJ_ERR_INVALID, "bad arguments (offset_bytes 4/8, idx_bytes 4/8)");
+    if (out_offsets == nullptr || d_values_len == nullptr || workspace == nullptr ||
+        (n > 0 && (idx == nullptr || offsets == nullptr)))
+        return fail(HJ_ERR_INVALID, "null pointer");
+    if (reinterpret_cast<uintptr_t>(dst_valid) & 7) return fail(HJ_ERR_INVALID, "dst_valid must be 8-byte aligned");
+    if (!is_device_ptr(offsets) || !is_device_ptr(values) || !is_device_ptr(src_valid) || !is_device_ptr(idx) ||
+        !is_device_ptr(out_offsets) || !is_device_ptr(out_values) || !is_device_ptr(dst_valid) ||
+        !is_device_ptr(d_values_len) || !is_device_ptr(workspace))
+        return fail(HJ_ERR_INVALID, "hj_gather_var takes device pointers");
+    HIP_TRY(launch_gather_var(offsets, offset_bytes, values, src_valid, src_voff, idx, idx_bytes, n, out_offsets,
+                              out_values, values_cap, dst_valid, d_values_len, workspace, (hipStream_t)stream));
+    return HJ_OK;
+}
+
 }  // extern "C"

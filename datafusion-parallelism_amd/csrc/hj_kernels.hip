@@ -34,18 +34,13 @@
 
 #include "hj_device.h"
 #include "hj_launch.h"
+#include "hj_util.h"
 
 namespace dfp {
 
 // ---------------------------------------------------------------------------
 // helpers
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ bool bit_valid(const uint8_t* v, int64_t off, int64_t i) {
-    if (v == nullptr) return true;
-    const int64_t b = off + i;
-    return (v[b >> 3] >> (b & 7)) & 1;
-}
-
 template <typename K>
 __device__ __forceinline__ int64_t ld_key(const void* keys, int64_t i) {
     return (int64_t)(reinterpret_cast<const K*>(keys)[i]);
@@ -64,46 +59,9 @@ __device__ __forceinline__ int find_seg(const Segment* segs, int nseg, int64_t r
     return lo;
 }
 
-template <typename T>
-__device__ __forceinline__ T wave_incl_scan(T v) {
-    const int lane = threadIdx.x & 63;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        T t = __shfl_up(v, (unsigned)d, 64);
-        if (lane >= d) v += t;
-    }
-    return v;
-}
-
-template <typename T>
-__device__ __forceinline__ T wave_sum(T v) {
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
-    return v;
-}
-
 // chunk of a key: the probe sequence of a key never leaves it
 __device__ __forceinline__ uint32_t home_bucket(int64_t key, uint32_t nb) {
     return bucket_of(mix64((uint64_t)key), nb);
-}
-
-// exclusive block scan of one value per thread (blockDim.x <= 1024), returns the
-// exclusive prefix, *total = block total. Uses s_w[blockDim.x / 64].
-template <typename T>
-__device__ __forceinline__ T block_excl_scan(T v, T* s_w, T* total) {
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
-    const T incl = wave_incl_scan(v);
-    if (lane == 63) s_w[wave] = incl;
-    __syncthreads();
-    T off = 0, tot = 0;
-    for (int w = 0; w < nw; ++w) {
-        const T x = s_w[w];
-        if (w < wave) off += x;
-        tot += x;
-    }
-    __syncthreads();
-    *total = tot;
-    return off + incl - v;
 }
 
 // ---------------------------------------------------------------------------
@@ -1491,6 +1449,12 @@ uint32_t coarse_shift(uint32_t nchunks) {
     uint32_t sh = 0;
     while ((nchunks >> sh) + 1 > (uint32_t)kCoarseBins) ++sh;
     return sh;
+}
+
+hipError_t launch_scan_u64(unsigned long long* a, int64_t len, void* scratch, unsigned long long* total,
+                           hipStream_t s) {
+    if (len <= 0) return total ? hipMemsetAsync(total, 0, 8, s) : hipSuccess;
+    return launch_scan<unsigned long long>(a, len, (unsigned long long*)scratch, total, s);
 }
 
 hipError_t launch_build(int key_bytes, const Segment* d_segs, int nseg, int64_t total, uint32_t nb, uint32_t clog2,

@@ -52,6 +52,25 @@ hipError_t launch_radix_partition(int key_bytes, const void* keys, const uint8_t
                                   int64_t* counts, void* workspace, hipStream_t s);
 int64_t radix_partition_workspace(int64_t n, int nparts);
 
+// in-place exclusive scan of u64 (scratch: scan_scratch_bytes(len)); *total = sum
+hipError_t launch_scan_u64(unsigned long long* a, int64_t len, void* scratch, unsigned long long* total,
+                           hipStream_t s);
+
+// ---- join-type and output primitives (hj_columns.hip) ----------------------
+hipError_t launch_mark_rows(const void* idx, int idx_bytes, int64_t n, uint8_t* flags, int64_t nflags,
+                            hipStream_t s);
+int64_t select_workspace(int64_t n);
+hipError_t launch_select_rows(const uint8_t* flags, int64_t n, uint8_t want, uint64_t* out, int64_t* d_count,
+                              void* workspace, hipStream_t s);
+hipError_t launch_gather_fixed(const void* src, const uint8_t* src_valid, int64_t src_voff, int elem_bytes,
+                               const void* idx, int idx_bytes, int64_t n, void* dst, uint8_t* dst_valid,
+                               hipStream_t s);
+int64_t gather_var_workspace(int64_t n);
+hipError_t launch_gather_var(const void* offsets, int offset_bytes, const uint8_t* values, const uint8_t* src_valid,
+                             int64_t src_voff, const void* idx, int idx_bytes, int64_t n, void* out_offsets,
+                             uint8_t* out_values, int64_t values_cap, uint8_t* dst_valid, int64_t* d_values_len,
+                             void* workspace, hipStream_t s);
+
 // ---- generators ----------------------------------------------------------
 hipError_t launch_gen_perm(int64_t* out, int64_t n, int64_t mul, int64_t range, hipStream_t s);
 hipError_t launch_gen_uniform(int64_t* out, int64_t n, uint64_t seed, int64_t range,

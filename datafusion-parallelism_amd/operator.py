@@ -22,9 +22,17 @@ whose build and probe run on the gfx950 kernels through the C ABI (``include/hj.
   ParallelHashJoin::execute (src/operator/parallel_hash_join.rs:140-167)
                                                               ParallelHashJoin.execute / collect
 
-Only the inner join without a non-equi JoinFilter and with a single Int32/Int64 key
-column is in scope; other join types and filters are SURVEY.md §8f rows.
-The reference's CPU strategies (Original, New..New10) are not part of this package.
+  ProbeLookupStreamImplementation (src/operator/probe_lookup_implementation/
+    probe_lookup_implementation.rs:19-80): Inner, Left, Right, Full, LeftSemi, LeftAnti,
+    RightSemi, RightAnti                                      JoinType + _probe_batch /
+                                                              _finalize_build_side
+  apply_join_filter_to_indices (src/shared/datafusion_private.rs:295-328)
+                                                              JoinFilter
+
+Single Int32/Int64 equi-join key column. Output columns are materialised on the GPU
+(columns.DeviceColumn.take: the build side is uploaded once after the barrier, each probe
+batch once). The reference's CPU strategies (Original, New..New10) are not part of this
+package.
 """
 from __future__ import annotations
 
@@ -36,8 +44,10 @@ from typing import Callable, Iterable, Sequence
 import numpy as np
 import pyarrow as pa
 import pyarrow.compute as pc
+import torch
 
 from ._lib import HjError, HJ_ERR_INVALID
+from .columns import DeviceColumn, mark_rows, select_rows
 from .table import HashTable
 
 
@@ -72,11 +82,62 @@ def _key_type(arr: pa.Array) -> str:
     raise HjError(HJ_ERR_INVALID, f"join key type {arr.type} is not supported (Int32/Int64 only)")
 
 
-class GpuIndexLookup:
-    """The read-only shared table handed to every partition (IndexLookup<u64>)."""
+class JoinType(enum.Enum):
+    """datafusion_common::JoinType as supported by the reference's probe side
+    (probe_lookup_implementation.rs:32-43). Left = build side, right = probe side."""
+    Inner = "inner"
+    Left = "left"
+    Right = "right"
+    Full = "full"
+    LeftSemi = "leftsemi"
+    LeftAnti = "leftanti"
+    RightSemi = "rightsemi"
+    RightAnti = "rightanti"
 
-    def __init__(self, table: HashTable):
+    @classmethod
+    def parse(cls, v: "JoinType | str") -> "JoinType":
+        if isinstance(v, JoinType):
+            return v
+        key = str(v).lower().replace("_", "").replace(" ", "").replace("outer", "")
+        for jt in cls:
+            if jt.value == key:
+                return jt
+        raise HjError(HJ_ERR_INVALID, f"unknown join type {v!r}")
+
+    @property
+    def marks_build(self) -> bool:  # build-side visited bitset (ConcurrentBitSet)
+        return self in (JoinType.Left, JoinType.Full, JoinType.LeftSemi, JoinType.LeftAnti)
+
+
+class JoinFilter:
+    """A non-equi join condition applied to the equal-key candidate pairs
+    (apply_join_filter_to_indices, src/shared/datafusion_private.rs:295-328):
+    `expression(left_rows, right_rows)` gets the candidate rows of the `left_columns` /
+    `right_columns` it reads (pyarrow RecordBatches, one row per pair) and returns a
+    BooleanArray; null counts as false."""
+
+    def __init__(self, expression: Callable[[pa.RecordBatch, pa.RecordBatch], pa.Array],
+                 left_columns: Sequence[str] | None = None, right_columns: Sequence[str] | None = None):
+        self.expression = expression
+        self.left_columns = left_columns
+        self.right_columns = right_columns
+
+
+def _batch(cols: Sequence[DeviceColumn], names: Sequence[str]) -> pa.RecordBatch:
+    return pa.RecordBatch.from_arrays([c.to_arrow() for c in cols], names=list(names))
+
+
+class GpuIndexLookup:
+    """The read-only shared table handed to every partition (IndexLookup<u64>), with the
+    build RecordBatch's columns resident in HBM for output materialisation."""
+
+    def __init__(self, table: HashTable, shared: "_SharedBuild | None" = None):
         self.table = table
+        self._shared = shared
+
+    @property
+    def device(self) -> torch.device:
+        return torch.device("cuda", self.table.device)
 
     def get_iter(self, key: int):
         """Build rows of `key` in chain order (newest first)
@@ -85,11 +146,31 @@ class GpuIndexLookup:
         internal), which the equality re-check makes equivalent."""
         return iter(self.table.lookup(key))
 
+    def matching_indices_device(self, probe_keys: pa.Array) -> tuple[torch.Tensor, torch.Tensor]:
+        """get_matching_indices + equal_rows_arr, fused on the GPU: ProbeBuildIndices
+        after the equality filter as device tensors (build int64, probe int32)."""
+        keys = DeviceColumn.from_arrow(probe_keys, self.device)
+        n = len(probe_keys)
+        if n == 0:
+            return (torch.empty(0, dtype=torch.int64, device=self.device),
+                    torch.empty(0, dtype=torch.int32, device=self.device))
+        dt = torch.int64 if pa.types.is_int64(probe_keys.type) else torch.int32
+        kt = keys.data.view(dt)[:n]
+        valid = None
+        if keys.valid is not None:
+            bits = np.unpackbits(keys.valid.cpu().numpy(), bitorder="little")[keys.voff:keys.voff + n]
+            valid = bits.astype(bool)
+        return self.table.probe(kt, valid, device_output=True)
+
     def matching_indices(self, probe_keys: pa.Array) -> tuple[pa.UInt64Array, pa.UInt32Array]:
-        """get_matching_indices + equal_rows_arr, fused on the GPU: returns
-        ProbeBuildIndices after the equality filter (build UInt64, probe UInt32)."""
+        """Host form of matching_indices_device (UInt64 build, UInt32 probe)."""
         b, p = self.table.probe(probe_keys)
         return pa.array(b, type=pa.uint64()), pa.array(p, type=pa.uint32())
+
+    def build_columns(self, build_side_records: pa.RecordBatch) -> list[DeviceColumn]:
+        if self._shared is not None:
+            return self._shared.device_columns(build_side_records, self.device)
+        return [DeviceColumn.from_arrow(c, self.device) for c in build_side_records.columns]
 
 
 class _SharedBuild:
@@ -106,6 +187,7 @@ class _SharedBuild:
         self.ready = threading.Barrier(parallelism)
         self.record_batch: pa.RecordBatch | None = None
         self.schema: pa.Schema | None = None
+        self._dev_cols: list[DeviceColumn] | None = None
 
     def table_for(self, key_type: str) -> HashTable:
         with self.lock:
@@ -130,6 +212,13 @@ class _SharedBuild:
                 else:
                     self.record_batch = pa.RecordBatch.from_pylist([], schema=self.schema or pa.schema([]))
             return self.record_batch
+
+    def device_columns(self, rb: pa.RecordBatch, device) -> list[DeviceColumn]:
+        """The concatenated build batch in HBM, uploaded once for all partitions."""
+        with self.lock:
+            if self._dev_cols is None:
+                self._dev_cols = [DeviceColumn.from_arrow(c, device) for c in rb.columns]
+            return self._dev_cols
 
 
 class BuildImplementation:
@@ -171,7 +260,78 @@ class BuildImplementation:
         sh.ready.wait()
         table = sh.table_for(sh.key_type or "int64")
         table.finish(partition)
-        return consumer.call(GpuIndexLookup(table), sh.concatenated())
+        return consumer.call(GpuIndexLookup(table, sh), sh.concatenated())
+
+
+def _apply_filter(flt: JoinFilter, build_cols: list[DeviceColumn], build_names: Sequence[str],
+                  probe_cols: list[DeviceColumn], probe_names: Sequence[str], b: torch.Tensor, p: torch.Tensor):
+    """apply_join_filter_to_indices: evaluate the filter on the candidate rows, keep the
+    pairs where it is true (order preserved)."""
+    if b.numel() == 0:
+        return b, p
+    lsel = [i for i, n in enumerate(build_names) if flt.left_columns is None or n in flt.left_columns]
+    rsel = [i for i, n in enumerate(probe_names) if flt.right_columns is None or n in flt.right_columns]
+    left = _batch([build_cols[i].take(b) for i in lsel], [build_names[i] for i in lsel])
+    right = _batch([probe_cols[i].take(p) for i in rsel], [probe_names[i] for i in rsel])
+    mask = flt.expression(left, right)
+    if isinstance(mask, pa.ChunkedArray):
+        mask = mask.combine_chunks()
+    keep = np.asarray(mask.fill_null(False).to_numpy(zero_copy_only=False), dtype=np.uint8)
+    rows = select_rows(torch.from_numpy(keep).to(b.device), 1, len(keep))
+    return b[rows], p[rows]
+
+
+def probe_batch(join_type: JoinType, probe_expressions: Sequence[str | int], build_expressions: Sequence[str | int],
+                filter: JoinFilter | None, build_side_records: pa.RecordBatch, read_only_join_map: GpuIndexLookup,
+                probe_batch: pa.RecordBatch, build_visited: torch.Tensor | None = None) -> pa.RecordBatch | None:
+    """One probe batch of any join type: the lookup_*_probe_batch functions of
+    src/operator/probe_lookup_implementation/{inner,left_outer,right_outer,full,left_semi,
+    left_anti,right_semi,right_anti}.rs. Build-side join types only mark `build_visited`
+    here (their rows are emitted by finalize_build_side)."""
+    jt = JoinType.parse(join_type)
+    lookup = read_only_join_map
+    dev = lookup.device
+    (probe_keys,) = evaluate_expressions(probe_expressions, probe_batch)
+    n = probe_batch.num_rows
+    b, p = lookup.matching_indices_device(probe_keys)
+    build_cols = lookup.build_columns(build_side_records)
+    bnames, pnames = list(build_side_records.schema.names), list(probe_batch.schema.names)
+    probe_cols = [DeviceColumn.from_arrow(c, dev) for c in probe_batch.columns]
+    if filter is not None:
+        b, p = _apply_filter(filter, build_cols, bnames, probe_cols, pnames, b, p)
+    if jt.marks_build and build_visited is not None:
+        mark_rows(b, build_side_records.num_rows, build_visited)
+    if jt in (JoinType.LeftSemi, JoinType.LeftAnti):
+        return None
+    if jt in (JoinType.RightSemi, JoinType.RightAnti):
+        flags = mark_rows(p, n)
+        rows = select_rows(flags, 1 if jt is JoinType.RightSemi else 0, n).to(torch.int32)
+        return _batch([c.take(rows) for c in probe_cols], pnames)
+    if jt in (JoinType.Right, JoinType.Full):
+        # append_right_indices(preserve_order = false): unmatched probe rows after the pairs
+        unmatched = select_rows(mark_rows(p, n), 0, n).to(torch.int32)
+        b = torch.cat([b, torch.full((unmatched.numel(),), -1, dtype=torch.int64, device=dev)])
+        p = torch.cat([p, unmatched])
+    return _batch([c.take(b) for c in build_cols] + [c.take(p) for c in probe_cols], bnames + pnames)
+
+
+def finalize_build_side(join_type: JoinType, build_side_records: pa.RecordBatch, lookup: GpuIndexLookup,
+                        build_visited: torch.Tensor, probe_schema: pa.Schema) -> pa.RecordBatch | None:
+    """The once-only build-side emission of the last finishing partition
+    (emit_matched_build_records / emit_unmatched_build_records, e.g.
+    left_semi.rs:166-178, left_outer.rs:174-193, full.rs:181-200)."""
+    jt = JoinType.parse(join_type)
+    if not jt.marks_build:
+        return None
+    nb = build_side_records.num_rows
+    rows = select_rows(build_visited, 1 if jt is JoinType.LeftSemi else 0, nb)
+    cols = lookup.build_columns(build_side_records)
+    out = [c.take(rows).to_arrow() for c in cols]
+    names = list(build_side_records.schema.names)
+    if jt in (JoinType.Left, JoinType.Full):
+        out += [pa.nulls(rows.numel(), type=f.type) for f in probe_schema]
+        names += list(probe_schema.names)
+    return pa.RecordBatch.from_arrays(out, names=names)
 
 
 def lookup_inner_join_probe_batch(probe_expressions: Sequence[str | int], build_expressions: Sequence[str | int],
@@ -179,55 +339,92 @@ def lookup_inner_join_probe_batch(probe_expressions: Sequence[str | int], build_
                                   probe_batch: pa.RecordBatch, output_schema: pa.Schema | None = None
                                   ) -> pa.RecordBatch:
     """src/operator/probe_lookup_implementation/inner.rs:79-129."""
-    if filter is not None:
-        raise NotImplementedError("non-equi JoinFilter is a SURVEY.md §8f row, not implemented")
-    (probe_keys,) = evaluate_expressions(probe_expressions, probe_batch)
-    if probe_batch.num_rows == 0 or build_side_records.num_rows == 0:
-        b = pa.array([], type=pa.uint64())
-        p = pa.array([], type=pa.uint32())
-    else:
-        b, p = read_only_join_map.matching_indices(probe_keys)
-    cols = [pc.take(c, b) for c in build_side_records.columns] + [pc.take(c, p) for c in probe_batch.columns]
-    names = list(build_side_records.schema.names) + list(probe_batch.schema.names)
+    rb = globals()["probe_batch"](JoinType.Inner, probe_expressions, build_expressions, filter, build_side_records,
+                                  read_only_join_map, probe_batch)
     if output_schema is not None:
-        return pa.RecordBatch.from_arrays(cols, schema=output_schema)
-    return pa.RecordBatch.from_arrays(cols, names=names)
+        return pa.RecordBatch.from_arrays(rb.columns, schema=output_schema)
+    return rb
+
+
+class _Finalizer:
+    """LimitedRc<()> over `parallelism` copies: the last release runs the build-side
+    emission (src/utils/limited_rc.rs, InitializeCopiesOnce)."""
+
+    def __init__(self, parallelism: int):
+        self.left = parallelism
+        self.lock = threading.Lock()
+        self.visited: torch.Tensor | None = None
+
+    def visited_for(self, nrows: int, device) -> torch.Tensor:
+        with self.lock:
+            if self.visited is None:
+                self.visited = torch.zeros(max(nrows, 1), dtype=torch.uint8, device=device)
+            return self.visited
+
+    def release(self) -> bool:
+        with self.lock:
+            self.left -= 1
+            return self.left == 0
 
 
 class _ProbeConsumer:
     """PerformProbeLookup (src/operator/parallel_hash_join_executor.rs:20-68)."""
 
-    def __init__(self, probe_stream, probe_expressions, build_expressions):
+    def __init__(self, probe_stream, probe_expressions, build_expressions, join_type=JoinType.Inner, filter=None,
+                 finalizer: _Finalizer | None = None, probe_schema: pa.Schema | None = None):
         self.probe_stream = probe_stream
         self.probe_expressions = probe_expressions
         self.build_expressions = build_expressions
+        self.join_type = JoinType.parse(join_type)
+        self.filter = filter
+        self.finalizer = finalizer
+        self.probe_schema = probe_schema
 
     def call(self, lookup: GpuIndexLookup, record_batch: pa.RecordBatch):
-        return [lookup_inner_join_probe_batch(self.probe_expressions, self.build_expressions, None, record_batch,
-                                              lookup, b) for b in self.probe_stream]
+        jt = self.join_type
+        visited = None
+        if jt.marks_build:
+            visited = self.finalizer.visited_for(record_batch.num_rows, lookup.device)
+        out = []
+        for b in self.probe_stream:
+            rb = probe_batch(jt, self.probe_expressions, self.build_expressions, self.filter, record_batch, lookup, b,
+                             visited)
+            if rb is not None:
+                out.append(rb)
+        if jt.marks_build and self.finalizer.release():
+            rb = finalize_build_side(jt, record_batch, lookup, visited, self.probe_schema)
+            if rb is not None:
+                out.append(rb)
+        return out
 
 
 class ParallelHashJoin:
-    """src/operator/parallel_hash_join.rs:16-168 for JoinType::Inner: `left` is the build
-    side, `right` the probe side, each a list of partitions (lists of RecordBatches).
-    Output partitioning follows the probe side (RoundRobinBatch(N), 85-91)."""
+    """src/operator/parallel_hash_join.rs:16-168: `left` is the build side, `right` the
+    probe side, each a list of partitions (lists of RecordBatches); `join_type` one of
+    JoinType (names as DataFusion's); `filter` an optional JoinFilter. Output
+    partitioning follows the probe side (RoundRobinBatch(N), 85-91); build-side rows of
+    Left / Full / LeftSemi / LeftAnti joins come from the last partition to finish."""
 
     def __init__(self, left: list[list[pa.RecordBatch]], right: list[list[pa.RecordBatch]],
-                 on: Sequence[tuple[str, str]], join_type: str = "inner", device: int = 0,
-                 replacement: JoinReplacement = JoinReplacement.Gpu):
-        if join_type != "inner":
-            raise NotImplementedError(f"join type {join_type} is a SURVEY.md §8f row")
+                 on: Sequence[tuple[str, str]], join_type: JoinType | str = JoinType.Inner, device: int = 0,
+                 replacement: JoinReplacement = JoinReplacement.Gpu, filter: JoinFilter | None = None,
+                 right_schema: pa.Schema | None = None):
         if len(on) != 1:
             raise HjError(HJ_ERR_INVALID, "only single-column equi-join keys are supported")
+        self.join_type = JoinType.parse(join_type)
         n = max(len(left), len(right), 1)
         self.left = list(left) + [[] for _ in range(n - len(left))]
         self.right = list(right) + [[] for _ in range(n - len(right))]
         self.parallelism = n
         self.on = list(on)
+        self.filter = filter
+        self.right_schema = right_schema or next((b.schema for part in self.right for b in part), None)
         self._build = BuildImplementation(replacement, n, device=device)
+        self._finalizer = _Finalizer(n)
 
     def execute(self, partition: int) -> list[pa.RecordBatch]:
-        consumer = _ProbeConsumer(self.right[partition], [self.on[0][1]], [self.on[0][0]])
+        consumer = _ProbeConsumer(self.right[partition], [self.on[0][1]], [self.on[0][0]], self.join_type,
+                                  self.filter, self._finalizer, self.right_schema)
         return self._build.build_side(partition, self.left[partition], [self.on[0][0]], consumer)
 
     def collect(self) -> list[pa.RecordBatch]:

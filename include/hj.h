@@ -193,6 +193,43 @@ hj_status hj_radix_partition(hj_key_type key_type, const void* keys,
                              void* out_keys, uint64_t* out_ids, int64_t* counts,
                              void* workspace, void* stream);
 
+/* ---- join types and output materialisation. Device pointers,
+ *      asynchronous on `stream`. Index arrays are uint32 (idx_bytes 4) or uint64 (8);
+ *      an all-ones index is a null index (the outer joins' missing side). ---------- */
+
+/* flags[idx[i]] = 1 for every idx[i] < nflags: ConcurrentBitSet::set_ones on matched
+ * build indices (src/utils/concurrent_bit_set.rs:28-60, used by
+ * src/operator/probe_lookup_implementation/{left_semi,left_anti,left_outer,full}.rs) and
+ * the matched-probe bitmap of get_semi_indices / get_anti_indices
+ * (src/shared/datafusion_private.rs:85-135). */
+hj_status hj_mark_rows(const void* idx, int idx_bytes, int64_t n, uint8_t* flags, int64_t nflags,
+                       void* stream);
+
+/* Ascending positions i < n with flags[i] == want into out (capacity n), count to
+ * *d_count (device int64): get_set_indices_array / get_unset_indices_array and
+ * get_semi_indices / get_anti_indices. workspace: hj_select_workspace_bytes(n). */
+int64_t hj_select_workspace_bytes(int64_t n);
+hj_status hj_select_rows(const uint8_t* flags, int64_t n, int want, uint64_t* out,
+                         int64_t* d_count, void* workspace, void* stream);
+
+/* Arrow take of a fixed-width column (elem_bytes 1/2/4/8/16) by indices:
+ * dst[i] = src[idx[i]]; dst_valid (optional, 8-byte aligned, ceil(n/64)*8 bytes) gets
+ * bit i = index not null and source row valid. take_multiple_record_batch
+ * (src/shared/shared.rs:83-92). */
+hj_status hj_gather_fixed(const void* src, const uint8_t* src_valid, int64_t src_voff,
+                          int elem_bytes, const void* idx, int idx_bytes, int64_t n, void* dst,
+                          uint8_t* dst_valid, void* stream);
+
+/* Arrow take of a Utf8/Binary (offset_bytes 4) or LargeUtf8/LargeBinary (8) column:
+ * out_offsets[n + 1], out_values (capacity values_cap bytes), dst_valid as above;
+ * *d_values_len (device int64) = bytes needed (values beyond values_cap are not
+ * written: retry with a larger buffer). workspace: hj_gather_var_workspace_bytes(n). */
+int64_t hj_gather_var_workspace_bytes(int64_t n);
+hj_status hj_gather_var(const void* offsets, int offset_bytes, const uint8_t* values,
+                        const uint8_t* src_valid, int64_t src_voff, const void* idx, int idx_bytes,
+                        int64_t n, void* out_offsets, uint8_t* out_values, int64_t values_cap,
+                        uint8_t* dst_valid, int64_t* d_values_len, void* workspace, void* stream);
+
 /* ---- synthetic generators of SURVEY.md §8(d) on the device (bench inputs) ----- */
 /* out[i] = (i * mul) mod range  (unique build keys when gcd(mul, range) = 1);
  * requires n * mul < 2^64 */

@@ -109,3 +109,17 @@ def test_probe_mode_switch(dfp):
     old = L.hj_set_probe_mode(3)
     assert L.hj_set_probe_mode(1) == 3
     assert L.hj_set_probe_mode(old) == 1
+
+
+def test_join_type_names():
+    """DataFusion JoinType names (probe_lookup_implementation.rs:32-43), host logic only."""
+    from datafusion_parallelism_amd.operator import JoinType
+
+    assert JoinType.parse("LEFT OUTER") is JoinType.Left
+    assert JoinType.parse("full_outer") is JoinType.Full
+    assert JoinType.parse("LeftSemi") is JoinType.LeftSemi
+    assert JoinType.parse(JoinType.RightAnti) is JoinType.RightAnti
+    assert [j for j in JoinType if j.marks_build] == [JoinType.Left, JoinType.Full, JoinType.LeftSemi,
+                                                      JoinType.LeftAnti]
+    with pytest.raises(Exception):
+        JoinType.parse("cross")
