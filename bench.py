@@ -173,6 +173,11 @@ def load_traffic(config_name):
 
 
 def main():
+    # The one JSON line goes to the original stdout; everything else that writes to fd 1
+    # (RCCL's version banner, HIP runtime messages) is sent to stderr.
+    json_out = os.fdopen(os.dup(1), "w")
+    sys.stdout.flush()
+    os.dup2(2, 1)
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
@@ -184,6 +189,13 @@ def main():
     args = ap.parse_args()
     cfg = CONFIGS[args.config]
 
+    if args.force_dist and "RANK" not in os.environ:  # one rank without a launcher
+        import socket
+
+        with socket.socket() as so:
+            so.bind(("127.0.0.1", 0))
+            port = so.getsockname()[1]
+        os.environ.update(RANK="0", WORLD_SIZE="1", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -291,7 +303,7 @@ def main():
         }
         if use_dist:
             line["exchange_ms"] = round(float(np.median(job.exchange_ms)), 4)
-        print(json.dumps(line), flush=True)
+        print(json.dumps(line), file=json_out, flush=True)
     if use_dist:
         dist.destroy_process_group()
 
@@ -310,7 +322,7 @@ class DistJob:
     def step(self):
         t0 = time.perf_counter()
         bk, bi, _ = self.dj.shard(self.bk, self.bbase)
-        pk, pi, _ = self.dj.shard(self.pk, self.pbase)
+        pk, pi, _ = self.dj.shard(self.pk, self.pbase, torch.int32)
         torch.cuda.synchronize(self.dev)
         t1 = time.perf_counter()
         self.exchange_ms.append((t1 - t0) * 1e3)

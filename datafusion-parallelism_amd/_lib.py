@@ -20,7 +20,7 @@ LIB_PATH = os.path.join(HERE, "lib", "libdfp_hj.so")
 
 HJ_OK, HJ_ERR_INVALID, HJ_ERR_OOM, HJ_ERR_HIP, HJ_ERR_RCCL, HJ_ERR_CAPACITY, HJ_ERR_NO_DEVICE = range(7)
 HJ_INT32, HJ_INT64 = 0, 1
-HJ_INPUT_DEVICE, HJ_BORROW, HJ_OUTPUT_HOST = 1, 2, 4
+HJ_INPUT_DEVICE, HJ_BORROW, HJ_OUTPUT_HOST, HJ_IDS_U31 = 1, 2, 4, 8
 
 STATUS_NAMES = {
     HJ_OK: "HJ_OK", HJ_ERR_INVALID: "HJ_ERR_INVALID", HJ_ERR_OOM: "HJ_ERR_OOM", HJ_ERR_HIP: "HJ_ERR_HIP",
@@ -71,7 +71,7 @@ SIGNATURES = [
     ("hj_probe_async_ids", I32, [P, P, P, I64, P, I64, P, P, I64, P, P, P]),
     ("hj_table_stream_wait", I32, [P, P]),
     ("hj_partition_workspace_bytes", I64, [I64, I32]),
-    ("hj_radix_partition", I32, [I32, P, P, I64, P, U64, I64, I32, P, P, P, P, P]),
+    ("hj_radix_partition", I32, [I32, P, P, I64, P, U64, I64, I32, P, P, I32, P, P, P]),
     ("hj_mark_rows", I32, [P, I32, I64, P, I64, P]),
     ("hj_select_workspace_bytes", I64, [I64]),
     ("hj_select_rows", I32, [P, I64, I32, P, P, P, P]),

@@ -216,6 +216,7 @@ struct hj_table {
     hj_status build_st = HJ_OK;
     std::string build_err;
     bool has_ids = false, has_no_ids = false;
+    bool ids_u31 = true;  // every id batch carries HJ_IDS_U31: ids replace row numbers
 
     std::vector<int64_t> part_off;
     int64_t total_rows = 0;
@@ -287,7 +288,8 @@ hj_status build_attempt(hj_table* t, const std::vector<Segment>& segs, double lf
     t->tbl = (Bucket*)p;
     if ((st = dev_alloc(t, t->allocs, &p, sizeof(uint32_t) * (size_t)(2 * total + 2))) != HJ_OK) return st;
     t->dup_rows = (uint32_t*)p;
-    if (t->has_ids) {
+    const bool ids_as_rows = t->has_ids && t->ids_u31;  // no id indirection at probe time
+    if (t->has_ids && !ids_as_rows) {
         if ((st = dev_alloc(t, t->allocs, &p, sizeof(uint64_t) * (size_t)std::max<int64_t>(total, 1))) != HJ_OK)
             return st;
         t->row_ids = (uint64_t*)p;
@@ -332,7 +334,8 @@ hj_status build_attempt(hj_table* t, const std::vector<Segment>& segs, double lf
     hipDeviceProp_t* prop = device_props(t->device);
     const int cus = prop ? prop->multiProcessorCount : 256;
     HIP_TRY(launch_build(t->key_bytes, d_segs, (int)segs.size(), total, t->nb, t->clog2, t->nchunks, hist, hist1,
-                         ntiles, scan, tkeys, trows, skeys, srows, t->row_ids, t->tbl, t->dup_rows, big, ctr, cus, s));
+                         ntiles, scan, tkeys, trows, skeys, srows, t->row_ids, ids_as_rows, t->tbl, t->dup_rows,
+                         big, ctr, cus, s));
     BuildCounters hc;
     HIP_TRY(hipMemcpyAsync(&hc, ctr, sizeof(hc), hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
@@ -506,8 +509,12 @@ hj_status hj_build_append(hj_table* t, int partition, const void* keys, const ui
         if (t->finished[partition])
             return fail(HJ_ERR_INVALID, "State already consumed for partition " + std::to_string(partition));
         if (n > 0) {
-            if (ids) t->has_ids = true;
-            else t->has_no_ids = true;
+            if (ids) {
+                t->has_ids = true;
+                if (!(flags & HJ_IDS_U31)) t->ids_u31 = false;
+            } else {
+                t->has_no_ids = true;
+            }
         }
     }
     HIP_TRY(hipSetDevice(t->device));
@@ -768,6 +775,7 @@ hj_status hj_table_lookup(const hj_table* t, int64_t key, uint64_t* rows, int64_
 hj_status hj_table_chain_links(const hj_table* t, int64_t* prev, int64_t n) {
     hj_status st = check_table(t);
     if (st != HJ_OK) return st;
+    if (t->has_ids) return fail(HJ_ERR_INVALID, "chain links are defined for canonical row numbering (no explicit ids)");
     if (n != t->total_rows || (n > 0 && prev == nullptr))
         return fail(HJ_ERR_INVALID, "prev must hold build_rows entries");
     if (n == 0) return HJ_OK;
@@ -808,16 +816,19 @@ int64_t hj_partition_workspace_bytes(int64_t n, int nparts) { return radix_parti
 
 hj_status hj_radix_partition(hj_key_type key_type, const void* keys, const uint8_t* validity, int64_t validity_offset,
                              const uint64_t* ids, uint64_t id_base, int64_t n, int nparts, void* out_keys,
-                             uint64_t* out_ids, int64_t* counts, void* workspace, void* stream) {
+                             void* out_ids, int id_bytes, int64_t* counts, void* workspace, void* stream) {
     if (device_count() == 0) return fail(HJ_ERR_NO_DEVICE, "no GPU visible");
     if (nparts < 1 || nparts > 64 || (nparts & (nparts - 1)))
         return fail(HJ_ERR_INVALID, "nparts must be a power of two <= 64");
     if (n < 0) return fail(HJ_ERR_INVALID, "negative length");
+    if (id_bytes != 4 && id_bytes != 8) return fail(HJ_ERR_INVALID, "id_bytes must be 4 or 8");
+    if (id_bytes == 4 && ids == nullptr && (uint64_t)id_base + (uint64_t)n > 0x100000000ull)
+        return fail(HJ_ERR_INVALID, "32-bit ids overflow: id_base + n > 2^32");
     if (!is_device_ptr(keys) || !is_device_ptr(validity) || !is_device_ptr(ids) || !is_device_ptr(out_keys) ||
         !is_device_ptr(out_ids) || !is_device_ptr(counts) || !is_device_ptr(workspace))
         return fail(HJ_ERR_INVALID, "hj_radix_partition takes device pointers");
     HIP_TRY(launch_radix_partition(key_type == HJ_INT64 ? 8 : 4, keys, validity, validity_offset, ids, id_base, n,
-                                   nparts, out_keys, out_ids, counts, workspace, (hipStream_t)stream));
+                                   nparts, out_keys, out_ids, id_bytes, counts, workspace, (hipStream_t)stream));
     return HJ_OK;
 }
 

@@ -8,6 +8,8 @@
 //                     bit 31 set:   offset of its duplicate segment in dup_rows
 //     uint32 meta     bit 0: an insert passed this bucket full (a lookup that misses
 //                     here continues to the next bucket only if set);
+//                     bits 1+6j..6+6j: row count of slot j's duplicated key if <= 63
+//                     (0: read it from dup_rows);
 //                     side bucket: rows of the key INT64_MIN
 //   A key's probe sequence stays inside its chunk of 2^clog2 buckets (linear probing
 //   modulo the chunk), so one workgroup can build a whole chunk in LDS.
@@ -32,6 +34,8 @@ constexpr int kSlots = 5;
 constexpr unsigned kDupFlag = 0x80000000u;
 constexpr unsigned kMiss = 0xFFFFFFFFu;
 constexpr int kSmallSeg = 16;  // dup segments up to this size are sorted by one thread
+constexpr unsigned kInlineCount = 63;           // dup row counts kept in the bucket's meta
+constexpr unsigned kCountUnknown = 0xFFFFFFFFu;  // count not inline: read dup_rows[off]
 
 struct alignas(64) Bucket {
     unsigned long long key[kSlots];

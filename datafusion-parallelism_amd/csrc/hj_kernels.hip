@@ -109,7 +109,7 @@ constexpr int kRowBatch = 8;
 template <typename K>
 __device__ __forceinline__ void load_rows(const Segment* __restrict__ segs, int nseg, int64_t base, int64_t r1,
                                           int64_t (&key)[kRowBatch], bool (&ok)[kRowBatch],
-                                          uint64_t* __restrict__ row_ids, int64_t* rows) {
+                                          uint64_t* __restrict__ row_ids, int64_t* rows, bool ids_as_rows) {
     if (nseg == 1) {  // the whole tile inside one append: uniform pointers, loads batch up
         const Segment sg = segs[0];
 #pragma unroll
@@ -121,6 +121,7 @@ __device__ __forceinline__ void load_rows(const Segment* __restrict__ segs, int 
             if (ok[u]) {
                 const int64_t i = r - sg.row_base;
                 if (row_ids != nullptr && sg.ids != nullptr) row_ids[r] = sg.ids[i];
+                if (ids_as_rows && rows) rows[u] = (int64_t)sg.ids[i];
                 ok[u] = bit_valid(sg.valid, sg.voff, i);
                 key[u] = ld_key<K>(sg.keys, i);
             }
@@ -137,6 +138,7 @@ __device__ __forceinline__ void load_rows(const Segment* __restrict__ segs, int 
             const Segment& sg = segs[find_seg(segs, nseg, r)];  // independent per row
             const int64_t i = r - sg.row_base;
             if (row_ids != nullptr && sg.ids != nullptr) row_ids[r] = sg.ids[i];
+            if (ids_as_rows && rows) rows[u] = (int64_t)sg.ids[i];
             ok[u] = bit_valid(sg.valid, sg.voff, i);
             key[u] = ld_key<K>(sg.keys, i);
         }
@@ -162,7 +164,7 @@ coarse_hist_kernel(const Segment* __restrict__ segs, int nseg, int64_t total, ui
     for (int64_t base = r0; base < r1; base += kHistThreads * kRowBatch) {
         int64_t key[kRowBatch];
         bool ok[kRowBatch];
-        load_rows<K>(tsegs, tns, base, r1, key, ok, nullptr, nullptr);
+        load_rows<K>(tsegs, tns, base, r1, key, ok, nullptr, nullptr, false);
 #pragma unroll
         for (int u = 0; u < kRowBatch; ++u)
             if (ok[u]) atomicAdd(&s_h[wave][chunk_of(key[u], nb, clog2, nchunks) >> gshift], 1u);
@@ -289,7 +291,7 @@ __global__ void __launch_bounds__(kHistThreads)
 coarse_scatter_kernel(const Segment* __restrict__ segs, int nseg, int64_t total, uint32_t nb, uint32_t clog2,
                       uint32_t nchunks, uint32_t gshift, uint32_t ngroups, const uint32_t* __restrict__ hist1,
                       int64_t ntiles, unsigned long long* __restrict__ tkeys, uint32_t* __restrict__ trows,
-                      uint64_t* __restrict__ row_ids) {
+                      uint64_t* __restrict__ row_ids, bool ids_as_rows) {
     __shared__ uint32_t s_cur[kCoarseBins];
     for (uint32_t g = threadIdx.x; g < ngroups; g += kHistThreads) s_cur[g] = hist1[(int64_t)g * ntiles + blockIdx.x];
     __syncthreads();
@@ -302,7 +304,7 @@ coarse_scatter_kernel(const Segment* __restrict__ segs, int nseg, int64_t total,
     for (int64_t base = r0; base < r1; base += kHistThreads * kRowBatch) {
         int64_t key[kRowBatch], row[kRowBatch];
         bool ok[kRowBatch];
-        load_rows<K>(tsegs, tns, base, r1, key, ok, row_ids, row);
+        load_rows<K>(tsegs, tns, base, r1, key, ok, row_ids, row, ids_as_rows);
 #pragma unroll
         for (int u = 0; u < kRowBatch; ++u) {
             if (!ok[u]) continue;
@@ -559,6 +561,9 @@ chunk_build_kernel(uint32_t nb, uint32_t clog2, uint32_t nchunks, const uint32_t
                 big[bi] = BigSeg{side ? kSign : (B.key[sl % kSlots] ^ kSign), d_off[li], 0u};
             }
             ref = kDupFlag | d_off[li];
+            // small row counts inline in meta (6 bits per slot): the probe's count pass
+            // then needs no dup_rows access
+            if (!side && d_cnt[li] <= kInlineCount) atomicOr(&B.meta, d_cnt[li] << (1 + 6 * (sl % kSlots)));
         }
     }
     __syncthreads();
@@ -588,7 +593,7 @@ constexpr int kBigLds = 4096;
 
 __global__ void __launch_bounds__(kBigThreads)
 dup_sort_big_kernel(uint32_t* dup_rows, const BigSeg* __restrict__ big, const BuildCounters* ctr,
-                    const Segment* __restrict__ segs, int nseg, int64_t total, int key_bytes) {
+                    const Segment* __restrict__ segs, int nseg, int64_t total, int key_bytes, bool ids_as_rows) {
     __shared__ uint32_t s_v[kBigLds];
     __shared__ unsigned s_wave[kBigThreads / 64];
     const unsigned long long nbig = ctr->n_big;
@@ -623,11 +628,13 @@ dup_sort_big_kernel(uint32_t* dup_rows, const BigSeg* __restrict__ big, const Bu
             for (int64_t base = 0; base < total; base += kBigThreads) {
                 const int64_t r = base + threadIdx.x;
                 bool hit = false;
+                uint32_t rv = (uint32_t)r;
                 if (r < total) {
                     while (si + 1 < nseg && segs[si + 1].row_base <= r) ++si;
                     const Segment& sg = segs[si];
                     const int64_t i = r - sg.row_base;
                     if (bit_valid(sg.valid, sg.voff, i)) hit = (seg_key(sg, i, key_bytes) == key);
+                    if (ids_as_rows) rv = (uint32_t)sg.ids[i];
                 }
                 const unsigned long long m = __ballot(hit);
                 const unsigned below = __popcll(m & ((1ull << lane) - 1));
@@ -640,7 +647,7 @@ dup_sort_big_kernel(uint32_t* dup_rows, const BigSeg* __restrict__ big, const Bu
                 }
                 if (hit) {
                     const unsigned long long rank = done + woff + below;  // ascending rank
-                    rows[n - 1 - rank] = (uint32_t)r;                    // descending layout
+                    rows[n - 1 - rank] = rv;                             // descending layout
                 }
                 done += tot;
                 __syncthreads();
@@ -695,7 +702,7 @@ __device__ __forceinline__ uint32_t ref_count(const uint32_t* dup_rows, uint32_t
 // the chunk. Slots fill in order and are never freed, so an empty slot ends a key's probe
 // sequence, and so does a full bucket that no insert ever passed. Branch-free.
 __device__ __forceinline__ uint32_t scan_line(const uint4& a0, const uint4& a1, const uint4& a2, const uint4& a3,
-                                              unsigned long long sk, bool* more) {
+                                              unsigned long long sk, bool* more, uint32_t* cnt) {
     const unsigned long long k0 = ((unsigned long long)a0.y << 32) | a0.x;
     const unsigned long long k1 = ((unsigned long long)a0.w << 32) | a0.z;
     const unsigned long long k2 = ((unsigned long long)a1.y << 32) | a1.x;
@@ -709,6 +716,16 @@ __device__ __forceinline__ uint32_t scan_line(const uint4& a0, const uint4& a1, 
     ref = e1 ? a2.w : ref;
     ref = e0 ? a2.z : ref;
     *more = (ref == kMiss) & !z & ((a3.w & 1u) != 0);
+    // row count: 0 miss, 1 single row, the inline meta count of a duplicated key, or
+    // kCountUnknown (read dup_rows[off])
+    const uint32_t m = a3.w;
+    uint32_t c = e4 ? (m >> 25) : 0u;
+    c = e3 ? (m >> 19) : c;
+    c = e2 ? (m >> 13) : c;
+    c = e1 ? (m >> 7) : c;
+    c = e0 ? (m >> 1) : c;
+    c &= 63u;
+    *cnt = ref == kMiss ? 0u : (!(ref & kDupFlag) ? 1u : (c ? c : kCountUnknown));
     return ref;
 }
 
@@ -716,7 +733,7 @@ __device__ __forceinline__ uint32_t scan_line(const uint4& a0, const uint4& a1, 
 template <typename K, bool HAS_VALID, bool NT = false>
 __device__ __forceinline__ void lookup4(const TableView& tv, const void* __restrict__ keys,
                                         const uint8_t* __restrict__ valid, int64_t voff, int64_t n, bool vec,
-                                        int64_t row0, uint32_t (&ref)[4]) {
+                                        int64_t row0, uint32_t (&ref)[4], uint32_t (&cnt)[4]) {
     const Bucket* __restrict__ tbl = tv.tbl;
     const uint32_t cmask = (1u << tv.clog2) - 1;
     int64_t k[4];
@@ -740,12 +757,13 @@ __device__ __forceinline__ void lookup4(const TableView& tv, const void* __restr
     bool more[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-        ref[q] = scan_line(L0[q], L1[q], L2[q], L3[q], sk[q], &more[q]);
-        if (sk[q] == 0) {  // INT64_MIN: the side bucket (ref[0] = word 10, meta = word 15)
+        ref[q] = scan_line(L0[q], L1[q], L2[q], L3[q], sk[q], &more[q], &cnt[q]);
+        if (sk[q] == 0) {  // INT64_MIN: the side bucket (ref[0] = word 10, meta = word 15 = rows)
             ref[q] = L3[q].w ? L2[q].z : kMiss;
+            cnt[q] = L3[q].w;
             more[q] = false;
         }
-        if (!in[q]) { ref[q] = kMiss; more[q] = false; }
+        if (!in[q]) { ref[q] = kMiss; cnt[q] = 0; more[q] = false; }
     }
     // rare: the home line is full and does not hold the key
 #pragma unroll
@@ -754,9 +772,13 @@ __device__ __forceinline__ void lookup4(const TableView& tv, const void* __restr
         for (uint32_t probes = 0; more[q] && probes < cmask; ++probes) {
             bb = (bb & ~cmask) | ((bb + 1) & cmask);
             const uint4* p = reinterpret_cast<const uint4*>(tbl + bb);
-            ref[q] = scan_line(p[0], p[1], p[2], p[3], sk[q], &more[q]);
+            ref[q] = scan_line(p[0], p[1], p[2], p[3], sk[q], &more[q], &cnt[q]);
         }
     }
+}
+
+__device__ __forceinline__ uint32_t resolve_count(const uint32_t* dup_rows, uint32_t ref, uint32_t cnt) {
+    return cnt == kCountUnknown ? dup_rows[ref & ~kDupFlag] : cnt;
 }
 
 template <typename K, bool HAS_VALID>
@@ -770,10 +792,10 @@ probe_lookup_kernel(TableView tv, const void* __restrict__ keys, const uint8_t* 
     for (int g = 0; g < kGroups; ++g) {
         const int64_t row0 = tile0 + (int64_t)g * (kProbeThreads * 4) + (int64_t)threadIdx.x * 4;
         if (row0 >= n) break;
-        uint32_t ref[4];
-        lookup4<K, HAS_VALID>(tv, keys, valid, voff, n, vec, row0, ref);
+        uint32_t ref[4], cnt[4];
+        lookup4<K, HAS_VALID>(tv, keys, valid, voff, n, vec, row0, ref, cnt);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) tsum += ref_count(tv.dup_rows, ref[q]);
+        for (int q = 0; q < 4; ++q) tsum += resolve_count(tv.dup_rows, ref[q], cnt[q]);
         if (vec && row0 + 4 <= n) {
             *reinterpret_cast<uint4*>(info + row0) = make_uint4(ref[0], ref[1], ref[2], ref[3]);
         } else {
@@ -888,16 +910,16 @@ probe_fused_kernel(TableView tv, const void* __restrict__ keys, const uint8_t* _
 #pragma unroll
     for (int g = 0; g < kGroups; ++g) {
         const int64_t row0 = tile0 + (int64_t)g * (kProbeThreads * 4) + (int64_t)threadIdx.x * 4;
-        uint32_t ref[4] = {kMiss, kMiss, kMiss, kMiss};
+        uint32_t ref[4] = {kMiss, kMiss, kMiss, kMiss}, cnt[4] = {0, 0, 0, 0};
         if (row0 < n) {
-            if (nt & 1) lookup4<K, HAS_VALID, true>(tv, keys, valid, voff, n, vec, row0, ref);
-            else lookup4<K, HAS_VALID, false>(tv, keys, valid, voff, n, vec, row0, ref);
+            if (nt & 1) lookup4<K, HAS_VALID, true>(tv, keys, valid, voff, n, vec, row0, ref, cnt);
+            else lookup4<K, HAS_VALID, false>(tv, keys, valid, voff, n, vec, row0, ref, cnt);
         }
         *reinterpret_cast<uint4*>(s_ref + g * (kProbeThreads * 4) + threadIdx.x * 4) =
             make_uint4(ref[0], ref[1], ref[2], ref[3]);
         unsigned long long s = 0;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) s += ref_count(tv.dup_rows, ref[q]);
+        for (int q = 0; q < 4; ++q) s += resolve_count(tv.dup_rows, ref[q], cnt[q]);
         const unsigned long long ws = wave_sum<unsigned long long>(s);
         if (lane == 0) s_w[g][wave] = ws;
     }
@@ -1234,12 +1256,13 @@ pp_lookup_kernel(TableView tv, PieceGeom pg, int64_t n, int64_t ntiles, const un
                     const uint32_t r = r0 + u * 64 + lane;
                     if (r >= R) continue;
                     bool more;
-                    uint32_t ref = scan_line(a0[u], a1[u], a2[u], a3[u], sk[u], &more);
+                    uint32_t c_unused;
+                    uint32_t ref = scan_line(a0[u], a1[u], a2[u], a3[u], sk[u], &more, &c_unused);
                     uint32_t bb = b0[u];
                     for (uint32_t probes = 0; more && probes < cmask; ++probes) {
                         bb = (bb & ~cmask) | ((bb + 1) & cmask);
                         const uint4* q = reinterpret_cast<const uint4*>(tbl + bb);
-                        ref = scan_line(q[0], q[1], q[2], q[3], sk[u], &more);
+                        ref = scan_line(q[0], q[1], q[2], q[3], sk[u], &more, &c_unused);
                     }
                     __builtin_nontemporal_store(ref, info + row[u]);
                     const uint32_t c = ref_count(tv.dup_rows, ref);
@@ -1362,10 +1385,10 @@ __global__ void part_counts_kernel(const uint32_t* hist, int64_t nblocks, int np
     }
 }
 
-template <typename K>
+template <typename K, typename ID>
 __global__ void __launch_bounds__(kPartThreads)
 part_scatter_kernel(const void* keys, const uint8_t* valid, int64_t voff, const uint64_t* ids, uint64_t id_base,
-                    int64_t n, int nparts, const uint32_t* hist, int64_t nblocks, K* out_keys, uint64_t* out_ids) {
+                    int64_t n, int nparts, const uint32_t* hist, int64_t nblocks, K* out_keys, ID* out_ids) {
     __shared__ unsigned long long s_off[kMaxParts];
     __shared__ unsigned s_wc[kPartThreads / 64][kMaxParts];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -1392,7 +1415,7 @@ part_scatter_kernel(const void* keys, const uint8_t* valid, int64_t voff, const 
             unsigned long long pos = s_off[p] + rank;
             for (int w = 0; w < wave; ++w) pos += s_wc[w][p];
             out_keys[pos] = (K)ld_key<K>(keys, i);
-            out_ids[pos] = ids ? ids[i] : id_base + (uint64_t)i;
+            out_ids[pos] = (ID)(ids ? ids[i] : id_base + (uint64_t)i);
         }
         __syncthreads();
         for (int q = threadIdx.x; q < nparts; q += kPartThreads) {
@@ -1460,8 +1483,8 @@ hipError_t launch_scan_u64(unsigned long long* a, int64_t len, void* scratch, un
 hipError_t launch_build(int key_bytes, const Segment* d_segs, int nseg, int64_t total, uint32_t nb, uint32_t clog2,
                         uint32_t nchunks, uint32_t* hist, uint32_t* hist1, int64_t ntiles, void* scan_scratch,
                         unsigned long long* tkeys, uint32_t* trows, unsigned long long* skeys, uint32_t* srows,
-                        uint64_t* row_ids, Bucket* tbl, uint32_t* dup_rows, BigSeg* big, BuildCounters* ctr,
-                        int big_grid, hipStream_t s) {
+                        uint64_t* row_ids, bool ids_as_rows, Bucket* tbl, uint32_t* dup_rows, BigSeg* big,
+                        BuildCounters* ctr, int big_grid, hipStream_t s) {
     const size_t hist_lds = sizeof(uint32_t) * (nchunks + 1);
     const int64_t hlen = (int64_t)(nchunks + 1) * ntiles;
     const uint32_t gshift = coarse_shift(nchunks);
@@ -1479,10 +1502,12 @@ hipError_t launch_build(int key_bytes, const Segment* d_segs, int nseg, int64_t 
         if (e != hipSuccess) return e;
         if (key_bytes == 8)
             coarse_scatter_kernel<int64_t><<<(unsigned)ntiles, kHistThreads, 0, s>>>(
-                d_segs, nseg, total, nb, clog2, nchunks, gshift, ngroups, hist1, ntiles, tkeys, trows, row_ids);
+                d_segs, nseg, total, nb, clog2, nchunks, gshift, ngroups, hist1, ntiles, tkeys, trows, row_ids,
+                ids_as_rows);
         else
             coarse_scatter_kernel<int32_t><<<(unsigned)ntiles, kHistThreads, 0, s>>>(
-                d_segs, nseg, total, nb, clog2, nchunks, gshift, ngroups, hist1, ntiles, tkeys, trows, row_ids);
+                d_segs, nseg, total, nb, clog2, nchunks, gshift, ngroups, hist1, ntiles, tkeys, trows, row_ids,
+                ids_as_rows);
         // level 2: chunk order (tiles over the n_valid group-ordered rows)
         if ((e = hipMemsetAsync(hist, 0, sizeof(uint32_t) * (size_t)hlen, s)) != hipSuccess) return e;
         fine_hist_kernel<<<(unsigned)ntiles, kHistThreads, hist_lds, s>>>(tkeys, ctr, nb, clog2, nchunks, gshift, hist,
@@ -1506,7 +1531,8 @@ hipError_t launch_build(int key_bytes, const Segment* d_segs, int nseg, int64_t 
     if (ntiles > 0) {
         chunk_build_kernel<<<nchunks + 1, kChunkThreads, lds, s>>>(nb, clog2, nchunks, hist, ntiles, skeys, srows, tbl,
                                                                    dup_rows, big, ctr, dupcap);
-        dup_sort_big_kernel<<<big_grid, kBigThreads, 0, s>>>(dup_rows, big, ctr, d_segs, nseg, total, key_bytes);
+        dup_sort_big_kernel<<<big_grid, kBigThreads, 0, s>>>(dup_rows, big, ctr, d_segs, nseg, total, key_bytes,
+                                                             ids_as_rows);
     }
     return hipGetLastError();
 }
@@ -1702,7 +1728,7 @@ int64_t radix_partition_workspace(int64_t n, int nparts) {
 
 hipError_t launch_radix_partition(int key_bytes, const void* keys, const uint8_t* valid, int64_t voff,
                                   const uint64_t* ids, uint64_t id_base, int64_t n, int nparts, void* out_keys,
-                                  uint64_t* out_ids, int64_t* counts, void* workspace, hipStream_t s) {
+                                  void* out_ids, int id_bytes, int64_t* counts, void* workspace, hipStream_t s) {
     if (nparts < 1 || nparts > kMaxParts || (nparts & (nparts - 1))) return hipErrorInvalidValue;
     const int64_t nblocks = (n + kPartChunk - 1) / kPartChunk;
     if (nblocks == 0) return hipMemsetAsync(counts, 0, sizeof(int64_t) * nparts, s);
@@ -1719,12 +1745,16 @@ hipError_t launch_radix_partition(int key_bytes, const void* keys, const uint8_t
     hipError_t e = launch_scan(hist, hlen, scratch, nullptr, s);
     if (e != hipSuccess) return e;
     part_counts_kernel<<<1, 64, 0, s>>>(hist, nblocks, nparts, total, counts);
-    if (key_bytes == 8)
-        part_scatter_kernel<int64_t><<<(unsigned)nblocks, kPartThreads, 0, s>>>(
-            keys, valid, voff, ids, id_base, n, nparts, hist, nblocks, (int64_t*)out_keys, out_ids);
-    else
-        part_scatter_kernel<int32_t><<<(unsigned)nblocks, kPartThreads, 0, s>>>(
-            keys, valid, voff, ids, id_base, n, nparts, hist, nblocks, (int32_t*)out_keys, out_ids);
+#define DFP_PS(K, ID)                                                                              \
+    part_scatter_kernel<K, ID><<<(unsigned)nblocks, kPartThreads, 0, s>>>(keys, valid, voff, ids, id_base, n, \
+                                                                         nparts, hist, nblocks, (K*)out_keys, \
+                                                                         (ID*)out_ids)
+    if (key_bytes == 8) {
+        if (id_bytes == 8) DFP_PS(int64_t, uint64_t); else DFP_PS(int64_t, uint32_t);
+    } else {
+        if (id_bytes == 8) DFP_PS(int32_t, uint64_t); else DFP_PS(int32_t, uint32_t);
+    }
+#undef DFP_PS
     return hipGetLastError();
 }
 

@@ -24,8 +24,8 @@ hipError_t launch_build(int key_bytes, const Segment* d_segs, int nseg, int64_t 
                         uint32_t nb, uint32_t clog2, uint32_t nchunks, uint32_t* hist,
                         uint32_t* hist1, int64_t ntiles, void* scan_scratch,
                         unsigned long long* tkeys, uint32_t* trows, unsigned long long* skeys,
-                        uint32_t* srows, uint64_t* row_ids, Bucket* tbl, uint32_t* dup_rows,
-                        BigSeg* big, BuildCounters* ctr, int big_grid, hipStream_t s);
+                        uint32_t* srows, uint64_t* row_ids, bool ids_as_rows, Bucket* tbl,
+                        uint32_t* dup_rows, BigSeg* big, BuildCounters* ctr, int big_grid, hipStream_t s);
 
 // ---- probe ---------------------------------------------------------------
 // 0 auto (= direct), 1 direct, 2 partitioned (L2-resident pieces per XCD)
@@ -48,7 +48,7 @@ hipError_t launch_chain_links(const TableView& tv, int64_t* prev, int64_t nrows,
 // ---- multi-GPU radix partition -------------------------------------------
 hipError_t launch_radix_partition(int key_bytes, const void* keys, const uint8_t* valid,
                                   int64_t voff, const uint64_t* ids, uint64_t id_base,
-                                  int64_t n, int nparts, void* out_keys, uint64_t* out_ids,
+                                  int64_t n, int nparts, void* out_keys, void* out_ids, int id_bytes,
                                   int64_t* counts, void* workspace, hipStream_t s);
 int64_t radix_partition_workspace(int64_t n, int nparts);
 

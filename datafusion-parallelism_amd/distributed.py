@@ -27,19 +27,20 @@ from .table import HashTable
 
 
 def gpu_radix_partition(keys: torch.Tensor, ids: torch.Tensor | None, id_base: int, nparts: int,
-                        stream: int | None = None):
-    """hj_radix_partition on device tensors -> (keys grouped by destination,
-    u64 ids as int64, counts[nparts] int64 device tensor)."""
+                        stream: int | None = None, id_dtype: torch.dtype = torch.int64):
+    """hj_radix_partition on device tensors -> (keys grouped by destination, ids
+    (int64 = u64 build ids, int32 = u32 probe ids), counts[nparts] int64 device tensor)."""
     L = _lib.load()
     n = keys.numel()
     kt = HJ_INT64 if keys.dtype == torch.int64 else HJ_INT32
     out_k = torch.empty(n, dtype=keys.dtype, device=keys.device)
-    out_i = torch.empty(n, dtype=torch.int64, device=keys.device)
+    out_i = torch.empty(n, dtype=id_dtype, device=keys.device)
     counts = torch.zeros(nparts, dtype=torch.int64, device=keys.device)
     ws = torch.empty(max(L.hj_partition_workspace_bytes(n, nparts), 8), dtype=torch.uint8, device=keys.device)
     s = stream if stream is not None else torch.cuda.current_stream(keys.device).cuda_stream
     check(L.hj_radix_partition(kt, keys.data_ptr(), None, 0, None if ids is None else ids.data_ptr(), id_base, n,
-                               nparts, out_k.data_ptr(), out_i.data_ptr(), counts.data_ptr(), ws.data_ptr(), s))
+                               nparts, out_k.data_ptr(), out_i.data_ptr(), 8 if id_dtype == torch.int64 else 4,
+                               counts.data_ptr(), ws.data_ptr(), s))
     return out_k, out_i, counts
 
 
@@ -49,11 +50,16 @@ def gpu_local_join(build_keys: torch.Tensor, build_ids: torch.Tensor, probe_keys
     probe ids -> (build_idx int64 [u64 values], probe_idx int32 [u32 values])."""
     dev = probe_keys.device
     kt = "int64" if build_keys.dtype == torch.int64 else "int32"
+    # received build ids ascend (stable partition, ranks in order): when they also fit
+    # 31 bits the table keeps them in place of row numbers (no id gather per pair)
+    nbi = build_ids.numel()
+    u31 = nbi == 0 or bool(((build_ids[-1] < 2**31) & (build_ids[0] >= 0) &
+                            (nbi < 2 or bool((build_ids[1:] > build_ids[:-1]).all()))).item())
     with HashTable(1, kt, dev.index or 0) as t:
-        t.append(0, build_keys, ids=build_ids)
+        t.append(0, build_keys, ids=build_ids, ids_u31=u31)
         t.finish(0)
         n = probe_keys.numel()
-        pid32 = probe_ids.to(torch.int32)
+        pid32 = probe_ids if probe_ids.dtype == torch.int32 else probe_ids.to(torch.int32)
         ws = torch.empty(HashTable.workspace_bytes(n), dtype=torch.uint8, device=dev)
         d_total = torch.zeros(1, dtype=torch.int64, device=dev)
         cap = max(capacity_hint or n, 1)
@@ -104,13 +110,19 @@ class DistributedHashJoin:
         self.partition_fn = partition_fn or gpu_radix_partition
         self.local_join_fn = local_join_fn or gpu_local_join
 
-    def shard(self, keys: torch.Tensor, id_base: int):
-        k, i, c = self.partition_fn(keys, None, id_base, self.world)
+    def shard(self, keys: torch.Tensor, id_base: int, id_dtype: torch.dtype = torch.int64):
+        """Partition by destination rank and exchange: -> (keys, global ids, stats).
+        Build rows carry u64 ids (int64), probe rows u32 ids (int32, the reference's
+        UInt32 probe index): 16 resp. 12 bytes per int64-key row on the wire."""
+        if self.partition_fn is gpu_radix_partition:
+            k, i, c = gpu_radix_partition(keys, None, id_base, self.world, id_dtype=id_dtype)
+        else:
+            k, i, c = self.partition_fn(keys, None, id_base, self.world)
         return all_to_all_rows(k, i, c, self.group)
 
     def run(self, build_keys: torch.Tensor, build_base: int, probe_keys: torch.Tensor, probe_base: int,
             capacity_hint: int | None = None):
         """-> this rank's share of the global pairs (build_idx, probe_idx)."""
         bk, bi, _ = self.shard(build_keys, build_base)
-        pk, pi, _ = self.shard(probe_keys, probe_base)
+        pk, pi, _ = self.shard(probe_keys, probe_base, torch.int32)
         return self.local_join_fn(bk, bi, pk, pi, capacity_hint)

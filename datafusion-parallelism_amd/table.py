@@ -14,7 +14,7 @@ import numpy as np
 import torch
 
 from . import _lib
-from ._lib import HJ_BORROW, HJ_INPUT_DEVICE, HJ_INT32, HJ_INT64, HJ_OUTPUT_HOST, check
+from ._lib import HJ_BORROW, HJ_IDS_U31, HJ_INPUT_DEVICE, HJ_INT32, HJ_INT64, HJ_OUTPUT_HOST, check
 
 try:  # pyarrow is optional for the device path
     import pyarrow as pa
@@ -109,11 +109,15 @@ class HashTable:
         self._keep = []  # borrowed device inputs stay alive until the barrier
 
     # -- build --------------------------------------------------------------
-    def append(self, partition: int, keys, valid=None, ids=None, borrow: bool = True) -> None:
+    def append(self, partition: int, keys, valid=None, ids=None, borrow: bool = True, ids_u31: bool = False) -> None:
+        """ids_u31: the explicit ids are < 2^31 and ascend in canonical row order (the
+        table then stores them in place of row numbers, HJ_IDS_U31)."""
         ki = as_key_input(keys, valid)
         if ki.n and ki.key_type != self.key_type:
             raise TypeError("key type of the batch differs from the table's")
         flags = ki.flags | (HJ_BORROW if (borrow and ki.flags & HJ_INPUT_DEVICE) else 0)
+        if ids is not None and ids_u31:
+            flags |= HJ_IDS_U31
         ids_ptr, keep_ids = None, None
         if ids is not None:
             if isinstance(ids, torch.Tensor):

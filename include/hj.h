@@ -48,7 +48,11 @@ enum {
     HJ_INPUT_DEVICE = 1u << 0, /* pointers are device memory (else host memory, copied) */
     HJ_BORROW = 1u << 1,       /* device input is not copied: caller keeps it alive until
                                   hj_build_finish returns on every partition */
-    HJ_OUTPUT_HOST = 1u << 2   /* hj_probe: return pairs in host memory (else device) */
+    HJ_OUTPUT_HOST = 1u << 2,  /* hj_probe: return pairs in host memory (else device) */
+    HJ_IDS_U31 = 1u << 3       /* hj_build_append: the explicit ids are < 2^31 and ascend in
+                                  canonical row order; when every id batch says so the table
+                                  stores the ids in place of row numbers (pairs carry them
+                                  with no id gather at probe time) */
 };
 
 typedef struct hj_table hj_table; /* opaque, device resident */
@@ -182,15 +186,16 @@ hj_status hj_table_stream_wait(const hj_table* t, void* stream);
  *      src/utils/partitioned_concurrent_self_hash_join_map.rs:13-16). ------------ */
 
 /* Partition n rows into `nparts` (power of two) by hash bits:
- * out_keys/out_ids are grouped by destination; counts[nparts] (device int64) receives
- * the rows per destination. ids may be NULL (then id = id_base + i). Null rows are
- * dropped. Device pointers, asynchronous on `stream`; `workspace` of
- * hj_partition_workspace_bytes(n, nparts) bytes. */
+ * out_keys/out_ids are grouped by destination (stable); counts[nparts] (device int64)
+ * receives the rows per destination. ids may be NULL (then id = id_base + i); out_ids
+ * holds uint64 (id_bytes 8, build rows) or uint32 (id_bytes 4, probe rows: the
+ * reference's UInt32 probe indices) ids. Null rows are dropped. Device pointers,
+ * asynchronous on `stream`; `workspace` of hj_partition_workspace_bytes(n, nparts) bytes. */
 int64_t hj_partition_workspace_bytes(int64_t n, int nparts);
 hj_status hj_radix_partition(hj_key_type key_type, const void* keys,
                              const uint8_t* validity, int64_t validity_offset,
                              const uint64_t* ids, uint64_t id_base, int64_t n, int nparts,
-                             void* out_keys, uint64_t* out_ids, int64_t* counts,
+                             void* out_keys, void* out_ids, int id_bytes, int64_t* counts,
                              void* workspace, void* stream);
 
 /* ---- join types and output materialisation. Device pointers,

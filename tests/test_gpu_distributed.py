@@ -25,12 +25,13 @@ def _mix64(k):
 
 
 @pytest.mark.parametrize("nparts", [1, 2, 8, 64])
-def test_radix_partition_kernel(dfp, nparts):
+@pytest.mark.parametrize("id_dtype", [torch.int64, torch.int32])
+def test_radix_partition_kernel(dfp, nparts, id_dtype):
     from datafusion_parallelism_amd.distributed import gpu_radix_partition
 
     rng = np.random.default_rng(nparts)
     k = rng.integers(-10**12, 10**12, 100003)
-    out_k, out_i, counts = gpu_radix_partition(torch.from_numpy(k).cuda(), None, 1000, nparts)
+    out_k, out_i, counts = gpu_radix_partition(torch.from_numpy(k).cuda(), None, 1000, nparts, id_dtype=id_dtype)
     dest = (_mix64(k) & np.uint64(nparts - 1)).astype(np.int64)
     order = np.argsort(dest, kind="stable")  # stable multi-split
     assert np.array_equal(counts.cpu().numpy(), np.bincount(dest, minlength=nparts))

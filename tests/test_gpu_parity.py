@@ -260,3 +260,28 @@ def test_c3_full_size_digest(dfp, oracle_mod):
     assert bool((pl[1:] >= pl[:-1]).all().item())
     same = pl[1:] == pl[:-1]
     assert bool((b[1:][same] < b[:-1][same]).all().item())
+
+
+@pytest.mark.parametrize("ids_u31", [False, True])
+@pytest.mark.parametrize("dups", [1, 300, 5000])
+def test_explicit_build_ids(dfp, oracle_mod, probe_mode, ids_u31, dups):
+    """Explicit (global) build ids, as the multi-GPU exchange hands them over: pairs carry
+    the ids, ordered by id descending within a probe row. ids_u31 stores the ids in place
+    of row numbers (HJ_IDS_U31); without it they are gathered from the id array. Covers
+    segments sorted in registers, in LDS and by the ordered rescan (> 4096 rows)."""
+    rng = np.random.default_rng(dups + ids_u31)
+    bk = np.concatenate([rng.integers(0, 3000, 20000), np.full(dups, 77)]).astype(np.int64)
+    rng.shuffle(bk)
+    bv = rng.random(len(bk)) > 0.05
+    ids = np.cumsum(rng.integers(1, 50, len(bk))).astype(np.int64) + 10**6  # ascending, sparse
+    pk = np.concatenate([rng.integers(0, 4000, 30000), [77, 77]]).astype(np.int64)
+    with dfp.HashTable(2, "int64", 0) as t:
+        h = len(bk) // 2
+        t.append(0, torch.from_numpy(bk[:h].copy()).cuda(), bv[:h], ids=torch.from_numpy(ids[:h].copy()).cuda(),
+                 ids_u31=ids_u31)
+        t.append(1, torch.from_numpy(bk[h:].copy()).cuda(), bv[h:], ids=torch.from_numpy(ids[h:].copy()).cuda(),
+                 ids_u31=ids_u31)
+        t.finish_all()
+        b, p = t.probe(torch.from_numpy(pk).cuda())
+    ob, op = oracle_mod.inner_join(bk, pk, bv, None)
+    assert_same(b, p, ids[ob.astype(np.int64)].astype(np.uint64), op)

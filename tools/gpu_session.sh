@@ -58,6 +58,21 @@ for s in $STEPS; do
           --output-format csv -- python3 tools/probe_one.py > $O/lf_$v.log 2>&1 || { tail -30 $O/lf_$v.log; exit 1; }
         unset DFP_HJ_LOAD_FACTOR
       done ;;
+    c3)
+      run timeout -k 10 400 python3 bench.py --config c3 --no-cpu-baseline > $O/bench_c3.json 2> $O/bench_c3.err \
+        || { tail -30 $O/bench_c3.err; exit 1; }
+      cat $O/bench_c3.json ;;
+    dist)
+      run timeout -k 10 400 python3 bench.py --force-dist --no-cpu-baseline --steps 5 > $O/bench_dist.json \
+        2> $O/bench_dist.err || { tail -30 $O/bench_dist.err; exit 1; }
+      cat $O/bench_dist.json
+      run timeout -k 10 400 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 \
+        --master-port 29533 bench.py --gpus 1 --steps 5 --warmup 2 --no-cpu-baseline > $O/bench_trun.json \
+        2> $O/bench_trun.err || { tail -30 $O/bench_trun.err; exit 1; }
+      cat $O/bench_trun.json ;;
+    pcie)
+      run timeout -k 10 400 python3 tools/pcie_rate.py > $O/pcie.json 2> $O/pcie.err || { tail -30 $O/pcie.err; exit 1; }
+      cat $O/pcie.json ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
