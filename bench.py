@@ -186,6 +186,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--force-dist", action="store_true",
                     help="use the radix-exchange path even with one rank (testing)")
+    ap.add_argument("--chunks", type=int, default=4,
+                    help="multi-GPU: probe-side chunks whose exchange overlaps the previous chunk's probe")
     args = ap.parse_args()
     cfg = CONFIGS[args.config]
 
@@ -215,7 +217,7 @@ def main():
     else:
         from datafusion_parallelism_amd.distributed import DistributedHashJoin
 
-        job = DistJob(DistributedHashJoin(), bk, pk, rank, dev)
+        job = DistJob(DistributedHashJoin(chunks=args.chunks), bk, pk, rank, dev)
 
     def barrier():
         if use_dist:
@@ -309,7 +311,10 @@ def main():
 
 
 class DistJob:
-    """One step = radix-partition + RCCL all-to-all of both sides + local build + probe."""
+    """One step = radix-partition + RCCL all-to-all of the build side, local build, then
+    the probe side in chunks whose all-to-all overlaps the previous chunk's probe.
+    exchange_ms = the build-side exchange; probe_ms (HIP events) = local build +
+    pipelined probe-side exchange and probes."""
 
     def __init__(self, dj, bk, pk, rank, dev):
         self.dj, self.bk, self.pk, self.dev = dj, bk, pk, dev
@@ -322,19 +327,22 @@ class DistJob:
     def step(self):
         t0 = time.perf_counter()
         bk, bi, _ = self.dj.shard(self.bk, self.bbase)
-        pk, pi, _ = self.dj.shard(self.pk, self.pbase, torch.int32)
         torch.cuda.synchronize(self.dev)
         t1 = time.perf_counter()
         self.exchange_ms.append((t1 - t0) * 1e3)
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
-        from datafusion_parallelism_amd.distributed import gpu_local_join
-
         ev[0].record()
-        b, p = gpu_local_join(bk, bi, pk, pi, self.cap)
+        if self.dj.chunks > 1:
+            outs = self.dj.run_pipelined(bk, bi, self.pk, self.pbase)
+        else:
+            from datafusion_parallelism_amd.distributed import gpu_local_join
+
+            pk, pi, _ = self.dj.shard(self.pk, self.pbase, torch.int32)
+            outs = [gpu_local_join(bk, bi, pk, pi, self.cap)]
         ev[1].record()
         self._ev = ev
         self._t1 = t1
-        self.matches = b.numel()
+        self.matches = sum(b.numel() for b, _ in outs)
 
     def collect(self):
         torch.cuda.synchronize(self.dev)

@@ -44,36 +44,66 @@ def gpu_radix_partition(keys: torch.Tensor, ids: torch.Tensor | None, id_base: i
     return out_k, out_i, counts
 
 
-def gpu_local_join(build_keys: torch.Tensor, build_ids: torch.Tensor, probe_keys: torch.Tensor,
-                   probe_ids: torch.Tensor, capacity_hint: int | None = None):
-    """Build this rank's shard with explicit global build ids and probe it with global
-    probe ids -> (build_idx int64 [u64 values], probe_idx int32 [u32 values])."""
-    dev = probe_keys.device
-    kt = "int64" if build_keys.dtype == torch.int64 else "int32"
-    # received build ids ascend (stable partition, ranks in order): when they also fit
-    # 31 bits the table keeps them in place of row numbers (no id gather per pair)
-    nbi = build_ids.numel()
-    u31 = nbi == 0 or bool(((build_ids[-1] < 2**31) & (build_ids[0] >= 0) &
-                            (nbi < 2 or bool((build_ids[1:] > build_ids[:-1]).all()))).item())
-    with HashTable(1, kt, dev.index or 0) as t:
-        t.append(0, build_keys, ids=build_ids, ids_u31=u31)
-        t.finish(0)
+class GpuLocalTable:
+    """One rank's shard table (global build ids held in place of row numbers when they
+    fit 31 bits and ascend, HJ_IDS_U31) and asynchronous probes of received chunks."""
+
+    def __init__(self, build_keys: torch.Tensor, build_ids: torch.Tensor):
+        dev = build_keys.device
+        kt = "int64" if build_keys.dtype == torch.int64 else "int32"
+        # received build ids ascend (stable partition, ranks in order): when they also
+        # fit 31 bits the table keeps them in place of row numbers (no id gather per pair)
+        nbi = build_ids.numel()
+        u31 = nbi == 0 or bool(((build_ids[-1] < 2**31) & (build_ids[0] >= 0) &
+                                (nbi < 2 or bool((build_ids[1:] > build_ids[:-1]).all()))).item())
+        self.table = HashTable(1, kt, dev.index or 0)
+        self.table.append(0, build_keys, ids=build_ids, ids_u31=u31)
+        self.table.finish(0)
+        self.device = dev
+
+    def probe(self, probe_keys: torch.Tensor, probe_ids: torch.Tensor, capacity: int | None = None):
+        """Enqueue the probe on the current stream (no host sync); returns a finaliser
+        that waits and yields (build_idx int64 [u64 values], probe_idx int32 [u32])."""
+        dev = self.device
         n = probe_keys.numel()
         pid32 = probe_ids if probe_ids.dtype == torch.int32 else probe_ids.to(torch.int32)
         ws = torch.empty(HashTable.workspace_bytes(n), dtype=torch.uint8, device=dev)
         d_total = torch.zeros(1, dtype=torch.int64, device=dev)
-        cap = max(capacity_hint or n, 1)
+        cap = max(capacity or n, 1)
         s = torch.cuda.current_stream(dev).cuda_stream
-        for _ in range(2):
-            ob = torch.empty(cap, dtype=torch.int64, device=dev)
-            op = torch.empty(cap, dtype=torch.int32, device=dev)
-            t.probe_async(probe_keys.data_ptr(), n, ob.data_ptr(), op.data_ptr(), cap, d_total.data_ptr(),
-                          ws.data_ptr(), s, probe_ids_ptr=pid32.data_ptr())
+
+        def launch(c):
+            ob = torch.empty(c, dtype=torch.int64, device=dev)
+            op = torch.empty(c, dtype=torch.int32, device=dev)
+            self.table.probe_async(probe_keys.data_ptr(), n, ob.data_ptr(), op.data_ptr(), c, d_total.data_ptr(),
+                                   ws.data_ptr(), s, probe_ids_ptr=pid32.data_ptr())
+            return ob, op
+
+        ob, op = launch(cap)
+
+        def result():
+            nonlocal ob, op
             total = int(d_total.item())
-            if total <= cap:
-                return ob[:total], op[:total]
-            cap = total
-    raise RuntimeError("unreachable")
+            if total > cap:  # rare (duplicate-heavy keys): once more with the exact size
+                ob, op = launch(total)
+                total = int(d_total.item())
+            return ob[:total], op[:total]
+
+        return result
+
+    def close(self):
+        self.table.close()
+
+
+def gpu_local_join(build_keys: torch.Tensor, build_ids: torch.Tensor, probe_keys: torch.Tensor,
+                   probe_ids: torch.Tensor, capacity_hint: int | None = None):
+    """Build this rank's shard with explicit global build ids and probe it with global
+    probe ids -> (build_idx int64 [u64 values], probe_idx int32 [u32 values])."""
+    t = GpuLocalTable(build_keys, build_ids)
+    try:
+        return t.probe(probe_keys, probe_ids, capacity_hint)()
+    finally:
+        t.close()
 
 
 @dataclass
@@ -83,9 +113,11 @@ class ExchangeStats:
 
 
 def all_to_all_rows(keys_by_dest: torch.Tensor, ids_by_dest: torch.Tensor, counts: torch.Tensor,
-                    group=None) -> tuple[torch.Tensor, torch.Tensor, ExchangeStats]:
-    """Exchange destination-grouped rows: counts first (all_to_all of G int64), then
-    keys and ids with uneven splits (all_to_all_single)."""
+                    group=None, async_op: bool = False):
+    """Exchange destination-grouped rows: counts first (all_to_all of G int64, host
+    sync for the split sizes), then keys and ids with uneven splits (all_to_all_single).
+    -> (keys, ids, stats[, works]); with async_op the row exchanges are left in flight
+    (wait on `works` before using keys / ids)."""
     world = dist.get_world_size(group)
     recv_counts = torch.empty_like(counts)
     dist.all_to_all_single(recv_counts, counts, group=group)
@@ -94,35 +126,80 @@ def all_to_all_rows(keys_by_dest: torch.Tensor, ids_by_dest: torch.Tensor, count
     assert len(send) == world
     rk = torch.empty(sum(recv), dtype=keys_by_dest.dtype, device=keys_by_dest.device)
     ri = torch.empty(sum(recv), dtype=ids_by_dest.dtype, device=ids_by_dest.device)
-    dist.all_to_all_single(rk, keys_by_dest, output_split_sizes=recv, input_split_sizes=send, group=group)
-    dist.all_to_all_single(ri, ids_by_dest, output_split_sizes=recv, input_split_sizes=send, group=group)
-    return rk, ri, ExchangeStats(sum(send), sum(recv))
+    w1 = dist.all_to_all_single(rk, keys_by_dest, output_split_sizes=recv, input_split_sizes=send, group=group,
+                                async_op=async_op)
+    w2 = dist.all_to_all_single(ri, ids_by_dest, output_split_sizes=recv, input_split_sizes=send, group=group,
+                                async_op=async_op)
+    st = ExchangeStats(sum(send), sum(recv))
+    if async_op:
+        return rk, ri, st, [w1, w2]
+    return rk, ri, st
 
 
 class DistributedHashJoin:
     """Inner equi-join of a build and a probe column that are each spread over the ranks
-    (rank r holds rows [base_r, base_r + n_r) of the global column)."""
+    (rank r holds rows [base_r, base_r + n_r) of the global column).
 
-    def __init__(self, group=None, partition_fn: Callable | None = None, local_join_fn: Callable | None = None):
+    chunks > 1 pipelines the probe side: the all-to-all of chunk c runs (RCCL stream)
+    while chunk c-1 is probed (compute stream); each rank's output is then canonical
+    per chunk (the concatenation of the chunks' canonical outputs). `local_build_fn(bk,
+    bi) -> table` with `table.probe(pk, pi, cap) -> result()` and `table.close()`
+    default to GpuLocalTable."""
+
+    def __init__(self, group=None, partition_fn: Callable | None = None, local_join_fn: Callable | None = None,
+                 chunks: int = 1, local_build_fn: Callable | None = None):
         self.group = group
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
         self.partition_fn = partition_fn or gpu_radix_partition
         self.local_join_fn = local_join_fn or gpu_local_join
+        self.local_build_fn = local_build_fn or GpuLocalTable
+        self.chunks = max(1, int(chunks))
 
-    def shard(self, keys: torch.Tensor, id_base: int, id_dtype: torch.dtype = torch.int64):
+    def _partition(self, keys: torch.Tensor, id_base: int, id_dtype: torch.dtype):
+        if self.partition_fn is gpu_radix_partition:
+            return gpu_radix_partition(keys, None, id_base, self.world, id_dtype=id_dtype)
+        return self.partition_fn(keys, None, id_base, self.world)
+
+    def shard(self, keys: torch.Tensor, id_base: int, id_dtype: torch.dtype = torch.int64, async_op: bool = False):
         """Partition by destination rank and exchange: -> (keys, global ids, stats).
         Build rows carry u64 ids (int64), probe rows u32 ids (int32, the reference's
         UInt32 probe index): 16 resp. 12 bytes per int64-key row on the wire."""
-        if self.partition_fn is gpu_radix_partition:
-            k, i, c = gpu_radix_partition(keys, None, id_base, self.world, id_dtype=id_dtype)
-        else:
-            k, i, c = self.partition_fn(keys, None, id_base, self.world)
-        return all_to_all_rows(k, i, c, self.group)
+        k, i, c = self._partition(keys, id_base, id_dtype)
+        return all_to_all_rows(k, i, c, self.group, async_op=async_op)
 
     def run(self, build_keys: torch.Tensor, build_base: int, probe_keys: torch.Tensor, probe_base: int,
             capacity_hint: int | None = None):
         """-> this rank's share of the global pairs (build_idx, probe_idx)."""
         bk, bi, _ = self.shard(build_keys, build_base)
-        pk, pi, _ = self.shard(probe_keys, probe_base, torch.int32)
-        return self.local_join_fn(bk, bi, pk, pi, capacity_hint)
+        if self.chunks <= 1:
+            pk, pi, _ = self.shard(probe_keys, probe_base, torch.int32)
+            return self.local_join_fn(bk, bi, pk, pi, capacity_hint)
+        outs = self.run_pipelined(bk, bi, probe_keys, probe_base)
+        return torch.cat([b for b, _ in outs]), torch.cat([p for _, p in outs])
+
+    def run_pipelined(self, bk: torch.Tensor, bi: torch.Tensor, probe_keys: torch.Tensor, probe_base: int):
+        """Local build, then the probe side in `chunks` slices: exchange of slice c in
+        flight while slice c-1 is probed. -> list of per-chunk (build_idx, probe_idx)."""
+        table = self.local_build_fn(bk, bi)
+        try:
+            n = probe_keys.numel()
+            bounds = [n * c // self.chunks for c in range(self.chunks + 1)]
+            results, pending = [], None
+            for c in range(self.chunks):
+                lo, hi = bounds[c], bounds[c + 1]
+                rk, ri, _, works = self.shard(probe_keys[lo:hi], probe_base + lo, torch.int32, async_op=True)
+                if pending is not None:
+                    results.append(self._probe_chunk(table, *pending))
+                pending = (rk, ri, works)
+            results.append(self._probe_chunk(table, *pending))
+            return [r() for r in results]
+        finally:
+            table.close()
+
+    @staticmethod
+    def _probe_chunk(table, rk, ri, works):
+        for w in works:
+            if w is not None:
+                w.wait()  # RCCL: the compute stream waits for the exchange (no host block)
+        return table.probe(rk, ri, rk.numel())

@@ -44,22 +44,50 @@ def oracle_local_join(bk, bi, pk, pi, cap=None):
     return torch.from_numpy(bi.numpy()[b.astype(np.int64)]), torch.from_numpy(pi.numpy()[p.astype(np.int64)])
 
 
-def _worker(rank, world, port, bks, pks, q):
+class CpuLocalTable:
+    """Test-local stand-in for GpuLocalTable (the oracle joins each received chunk)."""
+
+    def __init__(self, bk, bi):
+        self.bk, self.bi = bk, bi
+
+    def probe(self, pk, pi, cap=None):
+        b, p = oracle_local_join(self.bk, self.bi, pk, pi)
+        return lambda: (b, p)
+
+    def close(self):
+        pass
+
+
+def _canonical(b, p):
+    pl = p.numpy().astype(np.int64)
+    bl = b.numpy().astype(np.int64)
+    same = pl[1:] == pl[:-1]
+    return bool(np.all(pl[1:] >= pl[:-1]) and np.all(bl[1:][same] < bl[:-1][same]))
+
+
+def _worker(rank, world, port, bks, pks, q, chunks=1):
     sys.path.insert(0, ROOT)
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from datafusion_parallelism_amd.distributed import DistributedHashJoin
 
-    dj = DistributedHashJoin(partition_fn=cpu_partition, local_join_fn=oracle_local_join)
+    dj = DistributedHashJoin(partition_fn=cpu_partition, local_join_fn=oracle_local_join, chunks=chunks,
+                             local_build_fn=CpuLocalTable)
     bbase = sum(len(x) for x in bks[:rank])
     pbase = sum(len(x) for x in pks[:rank])
-    b, p = dj.run(torch.from_numpy(bks[rank]), bbase, torch.from_numpy(pks[rank]), pbase)
-    # every rank's local output is already canonical for its key subset
+    if chunks == 1:
+        b, p = dj.run(torch.from_numpy(bks[rank]), bbase, torch.from_numpy(pks[rank]), pbase)
+        segs = [(b, p)]
+    else:  # pipelined probe side: canonical per chunk
+        bk, bi, _ = dj.shard(torch.from_numpy(bks[rank]), bbase)
+        segs = dj.run_pipelined(bk, bi, torch.from_numpy(pks[rank]), pbase)
+        assert len(segs) == chunks
+        b, p = torch.cat([x for x, _ in segs]), torch.cat([y for _, y in segs])
+    # every rank's local output is canonical for its key subset (per chunk)
+    ok = all(_canonical(x, y) for x, y in segs)
     pl = p.numpy().astype(np.int64)
     bl = b.numpy().astype(np.int64)
-    same = pl[1:] == pl[:-1]
-    ok = bool(np.all(pl[1:] >= pl[:-1]) and np.all(bl[1:][same] < bl[:-1][same]))
     sizes = [None] * world
     dist.all_gather_object(sizes, (bl.tolist(), pl.tolist(), ok))
     if rank == 0:
@@ -75,8 +103,8 @@ def _free_port():
     return port
 
 
-@pytest.mark.parametrize("world", [2])
-def test_distributed_exchange_matches_single_join(oracle_mod, world):
+@pytest.mark.parametrize("world,chunks", [(2, 1), (2, 3)])
+def test_distributed_exchange_matches_single_join(oracle_mod, world, chunks):
     rng = np.random.default_rng(9)
     bk = rng.integers(0, 3000, 9000).astype(np.int64)
     pk = rng.integers(0, 5000, 14000).astype(np.int64)
@@ -85,7 +113,7 @@ def test_distributed_exchange_matches_single_join(oracle_mod, world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, bks, pks, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, bks, pks, q, chunks)) for r in range(world)]
     for pr in procs:
         pr.start()
     res = q.get(timeout=240)

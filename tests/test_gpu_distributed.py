@@ -39,7 +39,10 @@ def test_radix_partition_kernel(dfp, nparts, id_dtype):
     assert np.array_equal(out_i.cpu().numpy(), order + 1000)
 
 
-def test_distributed_join_one_rank(dfp, oracle_mod):
+@pytest.mark.parametrize("chunks", [1, 3])
+def test_distributed_join_one_rank(dfp, oracle_mod, chunks):
+    """One RCCL rank (the exchange is a self-copy): pairs equal the oracle's; with
+    chunks > 1 the probe side is pipelined (one rank keeps the global order)."""
     from datafusion_parallelism_amd.distributed import DistributedHashJoin
 
     s = socket.socket()
@@ -52,7 +55,7 @@ def test_distributed_join_one_rank(dfp, oracle_mod):
         rng = np.random.default_rng(4)
         bk = rng.integers(0, 30000, 100000)
         pk = rng.integers(0, 50000, 300000)
-        b, p = DistributedHashJoin().run(torch.from_numpy(bk).cuda(), 0, torch.from_numpy(pk).cuda(), 0)
+        b, p = DistributedHashJoin(chunks=chunks).run(torch.from_numpy(bk).cuda(), 0, torch.from_numpy(pk).cuda(), 0)
         ob, op = oracle_mod.inner_join(bk, pk)
         assert np.array_equal(b.cpu().numpy().astype(np.uint64), ob)
         assert np.array_equal(p.cpu().numpy().astype(np.uint32), op)

@@ -73,6 +73,10 @@ for s in $STEPS; do
     pcie)
       run timeout -k 10 400 python3 tools/pcie_rate.py > $O/pcie.json 2> $O/pcie.err || { tail -30 $O/pcie.err; exit 1; }
       cat $O/pcie.json ;;
+    distprof)
+      run timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/dist -o d --output-format csv \
+        -- python3 bench.py --force-dist --no-cpu-baseline --steps 5 > $O/distprof.json 2> $O/distprof.err \
+        || { tail -30 $O/distprof.err; exit 1; } ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
