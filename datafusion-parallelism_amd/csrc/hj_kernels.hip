@@ -286,52 +286,133 @@ scan_down_kernel(T* __restrict__ a, int64_t len, const unsigned long long* __res
 // build 2: the two scatters (positions from the scanned histograms; order inside a
 // group / chunk is canonicalised by the chunk build)
 // ---------------------------------------------------------------------------
+// LDS-staged scatter of one sub-batch (<= kHistThreads * kRowBatch rows) whose rows sit in
+// registers (key, row, bin in [0, R)): counting sort by bin in LDS, then stores in bin
+// order, so that consecutive lanes write consecutive addresses (whole lines instead of
+// one line per lane). s_cur[b] = next global position of bin b (advanced here).
+constexpr int kStageRows = kHistThreads * kRowBatch;  // 8192 rows: 64 KB keys + 32 KB rows
+constexpr int kStageMaxBins = 2048;
+constexpr size_t kStageLds = (size_t)kStageRows * 12 + (size_t)kStageMaxBins * 12;
+
+__device__ __forceinline__ void staged_scatter_batch(const unsigned long long (&key)[kRowBatch],
+                                                     const uint32_t (&row)[kRowBatch], const int (&bin)[kRowBatch],
+                                                     uint32_t R, unsigned long long* s_k, uint32_t* s_r,
+                                                     uint32_t* s_cur, uint32_t* s_cnt, uint32_t* s_st, uint32_t* s_w,
+                                                     unsigned long long* __restrict__ out_k,
+                                                     uint32_t* __restrict__ out_r) {
+    for (uint32_t b = threadIdx.x; b < R; b += kHistThreads) s_cnt[b] = 0;
+    __syncthreads();
+    uint32_t lrank[kRowBatch];
+#pragma unroll
+    for (int u = 0; u < kRowBatch; ++u) lrank[u] = bin[u] >= 0 ? atomicAdd(&s_cnt[bin[u]], 1u) : 0u;
+    __syncthreads();
+    // exclusive scan of the bin counts (R <= 2048: two bins per thread)
+    const uint32_t b0 = 2 * threadIdx.x;
+    const uint32_t c0 = b0 < R ? s_cnt[b0] : 0u, c1 = b0 + 1 < R ? s_cnt[b0 + 1] : 0u;
+    uint32_t nsub;
+    const uint32_t ex = block_excl_scan<uint32_t>(c0 + c1, s_w, &nsub);
+    if (b0 < R) s_st[b0] = ex;
+    if (b0 + 1 < R) s_st[b0 + 1] = ex + c0;
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < kRowBatch; ++u) {
+        if (bin[u] < 0) continue;
+        const uint32_t pos = s_st[bin[u]] + lrank[u];
+        s_k[pos] = key[u];
+        s_r[pos] = row[u];
+    }
+    __syncthreads();
+    // stores in bin order: the element's bin is found by a binary search of s_st
+    for (uint32_t i = threadIdx.x; i < nsub; i += kHistThreads) {
+        uint32_t lo = 0, hi = R - 1;
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi + 1) >> 1;
+            if (s_st[mid] <= i) lo = mid; else hi = mid - 1;
+        }
+        // empty bins share their start with the next bin: take the last bin starting <= i
+        const uint32_t g = s_cur[lo] + (i - s_st[lo]);
+        out_k[g] = s_k[i];
+        out_r[g] = s_r[i];
+    }
+    __syncthreads();
+    for (uint32_t b = threadIdx.x; b < R; b += kHistThreads) s_cur[b] += s_cnt[b];
+    __syncthreads();
+}
+
 template <typename K>
 __global__ void __launch_bounds__(kHistThreads)
-coarse_scatter_kernel(const Segment* __restrict__ segs, int nseg, int64_t total, uint32_t nb, uint32_t clog2,
-                      uint32_t nchunks, uint32_t gshift, uint32_t ngroups, const uint32_t* __restrict__ hist1,
-                      int64_t ntiles, unsigned long long* __restrict__ tkeys, uint32_t* __restrict__ trows,
-                      uint64_t* __restrict__ row_ids, bool ids_as_rows) {
-    __shared__ uint32_t s_cur[kCoarseBins];
-    for (uint32_t g = threadIdx.x; g < ngroups; g += kHistThreads) s_cur[g] = hist1[(int64_t)g * ntiles + blockIdx.x];
-    __syncthreads();
-    const int64_t r0 = (int64_t)blockIdx.x * kBuildTile;
-    const int64_t r1 = min<int64_t>(total, r0 + kBuildTile);
+coarse_scatter_staged_kernel(const Segment* __restrict__ segs, int nseg, int64_t total, uint32_t nb, uint32_t clog2,
+                             uint32_t nchunks, uint32_t gshift, uint32_t ngroups, const uint32_t* __restrict__ hist1,
+                             int64_t ntiles, unsigned long long* __restrict__ tkeys, uint32_t* __restrict__ trows,
+                             uint64_t* __restrict__ row_ids, bool ids_as_rows) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    unsigned long long* s_k = reinterpret_cast<unsigned long long*>(smem);
+    uint32_t* s_r = reinterpret_cast<uint32_t*>(s_k + kStageRows);
+    uint32_t* s_cur = s_r + kStageRows;
+    uint32_t* s_cnt = s_cur + kStageMaxBins;
+    uint32_t* s_st = s_cnt + kStageMaxBins;
+    __shared__ uint32_t s_w[kHistThreads / 64];
     __shared__ Segment s_seg[kTileSegs];
     __shared__ int s_info[2];
+    for (uint32_t g = threadIdx.x; g < ngroups; g += kHistThreads) s_cur[g] = hist1[(int64_t)g * ntiles + blockIdx.x];
+    const int64_t r0 = (int64_t)blockIdx.x * kBuildTile;
+    const int64_t r1 = min<int64_t>(total, r0 + kBuildTile);
     int tns;
-    const Segment* tsegs = tile_segments(segs, nseg, r0, r1, s_seg, s_info, &tns);
-    for (int64_t base = r0; base < r1; base += kHistThreads * kRowBatch) {
-        int64_t key[kRowBatch], row[kRowBatch];
+    const Segment* tsegs = tile_segments(segs, nseg, r0, r1, s_seg, s_info, &tns);  // syncs
+    for (int64_t base = r0; base < r1; base += kStageRows) {
+        int64_t k64[kRowBatch], rr[kRowBatch];
         bool ok[kRowBatch];
-        load_rows<K>(tsegs, tns, base, r1, key, ok, row_ids, row, ids_as_rows);
+        load_rows<K>(tsegs, tns, base, r1, k64, ok, row_ids, rr, ids_as_rows);
+        unsigned long long key[kRowBatch];
+        uint32_t row[kRowBatch];
+        int bin[kRowBatch];
 #pragma unroll
         for (int u = 0; u < kRowBatch; ++u) {
-            if (!ok[u]) continue;
-            const uint32_t pos = atomicAdd(&s_cur[chunk_of(key[u], nb, clog2, nchunks) >> gshift], 1u);
-            tkeys[pos] = (unsigned long long)key[u];
-            trows[pos] = (uint32_t)row[u];
+            key[u] = (unsigned long long)k64[u];
+            row[u] = (uint32_t)rr[u];
+            bin[u] = ok[u] ? (int)(chunk_of(k64[u], nb, clog2, nchunks) >> gshift) : -1;
         }
+        staged_scatter_batch(key, row, bin, ngroups, s_k, s_r, s_cur, s_cnt, s_st, s_w, tkeys, trows);
     }
 }
 
 __global__ void __launch_bounds__(kHistThreads)
-fine_scatter_kernel(const unsigned long long* __restrict__ tkeys, const uint32_t* __restrict__ trows,
-                    const BuildCounters* __restrict__ ctr, uint32_t nb, uint32_t clog2, uint32_t nchunks,
-                    uint32_t gshift, const uint32_t* __restrict__ hist, int64_t ntiles,
-                    unsigned long long* __restrict__ skeys, uint32_t* __restrict__ srows) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t s_cur[];
+fine_scatter_staged_kernel(const unsigned long long* __restrict__ tkeys, const uint32_t* __restrict__ trows,
+                           const BuildCounters* __restrict__ ctr, uint32_t nb, uint32_t clog2, uint32_t nchunks,
+                           uint32_t gshift, const uint32_t* __restrict__ hist, int64_t ntiles,
+                           unsigned long long* __restrict__ skeys, uint32_t* __restrict__ srows) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    unsigned long long* s_k = reinterpret_cast<unsigned long long*>(smem);
+    uint32_t* s_r = reinterpret_cast<uint32_t*>(s_k + kStageRows);
+    uint32_t* s_cur = s_r + kStageRows;
+    uint32_t* s_cnt = s_cur + kStageMaxBins;
+    uint32_t* s_st = s_cnt + kStageMaxBins;
+    __shared__ uint32_t s_w[kHistThreads / 64];
     const int64_t nvalid = (int64_t)ctr->n_valid;
     const int64_t r0 = (int64_t)blockIdx.x * kBuildTile;
     const int64_t r1 = min<int64_t>(nvalid, r0 + kBuildTile);
     if (r0 >= r1) return;
     uint32_t lo, hi;
     fine_range(tkeys, r0, r1, nb, clog2, nchunks, gshift, &lo, &hi);
-    for (uint32_t c = lo + threadIdx.x; c <= hi; c += kHistThreads) s_cur[c - lo] = hist[(int64_t)c * ntiles + blockIdx.x];
+    const uint32_t R = hi - lo + 1;
+    if (R > (uint32_t)kStageMaxBins) {  // a tile spanning many groups (tiny or skewed inputs): direct stores
+        uint32_t* s_c = reinterpret_cast<uint32_t*>(smem);  // staging area: (nchunks + 1) <= 16384 cursors
+        for (uint32_t c = lo + threadIdx.x; c <= hi; c += kHistThreads) s_c[c - lo] = hist[(int64_t)c * ntiles + blockIdx.x];
+        __syncthreads();
+        for (int64_t r = r0 + threadIdx.x; r < r1; r += kHistThreads) {
+            const unsigned long long key = tkeys[r];
+            const uint32_t pos = atomicAdd(&s_c[chunk_of((int64_t)key, nb, clog2, nchunks) - lo], 1u);
+            skeys[pos] = key;
+            srows[pos] = trows[r];
+        }
+        return;
+    }
+    for (uint32_t b = threadIdx.x; b < R; b += kHistThreads) s_cur[b] = hist[(int64_t)(lo + b) * ntiles + blockIdx.x];
     __syncthreads();
-    for (int64_t base = r0; base < r1; base += kHistThreads * kRowBatch) {
+    for (int64_t base = r0; base < r1; base += kStageRows) {
         unsigned long long key[kRowBatch];
         uint32_t row[kRowBatch];
+        int bin[kRowBatch];
 #pragma unroll
         for (int u = 0; u < kRowBatch; ++u) {
             const int64_t r = base + (int64_t)u * kHistThreads + threadIdx.x;
@@ -340,11 +421,10 @@ fine_scatter_kernel(const unsigned long long* __restrict__ tkeys, const uint32_t
         }
 #pragma unroll
         for (int u = 0; u < kRowBatch; ++u) {
-            if (base + (int64_t)u * kHistThreads + threadIdx.x >= r1) continue;
-            const uint32_t pos = atomicAdd(&s_cur[chunk_of((int64_t)key[u], nb, clog2, nchunks) - lo], 1u);
-            skeys[pos] = key[u];
-            srows[pos] = row[u];
+            const int64_t r = base + (int64_t)u * kHistThreads + threadIdx.x;
+            bin[u] = r < r1 ? (int)(chunk_of((int64_t)key[u], nb, clog2, nchunks) - lo) : -1;
         }
+        staged_scatter_batch(key, row, bin, R, s_k, s_r, s_cur, s_cnt, s_st, s_w, skeys, srows);
     }
 }
 
@@ -374,7 +454,9 @@ __device__ __forceinline__ void sort16_desc(uint32_t (&v)[16]) {
     }
 }
 
-// LDS slot of `key` inside the chunk image (insert = claim an empty slot with CAS)
+// LDS slot of `key` inside the chunk image (insert = claim an empty slot with CAS; the
+// claiming insert gets kSlotNew or-ed into the slot index)
+constexpr int kSlotNew = 1 << 30;
 template <bool INSERT>
 __device__ __forceinline__ int chunk_slot(Bucket* img, uint32_t cmask, uint32_t i0, unsigned long long sk) {
     uint32_t i = i0;
@@ -384,7 +466,8 @@ __device__ __forceinline__ int chunk_slot(Bucket* img, uint32_t cmask, uint32_t 
         for (int j = 0; j < kSlots; ++j) {
             unsigned long long kk = B.key[j];
             if (INSERT && kk == 0) kk = atomicCAS(&B.key[j], 0ull, sk);
-            if (kk == sk || (INSERT && kk == 0)) return (int)(i * kSlots + j);
+            if (INSERT && kk == 0) return (int)(i * kSlots + j) | kSlotNew;  // claimed here
+            if (kk == sk) return (int)(i * kSlots + j);
             if (!INSERT && kk == 0) return -1;
         }
         // passing a full bucket: mark it, so that a lookup missing in a full bucket
@@ -406,7 +489,7 @@ chunk_build_kernel(uint32_t nb, uint32_t clog2, uint32_t nchunks, const uint32_t
     uint32_t* d_off = reinterpret_cast<uint32_t*>(smem + (size_t)CB * sizeof(Bucket));
     uint32_t* d_cur = d_off + dupcap;
     uint32_t* d_cnt = d_cur + dupcap;
-    __shared__ unsigned s_ndup;
+    __shared__ unsigned s_ndup, s_dup;
     __shared__ unsigned long long s_w[kChunkThreads / 64];
     __shared__ unsigned long long s_base;
 
@@ -420,7 +503,10 @@ chunk_build_kernel(uint32_t nb, uint32_t clog2, uint32_t nchunks, const uint32_t
     {
         uint4* p = reinterpret_cast<uint4*>(img);
         for (uint32_t k = threadIdx.x; k < nimg * 4; k += kChunkThreads) p[k] = make_uint4(0, 0, 0, 0);
-        if (threadIdx.x == 0) s_ndup = 0;
+        if (threadIdx.x == 0) {
+            s_ndup = 0;
+            s_dup = side ? 1u : 0u;
+        }
     }
     __syncthreads();
 
@@ -438,21 +524,36 @@ chunk_build_kernel(uint32_t nb, uint32_t clog2, uint32_t nchunks, const uint32_t
             rk[u] = r < end ? skeys[r] : 0ull;
             rrow[u] = r < end ? srows[r] : 0u;
         }
-        // pass A: claim slots (LDS CAS), count rows per slot in ref[] (LDS atomics)
+        // pass A: claim slots (LDS CAS); the claiming insert stores its row in the ref
+        // (final if the key stays single); finding the key already present flags the
+        // chunk as holding duplicates
 #pragma unroll
         for (int u = 0; u < kChunkRegRows; ++u) {
             rslot[u] = -1;
             if (start + u * kChunkThreads + threadIdx.x >= end) continue;
             const unsigned long long sk = rk[u] ^ kSign;
             int slot = 0;
+            bool claimed = false;
             if (!side) {
-                slot = chunk_slot<true>(img, cmask, home_bucket((int64_t)rk[u], nb) & cmask, sk);
-                if (slot < 0) { atomicOr(&ctr->err, 1ull); continue; }  // chunk full
+                const int v = chunk_slot<true>(img, cmask, home_bucket((int64_t)rk[u], nb) & cmask, sk);
+                if (v < 0) { atomicOr(&ctr->err, 1ull); continue; }  // chunk full
+                slot = v & ~kSlotNew;
+                claimed = (v & kSlotNew) != 0;
             }
             rslot[u] = slot;
-            atomicAdd(&img[slot / kSlots].ref[slot % kSlots], 1u);
+            if (claimed) img[slot / kSlots].ref[slot % kSlots] = rrow[u];
+            else s_dup = 1u;
+        }
+        __syncthreads();
+        if (s_dup) {  // duplicates: turn refs into row counts
+            for (uint32_t sl = threadIdx.x; sl < nimg * kSlots; sl += kChunkThreads) img[sl / kSlots].ref[sl % kSlots] = 0;
+            __syncthreads();
+#pragma unroll
+            for (int u = 0; u < kChunkRegRows; ++u)
+                if (rslot[u] >= 0) atomicAdd(&img[rslot[u] / kSlots].ref[rslot[u] % kSlots], 1u);
         }
     } else {
+        if (threadIdx.x == 0) s_dup = 1u;
         // pass A (streamed)
         for (uint32_t r = start + threadIdx.x; r < end; r += kChunkThreads) {
             const unsigned long long sk = skeys[r] ^ kSign;
@@ -463,108 +564,114 @@ chunk_build_kernel(uint32_t nb, uint32_t clog2, uint32_t nchunks, const uint32_t
                 const uint32_t i0 = home_bucket((int64_t)(sk ^ kSign), nb) & cmask;
                 slot = chunk_slot<true>(img, cmask, i0, sk);
                 if (slot < 0) { atomicOr(&ctr->err, 1ull); continue; }  // chunk full
+                slot &= ~kSlotNew;
             }
             atomicAdd(&img[slot / kSlots].ref[slot % kSlots], 1u);
         }
     }
     __syncthreads();
 
-    // pass B: directory of duplicated keys (count > 1)
-    for (uint32_t sl = threadIdx.x; sl < nimg * kSlots; sl += kChunkThreads) {
-        unsigned& ref = img[sl / kSlots].ref[sl % kSlots];
-        const unsigned cnt = ref;
-        if (cnt > 1) {
-            const unsigned li = atomicAdd(&s_ndup, 1u);
-            if (li < dupcap) {
-                d_cnt[li] = cnt;
-                d_cur[li] = 0;
-                ref = kDupFlag | li;
-            } else {
-                atomicOr(&ctr->err, 2ull);  // dup directory full: the host retries at half load
+    // passes B-D only for chunks holding duplicated keys (block-uniform branch)
+    if (s_dup) {
+        // pass B: directory of duplicated keys (count > 1)
+        for (uint32_t sl = threadIdx.x; sl < nimg * kSlots; sl += kChunkThreads) {
+            unsigned& ref = img[sl / kSlots].ref[sl % kSlots];
+            const unsigned cnt = ref;
+            if (cnt > 1) {
+                const unsigned li = atomicAdd(&s_ndup, 1u);
+                if (li < dupcap) {
+                    d_cnt[li] = cnt;
+                    d_cur[li] = 0;
+                    ref = kDupFlag | li;
+                } else {
+                    atomicOr(&ctr->err, 2ull);  // dup directory full: the host retries at half load
+                }
             }
         }
-    }
-    __syncthreads();
-    const unsigned ndup = min(s_ndup, dupcap);
-    // segment offsets: exclusive scan of (count + 1) over the directory, one global
-    // reservation per chunk
-    {
-        unsigned long long carry = 0;
-        for (unsigned b = 0; b < ndup; b += kChunkThreads) {
-            const unsigned li = b + threadIdx.x;
-            const unsigned long long v = li < ndup ? (unsigned long long)d_cnt[li] + 1 : 0;
-            unsigned long long tot;
-            const unsigned long long ex = block_excl_scan<unsigned long long>(v, s_w, &tot);
-            if (li < ndup) d_off[li] = (uint32_t)(carry + ex);
-            carry += tot;
-        }
-        if (threadIdx.x == 0) s_base = carry ? atomicAdd(&ctr->dup_used, carry) : 0;
         __syncthreads();
+        const unsigned ndup = min(s_ndup, dupcap);
+        // segment offsets: exclusive scan of (count + 1) over the directory, one global
+        // reservation per chunk
+        {
+            unsigned long long carry = 0;
+            for (unsigned b = 0; b < ndup; b += kChunkThreads) {
+                const unsigned li = b + threadIdx.x;
+                const unsigned long long v = li < ndup ? (unsigned long long)d_cnt[li] + 1 : 0;
+                unsigned long long tot;
+                const unsigned long long ex = block_excl_scan<unsigned long long>(v, s_w, &tot);
+                if (li < ndup) d_off[li] = (uint32_t)(carry + ex);
+                carry += tot;
+            }
+            if (threadIdx.x == 0) s_base = carry ? atomicAdd(&ctr->dup_used, carry) : 0;
+            __syncthreads();
+            for (unsigned li = threadIdx.x; li < ndup; li += kChunkThreads) {
+                d_off[li] += (uint32_t)s_base;
+                dup_rows[d_off[li]] = d_cnt[li];  // segment header = row count
+            }
+        }
+        __syncthreads();
+
+        // pass C: place rows: single-row keys keep their row in ref, duplicated keys append
+        // to their segment (unordered here, sorted in pass D)
+        auto place = [&](int slot, uint32_t row) {
+            unsigned& ref = img[slot / kSlots].ref[slot % kSlots];
+            const unsigned rv = ref;
+            if (rv & kDupFlag) {
+                const unsigned li = rv & ~kDupFlag;
+                const unsigned k = atomicAdd(&d_cur[li], 1u);
+                dup_rows[d_off[li] + 1 + k] = row;
+            } else if (rv == 1) {
+                ref = row;  // the key's only row (rv == count == 1)
+            }
+        };
+        if (in_regs) {
+    #pragma unroll
+            for (int u = 0; u < kChunkRegRows; ++u)
+                if (rslot[u] >= 0) place(rslot[u], rrow[u]);
+        } else {
+            for (uint32_t r = start + threadIdx.x; r < end; r += kChunkThreads) {
+                const unsigned long long sk = skeys[r] ^ kSign;
+                int slot = 0;
+                if (!side) {
+                    const uint32_t i0 = home_bucket((int64_t)(sk ^ kSign), nb) & cmask;
+                    slot = chunk_slot<false>(img, cmask, i0, sk);
+                    if (slot < 0) continue;
+                }
+                place(slot, srows[r]);
+            }
+        }
+        __syncthreads();
+
+        // pass D: canonical order inside segments (descending rows), final refs
         for (unsigned li = threadIdx.x; li < ndup; li += kChunkThreads) {
-            d_off[li] += (uint32_t)s_base;
-            dup_rows[d_off[li]] = d_cnt[li];  // segment header = row count
-        }
-    }
-    __syncthreads();
-
-    // pass C: place rows: single-row keys keep their row in ref, duplicated keys append
-    // to their segment (unordered here, sorted in pass D)
-    auto place = [&](int slot, uint32_t row) {
-        unsigned& ref = img[slot / kSlots].ref[slot % kSlots];
-        const unsigned rv = ref;
-        if (rv & kDupFlag) {
-            const unsigned li = rv & ~kDupFlag;
-            const unsigned k = atomicAdd(&d_cur[li], 1u);
-            dup_rows[d_off[li] + 1 + k] = row;
-        } else if (rv == 1) {
-            ref = row;  // the key's only row (rv == count == 1)
-        }
-    };
-    if (in_regs) {
-#pragma unroll
-        for (int u = 0; u < kChunkRegRows; ++u)
-            if (rslot[u] >= 0) place(rslot[u], rrow[u]);
-    } else {
-        for (uint32_t r = start + threadIdx.x; r < end; r += kChunkThreads) {
-            const unsigned long long sk = skeys[r] ^ kSign;
-            int slot = 0;
-            if (!side) {
-                const uint32_t i0 = home_bucket((int64_t)(sk ^ kSign), nb) & cmask;
-                slot = chunk_slot<false>(img, cmask, i0, sk);
-                if (slot < 0) continue;
+            const unsigned n = d_cnt[li], off = d_off[li];
+            if (n <= (unsigned)kSmallSeg) {
+                uint32_t v[16];
+    #pragma unroll
+                for (int i = 0; i < 16; ++i) v[i] = (i < (int)n) ? dup_rows[off + 1 + i] : 0u;
+                sort16_desc(v);
+    #pragma unroll
+                for (int i = 0; i < 16; ++i)
+                    if (i < (int)n) dup_rows[off + 1 + i] = v[i];
             }
-            place(slot, srows[r]);
         }
-    }
-    __syncthreads();
-
-    // pass D: canonical order inside segments (descending rows), final refs
-    for (unsigned li = threadIdx.x; li < ndup; li += kChunkThreads) {
-        const unsigned n = d_cnt[li], off = d_off[li];
-        if (n <= (unsigned)kSmallSeg) {
-            uint32_t v[16];
-#pragma unroll
-            for (int i = 0; i < 16; ++i) v[i] = (i < (int)n) ? dup_rows[off + 1 + i] : 0u;
-            sort16_desc(v);
-#pragma unroll
-            for (int i = 0; i < 16; ++i)
-                if (i < (int)n) dup_rows[off + 1 + i] = v[i];
-        }
-    }
-    for (uint32_t sl = threadIdx.x; sl < nimg * kSlots; sl += kChunkThreads) {
-        Bucket& B = img[sl / kSlots];
-        unsigned& ref = B.ref[sl % kSlots];
-        if (ref & kDupFlag) {
-            const unsigned li = ref & ~kDupFlag;
-            if (d_cnt[li] > (unsigned)kSmallSeg) {
-                const unsigned bi = (unsigned)atomicAdd(&ctr->n_big, 1ull);  // rare: > 16 rows
-                big[bi] = BigSeg{side ? kSign : (B.key[sl % kSlots] ^ kSign), d_off[li], 0u};
+        for (uint32_t sl = threadIdx.x; sl < nimg * kSlots; sl += kChunkThreads) {
+            Bucket& B = img[sl / kSlots];
+            unsigned& ref = B.ref[sl % kSlots];
+            if (ref & kDupFlag) {
+                const unsigned li = ref & ~kDupFlag;
+                if (d_cnt[li] > (unsigned)kSmallSeg) {
+                    const unsigned bi = (unsigned)atomicAdd(&ctr->n_big, 1ull);  // rare: > 16 rows
+                    big[bi] = BigSeg{side ? kSign : (B.key[sl % kSlots] ^ kSign), d_off[li], 0u};
+                }
+                ref = kDupFlag | d_off[li];
+                // small row counts inline in meta (6 bits per slot): the probe's count pass
+                // then needs no dup_rows access
+                if (!side && d_cnt[li] <= kInlineCount) atomicOr(&B.meta, d_cnt[li] << (1 + 6 * (sl % kSlots)));
             }
-            ref = kDupFlag | d_off[li];
-            // small row counts inline in meta (6 bits per slot): the probe's count pass
-            // then needs no dup_rows access
-            if (!side && d_cnt[li] <= kInlineCount) atomicOr(&B.meta, d_cnt[li] << (1 + 6 * (sl % kSlots)));
         }
+        __syncthreads();
+
     }
     __syncthreads();
 
@@ -1500,12 +1607,21 @@ hipError_t launch_build(int key_bytes, const Segment* d_segs, int nseg, int64_t 
                                                                                  gshift, ngroups, hist1, ntiles);
         hipError_t e = launch_scan(hist1, (int64_t)ngroups * ntiles, scr, &ctr->n_valid, s);
         if (e != hipSuccess) return e;
+        static const bool lds_ok = [] {
+            return hipFuncSetAttribute((const void*)coarse_scatter_staged_kernel<int64_t>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)kStageLds) == hipSuccess &&
+                   hipFuncSetAttribute((const void*)coarse_scatter_staged_kernel<int32_t>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)kStageLds) == hipSuccess &&
+                   hipFuncSetAttribute((const void*)fine_scatter_staged_kernel,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)kStageLds) == hipSuccess;
+        }();
+        if (!lds_ok) return hipErrorInvalidConfiguration;
         if (key_bytes == 8)
-            coarse_scatter_kernel<int64_t><<<(unsigned)ntiles, kHistThreads, 0, s>>>(
+            coarse_scatter_staged_kernel<int64_t><<<(unsigned)ntiles, kHistThreads, kStageLds, s>>>(
                 d_segs, nseg, total, nb, clog2, nchunks, gshift, ngroups, hist1, ntiles, tkeys, trows, row_ids,
                 ids_as_rows);
         else
-            coarse_scatter_kernel<int32_t><<<(unsigned)ntiles, kHistThreads, 0, s>>>(
+            coarse_scatter_staged_kernel<int32_t><<<(unsigned)ntiles, kHistThreads, kStageLds, s>>>(
                 d_segs, nseg, total, nb, clog2, nchunks, gshift, ngroups, hist1, ntiles, tkeys, trows, row_ids,
                 ids_as_rows);
         // level 2: chunk order (tiles over the n_valid group-ordered rows)
@@ -1513,8 +1629,8 @@ hipError_t launch_build(int key_bytes, const Segment* d_segs, int nseg, int64_t 
         fine_hist_kernel<<<(unsigned)ntiles, kHistThreads, hist_lds, s>>>(tkeys, ctr, nb, clog2, nchunks, gshift, hist,
                                                                          ntiles);
         if ((e = launch_scan(hist, hlen, scr, &ctr->n_valid, s)) != hipSuccess) return e;
-        fine_scatter_kernel<<<(unsigned)ntiles, kHistThreads, hist_lds, s>>>(tkeys, trows, ctr, nb, clog2, nchunks,
-                                                                            gshift, hist, ntiles, skeys, srows);
+        fine_scatter_staged_kernel<<<(unsigned)ntiles, kHistThreads, kStageLds, s>>>(
+            tkeys, trows, ctr, nb, clog2, nchunks, gshift, hist, ntiles, skeys, srows);
     }
     // chunk build: LDS = bucket image + dup directory (3 u32 per entry)
     const uint32_t CB = 1u << clog2;
