@@ -268,10 +268,11 @@ hj_status build_attempt(hj_table* t, const std::vector<Segment>& segs, double lf
     const int64_t total = t->total_rows;
     // geometry: 5-slot buckets, chunks of 2^clog2 buckets (one workgroup builds one)
     const double want = (double)total / (kSlots * lf);
-    uint32_t clog2 = 10;
+    // smallest chunks that fit the chunk count limit (512 buckets build four per CU)
+    uint32_t clog2 = 9;
     uint64_t nchunks = (uint64_t)(want / (1u << clog2)) + 1;
-    if (nchunks > (uint64_t)kMaxChunks) {
-        clog2 = 11;
+    while (nchunks > (uint64_t)kMaxChunks && clog2 < 11) {
+        ++clog2;
         nchunks = (uint64_t)(want / (1u << clog2)) + 1;
     }
     if (nchunks > (uint64_t)kMaxChunks)
@@ -279,7 +280,9 @@ hj_status build_attempt(hj_table* t, const std::vector<Segment>& segs, double lf
     t->clog2 = clog2;
     t->nchunks = (uint32_t)nchunks;
     t->nb = (uint32_t)(nchunks << clog2);
-    const int64_t ntiles = build_tiles(total);
+    hipDeviceProp_t* prop0 = device_props(t->device);
+    const int64_t ntiles = build_tiles(total, prop0 ? prop0->multiProcessorCount : 256);
+    const int64_t tile_rows = build_tile_rows(total, ntiles);
     const int64_t hlen = (int64_t)(nchunks + 1) * ntiles;
 
     hj_status st;
@@ -334,7 +337,7 @@ hj_status build_attempt(hj_table* t, const std::vector<Segment>& segs, double lf
     hipDeviceProp_t* prop = device_props(t->device);
     const int cus = prop ? prop->multiProcessorCount : 256;
     HIP_TRY(launch_build(t->key_bytes, d_segs, (int)segs.size(), total, t->nb, t->clog2, t->nchunks, hist, hist1,
-                         ntiles, scan, tkeys, trows, skeys, srows, t->row_ids, ids_as_rows, t->tbl, t->dup_rows,
+                         ntiles, tile_rows, scan, tkeys, trows, skeys, srows, t->row_ids, ids_as_rows, t->tbl, t->dup_rows,
                          big, ctr, cus, s));
     BuildCounters hc;
     HIP_TRY(hipMemcpyAsync(&hc, ctr, sizeof(hc), hipMemcpyDeviceToHost, s));

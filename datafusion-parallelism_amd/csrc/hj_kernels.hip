@@ -150,13 +150,13 @@ template <typename K>
 __global__ void __launch_bounds__(kHistThreads)
 coarse_hist_kernel(const Segment* __restrict__ segs, int nseg, int64_t total, uint32_t nb, uint32_t clog2,
                    uint32_t nchunks, uint32_t gshift, uint32_t ngroups, uint32_t* __restrict__ hist1,
-                   int64_t ntiles) {
+                   int64_t ntiles, int64_t tile_rows) {
     __shared__ uint32_t s_h[kHistThreads / 64][kCoarseBins];  // per-wave copies: fewer LDS atomic collisions
     const int wave = threadIdx.x >> 6;
     for (uint32_t k = threadIdx.x; k < (kHistThreads / 64) * kCoarseBins; k += kHistThreads) (&s_h[0][0])[k] = 0;
     __syncthreads();
-    const int64_t r0 = (int64_t)blockIdx.x * kBuildTile;
-    const int64_t r1 = min<int64_t>(total, r0 + kBuildTile);
+    const int64_t r0 = (int64_t)blockIdx.x * tile_rows;
+    const int64_t r1 = min<int64_t>(total, r0 + tile_rows);
     __shared__ Segment s_seg[kTileSegs];
     __shared__ int s_info[2];
     int tns;
@@ -190,11 +190,12 @@ __device__ __forceinline__ void fine_range(const unsigned long long* tkeys, int6
 
 __global__ void __launch_bounds__(kHistThreads)
 fine_hist_kernel(const unsigned long long* __restrict__ tkeys, const BuildCounters* __restrict__ ctr, uint32_t nb,
-                 uint32_t clog2, uint32_t nchunks, uint32_t gshift, uint32_t* __restrict__ hist, int64_t ntiles) {
+                 uint32_t clog2, uint32_t nchunks, uint32_t gshift, uint32_t* __restrict__ hist, int64_t ntiles,
+                 int64_t tile_rows) {
     extern __shared__ __attribute__((aligned(16))) uint32_t s_h[];
     const int64_t nvalid = (int64_t)ctr->n_valid;
-    const int64_t r0 = (int64_t)blockIdx.x * kBuildTile;
-    const int64_t r1 = min<int64_t>(nvalid, r0 + kBuildTile);
+    const int64_t r0 = (int64_t)blockIdx.x * tile_rows;
+    const int64_t r1 = min<int64_t>(nvalid, r0 + tile_rows);
     if (r0 >= r1) return;
     uint32_t lo, hi;
     fine_range(tkeys, r0, r1, nb, clog2, nchunks, gshift, &lo, &hi);
@@ -344,7 +345,7 @@ __global__ void __launch_bounds__(kHistThreads)
 coarse_scatter_staged_kernel(const Segment* __restrict__ segs, int nseg, int64_t total, uint32_t nb, uint32_t clog2,
                              uint32_t nchunks, uint32_t gshift, uint32_t ngroups, const uint32_t* __restrict__ hist1,
                              int64_t ntiles, unsigned long long* __restrict__ tkeys, uint32_t* __restrict__ trows,
-                             uint64_t* __restrict__ row_ids, bool ids_as_rows) {
+                             uint64_t* __restrict__ row_ids, bool ids_as_rows, int64_t tile_rows) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     unsigned long long* s_k = reinterpret_cast<unsigned long long*>(smem);
     uint32_t* s_r = reinterpret_cast<uint32_t*>(s_k + kStageRows);
@@ -355,8 +356,8 @@ coarse_scatter_staged_kernel(const Segment* __restrict__ segs, int nseg, int64_t
     __shared__ Segment s_seg[kTileSegs];
     __shared__ int s_info[2];
     for (uint32_t g = threadIdx.x; g < ngroups; g += kHistThreads) s_cur[g] = hist1[(int64_t)g * ntiles + blockIdx.x];
-    const int64_t r0 = (int64_t)blockIdx.x * kBuildTile;
-    const int64_t r1 = min<int64_t>(total, r0 + kBuildTile);
+    const int64_t r0 = (int64_t)blockIdx.x * tile_rows;
+    const int64_t r1 = min<int64_t>(total, r0 + tile_rows);
     int tns;
     const Segment* tsegs = tile_segments(segs, nseg, r0, r1, s_seg, s_info, &tns);  // syncs
     for (int64_t base = r0; base < r1; base += kStageRows) {
@@ -380,7 +381,7 @@ __global__ void __launch_bounds__(kHistThreads)
 fine_scatter_staged_kernel(const unsigned long long* __restrict__ tkeys, const uint32_t* __restrict__ trows,
                            const BuildCounters* __restrict__ ctr, uint32_t nb, uint32_t clog2, uint32_t nchunks,
                            uint32_t gshift, const uint32_t* __restrict__ hist, int64_t ntiles,
-                           unsigned long long* __restrict__ skeys, uint32_t* __restrict__ srows) {
+                           unsigned long long* __restrict__ skeys, uint32_t* __restrict__ srows, int64_t tile_rows) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     unsigned long long* s_k = reinterpret_cast<unsigned long long*>(smem);
     uint32_t* s_r = reinterpret_cast<uint32_t*>(s_k + kStageRows);
@@ -389,8 +390,8 @@ fine_scatter_staged_kernel(const unsigned long long* __restrict__ tkeys, const u
     uint32_t* s_st = s_cnt + kStageMaxBins;
     __shared__ uint32_t s_w[kHistThreads / 64];
     const int64_t nvalid = (int64_t)ctr->n_valid;
-    const int64_t r0 = (int64_t)blockIdx.x * kBuildTile;
-    const int64_t r1 = min<int64_t>(nvalid, r0 + kBuildTile);
+    const int64_t r0 = (int64_t)blockIdx.x * tile_rows;
+    const int64_t r1 = min<int64_t>(nvalid, r0 + tile_rows);
     if (r0 >= r1) return;
     uint32_t lo, hi;
     fine_range(tkeys, r0, r1, nb, clog2, nchunks, gshift, &lo, &hi);
@@ -431,7 +432,6 @@ fine_scatter_staged_kernel(const unsigned long long* __restrict__ tkeys, const u
 // ---------------------------------------------------------------------------
 // build 3: one workgroup per chunk builds the chunk's buckets in LDS
 // ---------------------------------------------------------------------------
-constexpr int kChunkThreads = 1024;
 constexpr int kChunkRegRows = 4;  // rows per thread kept in registers across passes A-C
 
 __device__ __forceinline__ void sort16_desc(uint32_t (&v)[16]) {
@@ -478,6 +478,7 @@ __device__ __forceinline__ int chunk_slot(Bucket* img, uint32_t cmask, uint32_t 
     return -1;
 }
 
+template <int kChunkThreads>
 __global__ void __launch_bounds__(kChunkThreads)
 chunk_build_kernel(uint32_t nb, uint32_t clog2, uint32_t nchunks, const uint32_t* __restrict__ hist,
                    int64_t ntiles, const unsigned long long* __restrict__ skeys,
@@ -1557,7 +1558,13 @@ __global__ void gen_uniform_kernel(int64_t* out, int64_t n, uint64_t seed, int64
 // ---------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------
-int64_t build_tiles(int64_t total) { return (total + kBuildTile - 1) / kBuildTile; }
+int64_t build_tiles(int64_t total, int cus) {
+    // one tile per CU (the staged scatters hold one 123 KB workgroup per CU; a second
+    // partial round of tiles would double their time), at least kMinBuildTile rows each
+    const int64_t by_rows = (total + kMinBuildTile - 1) / kMinBuildTile;
+    return std::max<int64_t>(std::min<int64_t>(by_rows, std::max(cus, 1)), total > 0 ? 1 : 0);
+}
+int64_t build_tile_rows(int64_t total, int64_t ntiles) { return ntiles ? (total + ntiles - 1) / ntiles : 0; }
 
 int64_t scan_scratch_bytes(int64_t len) { return 8 * ((len + kScanSeg - 1) / kScanSeg + 2); }
 
@@ -1588,7 +1595,8 @@ hipError_t launch_scan_u64(unsigned long long* a, int64_t len, void* scratch, un
 }
 
 hipError_t launch_build(int key_bytes, const Segment* d_segs, int nseg, int64_t total, uint32_t nb, uint32_t clog2,
-                        uint32_t nchunks, uint32_t* hist, uint32_t* hist1, int64_t ntiles, void* scan_scratch,
+                        uint32_t nchunks, uint32_t* hist, uint32_t* hist1, int64_t ntiles, int64_t tile_rows,
+                        void* scan_scratch,
                         unsigned long long* tkeys, uint32_t* trows, unsigned long long* skeys, uint32_t* srows,
                         uint64_t* row_ids, bool ids_as_rows, Bucket* tbl, uint32_t* dup_rows, BigSeg* big,
                         BuildCounters* ctr, int big_grid, hipStream_t s) {
@@ -1601,10 +1609,12 @@ hipError_t launch_build(int key_bytes, const Segment* d_segs, int nseg, int64_t 
         // level 1: group order
         if (key_bytes == 8)
             coarse_hist_kernel<int64_t><<<(unsigned)ntiles, kHistThreads, 0, s>>>(d_segs, nseg, total, nb, clog2, nchunks,
-                                                                                 gshift, ngroups, hist1, ntiles);
+                                                                                 gshift, ngroups, hist1, ntiles,
+                                                                                 tile_rows);
         else
             coarse_hist_kernel<int32_t><<<(unsigned)ntiles, kHistThreads, 0, s>>>(d_segs, nseg, total, nb, clog2, nchunks,
-                                                                                 gshift, ngroups, hist1, ntiles);
+                                                                                 gshift, ngroups, hist1, ntiles,
+                                                                                 tile_rows);
         hipError_t e = launch_scan(hist1, (int64_t)ngroups * ntiles, scr, &ctr->n_valid, s);
         if (e != hipSuccess) return e;
         static const bool lds_ok = [] {
@@ -1619,34 +1629,38 @@ hipError_t launch_build(int key_bytes, const Segment* d_segs, int nseg, int64_t 
         if (key_bytes == 8)
             coarse_scatter_staged_kernel<int64_t><<<(unsigned)ntiles, kHistThreads, kStageLds, s>>>(
                 d_segs, nseg, total, nb, clog2, nchunks, gshift, ngroups, hist1, ntiles, tkeys, trows, row_ids,
-                ids_as_rows);
+                ids_as_rows, tile_rows);
         else
             coarse_scatter_staged_kernel<int32_t><<<(unsigned)ntiles, kHistThreads, kStageLds, s>>>(
                 d_segs, nseg, total, nb, clog2, nchunks, gshift, ngroups, hist1, ntiles, tkeys, trows, row_ids,
-                ids_as_rows);
+                ids_as_rows, tile_rows);
         // level 2: chunk order (tiles over the n_valid group-ordered rows)
         if ((e = hipMemsetAsync(hist, 0, sizeof(uint32_t) * (size_t)hlen, s)) != hipSuccess) return e;
         fine_hist_kernel<<<(unsigned)ntiles, kHistThreads, hist_lds, s>>>(tkeys, ctr, nb, clog2, nchunks, gshift, hist,
-                                                                         ntiles);
+                                                                         ntiles, tile_rows);
         if ((e = launch_scan(hist, hlen, scr, &ctr->n_valid, s)) != hipSuccess) return e;
         fine_scatter_staged_kernel<<<(unsigned)ntiles, kHistThreads, kStageLds, s>>>(
-            tkeys, trows, ctr, nb, clog2, nchunks, gshift, hist, ntiles, skeys, srows);
+            tkeys, trows, ctr, nb, clog2, nchunks, gshift, hist, ntiles, skeys, srows, tile_rows);
     }
-    // chunk build: LDS = bucket image + dup directory (3 u32 per entry)
+    // chunk build: LDS = bucket image + dup directory (3 u32 per entry). 512-bucket
+    // chunks run 512-thread workgroups, four per CU (32 KB image + directory in 38 KB);
+    // 1024-bucket chunks two per CU; 2048-bucket chunks one. A chunk with more
+    // duplicated keys than its directory holds makes the host rebuild at half load.
     const uint32_t CB = 1u << clog2;
     const size_t img = (size_t)CB * sizeof(Bucket);
-    // two workgroups per CU when the image is 64 KB (the duplicate directory takes the
-    // rest; a chunk with more duplicated keys than that makes the host rebuild at half
-    // load), one for 128 KB images
-    const size_t lds_cap = (CB <= 1024 ? 80 * 1024 : 160 * 1024) - 2048;
+    const size_t lds_cap = (CB <= 512 ? 40 * 1024 : CB <= 1024 ? 80 * 1024 : 160 * 1024) - 2048;
     uint32_t dupcap = (uint32_t)std::min<size_t>((size_t)CB * kSlots, (lds_cap - img) / 12);
     const size_t lds = img + (size_t)dupcap * 12;
-    hipError_t e = hipFuncSetAttribute((const void*)chunk_build_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       (int)lds);
+    const void* kfn = CB <= 512 ? (const void*)chunk_build_kernel<512> : (const void*)chunk_build_kernel<1024>;
+    hipError_t e = hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
     if (ntiles > 0) {
-        chunk_build_kernel<<<nchunks + 1, kChunkThreads, lds, s>>>(nb, clog2, nchunks, hist, ntiles, skeys, srows, tbl,
-                                                                   dup_rows, big, ctr, dupcap);
+        if (CB <= 512)
+            chunk_build_kernel<512><<<nchunks + 1, 512, lds, s>>>(nb, clog2, nchunks, hist, ntiles, skeys, srows, tbl,
+                                                                 dup_rows, big, ctr, dupcap);
+        else
+            chunk_build_kernel<1024><<<nchunks + 1, 1024, lds, s>>>(nb, clog2, nchunks, hist, ntiles, skeys, srows,
+                                                                   tbl, dup_rows, big, ctr, dupcap);
         dup_sort_big_kernel<<<big_grid, kBigThreads, 0, s>>>(dup_rows, big, ctr, d_segs, nseg, total, key_bytes,
                                                              ids_as_rows);
     }
