@@ -77,6 +77,16 @@ for s in $STEPS; do
       run timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/dist -o d --output-format csv \
         -- python3 bench.py --force-dist --no-cpu-baseline --steps 5 > $O/distprof.json 2> $O/distprof.err \
         || { tail -30 $O/distprof.err; exit 1; } ;;
+    smoke)
+      run timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 \
+        || { tail -30 $O/smoke.log; exit 1; }
+      tail -1 $O/smoke.log ;;
+    trun)
+      # the driver's N>1 launch shape, with one rank: stdout must be exactly one JSON line
+      run timeout -k 10 400 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 \
+        --master-port 29533 bench.py --gpus 1 --steps 5 --warmup 2 > $O/trun.out 2> $O/trun.err \
+        || { tail -30 $O/trun.err; exit 1; }
+      wc -l $O/trun.out && python3 -c "import json,sys; json.loads(open(sys.argv[1]).read()); print('one json line ok')" $O/trun.out ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
