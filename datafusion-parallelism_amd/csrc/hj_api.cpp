@@ -275,8 +275,13 @@ hj_status build_attempt(hj_table* t, const std::vector<Segment>& segs, double lf
         ++clog2;
         nchunks = (uint64_t)(want / (1u << clog2)) + 1;
     }
-    if (nchunks > (uint64_t)kMaxChunks)
-        return fail(HJ_ERR_INVALID, "build side too large for one device table; shard it (hj_radix_partition)");
+    if (nchunks > (uint64_t)kMaxChunks) {
+        // very large builds: fill the largest table geometry fuller (up to 0.8 slots/key)
+        const double full = (double)kMaxChunks * (1u << clog2) * kSlots;
+        if ((double)total / full > 0.8)
+            return fail(HJ_ERR_INVALID, "build side too large for one device table; shard it (hj_radix_partition)");
+        nchunks = kMaxChunks;
+    }
     t->clog2 = clog2;
     t->nchunks = (uint32_t)nchunks;
     t->nb = (uint32_t)(nchunks << clog2);
@@ -311,6 +316,9 @@ hj_status build_attempt(hj_table* t, const std::vector<Segment>& segs, double lf
         HJ_OK)
         return st;
     hist1 = (uint32_t*)p;
+    uint32_t* chunk_starts;
+    if ((st = dev_alloc(t, t->scratch, &p, sizeof(uint32_t) * (size_t)(nchunks + 2))) != HJ_OK) return st;
+    chunk_starts = (uint32_t*)p;
     if ((st = dev_alloc(t, t->scratch, &p, (size_t)scan_scratch_bytes(std::max<int64_t>(hlen, kCoarseBins * ntiles)))) !=
         HJ_OK)
         return st;
@@ -337,7 +345,7 @@ hj_status build_attempt(hj_table* t, const std::vector<Segment>& segs, double lf
     hipDeviceProp_t* prop = device_props(t->device);
     const int cus = prop ? prop->multiProcessorCount : 256;
     HIP_TRY(launch_build(t->key_bytes, d_segs, (int)segs.size(), total, t->nb, t->clog2, t->nchunks, hist, hist1,
-                         ntiles, tile_rows, scan, tkeys, trows, skeys, srows, t->row_ids, ids_as_rows, t->tbl, t->dup_rows,
+                         chunk_starts, ntiles, tile_rows, scan, tkeys, trows, skeys, srows, t->row_ids, ids_as_rows, t->tbl, t->dup_rows,
                          big, ctr, cus, s));
     BuildCounters hc;
     HIP_TRY(hipMemcpyAsync(&hc, ctr, sizeof(hc), hipMemcpyDeviceToHost, s));

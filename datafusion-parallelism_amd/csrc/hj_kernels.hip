@@ -73,6 +73,7 @@ __device__ __forceinline__ uint32_t home_bucket(int64_t key, uint32_t nb) {
 // both levels write long runs.
 // ---------------------------------------------------------------------------
 constexpr int kHistThreads = 1024;
+constexpr int kFineLdsBins = 8192;  // fine histogram in LDS (32 KB) up to this many chunks per tile
 
 __device__ __forceinline__ uint32_t chunk_of(int64_t key, uint32_t nb, uint32_t clog2, uint32_t nchunks) {
     return ((uint64_t)key ^ kSign) == 0 ? nchunks : (home_bucket(key, nb) >> clog2);
@@ -199,7 +200,10 @@ fine_hist_kernel(const unsigned long long* __restrict__ tkeys, const BuildCounte
     if (r0 >= r1) return;
     uint32_t lo, hi;
     fine_range(tkeys, r0, r1, nb, clog2, nchunks, gshift, &lo, &hi);
-    for (uint32_t c = lo + threadIdx.x; c <= hi; c += kHistThreads) s_h[c - lo] = 0;
+    // a tile spanning more than kFineLdsBins chunks (skewed groups) counts in global memory
+    const bool in_lds = hi - lo + 1 <= (uint32_t)kFineLdsBins;
+    if (in_lds)
+        for (uint32_t c = lo + threadIdx.x; c <= hi; c += kHistThreads) s_h[c - lo] = 0;
     __syncthreads();
     for (int64_t base = r0; base < r1; base += kHistThreads * kRowBatch) {
         unsigned long long key[kRowBatch];
@@ -209,11 +213,15 @@ fine_hist_kernel(const unsigned long long* __restrict__ tkeys, const BuildCounte
             key[u] = r < r1 ? tkeys[r] : 0ull;
         }
 #pragma unroll
-        for (int u = 0; u < kRowBatch; ++u)
-            if (base + (int64_t)u * kHistThreads + threadIdx.x < r1)
-                atomicAdd(&s_h[chunk_of((int64_t)key[u], nb, clog2, nchunks) - lo], 1u);
+        for (int u = 0; u < kRowBatch; ++u) {
+            if (base + (int64_t)u * kHistThreads + threadIdx.x >= r1) continue;
+            const uint32_t c = chunk_of((int64_t)key[u], nb, clog2, nchunks);
+            if (in_lds) atomicAdd(&s_h[c - lo], 1u);
+            else atomicAdd(&hist[(int64_t)c * ntiles + blockIdx.x], 1u);
+        }
     }
     __syncthreads();
+    if (!in_lds) return;
     for (uint32_t c = lo + threadIdx.x; c <= hi; c += kHistThreads) hist[(int64_t)c * ntiles + blockIdx.x] = s_h[c - lo];
 }
 
@@ -380,7 +388,7 @@ coarse_scatter_staged_kernel(const Segment* __restrict__ segs, int nseg, int64_t
 __global__ void __launch_bounds__(kHistThreads)
 fine_scatter_staged_kernel(const unsigned long long* __restrict__ tkeys, const uint32_t* __restrict__ trows,
                            const BuildCounters* __restrict__ ctr, uint32_t nb, uint32_t clog2, uint32_t nchunks,
-                           uint32_t gshift, const uint32_t* __restrict__ hist, int64_t ntiles,
+                           uint32_t gshift, uint32_t* __restrict__ hist, int64_t ntiles,
                            unsigned long long* __restrict__ skeys, uint32_t* __restrict__ srows, int64_t tile_rows) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     unsigned long long* s_k = reinterpret_cast<unsigned long long*>(smem);
@@ -396,13 +404,13 @@ fine_scatter_staged_kernel(const unsigned long long* __restrict__ tkeys, const u
     uint32_t lo, hi;
     fine_range(tkeys, r0, r1, nb, clog2, nchunks, gshift, &lo, &hi);
     const uint32_t R = hi - lo + 1;
-    if (R > (uint32_t)kStageMaxBins) {  // a tile spanning many groups (tiny or skewed inputs): direct stores
-        uint32_t* s_c = reinterpret_cast<uint32_t*>(smem);  // staging area: (nchunks + 1) <= 16384 cursors
-        for (uint32_t c = lo + threadIdx.x; c <= hi; c += kHistThreads) s_c[c - lo] = hist[(int64_t)c * ntiles + blockIdx.x];
-        __syncthreads();
+    if (R > (uint32_t)kStageMaxBins) {
+        // a tile spanning many chunks (skewed groups): direct stores, the tile's scanned
+        // histogram column is the cursor array (consumed; the chunk build reads chunk_starts)
         for (int64_t r = r0 + threadIdx.x; r < r1; r += kHistThreads) {
             const unsigned long long key = tkeys[r];
-            const uint32_t pos = atomicAdd(&s_c[chunk_of((int64_t)key, nb, clog2, nchunks) - lo], 1u);
+            const uint32_t c = chunk_of((int64_t)key, nb, clog2, nchunks);
+            const uint32_t pos = atomicAdd(&hist[(int64_t)c * ntiles + blockIdx.x], 1u);
             skeys[pos] = key;
             srows[pos] = trows[r];
         }
@@ -427,6 +435,13 @@ fine_scatter_staged_kernel(const unsigned long long* __restrict__ tkeys, const u
         }
         staged_scatter_batch(key, row, bin, R, s_k, s_r, s_cur, s_cnt, s_st, s_w, skeys, srows);
     }
+}
+
+// chunk c's rows are [starts[c], starts[c + 1]) of skeys / srows (chunk nchunks = side)
+__global__ void chunk_starts_kernel(const uint32_t* __restrict__ hist, int64_t ntiles, uint32_t nchunks,
+                                    const BuildCounters* __restrict__ ctr, uint32_t* __restrict__ starts) {
+    for (uint32_t c = blockIdx.x * blockDim.x + threadIdx.x; c <= nchunks + 1; c += gridDim.x * blockDim.x)
+        starts[c] = c <= nchunks ? hist[(int64_t)c * ntiles] : (uint32_t)ctr->n_valid;
 }
 
 // ---------------------------------------------------------------------------
@@ -480,8 +495,8 @@ __device__ __forceinline__ int chunk_slot(Bucket* img, uint32_t cmask, uint32_t 
 
 template <int kChunkThreads>
 __global__ void __launch_bounds__(kChunkThreads)
-chunk_build_kernel(uint32_t nb, uint32_t clog2, uint32_t nchunks, const uint32_t* __restrict__ hist,
-                   int64_t ntiles, const unsigned long long* __restrict__ skeys,
+chunk_build_kernel(uint32_t nb, uint32_t clog2, uint32_t nchunks, const uint32_t* __restrict__ starts,
+                   const unsigned long long* __restrict__ skeys,
                    const uint32_t* __restrict__ srows, Bucket* __restrict__ tbl, uint32_t* __restrict__ dup_rows,
                    BigSeg* __restrict__ big, BuildCounters* ctr, uint32_t dupcap) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -496,8 +511,8 @@ chunk_build_kernel(uint32_t nb, uint32_t clog2, uint32_t nchunks, const uint32_t
 
     const uint32_t c = blockIdx.x;
     const bool side = (c == nchunks);
-    const uint32_t start = hist[(int64_t)c * ntiles];
-    const uint32_t end = side ? (uint32_t)ctr->n_valid : hist[(int64_t)(c + 1) * ntiles];
+    const uint32_t start = starts[c];
+    const uint32_t end = starts[c + 1];
     const uint32_t nimg = side ? 1u : CB;
 
     // zero the chunk image
@@ -1595,12 +1610,11 @@ hipError_t launch_scan_u64(unsigned long long* a, int64_t len, void* scratch, un
 }
 
 hipError_t launch_build(int key_bytes, const Segment* d_segs, int nseg, int64_t total, uint32_t nb, uint32_t clog2,
-                        uint32_t nchunks, uint32_t* hist, uint32_t* hist1, int64_t ntiles, int64_t tile_rows,
-                        void* scan_scratch,
+                        uint32_t nchunks, uint32_t* hist, uint32_t* hist1, uint32_t* chunk_starts, int64_t ntiles,
+                        int64_t tile_rows, void* scan_scratch,
                         unsigned long long* tkeys, uint32_t* trows, unsigned long long* skeys, uint32_t* srows,
                         uint64_t* row_ids, bool ids_as_rows, Bucket* tbl, uint32_t* dup_rows, BigSeg* big,
                         BuildCounters* ctr, int big_grid, hipStream_t s) {
-    const size_t hist_lds = sizeof(uint32_t) * (nchunks + 1);
     const int64_t hlen = (int64_t)(nchunks + 1) * ntiles;
     const uint32_t gshift = coarse_shift(nchunks);
     const uint32_t ngroups = (nchunks >> gshift) + 1;
@@ -1636,9 +1650,12 @@ hipError_t launch_build(int key_bytes, const Segment* d_segs, int nseg, int64_t 
                 ids_as_rows, tile_rows);
         // level 2: chunk order (tiles over the n_valid group-ordered rows)
         if ((e = hipMemsetAsync(hist, 0, sizeof(uint32_t) * (size_t)hlen, s)) != hipSuccess) return e;
-        fine_hist_kernel<<<(unsigned)ntiles, kHistThreads, hist_lds, s>>>(tkeys, ctr, nb, clog2, nchunks, gshift, hist,
+        fine_hist_kernel<<<(unsigned)ntiles, kHistThreads, sizeof(uint32_t) * kFineLdsBins, s>>>(tkeys, ctr, nb, clog2,
+                                                                                         nchunks, gshift, hist,
                                                                          ntiles, tile_rows);
         if ((e = launch_scan(hist, hlen, scr, &ctr->n_valid, s)) != hipSuccess) return e;
+        chunk_starts_kernel<<<(unsigned)std::min<uint32_t>((nchunks + 2 + 255) / 256, 4096), 256, 0, s>>>(
+            hist, ntiles, nchunks, ctr, chunk_starts);
         fine_scatter_staged_kernel<<<(unsigned)ntiles, kHistThreads, kStageLds, s>>>(
             tkeys, trows, ctr, nb, clog2, nchunks, gshift, hist, ntiles, skeys, srows, tile_rows);
     }
@@ -1656,10 +1673,10 @@ hipError_t launch_build(int key_bytes, const Segment* d_segs, int nseg, int64_t 
     if (e != hipSuccess) return e;
     if (ntiles > 0) {
         if (CB <= 512)
-            chunk_build_kernel<512><<<nchunks + 1, 512, lds, s>>>(nb, clog2, nchunks, hist, ntiles, skeys, srows, tbl,
-                                                                 dup_rows, big, ctr, dupcap);
+            chunk_build_kernel<512><<<nchunks + 1, 512, lds, s>>>(nb, clog2, nchunks, chunk_starts, skeys, srows,
+                                                                 tbl, dup_rows, big, ctr, dupcap);
         else
-            chunk_build_kernel<1024><<<nchunks + 1, 1024, lds, s>>>(nb, clog2, nchunks, hist, ntiles, skeys, srows,
+            chunk_build_kernel<1024><<<nchunks + 1, 1024, lds, s>>>(nb, clog2, nchunks, chunk_starts, skeys, srows,
                                                                    tbl, dup_rows, big, ctr, dupcap);
         dup_sort_big_kernel<<<big_grid, kBigThreads, 0, s>>>(dup_rows, big, ctr, d_segs, nseg, total, key_bytes,
                                                              ids_as_rows);

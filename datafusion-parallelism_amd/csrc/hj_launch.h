@@ -9,7 +9,7 @@ namespace dfp {
 
 // ---- build ---------------------------------------------------------------
 constexpr int kMinBuildTile = 4096;  // build rows per histogram/scatter block, at least
-constexpr int kMaxChunks = 16383;    // + side partition -> LDS histogram <= 64 KB
+constexpr int kMaxChunks = 131071;   // (chunks + 1) x tiles histogram; 2^28 buckets max
 
 int64_t build_tiles(int64_t total, int cus);
 int64_t build_tile_rows(int64_t total, int64_t ntiles);
@@ -19,11 +19,13 @@ int64_t scan_scratch_bytes(int64_t len);
 constexpr int kCoarseBins = 128;     // level-1 partition groups (per-wave LDS copies)
 
 // scratch: hist u32[(nchunks + 1) * ntiles], hist1 u32[kCoarseBins * ntiles],
+// chunk_starts u32[nchunks + 2],
 // scan_scratch scan_scratch_bytes((nchunks + 1) * ntiles), tkeys/skeys u64[total],
 // trows/srows u32[total]
 hipError_t launch_build(int key_bytes, const Segment* d_segs, int nseg, int64_t total,
                         uint32_t nb, uint32_t clog2, uint32_t nchunks, uint32_t* hist,
-                        uint32_t* hist1, int64_t ntiles, int64_t tile_rows, void* scan_scratch,
+                        uint32_t* hist1, uint32_t* chunk_starts, int64_t ntiles, int64_t tile_rows,
+                        void* scan_scratch,
                         unsigned long long* tkeys, uint32_t* trows, unsigned long long* skeys,
                         uint32_t* srows, uint64_t* row_ids, bool ids_as_rows, Bucket* tbl,
                         uint32_t* dup_rows, BigSeg* big, BuildCounters* ctr, int big_grid, hipStream_t s);

@@ -285,3 +285,29 @@ def test_explicit_build_ids(dfp, oracle_mod, probe_mode, ids_u31, dups):
         b, p = t.probe(torch.from_numpy(pk).cuda())
     ob, op = oracle_mod.inner_join(bk, pk, bv, None)
     assert_same(b, p, ids[ob.astype(np.int64)].astype(np.uint64), op)
+
+
+def test_large_build_120m_rows(dfp):
+    """A 1.2e8-row build (past the 5.9e7-row limit of round-1's first table geometry):
+    size-independent properties on the GPU - every pair has equal keys, every probe key
+    below N matches exactly its one build row (a permutation build side), canonical
+    order, no pair for keys >= N."""
+    L = dfp.load()
+    N, P = 120_000_000, 10_000_000
+    s = torch.cuda.current_stream().cuda_stream
+    bk = torch.empty(N, dtype=torch.int64, device="cuda")
+    assert L.hj_gen_perm_keys(bk.data_ptr(), N, 7368787, N, s) == 0
+    pk = torch.empty(P, dtype=torch.int64, device="cuda")
+    assert L.hj_gen_uniform_keys(pk.data_ptr(), P, 99, 2 * N, s) == 0
+    with dfp.HashTable(1, "int64", 0) as t:
+        t.build(bk)
+        b, p = t.probe(pk, device_output=True)
+        st = t.stats()
+    assert st["distinct_keys"] == N and st["dup_keys"] == 0
+    want = int((pk < N).sum())
+    assert b.numel() == want
+    pl = p.to(torch.int64)
+    assert bool((bk[b] == pk[pl]).all())
+    assert bool((pl[1:] > pl[:-1]).all())  # unique build keys: one pair per matched row, ascending
+    del bk, pk, b, p
+    torch.cuda.empty_cache()
