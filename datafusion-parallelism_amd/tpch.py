@@ -28,6 +28,20 @@ Plan: customer filter -> build; orders filter -> probe (right-semi on o_custkey)
 build on o_orderkey; lineitem filter -> probe; per-order revenue sums; top 10. Both
 joins run on the hash-join kernels; filters, the group-by sum and the top-k are torch
 device ops.
+
+Q9 (BASELINE.json configs[4], the six-way join):
+    select nation, o_year, sum(l_extendedprice * (1 - l_discount)
+                               - ps_supplycost * l_quantity) as sum_profit
+    from part, supplier, lineitem, partsupp, orders, nation
+    where s_suppkey = l_suppkey and ps_suppkey = l_suppkey and ps_partkey = l_partkey
+      and p_partkey = l_partkey and o_orderkey = l_orderkey and s_nationkey = n_nationkey
+      and p_name like '%green%'
+    group by nation, o_year order by nation, o_year desc
+`generate(..., q9=True)` adds part (p_name's colour words reduced to the flag "contains
+green": 5 distinct words of the spec's 92, so probability 5/92), supplier (nation
+uniform), partsupp (4 suppliers per part by the spec's formula, supply cost 1.00-1000.00)
+and lineitem's partkey / suppkey / quantity consistent with partsupp. Five joins run on
+the hash-join kernels; (partkey, suppkey) is one int64 key partkey << 32 | suppkey.
 """
 from __future__ import annotations
 
@@ -79,6 +93,17 @@ class Tables:
     l_extendedprice: torch.Tensor  # int64 cents
     l_discount: torch.Tensor  # int32 percent 0..10
     l_shipdate: torch.Tensor  # int32 days
+    # Q9 columns (generate(..., q9=True))
+    l_partkey: torch.Tensor | None = None
+    l_suppkey: torch.Tensor | None = None
+    l_quantity: torch.Tensor | None = None
+    p_partkey: torch.Tensor | None = None
+    p_green: torch.Tensor | None = None  # bool: p_name like '%green%'
+    s_suppkey: torch.Tensor | None = None
+    s_nationkey: torch.Tensor | None = None
+    ps_partkey: torch.Tensor | None = None
+    ps_suppkey: torch.Tensor | None = None
+    ps_supplycost: torch.Tensor | None = None  # int64 cents
 
     @property
     def device(self):
@@ -95,10 +120,23 @@ class Tables:
                                "o_orderdate": h(self.o_orderdate), "o_shippriority": h(self.o_shippriority)})
         lineitem = pd.DataFrame({"l_orderkey": h(self.l_orderkey), "l_extendedprice": h(self.l_extendedprice),
                                  "l_discount": h(self.l_discount), "l_shipdate": h(self.l_shipdate)})
-        return customer, orders, lineitem
+        if self.l_partkey is None:
+            return customer, orders, lineitem
+        lineitem = lineitem.assign(l_partkey=h(self.l_partkey), l_suppkey=h(self.l_suppkey),
+                                   l_quantity=h(self.l_quantity))
+        part = pd.DataFrame({"p_partkey": h(self.p_partkey), "p_green": h(self.p_green)})
+        supplier = pd.DataFrame({"s_suppkey": h(self.s_suppkey), "s_nationkey": h(self.s_nationkey)})
+        partsupp = pd.DataFrame({"ps_partkey": h(self.ps_partkey), "ps_suppkey": h(self.ps_suppkey),
+                                 "ps_supplycost": h(self.ps_supplycost)})
+        return customer, orders, lineitem, part, supplier, partsupp
 
 
-def generate(sf: float, device="cuda:0", seed: int = 1) -> Tables:
+def _supplier_of(partkey: torch.Tensor, i: torch.Tensor, ns: int) -> torch.Tensor:
+    """The spec's i-th (0..3) supplier of a part: (ps_partkey + i * (S/4 + (ps_partkey-1)/S)) % S + 1."""
+    return (partkey + i * (ns // 4 + (partkey - 1) // ns)) % ns + 1
+
+
+def generate(sf: float, device="cuda:0", seed: int = 1, q9: bool = False) -> Tables:
     dev = torch.device(device)
     nc = int(150_000 * sf)
     no = int(1_500_000 * sf)
@@ -125,8 +163,21 @@ def generate(sf: float, device="cuda:0", seed: int = 1) -> Tables:
     l_discount = _uniform(nl, seed * 1000 + 7, 0, 10, dev).to(torch.int32)
     l_shipdate = (o_orderdate[l_order_row].to(torch.int64) + _uniform(nl, seed * 1000 + 8, 1, 121, dev)).to(
         torch.int32)
-    return Tables(sf, c_custkey, c_mktsegment, o_orderkey, o_custkey, o_orderdate, o_shippriority, l_orderkey,
-                  l_extendedprice, l_discount, l_shipdate)
+    t = Tables(sf, c_custkey, c_mktsegment, o_orderkey, o_custkey, o_orderdate, o_shippriority, l_orderkey,
+               l_extendedprice, l_discount, l_shipdate)
+    if q9:
+        ns = max(int(10_000 * sf), 4)
+        t.l_partkey, t.l_quantity = partkey, quantity
+        t.l_suppkey = _supplier_of(partkey, _uniform(nl, seed * 1000 + 9, 0, 3, dev), ns)
+        t.p_partkey = torch.arange(1, npart + 1, dtype=torch.int64, device=dev)
+        t.p_green = _uniform(npart, seed * 1000 + 10, 0, 91, dev) < 5
+        t.s_suppkey = torch.arange(1, ns + 1, dtype=torch.int64, device=dev)
+        t.s_nationkey = _uniform(ns, seed * 1000 + 11, 0, 24, dev)
+        pp = torch.repeat_interleave(t.p_partkey, 4)
+        t.ps_partkey = pp
+        t.ps_suppkey = _supplier_of(pp, torch.arange(4 * npart, device=dev) % 4, ns)
+        t.ps_supplycost = _uniform(4 * npart, seed * 1000 + 12, 100, 100_000, dev)
+    return t
 
 
 @dataclass
@@ -168,3 +219,57 @@ def q3(t: Tables, segment: str = "BUILDING", date: str = "1995-03-15", limit: in
     rows = sel[top]
     return Q3Result(t.o_orderkey[rows].tolist(), sums[top].tolist(), t.o_orderdate[rows].tolist(),
                     t.o_shippriority[rows].tolist(), int(g.numel()))
+
+
+NATIONS = ["ALGERIA", "ARGENTINA", "BRAZIL", "CANADA", "EGYPT", "ETHIOPIA", "FRANCE", "GERMANY", "INDIA",
+           "INDONESIA", "IRAN", "IRAQ", "JAPAN", "JORDAN", "KENYA", "MOROCCO", "PERU", "CHINA", "ROMANIA",
+           "SAUDI ARABIA", "VIETNAM", "RUSSIA", "UNITED KINGDOM", "UNITED STATES", "MOZAMBIQUE"]
+
+
+def year_of(days: torch.Tensor) -> torch.Tensor:
+    """Calendar year of days since 1992-01-01 (1992 .. 1998; leap years 1992, 1996)."""
+    starts = torch.tensor([day(f"{y}-01-01") for y in range(1992, 2000)], device=days.device)
+    return torch.bucketize(days.to(torch.int64), starts, right=True) - 1 + 1992
+
+
+def _join(build: torch.Tensor, probe: torch.Tensor):
+    """Inner-join pairs (build row int64, probe row int64) on the GPU hash join."""
+    dev = probe.device
+    with HashTable(1, "int64", dev.index or 0) as t:
+        t.build(build.contiguous())
+        b, p = t.probe(probe.contiguous(), device_output=True)
+    return b, p.to(torch.int64)
+
+
+def q9(t: Tables, color_flag: str = "green") -> list[tuple[str, int, int]]:
+    """-> [(nation, o_year, sum_profit in 1e-4 units)] ordered by nation, o_year desc."""
+    if t.l_partkey is None:
+        raise ValueError("generate(..., q9=True) tables are needed")
+    dev = t.device
+    # lineitem ⋈ part (p_name like '%green%')
+    _, li = _join(t.p_partkey[t.p_green], t.l_partkey)
+    lk = t.l_partkey[li]
+    ls = t.l_suppkey[li]
+    # ⋈ partsupp on (partkey, suppkey)
+    b_ps, p_l = _join((t.ps_partkey << 32) | t.ps_suppkey, (lk << 32) | ls)
+    li, ls = li[p_l], ls[p_l]
+    cost = t.ps_supplycost[b_ps]
+    # ⋈ supplier on suppkey -> nation
+    b_s, p_l = _join(t.s_suppkey, ls)
+    li, cost, nation = li[p_l], cost[p_l], t.s_nationkey[b_s]
+    # ⋈ orders on orderkey -> year
+    b_o, p_l = _join(t.o_orderkey, t.l_orderkey[li])
+    li, cost, nation = li[p_l], cost[p_l], nation[p_l]
+    year = year_of(t.o_orderdate[b_o])
+    amount = (t.l_extendedprice[li] * (100 - t.l_discount[li].to(torch.int64))
+              - cost * t.l_quantity[li] * 100)
+    # ⋈ nation is the 25-row dimension: group by (nationkey, year)
+    gid = nation * 8 + (year - 1992)
+    sums = torch.zeros(25 * 8, dtype=torch.int64, device=dev).index_add_(0, gid, amount)
+    present = torch.zeros(25 * 8, dtype=torch.bool, device=dev)
+    present[gid] = True
+    out = []
+    for g in torch.nonzero(present).squeeze(1).tolist():
+        out.append((NATIONS[g // 8], 1992 + g % 8, int(sums[g])))
+    out.sort(key=lambda r: (r[0], -r[1]))
+    return out

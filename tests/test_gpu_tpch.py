@@ -45,3 +45,33 @@ def test_generator_shape(dfp):
     n = len(t.l_orderkey)
     assert 15000 <= n <= 7 * 15000 and abs(n / 15000 - 4.0) < 0.2
     assert int(t.l_discount.max()) <= 10 and int(t.o_orderdate.max()) <= tpch.ORDERDATE_MAX
+
+
+def q9_pandas(orders, lineitem, part, supplier, partsupp):
+    import pandas as pd
+    from datafusion_parallelism_amd import tpch
+
+    p = part[part.p_green]
+    x = lineitem.merge(p, left_on="l_partkey", right_on="p_partkey")
+    x = x.merge(partsupp, left_on=["l_partkey", "l_suppkey"], right_on=["ps_partkey", "ps_suppkey"])
+    x = x.merge(supplier, left_on="l_suppkey", right_on="s_suppkey")
+    x = x.merge(orders, left_on="l_orderkey", right_on="o_orderkey")
+    dates = pd.to_datetime("1992-01-01") + pd.to_timedelta(x.o_orderdate, unit="D")
+    x = x.assign(o_year=dates.dt.year,
+                 amount=x.l_extendedprice.astype(np.int64) * (100 - x.l_discount.astype(np.int64))
+                 - x.ps_supplycost.astype(np.int64) * x.l_quantity.astype(np.int64) * 100,
+                 nation=[tpch.NATIONS[k] for k in x.s_nationkey])
+    g = x.groupby(["nation", "o_year"], as_index=False)["amount"].sum()
+    g = g.sort_values(["nation", "o_year"], ascending=[True, False], kind="mergesort")
+    return [(r.nation, int(r.o_year), int(r.amount)) for r in g.itertuples()]
+
+
+@pytest.mark.parametrize("sf", [0.01, 0.05])
+def test_q9_matches_pandas(dfp, sf):
+    from datafusion_parallelism_amd import tpch
+
+    t = tpch.generate(sf, "cuda:0", seed=5, q9=True)
+    got = tpch.q9(t)
+    _, orders, lineitem, part, supplier, partsupp = t.to_pandas()
+    want = q9_pandas(orders, lineitem, part, supplier, partsupp)
+    assert len(got) > 0 and got == want
