@@ -188,6 +188,8 @@ def main():
                     help="use the radix-exchange path even with one rank (testing)")
     ap.add_argument("--chunks", type=int, default=4,
                     help="multi-GPU: probe-side chunks whose exchange overlaps the previous chunk's probe")
+    ap.add_argument("--no-compress-keys", action="store_true",
+                    help="multi-GPU: exchange full int64 keys / u64 build ids even when 32 bits suffice")
     args = ap.parse_args()
     cfg = CONFIGS[args.config]
 
@@ -217,7 +219,8 @@ def main():
     else:
         from datafusion_parallelism_amd.distributed import DistributedHashJoin
 
-        job = DistJob(DistributedHashJoin(chunks=args.chunks), bk, pk, rank, dev)
+        job = DistJob(DistributedHashJoin(chunks=args.chunks, compress_keys=not args.no_compress_keys), bk, pk,
+                      rank, dev)
 
     def barrier():
         if use_dist:
@@ -326,18 +329,19 @@ class DistJob:
 
     def step(self):
         t0 = time.perf_counter()
-        bk, bi, _ = self.dj.shard(self.bk, self.bbase)
+        plan = self.dj.prepare(self.bk, self.pk, self.bbase)
+        bk, bi = self.dj.shard_build(self.bk, self.bbase, plan)
         torch.cuda.synchronize(self.dev)
         t1 = time.perf_counter()
         self.exchange_ms.append((t1 - t0) * 1e3)
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
         ev[0].record()
         if self.dj.chunks > 1:
-            outs = self.dj.run_pipelined(bk, bi, self.pk, self.pbase)
+            outs = self.dj.run_pipelined(bk, bi, self.pk, self.pbase, plan)
         else:
             from datafusion_parallelism_amd.distributed import gpu_local_join
 
-            pk, pi, _ = self.dj.shard(self.pk, self.pbase, torch.int32)
+            pk, pi, _ = self.dj.shard(self.pk, self.pbase, torch.int32, key_offset=plan.key_offset)
             outs = [gpu_local_join(bk, bi, pk, pi, self.cap)]
         ev[1].record()
         self._ev = ev

@@ -827,19 +827,25 @@ int64_t hj_partition_workspace_bytes(int64_t n, int nparts) { return radix_parti
 
 hj_status hj_radix_partition(hj_key_type key_type, const void* keys, const uint8_t* validity, int64_t validity_offset,
                              const uint64_t* ids, uint64_t id_base, int64_t n, int nparts, void* out_keys,
-                             void* out_ids, int id_bytes, int64_t* counts, void* workspace, void* stream) {
+                             int out_key_bytes, int64_t key_offset, void* out_ids, int id_bytes, int64_t* counts,
+                             void* workspace, void* stream) {
     if (device_count() == 0) return fail(HJ_ERR_NO_DEVICE, "no GPU visible");
     if (nparts < 1 || nparts > 64 || (nparts & (nparts - 1)))
         return fail(HJ_ERR_INVALID, "nparts must be a power of two <= 64");
     if (n < 0) return fail(HJ_ERR_INVALID, "negative length");
     if (id_bytes != 4 && id_bytes != 8) return fail(HJ_ERR_INVALID, "id_bytes must be 4 or 8");
+    const int kb = key_type == HJ_INT64 ? 8 : 4;
+    if ((out_key_bytes != 4 && out_key_bytes != 8) || out_key_bytes > kb)
+        return fail(HJ_ERR_INVALID, "out_key_bytes must be 4 or the key width");
+    if (kb == 4 && key_offset != 0) return fail(HJ_ERR_INVALID, "key_offset applies to int64 keys");
     if (id_bytes == 4 && ids == nullptr && (uint64_t)id_base + (uint64_t)n > 0x100000000ull)
         return fail(HJ_ERR_INVALID, "32-bit ids overflow: id_base + n > 2^32");
     if (!is_device_ptr(keys) || !is_device_ptr(validity) || !is_device_ptr(ids) || !is_device_ptr(out_keys) ||
         !is_device_ptr(out_ids) || !is_device_ptr(counts) || !is_device_ptr(workspace))
         return fail(HJ_ERR_INVALID, "hj_radix_partition takes device pointers");
     HIP_TRY(launch_radix_partition(key_type == HJ_INT64 ? 8 : 4, keys, validity, validity_offset, ids, id_base, n,
-                                   nparts, out_keys, out_ids, id_bytes, counts, workspace, (hipStream_t)stream));
+                                   nparts, out_keys, out_key_bytes, key_offset, out_ids, id_bytes, counts, workspace,
+                                   (hipStream_t)stream));
     return HJ_OK;
 }
 

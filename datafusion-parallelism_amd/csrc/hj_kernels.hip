@@ -1508,10 +1508,11 @@ __global__ void part_counts_kernel(const uint32_t* hist, int64_t nblocks, int np
     }
 }
 
-template <typename K, typename ID>
+template <typename K, typename OK, typename ID>
 __global__ void __launch_bounds__(kPartThreads)
 part_scatter_kernel(const void* keys, const uint8_t* valid, int64_t voff, const uint64_t* ids, uint64_t id_base,
-                    int64_t n, int nparts, const uint32_t* hist, int64_t nblocks, K* out_keys, ID* out_ids) {
+                    int64_t n, int nparts, const uint32_t* hist, int64_t nblocks, OK* out_keys, int64_t key_offset,
+                    ID* out_ids) {
     __shared__ unsigned long long s_off[kMaxParts];
     __shared__ unsigned s_wc[kPartThreads / 64][kMaxParts];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -1537,7 +1538,7 @@ part_scatter_kernel(const void* keys, const uint8_t* valid, int64_t voff, const 
         if (p >= 0) {
             unsigned long long pos = s_off[p] + rank;
             for (int w = 0; w < wave; ++w) pos += s_wc[w][p];
-            out_keys[pos] = (K)ld_key<K>(keys, i);
+            out_keys[pos] = (OK)(ld_key<K>(keys, i) - key_offset);  // OK narrower: caller checked the range
             out_ids[pos] = (ID)(ids ? ids[i] : id_base + (uint64_t)i);
         }
         __syncthreads();
@@ -1875,7 +1876,8 @@ int64_t radix_partition_workspace(int64_t n, int nparts) {
 
 hipError_t launch_radix_partition(int key_bytes, const void* keys, const uint8_t* valid, int64_t voff,
                                   const uint64_t* ids, uint64_t id_base, int64_t n, int nparts, void* out_keys,
-                                  void* out_ids, int id_bytes, int64_t* counts, void* workspace, hipStream_t s) {
+                                  int out_key_bytes, int64_t key_offset, void* out_ids, int id_bytes, int64_t* counts,
+                                  void* workspace, hipStream_t s) {
     if (nparts < 1 || nparts > kMaxParts || (nparts & (nparts - 1))) return hipErrorInvalidValue;
     const int64_t nblocks = (n + kPartChunk - 1) / kPartChunk;
     if (nblocks == 0) return hipMemsetAsync(counts, 0, sizeof(int64_t) * nparts, s);
@@ -1892,14 +1894,15 @@ hipError_t launch_radix_partition(int key_bytes, const void* keys, const uint8_t
     hipError_t e = launch_scan(hist, hlen, scratch, nullptr, s);
     if (e != hipSuccess) return e;
     part_counts_kernel<<<1, 64, 0, s>>>(hist, nblocks, nparts, total, counts);
-#define DFP_PS(K, ID)                                                                              \
-    part_scatter_kernel<K, ID><<<(unsigned)nblocks, kPartThreads, 0, s>>>(keys, valid, voff, ids, id_base, n, \
-                                                                         nparts, hist, nblocks, (K*)out_keys, \
-                                                                         (ID*)out_ids)
-    if (key_bytes == 8) {
-        if (id_bytes == 8) DFP_PS(int64_t, uint64_t); else DFP_PS(int64_t, uint32_t);
+#define DFP_PS(K, OK, ID)                                                                                 \
+    part_scatter_kernel<K, OK, ID><<<(unsigned)nblocks, kPartThreads, 0, s>>>(                                  \
+        keys, valid, voff, ids, id_base, n, nparts, hist, nblocks, (OK*)out_keys, key_offset, (ID*)out_ids)
+    if (key_bytes == 8 && out_key_bytes == 8) {
+        if (id_bytes == 8) DFP_PS(int64_t, int64_t, uint64_t); else DFP_PS(int64_t, int64_t, uint32_t);
+    } else if (key_bytes == 8) {
+        if (id_bytes == 8) DFP_PS(int64_t, int32_t, uint64_t); else DFP_PS(int64_t, int32_t, uint32_t);
     } else {
-        if (id_bytes == 8) DFP_PS(int32_t, uint64_t); else DFP_PS(int32_t, uint32_t);
+        if (id_bytes == 8) DFP_PS(int32_t, int32_t, uint64_t); else DFP_PS(int32_t, int32_t, uint32_t);
     }
 #undef DFP_PS
     return hipGetLastError();

@@ -27,20 +27,24 @@ from .table import HashTable
 
 
 def gpu_radix_partition(keys: torch.Tensor, ids: torch.Tensor | None, id_base: int, nparts: int,
-                        stream: int | None = None, id_dtype: torch.dtype = torch.int64):
+                        stream: int | None = None, id_dtype: torch.dtype = torch.int64,
+                        key_offset: int | None = None):
     """hj_radix_partition on device tensors -> (keys grouped by destination, ids
-    (int64 = u64 build ids, int32 = u32 probe ids), counts[nparts] int64 device tensor)."""
+    (int64 = u64 build ids, int32 = u32 probe ids), counts[nparts] int64 device tensor).
+    key_offset (int64 keys): the keys come out as int32(key - key_offset)."""
     L = _lib.load()
     n = keys.numel()
     kt = HJ_INT64 if keys.dtype == torch.int64 else HJ_INT32
-    out_k = torch.empty(n, dtype=keys.dtype, device=keys.device)
+    narrow = key_offset is not None and keys.dtype == torch.int64
+    out_k = torch.empty(n, dtype=torch.int32 if narrow else keys.dtype, device=keys.device)
     out_i = torch.empty(n, dtype=id_dtype, device=keys.device)
     counts = torch.zeros(nparts, dtype=torch.int64, device=keys.device)
     ws = torch.empty(max(L.hj_partition_workspace_bytes(n, nparts), 8), dtype=torch.uint8, device=keys.device)
     s = stream if stream is not None else torch.cuda.current_stream(keys.device).cuda_stream
     check(L.hj_radix_partition(kt, keys.data_ptr(), None, 0, None if ids is None else ids.data_ptr(), id_base, n,
-                               nparts, out_k.data_ptr(), out_i.data_ptr(), 8 if id_dtype == torch.int64 else 4,
-                               counts.data_ptr(), ws.data_ptr(), s))
+                               nparts, out_k.data_ptr(), out_k.element_size(), key_offset if narrow else 0,
+                               out_i.data_ptr(), 8 if id_dtype == torch.int64 else 4, counts.data_ptr(),
+                               ws.data_ptr(), s))
     return out_k, out_i, counts
 
 
@@ -107,6 +111,14 @@ def gpu_local_join(build_keys: torch.Tensor, build_ids: torch.Tensor, probe_keys
 
 
 @dataclass
+class ExchangePlan:
+    """What the exchange narrows (DistributedHashJoin.prepare): keys travel as
+    int32(key - key_offset) when key_offset is set, build ids as build_id_dtype."""
+    key_offset: int | None = None
+    build_id_dtype: torch.dtype = torch.int64
+
+
+@dataclass
 class ExchangeStats:
     sent_rows: int = 0
     recv_rows: int = 0
@@ -147,7 +159,7 @@ class DistributedHashJoin:
     default to GpuLocalTable."""
 
     def __init__(self, group=None, partition_fn: Callable | None = None, local_join_fn: Callable | None = None,
-                 chunks: int = 1, local_build_fn: Callable | None = None):
+                 chunks: int = 1, local_build_fn: Callable | None = None, compress_keys: bool = True):
         self.group = group
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
@@ -155,30 +167,69 @@ class DistributedHashJoin:
         self.local_join_fn = local_join_fn or gpu_local_join
         self.local_build_fn = local_build_fn or GpuLocalTable
         self.chunks = max(1, int(chunks))
+        self.compress_keys = compress_keys
 
-    def _partition(self, keys: torch.Tensor, id_base: int, id_dtype: torch.dtype):
+    def prepare(self, build_keys: torch.Tensor, probe_keys: torch.Tensor, build_base: int) -> ExchangePlan:
+        """Narrow what travels: when the global key range of both sides spans < 2^32,
+        the partition writes keys as int32(key - min - 2^31) (a bijection, so equality
+        and the join are unchanged; the local tables then use int32 keys), and build ids
+        travel as u32 when the global build side has < 2^31 rows. One pass over each
+        side (aminmax), two 8-byte all-reduces and one host read."""
+        plan = ExchangePlan()
+        if not self.compress_keys or build_keys.dtype != torch.int64:
+            return plan
+        dev = build_keys.device
+        big, small = 2**63 - 1, -(2**63)
+        lo = torch.full((1,), big, dtype=torch.int64, device=dev)
+        hi = torch.tensor([small, build_base + build_keys.numel()], dtype=torch.int64, device=dev)
+        for k in (build_keys, probe_keys):
+            if k.numel():
+                mn, mx = torch.aminmax(k)
+                lo = torch.minimum(lo, mn.view(1))
+                hi[0] = torch.maximum(hi[0], mx)
+        dist.all_reduce(lo, op=dist.ReduceOp.MIN, group=self.group)
+        dist.all_reduce(hi, op=dist.ReduceOp.MAX, group=self.group)
+        gmin, gmax, bend = torch.cat([lo, hi]).tolist()
+        if bend < 2**31:
+            plan.build_id_dtype = torch.int32
+        if gmin <= gmax and gmax - gmin < 2**32:
+            plan.key_offset = gmin + 2**31
+        return plan
+
+    def _partition(self, keys: torch.Tensor, id_base: int, id_dtype: torch.dtype, key_offset: int | None):
         if self.partition_fn is gpu_radix_partition:
-            return gpu_radix_partition(keys, None, id_base, self.world, id_dtype=id_dtype)
+            return gpu_radix_partition(keys, None, id_base, self.world, id_dtype=id_dtype, key_offset=key_offset)
+        if key_offset is not None and keys.dtype == torch.int64:  # host stand-ins: narrow first
+            keys = (keys - key_offset).to(torch.int32)
         return self.partition_fn(keys, None, id_base, self.world)
 
-    def shard(self, keys: torch.Tensor, id_base: int, id_dtype: torch.dtype = torch.int64, async_op: bool = False):
+    def shard(self, keys: torch.Tensor, id_base: int, id_dtype: torch.dtype = torch.int64, async_op: bool = False,
+              key_offset: int | None = None):
         """Partition by destination rank and exchange: -> (keys, global ids, stats).
         Build rows carry u64 ids (int64), probe rows u32 ids (int32, the reference's
-        UInt32 probe index): 16 resp. 12 bytes per int64-key row on the wire."""
-        k, i, c = self._partition(keys, id_base, id_dtype)
+        UInt32 probe index): 16 resp. 12 bytes per int64-key row on the wire, 8 with a
+        narrowing plan (prepare)."""
+        k, i, c = self._partition(keys, id_base, id_dtype, key_offset)
         return all_to_all_rows(k, i, c, self.group, async_op=async_op)
+
+    def shard_build(self, build_keys: torch.Tensor, build_base: int, plan: ExchangePlan):
+        """The build side's exchange under `plan`: -> (keys, int64 global ids)."""
+        bk, bi, _ = self.shard(build_keys, build_base, plan.build_id_dtype, key_offset=plan.key_offset)
+        return bk, (bi.to(torch.int64) if bi.dtype != torch.int64 else bi)
 
     def run(self, build_keys: torch.Tensor, build_base: int, probe_keys: torch.Tensor, probe_base: int,
             capacity_hint: int | None = None):
         """-> this rank's share of the global pairs (build_idx, probe_idx)."""
-        bk, bi, _ = self.shard(build_keys, build_base)
+        plan = self.prepare(build_keys, probe_keys, build_base)
+        bk, bi = self.shard_build(build_keys, build_base, plan)
         if self.chunks <= 1:
-            pk, pi, _ = self.shard(probe_keys, probe_base, torch.int32)
+            pk, pi, _ = self.shard(probe_keys, probe_base, torch.int32, key_offset=plan.key_offset)
             return self.local_join_fn(bk, bi, pk, pi, capacity_hint)
-        outs = self.run_pipelined(bk, bi, probe_keys, probe_base)
+        outs = self.run_pipelined(bk, bi, probe_keys, probe_base, plan)
         return torch.cat([b for b, _ in outs]), torch.cat([p for _, p in outs])
 
-    def run_pipelined(self, bk: torch.Tensor, bi: torch.Tensor, probe_keys: torch.Tensor, probe_base: int):
+    def run_pipelined(self, bk: torch.Tensor, bi: torch.Tensor, probe_keys: torch.Tensor, probe_base: int,
+                      plan: ExchangePlan | None = None):
         """Local build, then the probe side in `chunks` slices: exchange of slice c in
         flight while slice c-1 is probed. -> list of per-chunk (build_idx, probe_idx)."""
         table = self.local_build_fn(bk, bi)
@@ -188,7 +239,8 @@ class DistributedHashJoin:
             results, pending = [], None
             for c in range(self.chunks):
                 lo, hi = bounds[c], bounds[c + 1]
-                rk, ri, _, works = self.shard(probe_keys[lo:hi], probe_base + lo, torch.int32, async_op=True)
+                rk, ri, _, works = self.shard(probe_keys[lo:hi], probe_base + lo, torch.int32, async_op=True,
+                                              key_offset=plan.key_offset if plan else None)
                 if pending is not None:
                     results.append(self._probe_chunk(table, *pending))
                 pending = (rk, ri, works)

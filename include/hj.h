@@ -185,17 +185,21 @@ hj_status hj_table_stream_wait(const hj_table* t, void* stream);
  *      relative is the shard function of
  *      src/utils/partitioned_concurrent_self_hash_join_map.rs:13-16). ------------ */
 
-/* Partition n rows into `nparts` (power of two) by hash bits:
+/* Partition n rows into `nparts` (power of two) by hash bits of the key:
  * out_keys/out_ids are grouped by destination (stable); counts[nparts] (device int64)
  * receives the rows per destination. ids may be NULL (then id = id_base + i); out_ids
  * holds uint64 (id_bytes 8, build rows) or uint32 (id_bytes 4, probe rows: the
- * reference's UInt32 probe indices) ids. Null rows are dropped. Device pointers,
- * asynchronous on `stream`; `workspace` of hj_partition_workspace_bytes(n, nparts) bytes. */
+ * reference's UInt32 probe indices) ids. out_key_bytes 4 with int64 keys writes
+ * int32(key - key_offset) (the caller guarantees the range; a bijection, so the join is
+ * unchanged and the exchange moves 4 bytes per key). Null rows are dropped. Device
+ * pointers, asynchronous on `stream`; `workspace` of hj_partition_workspace_bytes(n,
+ * nparts) bytes. */
 int64_t hj_partition_workspace_bytes(int64_t n, int nparts);
 hj_status hj_radix_partition(hj_key_type key_type, const void* keys,
                              const uint8_t* validity, int64_t validity_offset,
                              const uint64_t* ids, uint64_t id_base, int64_t n, int nparts,
-                             void* out_keys, void* out_ids, int id_bytes, int64_t* counts,
+                             void* out_keys, int out_key_bytes, int64_t key_offset,
+                             void* out_ids, int id_bytes, int64_t* counts,
                              void* workspace, void* stream);
 
 /* ---- join types and output materialisation. Device pointers,

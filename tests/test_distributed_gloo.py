@@ -80,8 +80,10 @@ def _worker(rank, world, port, bks, pks, q, chunks=1):
         b, p = dj.run(torch.from_numpy(bks[rank]), bbase, torch.from_numpy(pks[rank]), pbase)
         segs = [(b, p)]
     else:  # pipelined probe side: canonical per chunk
-        bk, bi, _ = dj.shard(torch.from_numpy(bks[rank]), bbase)
-        segs = dj.run_pipelined(bk, bi, torch.from_numpy(pks[rank]), pbase)
+        plan = dj.prepare(torch.from_numpy(bks[rank]), torch.from_numpy(pks[rank]), bbase)
+        assert (plan.key_offset is None) == (bks[rank].max() - bks[rank].min() >= 2**32)
+        bk, bi = dj.shard_build(torch.from_numpy(bks[rank]), bbase, plan)
+        segs = dj.run_pipelined(bk, bi, torch.from_numpy(pks[rank]), pbase, plan)
         assert len(segs) == chunks
         b, p = torch.cat([x for x, _ in segs]), torch.cat([y for _, y in segs])
     # every rank's local output is canonical for its key subset (per chunk)
@@ -103,11 +105,15 @@ def _free_port():
     return port
 
 
-@pytest.mark.parametrize("world,chunks", [(2, 1), (2, 3)])
-def test_distributed_exchange_matches_single_join(oracle_mod, world, chunks):
+@pytest.mark.parametrize("world,chunks,wide", [(2, 1, False), (2, 3, False), (2, 3, True)])
+def test_distributed_exchange_matches_single_join(oracle_mod, world, chunks, wide):
+    """wide: keys spread over > 2^32 values, so they travel as full int64 (otherwise
+    DistributedHashJoin.prepare narrows them to int32 offsets)."""
     rng = np.random.default_rng(9)
     bk = rng.integers(0, 3000, 9000).astype(np.int64)
     pk = rng.integers(0, 5000, 14000).astype(np.int64)
+    if wide:
+        bk, pk = bk * (2**33) - 2**40, pk * (2**33) - 2**40
     bks = [bk[:4000], bk[4000:]]
     pks = [pk[:9000], pk[9000:]]
     ctx = mp.get_context("spawn")

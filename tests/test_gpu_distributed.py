@@ -26,16 +26,22 @@ def _mix64(k):
 
 @pytest.mark.parametrize("nparts", [1, 2, 8, 64])
 @pytest.mark.parametrize("id_dtype", [torch.int64, torch.int32])
-def test_radix_partition_kernel(dfp, nparts, id_dtype):
+@pytest.mark.parametrize("narrow", [False, True])
+def test_radix_partition_kernel(dfp, nparts, id_dtype, narrow):
+    """Stable multi-split by the low hash bits; narrow: keys written as int32(key - off)."""
     from datafusion_parallelism_amd.distributed import gpu_radix_partition
 
     rng = np.random.default_rng(nparts)
-    k = rng.integers(-10**12, 10**12, 100003)
-    out_k, out_i, counts = gpu_radix_partition(torch.from_numpy(k).cuda(), None, 1000, nparts, id_dtype=id_dtype)
+    k = rng.integers(-10**12, 10**12, 100003) if not narrow else rng.integers(5 * 10**9, 9 * 10**9, 100003)
+    off = 5 * 10**9 + 2**31 if narrow else None
+    out_k, out_i, counts = gpu_radix_partition(torch.from_numpy(k).cuda(), None, 1000, nparts, id_dtype=id_dtype,
+                                               key_offset=off)
     dest = (_mix64(k) & np.uint64(nparts - 1)).astype(np.int64)
     order = np.argsort(dest, kind="stable")  # stable multi-split
     assert np.array_equal(counts.cpu().numpy(), np.bincount(dest, minlength=nparts))
-    assert np.array_equal(out_k.cpu().numpy(), k[order])
+    want_k = k[order] if not narrow else (k[order] - off).astype(np.int32)
+    assert out_k.dtype == (torch.int32 if narrow else torch.int64)
+    assert np.array_equal(out_k.cpu().numpy(), want_k)
     assert np.array_equal(out_i.cpu().numpy(), order + 1000)
 
 
