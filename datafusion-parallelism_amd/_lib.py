@@ -67,6 +67,7 @@ SIGNATURES = [
     ("hj_pairs_free", None, [ctypes.POINTER(HjPairs)]),
     ("hj_probe_workspace_bytes", I64, [I64]),
     ("hj_set_probe_mode", I32, [I32]),
+    ("hj_set_build_mode", I32, [I32]),
     ("hj_probe_async", I32, [P, P, P, I64, I64, P, P, I64, P, P, P]),
     ("hj_probe_async_ids", I32, [P, P, P, I64, P, I64, P, P, I64, P, P, P]),
     ("hj_table_stream_wait", I32, [P, P]),

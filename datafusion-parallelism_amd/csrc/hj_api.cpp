@@ -26,6 +26,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <condition_variable>
 #include <mutex>
@@ -182,6 +183,20 @@ bool is_device_ptr(const void* p) {
 // 2150 us at 0.5, build unchanged; profiles/r01_load_factor.txt): fewer full buckets,
 // so fewer second bucket lines on the miss path. Override with DFP_HJ_LOAD_FACTOR.
 constexpr double kDefaultLoadFactor = 0.35;
+
+// Table layout: 0 auto (direct-addressed when the key range is at most kDenseFactor x the
+// build rows, else hashed buckets), 1 hashed always. DFP_HJ_DENSE=0 selects 1.
+constexpr uint64_t kDenseFactor = 8;
+std::atomic<int> g_build_mode{-1};
+int build_mode() {
+    int m = g_build_mode.load(std::memory_order_relaxed);
+    if (m < 0) {
+        const char* e = getenv("DFP_HJ_DENSE");
+        m = (e && e[0] == '0') ? 1 : 0;
+        g_build_mode.store(m, std::memory_order_relaxed);
+    }
+    return m;
+}
 double load_factor() {
     const char* e = getenv("DFP_HJ_LOAD_FACTOR");
     double lf = e ? atof(e) : kDefaultLoadFactor;
@@ -226,6 +241,9 @@ struct hj_table {
     uint32_t nb = 0, clog2 = 10, nchunks = 0;
     uint32_t* dup_rows = nullptr;
     uint64_t* row_ids = nullptr;
+    uint32_t* dense = nullptr;  // direct-addressed layout (dense key range), else buckets
+    int64_t dmin = 0;
+    uint64_t drange = 0;
     BuildResources res;
     int64_t build_ns = 0;
     std::vector<std::pair<void*, size_t>> allocs;   // live for the table's lifetime
@@ -266,34 +284,80 @@ hipDeviceProp_t* device_props(int dev) {
 hj_status build_attempt(hj_table* t, const std::vector<Segment>& segs, double lf, bool* retry) {
     *retry = false;
     const int64_t total = t->total_rows;
-    // geometry: 5-slot buckets, chunks of 2^clog2 buckets (one workgroup builds one)
-    const double want = (double)total / (kSlots * lf);
-    // smallest chunks that fit the chunk count limit (512 buckets build four per CU)
-    uint32_t clog2 = 9;
-    uint64_t nchunks = (uint64_t)(want / (1u << clog2)) + 1;
-    while (nchunks > (uint64_t)kMaxChunks && clog2 < 11) {
-        ++clog2;
-        nchunks = (uint64_t)(want / (1u << clog2)) + 1;
+    hj_status st;
+    void* p;
+    hipStream_t s = t->res.stream;
+    Segment* d_segs;
+    BuildCounters* ctr;
+    int64_t* d_minmax;
+    if ((st = dev_alloc(t, t->scratch, &p, sizeof(Segment) * std::max<size_t>(segs.size(), 1))) != HJ_OK) return st;
+    d_segs = (Segment*)p;
+    if ((st = dev_alloc(t, t->scratch, &p, sizeof(BuildCounters))) != HJ_OK) return st;
+    ctr = (BuildCounters*)p;
+    if ((st = dev_alloc(t, t->scratch, &p, 2 * sizeof(int64_t))) != HJ_OK) return st;
+    d_minmax = (int64_t*)p;
+    if (!segs.empty())
+        HIP_TRY(hipMemcpyAsync(d_segs, segs.data(), sizeof(Segment) * segs.size(), hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemsetAsync(ctr, 0, sizeof(BuildCounters), s));
+
+    // layout: a dense key range gets the direct-addressed table (one u32 ref per key value)
+    ChunkGeom g{};
+    bool dense = false;
+    if (total > 0 && build_mode() == 0) {
+        int64_t mm[2];
+        HIP_TRY(launch_key_minmax(t->key_bytes, d_segs, (int)segs.size(), total, d_minmax, s));
+        HIP_TRY(hipMemcpyAsync(mm, d_minmax, sizeof(mm), hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        if (mm[0] <= mm[1]) {
+            const uint64_t range = (uint64_t)mm[1] - (uint64_t)mm[0] + 1;
+            const uint64_t nch = (range + (1u << kDenseShift) - 1) >> kDenseShift;
+            if (range != 0 && range <= kDenseFactor * (uint64_t)total && nch <= (uint64_t)kMaxChunks) {
+                dense = true;
+                g = ChunkGeom{0, 0, (uint32_t)nch, kDenseShift, mm[0], 1};
+                t->dmin = mm[0];
+                t->drange = range;
+            }
+        }
     }
-    if (nchunks > (uint64_t)kMaxChunks) {
-        // very large builds: fill the largest table geometry fuller (up to 0.8 slots/key)
-        const double full = (double)kMaxChunks * (1u << clog2) * kSlots;
-        if ((double)total / full > 0.8)
-            return fail(HJ_ERR_INVALID, "build side too large for one device table; shard it (hj_radix_partition)");
-        nchunks = kMaxChunks;
+    if (!dense) {
+        // geometry: 5-slot buckets, chunks of 2^clog2 buckets (one workgroup builds one)
+        const double want = (double)total / (kSlots * lf);
+        // smallest chunks that fit the chunk count limit (512 buckets build four per CU)
+        uint32_t clog2 = 9;
+        uint64_t nchunks = (uint64_t)(want / (1u << clog2)) + 1;
+        while (nchunks > (uint64_t)kMaxChunks && clog2 < 11) {
+            ++clog2;
+            nchunks = (uint64_t)(want / (1u << clog2)) + 1;
+        }
+        if (nchunks > (uint64_t)kMaxChunks) {
+            // very large builds: fill the largest table geometry fuller (up to 0.8 slots/key)
+            const double full = (double)kMaxChunks * (1u << clog2) * kSlots;
+            if ((double)total / full > 0.8)
+                return fail(HJ_ERR_INVALID, "build side too large for one device table; shard it (hj_radix_partition)");
+            nchunks = kMaxChunks;
+        }
+        g = ChunkGeom{(uint32_t)(nchunks << clog2), clog2, (uint32_t)nchunks, 0, 0, 0};
+        t->dmin = 0;
+        t->drange = 0;
     }
-    t->clog2 = clog2;
-    t->nchunks = (uint32_t)nchunks;
-    t->nb = (uint32_t)(nchunks << clog2);
+    t->clog2 = g.clog2;
+    t->nchunks = g.nchunks;
+    t->nb = g.nb;
+    const uint64_t nchunks = g.nchunks;
     hipDeviceProp_t* prop0 = device_props(t->device);
     const int64_t ntiles = build_tiles(total, prop0 ? prop0->multiProcessorCount : 256);
     const int64_t tile_rows = build_tile_rows(total, ntiles);
     const int64_t hlen = (int64_t)(nchunks + 1) * ntiles;
 
-    hj_status st;
-    void* p;
-    if ((st = dev_alloc(t, t->allocs, &p, (size_t)(t->nb + 1) * sizeof(Bucket))) != HJ_OK) return st;
-    t->tbl = (Bucket*)p;
+    t->tbl = nullptr;
+    t->dense = nullptr;
+    if (dense) {
+        if ((st = dev_alloc(t, t->allocs, &p, sizeof(uint32_t) * (size_t)(nchunks << kDenseShift))) != HJ_OK) return st;
+        t->dense = (uint32_t*)p;
+    } else {
+        if ((st = dev_alloc(t, t->allocs, &p, (size_t)(t->nb + 1) * sizeof(Bucket))) != HJ_OK) return st;
+        t->tbl = (Bucket*)p;
+    }
     if ((st = dev_alloc(t, t->allocs, &p, sizeof(uint32_t) * (size_t)(2 * total + 2))) != HJ_OK) return st;
     t->dup_rows = (uint32_t*)p;
     const bool ids_as_rows = t->has_ids && t->ids_u31;  // no id indirection at probe time
@@ -302,14 +366,10 @@ hj_status build_attempt(hj_table* t, const std::vector<Segment>& segs, double lf
             return st;
         t->row_ids = (uint64_t*)p;
     }
-    Segment* d_segs;
     uint32_t *hist, *hist1, *srows, *trows;
     unsigned long long *skeys, *tkeys;
     BigSeg* big;
-    BuildCounters* ctr;
     void* scan;
-    if ((st = dev_alloc(t, t->scratch, &p, sizeof(Segment) * std::max<size_t>(segs.size(), 1))) != HJ_OK) return st;
-    d_segs = (Segment*)p;
     if ((st = dev_alloc(t, t->scratch, &p, sizeof(uint32_t) * (size_t)std::max<int64_t>(hlen, 1))) != HJ_OK) return st;
     hist = (uint32_t*)p;
     if ((st = dev_alloc(t, t->scratch, &p, sizeof(uint32_t) * (size_t)std::max<int64_t>(kCoarseBins * ntiles, 1))) !=
@@ -334,19 +394,13 @@ hj_status build_attempt(hj_table* t, const std::vector<Segment>& segs, double lf
     if ((st = dev_alloc(t, t->scratch, &p, sizeof(BigSeg) * (size_t)(total / (kSmallSeg + 1) + 2))) != HJ_OK)
         return st;
     big = (BigSeg*)p;
-    if ((st = dev_alloc(t, t->scratch, &p, sizeof(BuildCounters))) != HJ_OK) return st;
-    ctr = (BuildCounters*)p;
 
-    hipStream_t s = t->res.stream;
-    if (!segs.empty())
-        HIP_TRY(hipMemcpyAsync(d_segs, segs.data(), sizeof(Segment) * segs.size(), hipMemcpyHostToDevice, s));
-    HIP_TRY(hipMemsetAsync(ctr, 0, sizeof(BuildCounters), s));
     if (total == 0) HIP_TRY(hipMemsetAsync(t->tbl, 0, (size_t)(t->nb + 1) * sizeof(Bucket), s));
     hipDeviceProp_t* prop = device_props(t->device);
     const int cus = prop ? prop->multiProcessorCount : 256;
-    HIP_TRY(launch_build(t->key_bytes, d_segs, (int)segs.size(), total, t->nb, t->clog2, t->nchunks, hist, hist1,
-                         chunk_starts, ntiles, tile_rows, scan, tkeys, trows, skeys, srows, t->row_ids, ids_as_rows, t->tbl, t->dup_rows,
-                         big, ctr, cus, s));
+    HIP_TRY(launch_build(t->key_bytes, d_segs, (int)segs.size(), total, g, hist, hist1, chunk_starts, ntiles, tile_rows,
+                         scan, tkeys, trows, skeys, srows, t->row_ids, ids_as_rows, t->tbl, t->dense, t->dup_rows, big,
+                         ctr, cus, s));
     BuildCounters hc;
     HIP_TRY(hipMemcpyAsync(&hc, ctr, sizeof(hc), hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
@@ -410,7 +464,9 @@ hj_status check_table(const hj_table* t) {
     return HJ_OK;
 }
 
-TableView view_of(const hj_table* t) { return TableView{t->tbl, t->dup_rows, t->row_ids, t->nb, t->clog2}; }
+TableView view_of(const hj_table* t) {
+    return TableView{t->tbl, t->dup_rows, t->row_ids, t->nb, t->clog2, t->dense, t->dmin, t->drange};
+}
 
 // device copy of host input (keys + validity bitmap slice)
 struct TmpInput {
@@ -631,8 +687,9 @@ hj_status hj_table_stats_get(const hj_table* t, hj_table_stats* out) {
     out->dup_rows = (int64_t)h[2];
     out->max_key_rows = (int64_t)h[3];
     out->inserted_rows = (int64_t)h[0] - (int64_t)h[1] + (int64_t)h[2];
-    out->buckets = t->nb;
-    out->table_bytes = (int64_t)(t->nb + 1) * (int64_t)sizeof(Bucket);
+    out->buckets = t->dense ? 0 : t->nb;
+    out->table_bytes = t->dense ? (int64_t)sizeof(uint32_t) * ((int64_t)t->nchunks << kDenseShift)
+                                : (int64_t)(t->nb + 1) * (int64_t)sizeof(Bucket);
     out->build_ns = t->build_ns;
     return HJ_OK;
 }
@@ -643,6 +700,13 @@ int64_t hj_table_build_ns(const hj_table* t) {
 }
 
 int64_t hj_probe_workspace_bytes(int64_t n) { return probe_workspace(n); }
+
+int hj_set_build_mode(int mode) {
+    if (mode < 0 || mode > 1) return -1;
+    const int old = build_mode();
+    g_build_mode.store(mode, std::memory_order_relaxed);
+    return old;
+}
 
 int hj_set_probe_mode(int mode) {
     if (mode < 0 || mode > 3) return -1;

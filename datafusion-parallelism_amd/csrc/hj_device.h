@@ -94,6 +94,19 @@ struct TableView {
     const uint64_t* row_ids;
     uint32_t nb;      // buckets (excl. side bucket) = nchunks << clog2
     uint32_t clog2;   // log2 buckets per chunk
+    // dense layout (dense != nullptr): ref of key k = dense[k - dmin] for k - dmin < drange
+    const uint32_t* dense;
+    int64_t dmin;
+    uint64_t drange;
+};
+
+// Build partition geometry: hashed chunks of 2^clog2 buckets (chunk nchunks = the side
+// bucket of INT64_MIN) or, dense, chunks of 2^kDenseShift consecutive key values from dmin.
+constexpr uint32_t kDenseShift = 11;
+struct ChunkGeom {
+    uint32_t nb, clog2, nchunks, dshift;
+    int64_t dmin;
+    int dense;
 };
 
 }  // namespace dfp

@@ -31,6 +31,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <climits>
 
 #include "hj_device.h"
 #include "hj_launch.h"
@@ -75,8 +76,9 @@ __device__ __forceinline__ uint32_t home_bucket(int64_t key, uint32_t nb) {
 constexpr int kHistThreads = 1024;
 constexpr int kFineLdsBins = 8192;  // fine histogram in LDS (32 KB) up to this many chunks per tile
 
-__device__ __forceinline__ uint32_t chunk_of(int64_t key, uint32_t nb, uint32_t clog2, uint32_t nchunks) {
-    return ((uint64_t)key ^ kSign) == 0 ? nchunks : (home_bucket(key, nb) >> clog2);
+__device__ __forceinline__ uint32_t chunk_of(int64_t key, const ChunkGeom& g) {
+    if (g.dense) return (uint32_t)(((uint64_t)key - (uint64_t)g.dmin) >> g.dshift);
+    return ((uint64_t)key ^ kSign) == 0 ? g.nchunks : (home_bucket(key, g.nb) >> g.clog2);
 }
 
 // The segment descriptors of one tile's rows in LDS (per-row lookups in global memory
@@ -149,8 +151,7 @@ __device__ __forceinline__ void load_rows(const Segment* __restrict__ segs, int 
 // level 1: rows per (group, tile); hist1[g * ntiles + tile]
 template <typename K>
 __global__ void __launch_bounds__(kHistThreads)
-coarse_hist_kernel(const Segment* __restrict__ segs, int nseg, int64_t total, uint32_t nb, uint32_t clog2,
-                   uint32_t nchunks, uint32_t gshift, uint32_t ngroups, uint32_t* __restrict__ hist1,
+coarse_hist_kernel(const Segment* __restrict__ segs, int nseg, int64_t total, ChunkGeom g, uint32_t gshift, uint32_t ngroups, uint32_t* __restrict__ hist1,
                    int64_t ntiles, int64_t tile_rows) {
     __shared__ uint32_t s_h[kHistThreads / 64][kCoarseBins];  // per-wave copies: fewer LDS atomic collisions
     const int wave = threadIdx.x >> 6;
@@ -168,7 +169,7 @@ coarse_hist_kernel(const Segment* __restrict__ segs, int nseg, int64_t total, ui
         load_rows<K>(tsegs, tns, base, r1, key, ok, nullptr, nullptr, false);
 #pragma unroll
         for (int u = 0; u < kRowBatch; ++u)
-            if (ok[u]) atomicAdd(&s_h[wave][chunk_of(key[u], nb, clog2, nchunks) >> gshift], 1u);
+            if (ok[u]) atomicAdd(&s_h[wave][chunk_of(key[u], g) >> gshift], 1u);
     }
     __syncthreads();
     for (uint32_t g = threadIdx.x; g < ngroups; g += kHistThreads) {
@@ -180,18 +181,16 @@ coarse_hist_kernel(const Segment* __restrict__ segs, int nseg, int64_t total, ui
 
 // level 2: rows per (chunk, tile) over the group-ordered rows tkeys[0, n_valid); a tile
 // touches only the chunks of the groups it spans: hist2 must be zeroed beforehand
-__device__ __forceinline__ void fine_range(const unsigned long long* tkeys, int64_t r0, int64_t r1, uint32_t nb,
-                                           uint32_t clog2, uint32_t nchunks, uint32_t gshift, uint32_t* lo,
+__device__ __forceinline__ void fine_range(const unsigned long long* tkeys, int64_t r0, int64_t r1, ChunkGeom g, uint32_t gshift, uint32_t* lo,
                                            uint32_t* hi) {
-    const uint32_t g0 = chunk_of((int64_t)tkeys[r0], nb, clog2, nchunks) >> gshift;
-    const uint32_t g1 = chunk_of((int64_t)tkeys[r1 - 1], nb, clog2, nchunks) >> gshift;
+    const uint32_t g0 = chunk_of((int64_t)tkeys[r0], g) >> gshift;
+    const uint32_t g1 = chunk_of((int64_t)tkeys[r1 - 1], g) >> gshift;
     *lo = g0 << gshift;
-    *hi = min(nchunks, ((g1 + 1) << gshift) - 1);  // inclusive
+    *hi = min(g.nchunks, ((g1 + 1) << gshift) - 1);  // inclusive
 }
 
 __global__ void __launch_bounds__(kHistThreads)
-fine_hist_kernel(const unsigned long long* __restrict__ tkeys, const BuildCounters* __restrict__ ctr, uint32_t nb,
-                 uint32_t clog2, uint32_t nchunks, uint32_t gshift, uint32_t* __restrict__ hist, int64_t ntiles,
+fine_hist_kernel(const unsigned long long* __restrict__ tkeys, const BuildCounters* __restrict__ ctr, ChunkGeom g, uint32_t gshift, uint32_t* __restrict__ hist, int64_t ntiles,
                  int64_t tile_rows) {
     extern __shared__ __attribute__((aligned(16))) uint32_t s_h[];
     const int64_t nvalid = (int64_t)ctr->n_valid;
@@ -199,7 +198,7 @@ fine_hist_kernel(const unsigned long long* __restrict__ tkeys, const BuildCounte
     const int64_t r1 = min<int64_t>(nvalid, r0 + tile_rows);
     if (r0 >= r1) return;
     uint32_t lo, hi;
-    fine_range(tkeys, r0, r1, nb, clog2, nchunks, gshift, &lo, &hi);
+    fine_range(tkeys, r0, r1, g, gshift, &lo, &hi);
     // a tile spanning more than kFineLdsBins chunks (skewed groups) counts in global memory
     const bool in_lds = hi - lo + 1 <= (uint32_t)kFineLdsBins;
     if (in_lds)
@@ -215,7 +214,7 @@ fine_hist_kernel(const unsigned long long* __restrict__ tkeys, const BuildCounte
 #pragma unroll
         for (int u = 0; u < kRowBatch; ++u) {
             if (base + (int64_t)u * kHistThreads + threadIdx.x >= r1) continue;
-            const uint32_t c = chunk_of((int64_t)key[u], nb, clog2, nchunks);
+            const uint32_t c = chunk_of((int64_t)key[u], g);
             if (in_lds) atomicAdd(&s_h[c - lo], 1u);
             else atomicAdd(&hist[(int64_t)c * ntiles + blockIdx.x], 1u);
         }
@@ -350,8 +349,7 @@ __device__ __forceinline__ void staged_scatter_batch(const unsigned long long (&
 
 template <typename K>
 __global__ void __launch_bounds__(kHistThreads)
-coarse_scatter_staged_kernel(const Segment* __restrict__ segs, int nseg, int64_t total, uint32_t nb, uint32_t clog2,
-                             uint32_t nchunks, uint32_t gshift, uint32_t ngroups, const uint32_t* __restrict__ hist1,
+coarse_scatter_staged_kernel(const Segment* __restrict__ segs, int nseg, int64_t total, ChunkGeom g, uint32_t gshift, uint32_t ngroups, const uint32_t* __restrict__ hist1,
                              int64_t ntiles, unsigned long long* __restrict__ tkeys, uint32_t* __restrict__ trows,
                              uint64_t* __restrict__ row_ids, bool ids_as_rows, int64_t tile_rows) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -379,7 +377,7 @@ coarse_scatter_staged_kernel(const Segment* __restrict__ segs, int nseg, int64_t
         for (int u = 0; u < kRowBatch; ++u) {
             key[u] = (unsigned long long)k64[u];
             row[u] = (uint32_t)rr[u];
-            bin[u] = ok[u] ? (int)(chunk_of(k64[u], nb, clog2, nchunks) >> gshift) : -1;
+            bin[u] = ok[u] ? (int)(chunk_of(k64[u], g) >> gshift) : -1;
         }
         staged_scatter_batch(key, row, bin, ngroups, s_k, s_r, s_cur, s_cnt, s_st, s_w, tkeys, trows);
     }
@@ -387,7 +385,7 @@ coarse_scatter_staged_kernel(const Segment* __restrict__ segs, int nseg, int64_t
 
 __global__ void __launch_bounds__(kHistThreads)
 fine_scatter_staged_kernel(const unsigned long long* __restrict__ tkeys, const uint32_t* __restrict__ trows,
-                           const BuildCounters* __restrict__ ctr, uint32_t nb, uint32_t clog2, uint32_t nchunks,
+                           const BuildCounters* __restrict__ ctr, ChunkGeom g,
                            uint32_t gshift, uint32_t* __restrict__ hist, int64_t ntiles,
                            unsigned long long* __restrict__ skeys, uint32_t* __restrict__ srows, int64_t tile_rows) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -402,14 +400,14 @@ fine_scatter_staged_kernel(const unsigned long long* __restrict__ tkeys, const u
     const int64_t r1 = min<int64_t>(nvalid, r0 + tile_rows);
     if (r0 >= r1) return;
     uint32_t lo, hi;
-    fine_range(tkeys, r0, r1, nb, clog2, nchunks, gshift, &lo, &hi);
+    fine_range(tkeys, r0, r1, g, gshift, &lo, &hi);
     const uint32_t R = hi - lo + 1;
     if (R > (uint32_t)kStageMaxBins) {
         // a tile spanning many chunks (skewed groups): direct stores, the tile's scanned
         // histogram column is the cursor array (consumed; the chunk build reads chunk_starts)
         for (int64_t r = r0 + threadIdx.x; r < r1; r += kHistThreads) {
             const unsigned long long key = tkeys[r];
-            const uint32_t c = chunk_of((int64_t)key, nb, clog2, nchunks);
+            const uint32_t c = chunk_of((int64_t)key, g);
             const uint32_t pos = atomicAdd(&hist[(int64_t)c * ntiles + blockIdx.x], 1u);
             skeys[pos] = key;
             srows[pos] = trows[r];
@@ -431,7 +429,7 @@ fine_scatter_staged_kernel(const unsigned long long* __restrict__ tkeys, const u
 #pragma unroll
         for (int u = 0; u < kRowBatch; ++u) {
             const int64_t r = base + (int64_t)u * kHistThreads + threadIdx.x;
-            bin[u] = r < r1 ? (int)(chunk_of((int64_t)key[u], nb, clog2, nchunks) - lo) : -1;
+            bin[u] = r < r1 ? (int)(chunk_of((int64_t)key[u], g) - lo) : -1;
         }
         staged_scatter_batch(key, row, bin, R, s_k, s_r, s_cur, s_cnt, s_st, s_w, skeys, srows);
     }
@@ -707,6 +705,146 @@ chunk_build_kernel(uint32_t nb, uint32_t clog2, uint32_t nchunks, const uint32_t
 }
 
 // ---------------------------------------------------------------------------
+// build 3 (dense): key ranges of at most 8 x the build rows get a direct-addressed table
+// of one u32 ref per key value (dense[key - dmin]; kMiss = absent), same ref / dup_rows
+// encoding as the buckets. One 512-thread workgroup builds 2^dshift = 2048 consecutive
+// key values: refs in LDS, the first insert of a key stores its row (atomicExch); a key
+// seen twice switches the chunk to the duplicate passes (counts, directory, canonical
+// descending segments), which cannot overflow (a chunk has at most 2048 keys).
+// ---------------------------------------------------------------------------
+constexpr int kDenseThreads = 512;
+constexpr int kDenseRegRows = 4;
+
+__global__ void __launch_bounds__(kDenseThreads)
+dense_chunk_build_kernel(ChunkGeom g, const uint32_t* __restrict__ starts, const unsigned long long* __restrict__ skeys,
+                         const uint32_t* __restrict__ srows, uint32_t* __restrict__ dense,
+                         uint32_t* __restrict__ dup_rows, BigSeg* __restrict__ big, BuildCounters* ctr) {
+    constexpr uint32_t CV = 1u << kDenseShift;
+    __shared__ uint32_t refs[CV];
+    __shared__ uint32_t d_off[CV], d_cur[CV], d_cnt[CV];
+    __shared__ unsigned s_ndup, s_dup;
+    __shared__ unsigned long long s_w[kDenseThreads / 64];
+    __shared__ unsigned long long s_base;
+    const uint32_t c = blockIdx.x;
+    const uint32_t start = starts[c], end = starts[c + 1];
+    const uint64_t cbase = (uint64_t)c << kDenseShift;  // key index of refs[0]
+    for (uint32_t i = threadIdx.x; i < CV; i += kDenseThreads) refs[i] = kMiss;
+    if (threadIdx.x == 0) {
+        s_ndup = 0;
+        s_dup = 0;
+    }
+    __syncthreads();
+    const bool in_regs = end - start <= (uint32_t)(kDenseThreads * kDenseRegRows);
+    uint32_t rrow[kDenseRegRows];
+    int ridx[kDenseRegRows];
+    auto index_of = [&](unsigned long long key) {
+        return (int)(((uint64_t)key - (uint64_t)g.dmin) - cbase);
+    };
+    if (in_regs) {
+#pragma unroll
+        for (int u = 0; u < kDenseRegRows; ++u) {
+            const uint32_t r = start + u * kDenseThreads + threadIdx.x;
+            ridx[u] = r < end ? index_of(skeys[r]) : -1;
+            rrow[u] = r < end ? srows[r] : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < kDenseRegRows; ++u)
+            if (ridx[u] >= 0 && atomicExch(&refs[ridx[u]], rrow[u]) != kMiss) s_dup = 1u;
+    } else if (threadIdx.x == 0) {
+        s_dup = 1u;  // more rows than key values: duplicates for sure
+    }
+    __syncthreads();
+    if (s_dup) {
+        // counts
+        for (uint32_t i = threadIdx.x; i < CV; i += kDenseThreads) refs[i] = 0;
+        __syncthreads();
+        if (in_regs) {
+#pragma unroll
+            for (int u = 0; u < kDenseRegRows; ++u)
+                if (ridx[u] >= 0) atomicAdd(&refs[ridx[u]], 1u);
+        } else {
+            for (uint32_t r = start + threadIdx.x; r < end; r += kDenseThreads) atomicAdd(&refs[index_of(skeys[r])], 1u);
+        }
+        __syncthreads();
+        // directory of duplicated keys; absent keys become kMiss before rows are placed
+        for (uint32_t i = threadIdx.x; i < CV; i += kDenseThreads) {
+            const uint32_t cnt = refs[i];
+            if (cnt == 0) {
+                refs[i] = kMiss;
+            } else if (cnt > 1) {
+                const unsigned li = atomicAdd(&s_ndup, 1u);
+                d_cnt[li] = cnt;
+                d_cur[li] = 0;
+                refs[i] = kDupFlag | li;
+            }
+        }
+        __syncthreads();
+        const unsigned ndup = s_ndup;
+        unsigned long long carry = 0;
+        for (unsigned b = 0; b < ndup; b += kDenseThreads) {
+            const unsigned li = b + threadIdx.x;
+            const unsigned long long v = li < ndup ? (unsigned long long)d_cnt[li] + 1 : 0;
+            unsigned long long tot;
+            const unsigned long long ex = block_excl_scan<unsigned long long>(v, s_w, &tot);
+            if (li < ndup) d_off[li] = (uint32_t)(carry + ex);
+            carry += tot;
+        }
+        if (threadIdx.x == 0) s_base = carry ? atomicAdd(&ctr->dup_used, carry) : 0;
+        __syncthreads();
+        for (unsigned li = threadIdx.x; li < ndup; li += kDenseThreads) {
+            d_off[li] += (uint32_t)s_base;
+            dup_rows[d_off[li]] = d_cnt[li];
+        }
+        __syncthreads();
+        auto place = [&](int i, uint32_t row) {
+            const uint32_t rv = refs[i];
+            if (rv & kDupFlag) {
+                const unsigned li = rv & ~kDupFlag;
+                dup_rows[d_off[li] + 1 + atomicAdd(&d_cur[li], 1u)] = row;
+            } else {
+                refs[i] = row;  // count was 1
+            }
+        };
+        if (in_regs) {
+#pragma unroll
+            for (int u = 0; u < kDenseRegRows; ++u)
+                if (ridx[u] >= 0) place(ridx[u], rrow[u]);
+        } else {
+            for (uint32_t r = start + threadIdx.x; r < end; r += kDenseThreads) place(index_of(skeys[r]), srows[r]);
+        }
+        __syncthreads();
+        for (unsigned li = threadIdx.x; li < ndup; li += kDenseThreads) {
+            const unsigned n = d_cnt[li], off = d_off[li];
+            if (n <= (unsigned)kSmallSeg) {
+                uint32_t v[16];
+#pragma unroll
+                for (int i = 0; i < 16; ++i) v[i] = (i < (int)n) ? dup_rows[off + 1 + i] : 0u;
+                sort16_desc(v);
+#pragma unroll
+                for (int i = 0; i < 16; ++i)
+                    if (i < (int)n) dup_rows[off + 1 + i] = v[i];
+            }
+        }
+        for (uint32_t i = threadIdx.x; i < CV; i += kDenseThreads) {
+            const uint32_t rv = refs[i];
+            if (rv != kMiss && (rv & kDupFlag)) {
+                const unsigned li = rv & ~kDupFlag;
+                if (d_cnt[li] > (unsigned)kSmallSeg) {
+                    const unsigned bi = (unsigned)atomicAdd(&ctr->n_big, 1ull);
+                    big[bi] = BigSeg{(unsigned long long)((uint64_t)g.dmin + cbase + i), d_off[li], 0u};
+                }
+                refs[i] = kDupFlag | d_off[li];
+            }
+        }
+        __syncthreads();
+    }
+    // write out (coalesced)
+    uint4* dst = reinterpret_cast<uint4*>(dense + cbase);
+    const uint4* src = reinterpret_cast<const uint4*>(refs);
+    for (uint32_t i = threadIdx.x; i < CV / 4; i += kDenseThreads) dst[i] = src[i];
+}
+
+// ---------------------------------------------------------------------------
 // build 4: large duplicate segments (> 16 rows; rare). <= 4096 rows: bitonic sort in
 // LDS. Larger: rebuild the segment by an ordered scan of the build input (stream
 // compaction of the rows equal to the key; deterministic, no scratch).
@@ -857,6 +995,23 @@ template <typename K, bool HAS_VALID, bool NT = false>
 __device__ __forceinline__ void lookup4(const TableView& tv, const void* __restrict__ keys,
                                         const uint8_t* __restrict__ valid, int64_t voff, int64_t n, bool vec,
                                         int64_t row0, uint32_t (&ref)[4], uint32_t (&cnt)[4]) {
+    if (tv.dense != nullptr) {  // direct-addressed table: range check + one 4-byte read per row
+        int64_t k[4];
+        load4<K, NT>(keys, row0, n, vec, k);
+        uint32_t r[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const bool in = (row0 + q < n) && (!HAS_VALID || bit_valid(valid, voff, row0 + q));
+            const uint64_t idx = (uint64_t)k[q] - (uint64_t)tv.dmin;
+            r[q] = (in && idx < tv.drange) ? tv.dense[idx] : kMiss;
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            ref[q] = r[q];
+            cnt[q] = r[q] == kMiss ? 0u : (!(r[q] & kDupFlag) ? 1u : kCountUnknown);
+        }
+        return;
+    }
     const Bucket* __restrict__ tbl = tv.tbl;
     const uint32_t cmask = (1u << tv.clog2) - 1;
     int64_t k[4];
@@ -1415,10 +1570,12 @@ __global__ void pp_count_kernel(const uint32_t* __restrict__ cnt2, uint32_t nbin
 // ---------------------------------------------------------------------------
 __global__ void table_stats_kernel(TableView tv, unsigned long long* out) {
     unsigned long long distinct = 0, dupk = 0, dupr = 0, mx = 0;
-    const uint64_t nslots = (uint64_t)tv.nb * kSlots;
+    const uint64_t nslots = tv.dense ? tv.drange - 1 : (uint64_t)tv.nb * kSlots;
     for (uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s <= nslots; s += (uint64_t)gridDim.x * blockDim.x) {
         uint32_t c = 0;
-        if (s == nslots) {  // side bucket
+        if (tv.dense) {
+            c = ref_count(tv.dup_rows, tv.dense[s]);
+        } else if (s == nslots) {  // side bucket
             c = tv.tbl[tv.nb].meta;
         } else if (tv.tbl[s / kSlots].key[s % kSlots] != 0) {
             c = ref_count(tv.dup_rows, tv.tbl[s / kSlots].ref[s % kSlots]);
@@ -1451,10 +1608,13 @@ __global__ void chain_fill_kernel(int64_t* prev, int64_t n) {
 }
 
 __global__ void chain_links_kernel(TableView tv, int64_t* prev) {
-    const uint64_t nslots = (uint64_t)tv.nb * kSlots;
+    const uint64_t nslots = tv.dense ? tv.drange - 1 : (uint64_t)tv.nb * kSlots;
     for (uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s <= nslots; s += (uint64_t)gridDim.x * blockDim.x) {
         uint32_t ref;
-        if (s == nslots) {
+        if (tv.dense) {
+            ref = tv.dense[s];
+            if (ref == kMiss) continue;
+        } else if (s == nslots) {
             if (tv.tbl[tv.nb].meta < 2) continue;
             ref = tv.tbl[tv.nb].ref[0];
         } else {
@@ -1610,12 +1770,76 @@ hipError_t launch_scan_u64(unsigned long long* a, int64_t len, void* scratch, un
     return launch_scan<unsigned long long>(a, len, (unsigned long long*)scratch, total, s);
 }
 
-hipError_t launch_build(int key_bytes, const Segment* d_segs, int nseg, int64_t total, uint32_t nb, uint32_t clog2,
-                        uint32_t nchunks, uint32_t* hist, uint32_t* hist1, uint32_t* chunk_starts, int64_t ntiles,
+template <typename K>
+__global__ void __launch_bounds__(256)
+key_minmax_kernel(const Segment* __restrict__ segs, int nseg, int64_t total, long long* out) {
+    __shared__ long long s_mn[4], s_mx[4];
+    long long mn = LLONG_MAX, mx = LLONG_MIN;
+    for (int si = 0; si < nseg; ++si) {
+        const Segment sg = segs[si];
+        const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+        for (int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i0 < sg.n; i0 += 4 * stride) {
+            long long k[4];
+            bool ok[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {  // four independent loads in flight
+                const int64_t i = i0 + u * stride;
+                ok[u] = i < sg.n && bit_valid(sg.valid, sg.voff, i);
+                k[u] = i < sg.n ? (long long)ld_key<K>(sg.keys, i) : 0;
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                if (!ok[u]) continue;
+                mn = k[u] < mn ? k[u] : mn;
+                mx = k[u] > mx ? k[u] : mx;
+            }
+        }
+    }
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+        const long long a = __shfl_xor(mn, d, 64), b = __shfl_xor(mx, d, 64);
+        mn = a < mn ? a : mn;
+        mx = b > mx ? b : mx;
+    }
+    if ((threadIdx.x & 63) == 0) {
+        s_mn[threadIdx.x >> 6] = mn;
+        s_mx[threadIdx.x >> 6] = mx;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < 4; ++w) {
+            mn = s_mn[w] < mn ? s_mn[w] : mn;
+            mx = s_mx[w] > mx ? s_mx[w] : mx;
+        }
+        atomicMin(&out[0], mn);
+        atomicMax(&out[1], mx);
+    }
+}
+
+__global__ void minmax_init_kernel(long long* out) {
+    out[0] = LLONG_MAX;
+    out[1] = LLONG_MIN;
+}
+
+hipError_t launch_key_minmax(int key_bytes, const Segment* d_segs, int nseg, int64_t total, int64_t* out,
+                             hipStream_t s) {
+    minmax_init_kernel<<<1, 1, 0, s>>>((long long*)out);
+    // <= 256 blocks: each ends with one atomicMin/Max on the same two words (~88/us each)
+    const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>((total + 4095) / 4096, 256));
+    if (key_bytes == 8)
+        key_minmax_kernel<int64_t><<<grid, 256, 0, s>>>(d_segs, nseg, total, (long long*)out);
+    else
+        key_minmax_kernel<int32_t><<<grid, 256, 0, s>>>(d_segs, nseg, total, (long long*)out);
+    return hipGetLastError();
+}
+
+hipError_t launch_build(int key_bytes, const Segment* d_segs, int nseg, int64_t total, const ChunkGeom& g,
+                        uint32_t* hist, uint32_t* hist1, uint32_t* chunk_starts, int64_t ntiles,
                         int64_t tile_rows, void* scan_scratch,
                         unsigned long long* tkeys, uint32_t* trows, unsigned long long* skeys, uint32_t* srows,
-                        uint64_t* row_ids, bool ids_as_rows, Bucket* tbl, uint32_t* dup_rows, BigSeg* big,
-                        BuildCounters* ctr, int big_grid, hipStream_t s) {
+                        uint64_t* row_ids, bool ids_as_rows, Bucket* tbl, uint32_t* dense, uint32_t* dup_rows,
+                        BigSeg* big, BuildCounters* ctr, int big_grid, hipStream_t s) {
+    const uint32_t nb = g.nb, clog2 = g.clog2, nchunks = g.nchunks;
     const int64_t hlen = (int64_t)(nchunks + 1) * ntiles;
     const uint32_t gshift = coarse_shift(nchunks);
     const uint32_t ngroups = (nchunks >> gshift) + 1;
@@ -1623,11 +1847,11 @@ hipError_t launch_build(int key_bytes, const Segment* d_segs, int nseg, int64_t 
         unsigned long long* scr = (unsigned long long*)scan_scratch;
         // level 1: group order
         if (key_bytes == 8)
-            coarse_hist_kernel<int64_t><<<(unsigned)ntiles, kHistThreads, 0, s>>>(d_segs, nseg, total, nb, clog2, nchunks,
+            coarse_hist_kernel<int64_t><<<(unsigned)ntiles, kHistThreads, 0, s>>>(d_segs, nseg, total, g,
                                                                                  gshift, ngroups, hist1, ntiles,
                                                                                  tile_rows);
         else
-            coarse_hist_kernel<int32_t><<<(unsigned)ntiles, kHistThreads, 0, s>>>(d_segs, nseg, total, nb, clog2, nchunks,
+            coarse_hist_kernel<int32_t><<<(unsigned)ntiles, kHistThreads, 0, s>>>(d_segs, nseg, total, g,
                                                                                  gshift, ngroups, hist1, ntiles,
                                                                                  tile_rows);
         hipError_t e = launch_scan(hist1, (int64_t)ngroups * ntiles, scr, &ctr->n_valid, s);
@@ -1643,22 +1867,30 @@ hipError_t launch_build(int key_bytes, const Segment* d_segs, int nseg, int64_t 
         if (!lds_ok) return hipErrorInvalidConfiguration;
         if (key_bytes == 8)
             coarse_scatter_staged_kernel<int64_t><<<(unsigned)ntiles, kHistThreads, kStageLds, s>>>(
-                d_segs, nseg, total, nb, clog2, nchunks, gshift, ngroups, hist1, ntiles, tkeys, trows, row_ids,
+                d_segs, nseg, total, g, gshift, ngroups, hist1, ntiles, tkeys, trows, row_ids,
                 ids_as_rows, tile_rows);
         else
             coarse_scatter_staged_kernel<int32_t><<<(unsigned)ntiles, kHistThreads, kStageLds, s>>>(
-                d_segs, nseg, total, nb, clog2, nchunks, gshift, ngroups, hist1, ntiles, tkeys, trows, row_ids,
+                d_segs, nseg, total, g, gshift, ngroups, hist1, ntiles, tkeys, trows, row_ids,
                 ids_as_rows, tile_rows);
         // level 2: chunk order (tiles over the n_valid group-ordered rows)
         if ((e = hipMemsetAsync(hist, 0, sizeof(uint32_t) * (size_t)hlen, s)) != hipSuccess) return e;
-        fine_hist_kernel<<<(unsigned)ntiles, kHistThreads, sizeof(uint32_t) * kFineLdsBins, s>>>(tkeys, ctr, nb, clog2,
-                                                                                         nchunks, gshift, hist,
-                                                                         ntiles, tile_rows);
+        fine_hist_kernel<<<(unsigned)ntiles, kHistThreads, sizeof(uint32_t) * kFineLdsBins, s>>>(tkeys, ctr, g, gshift,
+                                                                                         hist, ntiles, tile_rows);
         if ((e = launch_scan(hist, hlen, scr, &ctr->n_valid, s)) != hipSuccess) return e;
         chunk_starts_kernel<<<(unsigned)std::min<uint32_t>((nchunks + 2 + 255) / 256, 4096), 256, 0, s>>>(
             hist, ntiles, nchunks, ctr, chunk_starts);
         fine_scatter_staged_kernel<<<(unsigned)ntiles, kHistThreads, kStageLds, s>>>(
-            tkeys, trows, ctr, nb, clog2, nchunks, gshift, hist, ntiles, skeys, srows, tile_rows);
+            tkeys, trows, ctr, g, gshift, hist, ntiles, skeys, srows, tile_rows);
+    }
+    if (g.dense) {
+        if (ntiles > 0) {
+            dense_chunk_build_kernel<<<nchunks, kDenseThreads, 0, s>>>(g, chunk_starts, skeys, srows, dense, dup_rows,
+                                                                       big, ctr);
+            dup_sort_big_kernel<<<big_grid, kBigThreads, 0, s>>>(dup_rows, big, ctr, d_segs, nseg, total, key_bytes,
+                                                                 ids_as_rows);
+        }
+        return hipGetLastError();
     }
     // chunk build: LDS = bucket image + dup directory (3 u32 per entry). 512-bucket
     // chunks run 512-thread workgroups, four per CU (32 KB image + directory in 38 KB);
@@ -1755,8 +1987,8 @@ hipError_t launch_probe(int key_bytes, const TableView& tv, const void* keys, co
     // line accesses stay bound by the L2 request rate, and its two extra passes cost
     // more than it saves at C2 (profiles/r01_*). DESIGN.md §5.
     const int mode = probe_mode();
-    const bool part = mode == 2;
-    if (mode == 0 || mode == 3) {
+    const bool part = mode == 2 && tv.dense == nullptr;  // dense tables: no pieces to partition by
+    if (mode == 0 || mode == 3 || (mode == 2 && !part)) {
         static const int fused_nt = [] {  // 1: keys nontemporal, 2: pair stores nontemporal
             const char* e = getenv("DFP_HJ_NT");
             return e ? atoi(e) : 0;

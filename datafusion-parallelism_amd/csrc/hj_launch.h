@@ -23,12 +23,15 @@ constexpr int kCoarseBins = 128;     // level-1 partition groups (per-wave LDS c
 // scan_scratch scan_scratch_bytes((nchunks + 1) * ntiles), tkeys/skeys u64[total],
 // trows/srows u32[total]
 hipError_t launch_build(int key_bytes, const Segment* d_segs, int nseg, int64_t total,
-                        uint32_t nb, uint32_t clog2, uint32_t nchunks, uint32_t* hist,
-                        uint32_t* hist1, uint32_t* chunk_starts, int64_t ntiles, int64_t tile_rows,
-                        void* scan_scratch,
+                        const ChunkGeom& g, uint32_t* hist, uint32_t* hist1, uint32_t* chunk_starts,
+                        int64_t ntiles, int64_t tile_rows, void* scan_scratch,
                         unsigned long long* tkeys, uint32_t* trows, unsigned long long* skeys,
                         uint32_t* srows, uint64_t* row_ids, bool ids_as_rows, Bucket* tbl,
-                        uint32_t* dup_rows, BigSeg* big, BuildCounters* ctr, int big_grid, hipStream_t s);
+                        uint32_t* dense, uint32_t* dup_rows, BigSeg* big, BuildCounters* ctr,
+                        int big_grid, hipStream_t s);
+// min and max of the valid keys of the build segments -> out[0], out[1] (int64)
+hipError_t launch_key_minmax(int key_bytes, const Segment* d_segs, int nseg, int64_t total, int64_t* out,
+                             hipStream_t s);
 
 // ---- probe ---------------------------------------------------------------
 // 0 auto (= direct), 1 direct, 2 partitioned (L2-resident pieces per XCD)

@@ -74,8 +74,8 @@ typedef struct hj_table_stats {
     int64_t dup_keys;       /* keys with > 1 row */
     int64_t dup_rows;       /* rows belonging to keys with > 1 row */
     int64_t max_key_rows;   /* largest chain length */
-    int64_t buckets;        /* 64-byte buckets of 4 slots */
-    int64_t table_bytes;    /* device bytes of the slot table */
+    int64_t buckets;        /* 64-byte buckets of 5 slots (0: direct-addressed table) */
+    int64_t table_bytes;    /* device bytes of the bucket / direct-addressed table */
     int64_t build_ns;       /* device time of the last build (HIP events) */
 } hj_table_stats;
 
@@ -177,6 +177,13 @@ hj_status hj_probe_async_ids(const hj_table* t, const void* keys, const uint8_t*
  * Results are identical; returns the previous mode, -1 for a bad value. Also settable
  * with DFP_HJ_PROBE_MODE=fused|two-pass|partitioned. */
 int hj_set_probe_mode(int mode);
+
+/* Table layout for later builds of this process: 0 auto (a direct-addressed table - one
+ * u32 ref per key value - when the build keys' range is at most 8x the build rows, the
+ * "perfect hash" of dense integer keys; else 5-slot hashed buckets), 1 hashed buckets
+ * always. Results are identical; returns the previous mode, -1 for a bad value. Also
+ * settable with DFP_HJ_DENSE=0 (hashed). */
+int hj_set_build_mode(int mode);
 
 /* Makes `stream` wait for the build of `t` (for probes on other streams). */
 hj_status hj_table_stream_wait(const hj_table* t, void* stream);

@@ -123,3 +123,13 @@ def test_join_type_names():
                                                       JoinType.LeftAnti]
     with pytest.raises(Exception):
         JoinType.parse("cross")
+
+
+def test_build_mode_switch(dfp):
+    """hj_set_build_mode: 0 auto (dense layout when it pays), 1 hashed; bad -> -1."""
+    from datafusion_parallelism_amd import _lib
+
+    L = _lib.load()
+    assert L.hj_set_build_mode(2) == -1
+    old = L.hj_set_build_mode(1)
+    assert L.hj_set_build_mode(old) == 1

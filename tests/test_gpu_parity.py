@@ -13,16 +13,21 @@ pytestmark = pytest.mark.gpu
 I64_MIN = np.iinfo(np.int64).min
 
 
-MODES = {"fused": 3, "two-pass": 1, "partitioned": 2}
+# (probe mode, table layout): hj_set_probe_mode 3 fused / 1 two-pass / 2 partitioned;
+# hj_set_build_mode 0 auto (direct-addressed for dense key ranges) / 1 hashed buckets
+MODES = {"fused": (3, 0), "fused-hashed": (3, 1), "two-pass": (1, 0), "partitioned-hashed": (2, 1)}
 
 
 @pytest.fixture(params=list(MODES))
 def probe_mode(request, dfp):
-    """Run a test under every probe strategy (identical results required)."""
+    """Run a test under every probe strategy and table layout (identical results required)."""
     L = dfp.load()
-    old = L.hj_set_probe_mode(MODES[request.param])
+    pm, bm = MODES[request.param]
+    old_p = L.hj_set_probe_mode(pm)
+    old_b = L.hj_set_build_mode(bm)
     yield request.param
-    L.hj_set_probe_mode(old)
+    L.hj_set_probe_mode(old_p)
+    L.hj_set_build_mode(old_b)
 
 
 def gpu_join(dfp, bkeys, pkeys, bvalid=None, pvalid=None, key_type="int64", device_input=True, parts=None):
@@ -198,13 +203,21 @@ def test_exponential_keys_parity(dfp, oracle_mod, probe_mode):
     assert st["dup_keys"] > 0
 
 
-def test_stats(dfp):
-    bk = np.array([5, 5, 5, 6, 7, 7], np.int64)
-    with dfp.HashTable(1, "int64", 0) as t:
-        t.build(bk, np.array([1, 1, 1, 1, 1, 0], bool))
-        s = t.stats()
+@pytest.mark.parametrize("layout", [0, 1])
+def test_stats(dfp, layout):
+    L = dfp.load()
+    old = L.hj_set_build_mode(layout)
+    try:
+        bk = np.array([5, 5, 5, 6, 7, 7], np.int64)
+        with dfp.HashTable(1, "int64", 0) as t:
+            t.build(bk, np.array([1, 1, 1, 1, 1, 0], bool))
+            s = t.stats()
+    finally:
+        L.hj_set_build_mode(old)
     assert s["build_rows"] == 6 and s["inserted_rows"] == 5
     assert s["distinct_keys"] == 3 and s["dup_keys"] == 1 and s["dup_rows"] == 3 and s["max_key_rows"] == 3
+    # layout 0 chooses the direct-addressed table for this dense range (3 values, 6 rows)
+    assert (s["buckets"] == 0) == (layout == 0)
 
 
 # ---- full-size properties (BASELINE configs) -------------------------------------
