@@ -242,6 +242,7 @@ struct hj_table {
     uint32_t* dup_rows = nullptr;
     uint64_t* row_ids = nullptr;
     uint32_t* dense = nullptr;  // direct-addressed layout (dense key range), else buckets
+    bool packed = false;        // dense refs with inline counts (dup_rows offsets < 2^27)
     int64_t dmin = 0;
     uint64_t drange = 0;
     BuildResources res;
@@ -313,7 +314,8 @@ hj_status build_attempt(hj_table* t, const std::vector<Segment>& segs, double lf
             const uint64_t nch = (range + (1u << kDenseShift) - 1) >> kDenseShift;
             if (range != 0 && range <= kDenseFactor * (uint64_t)total && nch <= (uint64_t)kMaxChunks) {
                 dense = true;
-                g = ChunkGeom{0, 0, (uint32_t)nch, kDenseShift, mm[0], 1};
+                const bool packed = (uint64_t)(2 * total + 2) < (1ull << 27);  // every dup_rows offset fits
+                g = ChunkGeom{0, 0, (uint32_t)nch, kDenseShift, mm[0], 1, packed ? 1 : 0};
                 t->dmin = mm[0];
                 t->drange = range;
             }
@@ -336,12 +338,13 @@ hj_status build_attempt(hj_table* t, const std::vector<Segment>& segs, double lf
                 return fail(HJ_ERR_INVALID, "build side too large for one device table; shard it (hj_radix_partition)");
             nchunks = kMaxChunks;
         }
-        g = ChunkGeom{(uint32_t)(nchunks << clog2), clog2, (uint32_t)nchunks, 0, 0, 0};
+        g = ChunkGeom{(uint32_t)(nchunks << clog2), clog2, (uint32_t)nchunks, 0, 0, 0, 0};
         t->dmin = 0;
         t->drange = 0;
     }
     t->clog2 = g.clog2;
     t->nchunks = g.nchunks;
+    t->packed = g.packed != 0;
     t->nb = g.nb;
     const uint64_t nchunks = g.nchunks;
     hipDeviceProp_t* prop0 = device_props(t->device);
@@ -465,7 +468,8 @@ hj_status check_table(const hj_table* t) {
 }
 
 TableView view_of(const hj_table* t) {
-    return TableView{t->tbl, t->dup_rows, t->row_ids, t->nb, t->clog2, t->dense, t->dmin, t->drange};
+    return TableView{t->tbl, t->dup_rows, t->row_ids, t->nb, t->clog2, t->dense, t->dmin, t->drange,
+                     t->packed ? kPackedMask : kFullMask};
 }
 
 // device copy of host input (keys + validity bitmap slice)

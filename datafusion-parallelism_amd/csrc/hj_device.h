@@ -98,7 +98,12 @@ struct TableView {
     const uint32_t* dense;
     int64_t dmin;
     uint64_t drange;
+    // offset bits of a duplicated key's ref: 31 (kDupFlag | offset), or kPackedMask for
+    // dense tables whose refs also carry counts <= 15 in bits 27-30 (dup_rows < 2^27)
+    uint32_t off_mask;
 };
+constexpr uint32_t kFullMask = 0x7FFFFFFFu;
+constexpr uint32_t kPackedMask = 0x07FFFFFFu;
 
 // Build partition geometry: hashed chunks of 2^clog2 buckets (chunk nchunks = the side
 // bucket of INT64_MIN) or, dense, chunks of 2^kDenseShift consecutive key values from dmin.
@@ -107,6 +112,7 @@ struct ChunkGeom {
     uint32_t nb, clog2, nchunks, dshift;
     int64_t dmin;
     int dense;
+    int packed;  // dense refs carry small counts (kPackedMask)
 };
 
 }  // namespace dfp

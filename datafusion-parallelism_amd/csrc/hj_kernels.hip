@@ -833,7 +833,8 @@ dense_chunk_build_kernel(ChunkGeom g, const uint32_t* __restrict__ starts, const
                     const unsigned bi = (unsigned)atomicAdd(&ctr->n_big, 1ull);
                     big[bi] = BigSeg{(unsigned long long)((uint64_t)g.dmin + cbase + i), d_off[li], 0u};
                 }
-                refs[i] = kDupFlag | d_off[li];
+                const uint32_t c4 = (g.packed && d_cnt[li] <= 15u) ? d_cnt[li] : 0u;
+                refs[i] = kDupFlag | (c4 << 27) | d_off[li];
             }
         }
         __syncthreads();
@@ -953,9 +954,9 @@ __device__ __forceinline__ void load4(const void* keys, int64_t row0, int64_t n,
 }
 
 // count of build rows behind a match ref
-__device__ __forceinline__ uint32_t ref_count(const uint32_t* dup_rows, uint32_t ref) {
+__device__ __forceinline__ uint32_t ref_count(const uint32_t* dup_rows, uint32_t ref, uint32_t off_mask) {
     if (ref == kMiss) return 0;
-    return (ref & kDupFlag) ? dup_rows[ref & ~kDupFlag] : 1u;
+    return (ref & kDupFlag) ? dup_rows[ref & off_mask] : 1u;
 }
 
 // One bucket line: ref of `sk` if present, else kMiss; *more = the line is full, does
@@ -1008,7 +1009,9 @@ __device__ __forceinline__ void lookup4(const TableView& tv, const void* __restr
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             ref[q] = r[q];
-            cnt[q] = r[q] == kMiss ? 0u : (!(r[q] & kDupFlag) ? 1u : kCountUnknown);
+            // packed dense refs carry counts <= 15 in bits 27-30 (kPackedMask tables)
+            const uint32_t c4 = tv.off_mask == kPackedMask ? ((r[q] >> 27) & 15u) : 0u;
+            cnt[q] = r[q] == kMiss ? 0u : (!(r[q] & kDupFlag) ? 1u : (c4 ? c4 : kCountUnknown));
         }
         return;
     }
@@ -1055,8 +1058,9 @@ __device__ __forceinline__ void lookup4(const TableView& tv, const void* __restr
     }
 }
 
-__device__ __forceinline__ uint32_t resolve_count(const uint32_t* dup_rows, uint32_t ref, uint32_t cnt) {
-    return cnt == kCountUnknown ? dup_rows[ref & ~kDupFlag] : cnt;
+__device__ __forceinline__ uint32_t resolve_count(const uint32_t* dup_rows, uint32_t ref, uint32_t cnt,
+                                                  uint32_t off_mask) {
+    return cnt == kCountUnknown ? dup_rows[ref & off_mask] : cnt;
 }
 
 template <typename K, bool HAS_VALID>
@@ -1073,7 +1077,7 @@ probe_lookup_kernel(TableView tv, const void* __restrict__ keys, const uint8_t* 
         uint32_t ref[4], cnt[4];
         lookup4<K, HAS_VALID>(tv, keys, valid, voff, n, vec, row0, ref, cnt);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) tsum += resolve_count(tv.dup_rows, ref[q], cnt[q]);
+        for (int q = 0; q < 4; ++q) tsum += resolve_count(tv.dup_rows, ref[q], cnt[q], tv.off_mask);
         if (vec && row0 + 4 <= n) {
             *reinterpret_cast<uint4*>(info + row0) = make_uint4(ref[0], ref[1], ref[2], ref[3]);
         } else {
@@ -1102,12 +1106,12 @@ __device__ __forceinline__ void emit4(const TableView& tv, const uint32_t* __res
         const uint32_t r = ref[q];
         if (c == 1) {
             if (pos < (unsigned long long)cap) {
-                const uint32_t br = (r & kDupFlag) ? tv.dup_rows[(r & ~kDupFlag) + 1] : r;
+                const uint32_t br = (r & kDupFlag) ? tv.dup_rows[(r & tv.off_mask) + 1] : r;
                 out_b[pos] = HAS_ROW_IDS ? tv.row_ids[br] : (uint64_t)br;
                 out_p[pos] = pidx;
             }
         } else {
-            const uint32_t* seg = tv.dup_rows + (r & ~kDupFlag) + 1;
+            const uint32_t* seg = tv.dup_rows + (r & tv.off_mask) + 1;
             for (uint32_t t = 0; t < c; ++t) {
                 if (pos + t < (unsigned long long)cap) {
                     const uint32_t br = seg[t];
@@ -1197,7 +1201,7 @@ probe_fused_kernel(TableView tv, const void* __restrict__ keys, const uint8_t* _
             make_uint4(ref[0], ref[1], ref[2], ref[3]);
         unsigned long long s = 0;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) s += resolve_count(tv.dup_rows, ref[q], cnt[q]);
+        for (int q = 0; q < 4; ++q) s += resolve_count(tv.dup_rows, ref[q], cnt[q], tv.off_mask);
         const unsigned long long ws = wave_sum<unsigned long long>(s);
         if (lane == 0) s_w[g][wave] = ws;
     }
@@ -1242,7 +1246,7 @@ probe_fused_kernel(TableView tv, const void* __restrict__ keys, const uint8_t* _
         unsigned long long c_sum = 0;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-            cnt[q] = ref_count(tv.dup_rows, ref[g][q]);
+            cnt[q] = ref_count(tv.dup_rows, ref[g][q], tv.off_mask);
             c_sum += cnt[q];
         }
         unsigned long long lpos = wave_incl_scan<unsigned long long>(c_sum) - c_sum;  // inside the group
@@ -1266,7 +1270,7 @@ probe_fused_kernel(TableView tv, const void* __restrict__ keys, const uint8_t* _
                     if (a < b) {
                         const uint32_t r = ref[g][q];
                         const uint32_t pidx = HAS_PROBE_IDS ? probe_ids[row0 + q] : (uint32_t)(row0 + q);
-                        const uint32_t* seg = (r & kDupFlag) ? tv.dup_rows + (r & ~kDupFlag) + 1 : nullptr;
+                        const uint32_t* seg = (r & kDupFlag) ? tv.dup_rows + (r & tv.off_mask) + 1 : nullptr;
                         for (unsigned long long t = a; t < b; ++t) {
                             const uint32_t br = seg ? seg[t - p] : r;
                             s_b[t - w0] = HAS_ROW_IDS ? tv.row_ids[br] : (uint64_t)br;
@@ -1341,7 +1345,7 @@ probe_emit_kernel(TableView tv, const uint32_t* __restrict__ info, const uint16_
         unsigned long long s = 0;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-            cnt[g][q] = ref_count(tv.dup_rows, ref[g][q]);
+            cnt[g][q] = ref_count(tv.dup_rows, ref[g][q], tv.off_mask);
             s += cnt[g][q];
         }
         gsum[g] = s;
@@ -1445,7 +1449,7 @@ pp_partition_kernel(TableView tv, PieceGeom pg, const void* __restrict__ keys, c
                         ref = S.meta ? S.ref[0] : kMiss;
                     }
                     info[tile0 + pos[q]] = ref;
-                    direct_cnt += ref_count(tv.dup_rows, ref);
+                    direct_cnt += ref_count(tv.dup_rows, ref, tv.off_mask);
                 }
             }
         }
@@ -1543,7 +1547,7 @@ pp_lookup_kernel(TableView tv, PieceGeom pg, int64_t n, int64_t ntiles, const un
                         ref = scan_line(q[0], q[1], q[2], q[3], sk[u], &more, &c_unused);
                     }
                     __builtin_nontemporal_store(ref, info + row[u]);
-                    const uint32_t c = ref_count(tv.dup_rows, ref);
+                    const uint32_t c = ref_count(tv.dup_rows, ref, tv.off_mask);
                     if (c) atomicAdd(&s_cnt[wave][own[u]], c);
                 }
             }
@@ -1574,11 +1578,11 @@ __global__ void table_stats_kernel(TableView tv, unsigned long long* out) {
     for (uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s <= nslots; s += (uint64_t)gridDim.x * blockDim.x) {
         uint32_t c = 0;
         if (tv.dense) {
-            c = ref_count(tv.dup_rows, tv.dense[s]);
+            c = ref_count(tv.dup_rows, tv.dense[s], tv.off_mask);
         } else if (s == nslots) {  // side bucket
             c = tv.tbl[tv.nb].meta;
         } else if (tv.tbl[s / kSlots].key[s % kSlots] != 0) {
-            c = ref_count(tv.dup_rows, tv.tbl[s / kSlots].ref[s % kSlots]);
+            c = ref_count(tv.dup_rows, tv.tbl[s / kSlots].ref[s % kSlots], tv.off_mask);
         }
         if (c) {
             distinct++;
@@ -1622,7 +1626,7 @@ __global__ void chain_links_kernel(TableView tv, int64_t* prev) {
             ref = tv.tbl[s / kSlots].ref[s % kSlots];
         }
         if (!(ref & kDupFlag)) continue;
-        const uint32_t* seg = tv.dup_rows + (ref & ~kDupFlag);
+        const uint32_t* seg = tv.dup_rows + (ref & tv.off_mask);
         const uint32_t c = seg[0];
         for (uint32_t t = 0; t + 1 < c; ++t) prev[seg[1 + t]] = seg[2 + t];
     }
@@ -1771,9 +1775,9 @@ hipError_t launch_scan_u64(unsigned long long* a, int64_t len, void* scratch, un
 }
 
 template <typename K>
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(1024)
 key_minmax_kernel(const Segment* __restrict__ segs, int nseg, int64_t total, long long* out) {
-    __shared__ long long s_mn[4], s_mx[4];
+    __shared__ long long s_mn[16], s_mx[16];
     long long mn = LLONG_MAX, mx = LLONG_MIN;
     for (int si = 0; si < nseg; ++si) {
         const Segment sg = segs[si];
@@ -1807,7 +1811,7 @@ key_minmax_kernel(const Segment* __restrict__ segs, int nseg, int64_t total, lon
     }
     __syncthreads();
     if (threadIdx.x == 0) {
-        for (int w = 1; w < 4; ++w) {
+        for (int w = 1; w < 16; ++w) {
             mn = s_mn[w] < mn ? s_mn[w] : mn;
             mx = s_mx[w] > mx ? s_mx[w] : mx;
         }
@@ -1825,11 +1829,11 @@ hipError_t launch_key_minmax(int key_bytes, const Segment* d_segs, int nseg, int
                              hipStream_t s) {
     minmax_init_kernel<<<1, 1, 0, s>>>((long long*)out);
     // <= 256 blocks: each ends with one atomicMin/Max on the same two words (~88/us each)
-    const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>((total + 4095) / 4096, 256));
+    const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>((total + 16383) / 16384, 256));
     if (key_bytes == 8)
-        key_minmax_kernel<int64_t><<<grid, 256, 0, s>>>(d_segs, nseg, total, (long long*)out);
+        key_minmax_kernel<int64_t><<<grid, 1024, 0, s>>>(d_segs, nseg, total, (long long*)out);
     else
-        key_minmax_kernel<int32_t><<<grid, 256, 0, s>>>(d_segs, nseg, total, (long long*)out);
+        key_minmax_kernel<int32_t><<<grid, 1024, 0, s>>>(d_segs, nseg, total, (long long*)out);
     return hipGetLastError();
 }
 
