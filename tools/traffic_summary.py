@@ -22,9 +22,9 @@ import sys
 PROBE_KERNELS = ("probe_fused_kernel", "probe_lookup_kernel", "probe_emit_kernel", "scan_reduce_kernel<unsigned long long>",
                  "scan_down_kernel<unsigned long long>", "pp_partition_kernel", "pp_lookup_kernel",
                  "pp_count_kernel")
-BUILD_KERNELS = ("coarse_hist_kernel", "coarse_scatter_kernel", "fine_hist_kernel", "fine_scatter_kernel",
-                 "scan_reduce_kernel<unsigned int>", "scan_down_kernel<unsigned int>", "chunk_build_kernel",
-                 "dup_sort_big_kernel")
+BUILD_KERNELS = ("key_minmax_kernel", "coarse_hist_kernel", "coarse_scatter", "fine_hist_kernel", "fine_scatter",
+                 "chunk_starts_kernel", "scan_reduce_kernel<unsigned int>", "scan_down_kernel<unsigned int>",
+                 "chunk_build_kernel", "dup_sort_big_kernel")
 
 
 def per_kernel(path):
