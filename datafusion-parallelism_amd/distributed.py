@@ -255,3 +255,61 @@ class DistributedHashJoin:
             if w is not None:
                 w.wait()  # RCCL: the compute stream waits for the exchange (no host block)
         return table.probe(rk, ri, rk.numel())
+
+
+# ---- relational exchanges for multi-GPU query plans (TPC-H C4/C5, tpch.py) -------------
+
+def all_gather_rows(cols: list[torch.Tensor], group=None) -> list[torch.Tensor]:
+    """Broadcast exchange: every rank receives the concatenation, in rank order, of all
+    ranks' rows of `cols` (equal-length columns). For the small, filtered dimension
+    sides of a plan (broadcast join: SURVEY.md §8e, cheaper than a radix exchange
+    whenever B·G < B + P). One all_gather of the row counts, then one per column."""
+    world = dist.get_world_size(group)
+    dev = cols[0].device
+    n = torch.tensor([cols[0].numel()], dtype=torch.int64, device=dev)
+    ns = [torch.empty_like(n) for _ in range(world)]
+    dist.all_gather(ns, n, group=group)
+    ns = [int(x) for x in torch.cat(ns).tolist()]
+    m = max(max(ns), 1)
+    out = []
+    for c in cols:
+        assert c.numel() == ns[dist.get_rank(group)], "all_gather_rows: columns of unequal length"
+        pad = torch.zeros(m, dtype=c.dtype, device=c.device)
+        pad[:c.numel()] = c
+        parts = [torch.empty_like(pad) for _ in range(world)]
+        dist.all_gather(parts, pad, group=group)
+        out.append(torch.cat([p[:k] for p, k in zip(parts, ns)]))
+    return out
+
+
+def shuffle(keys: torch.Tensor, payload: list[torch.Tensor], group=None, partition_fn: Callable | None = None):
+    """Hash-repartition exchange (DataFusion's RepartitionExec Hash, over RCCL): row i goes
+    to rank ``mix64(key) & (G-1)`` — the same map as DistributedHashJoin, so two sides
+    shuffled on the same key meet on one rank — carrying its payload columns.
+
+    hj_radix_partition is run with ids = local row numbers, so its id output is the
+    stable destination permutation; payload columns are gathered by it and sent with the
+    keys' split sizes (all_to_all_single, all columns in flight together).
+    -> (received keys, received payload), ordered by (source rank, source row)."""
+    world = dist.get_world_size(group)
+    if partition_fn is None or partition_fn is gpu_radix_partition:
+        k, perm, counts = gpu_radix_partition(keys, None, 0, world, id_dtype=torch.int64)
+    else:
+        k, perm, counts = partition_fn(keys, None, 0, world)
+    perm = perm.to(torch.int64)
+    recv_counts = torch.empty_like(counts)
+    dist.all_to_all_single(recv_counts, counts, group=group)
+    send = counts.cpu().tolist()
+    recv = recv_counts.cpu().tolist()
+    n = sum(recv)
+    cols = [k] + [p[perm] for p in payload]
+    outs, works = [], []
+    for c in cols:
+        o = torch.empty(n, dtype=c.dtype, device=c.device)
+        works.append(dist.all_to_all_single(o, c, output_split_sizes=recv, input_split_sizes=send, group=group,
+                                            async_op=True))
+        outs.append(o)
+    for w in works:
+        if w is not None:
+            w.wait()
+    return outs[0], outs[1:]

@@ -2,7 +2,8 @@
 configs[3]: TPC-H Q3, lineitem ⋈ orders ⋈ customer).
 
 There is no network for dbgen / tpchgen-cli, so `generate` builds the three tables Q3
-reads on the device from a counter-based generator (splitmix64, `hj_gen_uniform_keys`),
+reads on the device from a counter-based generator (splitmix64 of (stream, row counter);
+lineitem columns are keyed by (order, line number), as in dbgen),
 following the TPC-H specification's key structure and value domains: SF·150,000
 customers, 5 market segments; SF·1,500,000 orders with sparse order keys (8 of every 32),
 customer keys drawn from the 2/3 of customers that have orders, order dates in
@@ -29,6 +30,14 @@ build on o_orderkey; lineitem filter -> probe; per-order revenue sums; top 10. B
 joins run on the hash-join kernels; filters, the group-by sum and the top-k are torch
 device ops.
 
+Multi-GPU (C4/C5: Q3 at SF100 and Q9 at SF300 on 8 GPUs): `generate(..., rank, world)`
+produces rank r's block of every table (the same rows the one-GPU tables hold at those
+positions), and `q3_dist` / `q9_dist` run the plans with one process per GPU: filtered
+dimension sides are broadcast (`all_gather_rows`), the large sides are hash-repartitioned
+on the join key with their payload (`shuffle`, RCCL all-to-all), every join is a local
+GPU hash join, and the group-by results merge with one all-reduce (Q9) or an all-gather
+of per-rank top-k candidates (Q3).
+
 Q9 (BASELINE.json configs[4], the six-way join):
     select nation, o_year, sum(l_extendedprice * (1 - l_discount)
                                - ps_supplycost * l_quantity) as sum_profit
@@ -50,8 +59,6 @@ from dataclasses import dataclass
 
 import torch
 
-from . import _lib
-from ._lib import check
 from .table import HashTable
 
 SEGMENTS = ["AUTOMOBILE", "BUILDING", "FURNITURE", "HOUSEHOLD", "MACHINERY"]
@@ -68,13 +75,29 @@ def day(d: str | _dt.date) -> int:
 ORDERDATE_MAX = day("1998-08-02")  # STARTDATE .. ENDDATE - 151 days
 
 
-def _uniform(n: int, seed: int, lo: int, hi: int, device) -> torch.Tensor:
-    """n int64 values in [lo, hi] (splitmix64 counter stream on the device)."""
-    out = torch.empty(max(n, 1), dtype=torch.int64, device=device)
-    if n:
-        check(_lib.load().hj_gen_uniform_keys(out.data_ptr(), n, seed, hi - lo + 1,
-                                              torch.cuda.current_stream(device).cuda_stream))
-    return out[:n] + lo
+def _s64(c: int) -> int:
+    return c - (1 << 64) if c >= 1 << 63 else c
+
+
+def _mix(x: torch.Tensor) -> torch.Tensor:
+    """splitmix64 finaliser on int64 tensors (two's-complement wrap = uint64 arithmetic;
+    logical shifts by masking)."""
+    z = x + _s64(0x9E3779B97F4A7C15)
+    z = (z ^ ((z >> 30) & ((1 << 34) - 1))) * _s64(0xBF58476D1CE4E5B9)
+    z = (z ^ ((z >> 27) & ((1 << 37) - 1))) * _s64(0x94D049BB133111EB)
+    return z ^ ((z >> 31) & ((1 << 33) - 1))
+
+
+def _uni(counter: torch.Tensor, stream: int, lo: int, hi: int) -> torch.Tensor:
+    """Values in [lo, hi] for the given row counters (< 2^40) of one random stream: a
+    pure function of (stream, counter), so any block of rows can be generated alone."""
+    z = _mix(counter + (stream << 40))
+    return ((z >> 11) & ((1 << 53) - 1)) % (hi - lo + 1) + lo
+
+
+def _span(n: int, rank: int, world: int) -> tuple[int, int]:
+    """Rank's block [lo, hi) of n rows."""
+    return n * rank // world, n * (rank + 1) // world
 
 
 @dataclass
@@ -136,47 +159,62 @@ def _supplier_of(partkey: torch.Tensor, i: torch.Tensor, ns: int) -> torch.Tenso
     return (partkey + i * (ns // 4 + (partkey - 1) // ns)) % ns + 1
 
 
-def generate(sf: float, device="cuda:0", seed: int = 1, q9: bool = False) -> Tables:
+def generate(sf: float, device="cuda:0", seed: int = 1, q9: bool = False, rank: int = 0, world: int = 1) -> Tables:
+    """TPC-H-shaped tables at scale factor sf; with world > 1, rank's block of each table
+    (customer, orders + their lineitems, part + its partsupp, supplier by row blocks)."""
     dev = torch.device(device)
+    assert 0 <= seed < 1 << 16 and 0 <= rank < world
+
+    def st(k):  # stream id of column k
+        return seed * 64 + k
+
     nc = int(150_000 * sf)
     no = int(1_500_000 * sf)
     # customer
-    c_custkey = torch.arange(1, nc + 1, dtype=torch.int64, device=dev)
-    c_mktsegment = _uniform(nc, seed * 1000 + 1, 0, 4, dev).to(torch.int8)
+    c0, c1 = _span(nc, rank, world)
+    ci = torch.arange(c0, c1, dtype=torch.int64, device=dev)
+    c_custkey = ci + 1
+    c_mktsegment = _uni(ci, st(1), 0, 4).to(torch.int8)
     # orders: sparse keys (8 used of every 32), customers not divisible by 3
-    i = torch.arange(no, dtype=torch.int64, device=dev)
+    o0, o1 = _span(no, rank, world)
+    i = torch.arange(o0, o1, dtype=torch.int64, device=dev)
     o_orderkey = (i // 8) * 32 + (i % 8) + 1
-    ck = _uniform(no, seed * 1000 + 2, 1, nc, dev)
+    ck = _uni(i, st(2), 1, nc)
     o_custkey = torch.where(ck % 3 == 0, torch.where(ck > 1, ck - 1, ck + 1), ck)
-    o_orderdate = _uniform(no, seed * 1000 + 3, 0, ORDERDATE_MAX, dev).to(torch.int32)
-    o_shippriority = torch.zeros(no, dtype=torch.int32, device=dev)
-    # lineitem: 1..7 per order
-    nl_per = _uniform(no, seed * 1000 + 4, 1, 7, dev)
-    l_order_row = torch.repeat_interleave(torch.arange(no, device=dev), nl_per)
+    o_orderdate = _uni(i, st(3), 0, ORDERDATE_MAX).to(torch.int32)
+    o_shippriority = torch.zeros(i.numel(), dtype=torch.int32, device=dev)
+    # lineitem: 1..7 per order, columns keyed by (order, line number)
+    nl_per = _uni(i, st(4), 1, 7)
+    l_order_row = torch.repeat_interleave(torch.arange(i.numel(), device=dev), nl_per)
     nl = l_order_row.numel()
+    first = torch.cumsum(nl_per, 0) - nl_per
+    lc = i[l_order_row] * 8 + (torch.arange(nl, device=dev) - first[l_order_row])
     l_orderkey = o_orderkey[l_order_row]
     npart = int(200_000 * sf) if sf >= 0.005 else 1000
-    partkey = _uniform(nl, seed * 1000 + 5, 1, npart, dev)
+    partkey = _uni(lc, st(5), 1, npart)
     retail_cents = 90000 + (partkey // 10) % 20001 + 100 * (partkey % 1000)
-    quantity = _uniform(nl, seed * 1000 + 6, 1, 50, dev)
+    quantity = _uni(lc, st(6), 1, 50)
     l_extendedprice = quantity * retail_cents
-    l_discount = _uniform(nl, seed * 1000 + 7, 0, 10, dev).to(torch.int32)
-    l_shipdate = (o_orderdate[l_order_row].to(torch.int64) + _uniform(nl, seed * 1000 + 8, 1, 121, dev)).to(
-        torch.int32)
+    l_discount = _uni(lc, st(7), 0, 10).to(torch.int32)
+    l_shipdate = (o_orderdate[l_order_row].to(torch.int64) + _uni(lc, st(8), 1, 121)).to(torch.int32)
     t = Tables(sf, c_custkey, c_mktsegment, o_orderkey, o_custkey, o_orderdate, o_shippriority, l_orderkey,
                l_extendedprice, l_discount, l_shipdate)
     if q9:
         ns = max(int(10_000 * sf), 4)
         t.l_partkey, t.l_quantity = partkey, quantity
-        t.l_suppkey = _supplier_of(partkey, _uniform(nl, seed * 1000 + 9, 0, 3, dev), ns)
-        t.p_partkey = torch.arange(1, npart + 1, dtype=torch.int64, device=dev)
-        t.p_green = _uniform(npart, seed * 1000 + 10, 0, 91, dev) < 5
-        t.s_suppkey = torch.arange(1, ns + 1, dtype=torch.int64, device=dev)
-        t.s_nationkey = _uniform(ns, seed * 1000 + 11, 0, 24, dev)
-        pp = torch.repeat_interleave(t.p_partkey, 4)
-        t.ps_partkey = pp
-        t.ps_suppkey = _supplier_of(pp, torch.arange(4 * npart, device=dev) % 4, ns)
-        t.ps_supplycost = _uniform(4 * npart, seed * 1000 + 12, 100, 100_000, dev)
+        t.l_suppkey = _supplier_of(partkey, _uni(lc, st(9), 0, 3), ns)
+        p0, p1 = _span(npart, rank, world)
+        pi = torch.arange(p0, p1, dtype=torch.int64, device=dev)
+        t.p_partkey = pi + 1
+        t.p_green = _uni(pi, st(10), 0, 91) < 5
+        s0, s1 = _span(ns, rank, world)
+        si = torch.arange(s0, s1, dtype=torch.int64, device=dev)
+        t.s_suppkey = si + 1
+        t.s_nationkey = _uni(si, st(11), 0, 24)
+        psi = torch.arange(4 * p0, 4 * p1, dtype=torch.int64, device=dev)  # partsupp rows of the part block
+        t.ps_partkey = psi // 4 + 1
+        t.ps_suppkey = _supplier_of(t.ps_partkey, psi % 4, ns)
+        t.ps_supplycost = _uni(psi, st(12), 100, 100_000)
     return t
 
 
@@ -271,5 +309,93 @@ def q9(t: Tables, color_flag: str = "green") -> list[tuple[str, int, int]]:
     out = []
     for g in torch.nonzero(present).squeeze(1).tolist():
         out.append((NATIONS[g // 8], 1992 + g % 8, int(sums[g])))
+    out.sort(key=lambda r: (r[0], -r[1]))
+    return out
+
+
+# ---- multi-GPU plans (one process per GPU; C4 = Q3 SF100, C5 = Q9 SF300 on 8 GPUs) -----
+
+def _order_q3(okey: torch.Tensor, rev: torch.Tensor, odate: torch.Tensor) -> torch.Tensor:
+    """Permutation for: revenue desc, o_orderdate asc, l_orderkey asc (stable sorts, last
+    key first) — the one-GPU q3's order, whose groups are already in orderkey order."""
+    o = torch.argsort(okey, stable=True)
+    o = o[torch.argsort(odate[o], stable=True)]
+    return o[torch.argsort(-rev[o], stable=True)]
+
+
+def q3_dist(t: Tables, segment: str = "BUILDING", date: str = "1995-03-15", limit: int = 10, group=None,
+            join_fn=None, partition_fn=None) -> Q3Result:
+    """Q3 over rank-sharded tables (generate(..., rank, world)); the result on every rank.
+
+    customer (filtered) is broadcast; the qualifying orders and the ship-date-filtered
+    lines are hash-repartitioned on orderkey with their payload, so each order's group
+    lives on exactly one rank; the per-rank top-`limit` candidates are gathered and
+    merged. `join_fn(build, probe) -> (build rows, probe rows)` defaults to the GPU hash
+    join (the stand-in hook exists only for the CPU gloo tests)."""
+    import torch.distributed as dist
+
+    from .distributed import all_gather_rows, shuffle
+
+    join = join_fn or _join
+    seg = SEGMENTS.index(segment)
+    d = day(date)
+    (cust,) = all_gather_rows([t.c_custkey[t.c_mktsegment == seg]], group)
+    o_rows = torch.nonzero(t.o_orderdate < d).squeeze(1)
+    _, po = join(cust, t.o_custkey[o_rows])
+    sel = o_rows[po]
+    ok, (od, osp) = shuffle(t.o_orderkey[sel], [t.o_orderdate[sel], t.o_shippriority[sel]], group, partition_fn)
+    l_rows = torch.nonzero(t.l_shipdate > d).squeeze(1)
+    rev = t.l_extendedprice[l_rows] * (100 - t.l_discount[l_rows].to(torch.int64))
+    lk, (lrev,) = shuffle(t.l_orderkey[l_rows], [rev], group, partition_fn)
+    bo, pl = join(ok, lk)
+    sums = torch.zeros(ok.numel(), dtype=torch.int64, device=ok.device).index_add_(0, bo, lrev[pl])
+    has = torch.zeros(ok.numel(), dtype=torch.bool, device=ok.device)
+    has[bo] = True
+    g = torch.nonzero(has).squeeze(1)
+    okey, r, dt, sp = ok[g], sums[g], od[g], osp[g]
+    top = _order_q3(okey, r, dt)[:limit]
+    ngroups = torch.tensor([g.numel()], dtype=torch.int64, device=ok.device)
+    dist.all_reduce(ngroups, group=group)
+    okey, r, dt, sp = all_gather_rows([okey[top], r[top], dt[top], sp[top]], group)
+    top = _order_q3(okey, r, dt)[:limit]
+    return Q3Result(okey[top].tolist(), r[top].tolist(), dt[top].tolist(), sp[top].tolist(), int(ngroups.item()))
+
+
+def q9_dist(t: Tables, group=None, join_fn=None, partition_fn=None) -> list[tuple[str, int, int]]:
+    """Q9 over rank-sharded tables; the result on every rank.
+
+    green part keys and supplier are broadcast; lineitem (green parts only) and partsupp
+    are repartitioned on (partkey, suppkey), then the joined lines and orders on
+    orderkey; the (nation, year) sums merge with one int64 all-reduce."""
+    import torch.distributed as dist
+
+    from .distributed import all_gather_rows, shuffle
+
+    if t.l_partkey is None:
+        raise ValueError("generate(..., q9=True) tables are needed")
+    join = join_fn or _join
+    dev = t.device
+    (green,) = all_gather_rows([t.p_partkey[t.p_green]], group)
+    _, li = join(green, t.l_partkey)
+    gross = t.l_extendedprice[li] * (100 - t.l_discount[li].to(torch.int64))
+    psk = (t.l_partkey[li] << 32) | t.l_suppkey[li]
+    lk, (ls, lok, gross, qty) = shuffle(psk, [t.l_suppkey[li], t.l_orderkey[li], gross, t.l_quantity[li]], group,
+                                        partition_fn)
+    pk, (cost,) = shuffle((t.ps_partkey << 32) | t.ps_suppkey, [t.ps_supplycost], group, partition_fn)
+    b_ps, p_l = join(pk, lk)
+    amount = gross[p_l] - cost[b_ps] * qty[p_l] * 100
+    ls, lok = ls[p_l], lok[p_l]
+    s_key, s_nat = all_gather_rows([t.s_suppkey, t.s_nationkey], group)
+    b_s, p_l = join(s_key, ls)
+    nation, amount, lok = s_nat[b_s], amount[p_l], lok[p_l]
+    ok, (year,) = shuffle(t.o_orderkey, [year_of(t.o_orderdate)], group, partition_fn)
+    lk2, (nat2, amt2) = shuffle(lok, [nation, amount], group, partition_fn)
+    b_o, p_l = join(ok, lk2)
+    gid = nat2[p_l] * 8 + (year[b_o] - 1992)
+    sums = torch.zeros(25 * 8, dtype=torch.int64, device=dev).index_add_(0, gid, amt2[p_l])
+    cnt = torch.zeros(25 * 8, dtype=torch.int64, device=dev).index_add_(0, gid, torch.ones_like(gid))
+    dist.all_reduce(sums, group=group)
+    dist.all_reduce(cnt, group=group)
+    out = [(NATIONS[g // 8], 1992 + g % 8, int(sums[g])) for g in torch.nonzero(cnt).squeeze(1).tolist()]
     out.sort(key=lambda r: (r[0], -r[1]))
     return out

@@ -4,19 +4,9 @@ dbgen's data, which cannot be generated here)."""
 import numpy as np
 import pytest
 
+from tpch_ref import q3_pandas, q9_pandas
+
 pytestmark = pytest.mark.gpu
-
-
-def q3_pandas(customer, orders, lineitem, seg, d, limit=10):
-    c = customer[customer.c_mktsegment == seg]
-    o = orders[orders.o_orderdate < d]
-    li = lineitem[lineitem.l_shipdate > d]
-    co = c.merge(o, left_on="c_custkey", right_on="o_custkey")
-    col = co.merge(li, left_on="o_orderkey", right_on="l_orderkey")
-    col = col.assign(revenue=col.l_extendedprice.astype(np.int64) * (100 - col.l_discount.astype(np.int64)))
-    g = col.groupby(["l_orderkey", "o_orderdate", "o_shippriority"], as_index=False)["revenue"].sum()
-    g = g.sort_values(["revenue", "o_orderdate"], ascending=[False, True], kind="mergesort")
-    return g.head(limit), len(g)
 
 
 @pytest.mark.parametrize("sf,date", [(0.01, "1995-03-15"), (0.05, "1995-03-15"), (0.05, "1993-06-01")])
@@ -47,25 +37,6 @@ def test_generator_shape(dfp):
     assert int(t.l_discount.max()) <= 10 and int(t.o_orderdate.max()) <= tpch.ORDERDATE_MAX
 
 
-def q9_pandas(orders, lineitem, part, supplier, partsupp):
-    import pandas as pd
-    from datafusion_parallelism_amd import tpch
-
-    p = part[part.p_green]
-    x = lineitem.merge(p, left_on="l_partkey", right_on="p_partkey")
-    x = x.merge(partsupp, left_on=["l_partkey", "l_suppkey"], right_on=["ps_partkey", "ps_suppkey"])
-    x = x.merge(supplier, left_on="l_suppkey", right_on="s_suppkey")
-    x = x.merge(orders, left_on="l_orderkey", right_on="o_orderkey")
-    dates = pd.to_datetime("1992-01-01") + pd.to_timedelta(x.o_orderdate, unit="D")
-    x = x.assign(o_year=dates.dt.year,
-                 amount=x.l_extendedprice.astype(np.int64) * (100 - x.l_discount.astype(np.int64))
-                 - x.ps_supplycost.astype(np.int64) * x.l_quantity.astype(np.int64) * 100,
-                 nation=[tpch.NATIONS[k] for k in x.s_nationkey])
-    g = x.groupby(["nation", "o_year"], as_index=False)["amount"].sum()
-    g = g.sort_values(["nation", "o_year"], ascending=[True, False], kind="mergesort")
-    return [(r.nation, int(r.o_year), int(r.amount)) for r in g.itertuples()]
-
-
 @pytest.mark.parametrize("sf", [0.01, 0.05])
 def test_q9_matches_pandas(dfp, sf):
     from datafusion_parallelism_amd import tpch
@@ -75,3 +46,34 @@ def test_q9_matches_pandas(dfp, sf):
     _, orders, lineitem, part, supplier, partsupp = t.to_pandas()
     want = q9_pandas(orders, lineitem, part, supplier, partsupp)
     assert len(got) > 0 and got == want
+
+
+def test_distributed_plans_one_rank(dfp):
+    """q3_dist / q9_dist through RCCL with one rank (broadcasts and shuffles are
+    self-copies; the GPU partition kernel and hash joins run for real): equal to the
+    one-GPU plans and to pandas."""
+    import os
+    import socket
+
+    import torch
+    import torch.distributed as dist
+
+    from datafusion_parallelism_amd import tpch
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1")
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        t = tpch.generate(0.05, "cuda:0", seed=11, q9=True)
+        got3 = tpch.q3_dist(t, "BUILDING", "1995-03-15")
+        one3 = tpch.q3(t, "BUILDING", "1995-03-15")
+        assert got3 == one3
+        got9 = tpch.q9_dist(t)
+        assert got9 == tpch.q9(t)
+        _, orders, lineitem, part, supplier, partsupp = t.to_pandas()
+        assert got9 == q9_pandas(orders, lineitem, part, supplier, partsupp)
+    finally:
+        dist.destroy_process_group()

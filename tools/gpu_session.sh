@@ -87,6 +87,13 @@ for s in $STEPS; do
         --master-port 29533 bench.py --gpus 1 --steps 5 --warmup 2 > $O/trun.out 2> $O/trun.err \
         || { tail -30 $O/trun.err; exit 1; }
       wc -l $O/trun.out && python3 -c "import json,sys; json.loads(open(sys.argv[1]).read()); print('one json line ok')" $O/trun.out ;;
+    tpch)
+      run timeout -k 10 600 python3 tools/bench_tpch.py q3:100 q9:100 > $O/tpch_single.json 2> $O/tpch_single.err \
+        || { tail -30 $O/tpch_single.err; exit 1; }
+      cat $O/tpch_single.json
+      run timeout -k 10 600 python3 tools/bench_tpch.py --dist ${TPCH_DIST:-q3:100 q9:100 q9:300} > $O/tpch_dist.json \
+        2> $O/tpch_dist.err || { tail -30 $O/tpch_dist.err; exit 1; }
+      cat $O/tpch_dist.json ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
