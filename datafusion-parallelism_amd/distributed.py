@@ -124,27 +124,73 @@ class ExchangeStats:
     recv_rows: int = 0
 
 
+# Bytes one rank sends or receives per all_to_all_single call. RCCL self-copies above
+# ~800 MB come back wrong on this stack (tools/debug_shuffle.py: 1.6 GB -> the second
+# half differs), so larger exchanges run in rounds of at most this size.
+A2A_MAX_BYTES = 256 << 20
+
+
+def _count_matrix(counts: torch.Tensor, group=None) -> list[list[int]]:
+    """m[s][d] = rows rank s sends to rank d (one all_gather of G int64, one host sync):
+    every rank learns its receive sizes and everyone's, so all ranks agree on the
+    number of exchange rounds without another collective."""
+    world = dist.get_world_size(group)
+    parts = [torch.empty_like(counts) for _ in range(world)]
+    dist.all_gather(parts, counts, group=group)
+    return torch.stack(parts).cpu().tolist()
+
+
+def _exchange_cols(cols: list[torch.Tensor], m: list[list[int]], group=None, async_op: bool = False):
+    """all_to_all_single of destination-grouped columns with the split sizes of count
+    matrix m. -> (received columns, works still in flight). Exchanges larger than
+    A2A_MAX_BYTES per rank run in rounds (each round moves the same fraction of every
+    peer's segment; all ranks derive the round count from m)."""
+    me = dist.get_rank(group)
+    world = len(m)
+    send = m[me]
+    recv = [m[s][me] for s in range(world)]
+    widest = max(c.element_size() for c in cols) if cols else 1
+    peak = max(max(sum(m[r]), sum(m[s][r] for s in range(world))) for r in range(world)) * widest
+    rounds = max(1, -(-peak // A2A_MAX_BYTES))
+    outs = [torch.empty(sum(recv), dtype=c.dtype, device=c.device) for c in cols]
+    if rounds == 1:
+        works = [dist.all_to_all_single(o, c, output_split_sizes=recv, input_split_sizes=send, group=group,
+                                        async_op=async_op) for o, c in zip(outs, cols)]
+        return outs, works
+    s_off = [sum(send[:p]) for p in range(world)]
+    r_off = [sum(recv[:p]) for p in range(world)]
+
+    def piece(n, j):
+        return n * j // rounds, n * (j + 1) // rounds
+
+    for j in range(rounds):
+        sj = [piece(send[p], j) for p in range(world)]
+        rj = [piece(recv[p], j) for p in range(world)]
+        ssz = [b - a for a, b in sj]
+        rsz = [b - a for a, b in rj]
+        for o, c in zip(outs, cols):
+            tin = torch.cat([c[s_off[p] + a:s_off[p] + b] for p, (a, b) in enumerate(sj)])
+            tout = torch.empty(sum(rsz), dtype=c.dtype, device=c.device)
+            dist.all_to_all_single(tout, tin, output_split_sizes=rsz, input_split_sizes=ssz, group=group)
+            q = 0
+            for p, (a, b) in enumerate(rj):
+                o[r_off[p] + a:r_off[p] + b].copy_(tout[q:q + b - a])
+                q += b - a
+    return outs, []
+
+
 def all_to_all_rows(keys_by_dest: torch.Tensor, ids_by_dest: torch.Tensor, counts: torch.Tensor,
                     group=None, async_op: bool = False):
-    """Exchange destination-grouped rows: counts first (all_to_all of G int64, host
+    """Exchange destination-grouped rows: counts first (all_gather of G int64, host
     sync for the split sizes), then keys and ids with uneven splits (all_to_all_single).
     -> (keys, ids, stats[, works]); with async_op the row exchanges are left in flight
     (wait on `works` before using keys / ids)."""
-    world = dist.get_world_size(group)
-    recv_counts = torch.empty_like(counts)
-    dist.all_to_all_single(recv_counts, counts, group=group)
-    send = counts.cpu().tolist()
-    recv = recv_counts.cpu().tolist()
-    assert len(send) == world
-    rk = torch.empty(sum(recv), dtype=keys_by_dest.dtype, device=keys_by_dest.device)
-    ri = torch.empty(sum(recv), dtype=ids_by_dest.dtype, device=ids_by_dest.device)
-    w1 = dist.all_to_all_single(rk, keys_by_dest, output_split_sizes=recv, input_split_sizes=send, group=group,
-                                async_op=async_op)
-    w2 = dist.all_to_all_single(ri, ids_by_dest, output_split_sizes=recv, input_split_sizes=send, group=group,
-                                async_op=async_op)
-    st = ExchangeStats(sum(send), sum(recv))
+    m = _count_matrix(counts, group)
+    me = dist.get_rank(group)
+    (rk, ri), works = _exchange_cols([keys_by_dest, ids_by_dest], m, group, async_op)
+    st = ExchangeStats(sum(m[me]), sum(r[me] for r in m))
     if async_op:
-        return rk, ri, st, [w1, w2]
+        return rk, ri, st, works
     return rk, ri, st
 
 
@@ -297,18 +343,8 @@ def shuffle(keys: torch.Tensor, payload: list[torch.Tensor], group=None, partiti
     else:
         k, perm, counts = partition_fn(keys, None, 0, world)
     perm = perm.to(torch.int64)
-    recv_counts = torch.empty_like(counts)
-    dist.all_to_all_single(recv_counts, counts, group=group)
-    send = counts.cpu().tolist()
-    recv = recv_counts.cpu().tolist()
-    n = sum(recv)
-    cols = [k] + [p[perm] for p in payload]
-    outs, works = [], []
-    for c in cols:
-        o = torch.empty(n, dtype=c.dtype, device=c.device)
-        works.append(dist.all_to_all_single(o, c, output_split_sizes=recv, input_split_sizes=send, group=group,
-                                            async_op=True))
-        outs.append(o)
+    m = _count_matrix(counts, group)
+    outs, works = _exchange_cols([k] + [p[perm] for p in payload], m, group, async_op=True)
     for w in works:
         if w is not None:
             w.wait()

@@ -392,6 +392,8 @@ def q9_dist(t: Tables, group=None, join_fn=None, partition_fn=None) -> list[tupl
     lk2, (nat2, amt2) = shuffle(lok, [nation, amount], group, partition_fn)
     b_o, p_l = join(ok, lk2)
     gid = nat2[p_l] * 8 + (year[b_o] - 1992)
+    if gid.numel() and bool(((gid < 0) | (gid >= 25 * 8)).any()):  # exchanged payload must be intact
+        raise RuntimeError("q9_dist: (nation, year) group id out of range after the exchange")
     sums = torch.zeros(25 * 8, dtype=torch.int64, device=dev).index_add_(0, gid, amt2[p_l])
     cnt = torch.zeros(25 * 8, dtype=torch.int64, device=dev).index_add_(0, gid, torch.ones_like(gid))
     dist.all_reduce(sums, group=group)

@@ -65,12 +65,16 @@ def _canonical(b, p):
     return bool(np.all(pl[1:] >= pl[:-1]) and np.all(bl[1:][same] < bl[:-1][same]))
 
 
-def _worker(rank, world, port, bks, pks, q, chunks=1):
+def _worker(rank, world, port, bks, pks, q, chunks=1, max_bytes=None):
     sys.path.insert(0, ROOT)
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
+    from datafusion_parallelism_amd import distributed
     from datafusion_parallelism_amd.distributed import DistributedHashJoin
+
+    if max_bytes:  # force the multi-round exchange path
+        distributed.A2A_MAX_BYTES = max_bytes
 
     dj = DistributedHashJoin(partition_fn=cpu_partition, local_join_fn=oracle_local_join, chunks=chunks,
                              local_build_fn=CpuLocalTable)
@@ -105,8 +109,9 @@ def _free_port():
     return port
 
 
-@pytest.mark.parametrize("world,chunks,wide", [(2, 1, False), (2, 3, False), (2, 3, True)])
-def test_distributed_exchange_matches_single_join(oracle_mod, world, chunks, wide):
+@pytest.mark.parametrize("world,chunks,wide,max_bytes", [(2, 1, False, None), (2, 3, False, None),
+                                                         (2, 3, True, None), (2, 1, False, 5000), (2, 3, True, 7000)])
+def test_distributed_exchange_matches_single_join(oracle_mod, world, chunks, wide, max_bytes):
     """wide: keys spread over > 2^32 values, so they travel as full int64 (otherwise
     DistributedHashJoin.prepare narrows them to int32 offsets)."""
     rng = np.random.default_rng(9)
@@ -119,7 +124,7 @@ def test_distributed_exchange_matches_single_join(oracle_mod, world, chunks, wid
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, bks, pks, q, chunks)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, bks, pks, q, chunks, max_bytes)) for r in range(world)]
     for pr in procs:
         pr.start()
     res = q.get(timeout=240)

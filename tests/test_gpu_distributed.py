@@ -67,3 +67,29 @@ def test_distributed_join_one_rank(dfp, oracle_mod, chunks):
         assert np.array_equal(p.cpu().numpy().astype(np.uint32), op)
     finally:
         dist.destroy_process_group()
+
+
+def test_large_exchange_one_rank(dfp):
+    """A 1.3 GB exchange (above the size where single RCCL self-copies come back wrong,
+    tools/debug_shuffle.py) runs in rounds and arrives exact."""
+    from datafusion_parallelism_amd import distributed
+    from datafusion_parallelism_amd.distributed import all_to_all_rows, gpu_radix_partition
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1")
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        n = 160_000_000
+        dev = torch.device("cuda", 0)
+        keys = torch.randint(-(2**40), 2**40, (n,), dtype=torch.int64, device=dev)
+        k, perm, counts = gpu_radix_partition(keys, None, 0, 1, id_dtype=torch.int64)
+        assert 8 * n > 4 * distributed.A2A_MAX_BYTES
+        rk, ri, st = all_to_all_rows(k, perm, counts)
+        assert st.recv_rows == n
+        assert torch.equal(rk, keys)
+        assert torch.equal(ri, torch.arange(n, device=dev))
+    finally:
+        dist.destroy_process_group()

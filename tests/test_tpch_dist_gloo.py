@@ -24,13 +24,16 @@ def oracle_join(build, probe):
     return torch.from_numpy(b.astype(np.int64)), torch.from_numpy(p.astype(np.int64))
 
 
-def _worker(rank, world, port, sf, q):
+def _worker(rank, world, port, sf, q, max_bytes=None):
     sys.path[:0] = [ROOT, HERE, os.path.join(ROOT, "oracle")]
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from test_distributed_gloo import cpu_partition
 
-    from datafusion_parallelism_amd import tpch
+    from datafusion_parallelism_amd import distributed, tpch
+
+    if max_bytes:  # force the multi-round exchange path
+        distributed.A2A_MAX_BYTES = max_bytes
 
     t = tpch.generate(sf, "cpu", seed=7, q9=True, rank=rank, world=world)
     r3 = tpch.q3_dist(t, "BUILDING", "1995-03-15", group=None, join_fn=oracle_join, partition_fn=cpu_partition)
@@ -78,8 +81,8 @@ def test_generator_shape_cpu():
     assert all((a, b) in ps for a, b in zip(t.l_partkey[:2000].tolist(), t.l_suppkey[:2000].tolist()))
 
 
-@pytest.mark.parametrize("world", [2])
-def test_q3_q9_distributed_match_pandas(oracle_mod, world):
+@pytest.mark.parametrize("world,max_bytes", [(2, None), (2, 20000)])
+def test_q3_q9_distributed_match_pandas(oracle_mod, world, max_bytes):
     from tpch_ref import frames, q3_pandas, q9_pandas
 
     from datafusion_parallelism_amd import tpch
@@ -88,7 +91,7 @@ def test_q3_q9_distributed_match_pandas(oracle_mod, world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, sf, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, sf, q, max_bytes)) for r in range(world)]
     for pr in procs:
         pr.start()
     res = q.get(timeout=300)

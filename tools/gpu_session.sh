@@ -94,6 +94,9 @@ for s in $STEPS; do
       run timeout -k 10 600 python3 tools/bench_tpch.py --dist ${TPCH_DIST:-q3:100 q9:100 q9:300} > $O/tpch_dist.json \
         2> $O/tpch_dist.err || { tail -30 $O/tpch_dist.err; exit 1; }
       cat $O/tpch_dist.json ;;
+    dbgshuf)
+      run timeout -k 10 300 python3 tools/debug_shuffle.py > $O/dbgshuf.log 2>&1 || { tail -30 $O/dbgshuf.log; exit 1; }
+      grep "^n=" $O/dbgshuf.log ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
