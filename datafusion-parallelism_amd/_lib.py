@@ -47,6 +47,10 @@ class HjTableStats(ctypes.Structure):
         "table_bytes", "build_ns")]
 
 
+class HjPartSpec(ctypes.Structure):
+    _fields_ = [("by_range", ctypes.c_int), ("key_lo", ctypes.c_int64), ("key_hi", ctypes.c_int64)]
+
+
 # (name, restype, argtypes) of every entry point declared in include/hj.h
 P, I64, I32, U32, U64 = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_uint32, ctypes.c_uint64
 PP = ctypes.POINTER(ctypes.c_void_p)
@@ -73,6 +77,7 @@ SIGNATURES = [
     ("hj_table_stream_wait", I32, [P, P]),
     ("hj_partition_workspace_bytes", I64, [I64, I32]),
     ("hj_radix_partition", I32, [I32, P, P, I64, P, U64, I64, I32, P, I32, I64, P, I32, P, P, P]),
+    ("hj_partition_rows", I32, [I32, P, P, I64, P, U64, I64, I32, P, P, I32, I64, P, I32, P, P, P]),
     ("hj_mark_rows", I32, [P, I32, I64, P, I64, P]),
     ("hj_select_workspace_bytes", I64, [I64]),
     ("hj_select_rows", I32, [P, I64, I32, P, P, P, P]),

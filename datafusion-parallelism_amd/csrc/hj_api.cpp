@@ -897,6 +897,14 @@ hj_status hj_radix_partition(hj_key_type key_type, const void* keys, const uint8
                              const uint64_t* ids, uint64_t id_base, int64_t n, int nparts, void* out_keys,
                              int out_key_bytes, int64_t key_offset, void* out_ids, int id_bytes, int64_t* counts,
                              void* workspace, void* stream) {
+    return hj_partition_rows(key_type, keys, validity, validity_offset, ids, id_base, n, nparts, nullptr, out_keys,
+                             out_key_bytes, key_offset, out_ids, id_bytes, counts, workspace, stream);
+}
+
+hj_status hj_partition_rows(hj_key_type key_type, const void* keys, const uint8_t* validity, int64_t validity_offset,
+                            const uint64_t* ids, uint64_t id_base, int64_t n, int nparts, const hj_part_spec* spec,
+                            void* out_keys, int out_key_bytes, int64_t key_offset, void* out_ids, int id_bytes,
+                            int64_t* counts, void* workspace, void* stream) {
     if (device_count() == 0) return fail(HJ_ERR_NO_DEVICE, "no GPU visible");
     if (nparts < 1 || nparts > 64 || (nparts & (nparts - 1)))
         return fail(HJ_ERR_INVALID, "nparts must be a power of two <= 64");
@@ -910,10 +918,23 @@ hj_status hj_radix_partition(hj_key_type key_type, const void* keys, const uint8
         return fail(HJ_ERR_INVALID, "32-bit ids overflow: id_base + n > 2^32");
     if (!is_device_ptr(keys) || !is_device_ptr(validity) || !is_device_ptr(ids) || !is_device_ptr(out_keys) ||
         !is_device_ptr(out_ids) || !is_device_ptr(counts) || !is_device_ptr(workspace))
-        return fail(HJ_ERR_INVALID, "hj_radix_partition takes device pointers");
+        return fail(HJ_ERR_INVALID, "hj_partition_rows takes device pointers");
+    PartSpec ps{INT64_MIN, INT64_MAX, 0, 0};
+    if (spec != nullptr) {
+        if (spec->key_lo > spec->key_hi) return fail(HJ_ERR_INVALID, "hj_part_spec: key_lo > key_hi");
+        ps.lo = spec->key_lo;
+        ps.hi = spec->key_hi;
+        ps.by_range = spec->by_range != 0;
+        if (ps.by_range) {
+            // mul = floor(2^64 * nparts / range), range = hi - lo + 1 in [1, 2^64]
+            const unsigned __int128 range = (unsigned __int128)((uint64_t)ps.hi - (uint64_t)ps.lo) + 1;
+            const unsigned __int128 m = ((unsigned __int128)nparts << 64) / range;
+            ps.mul = m > (unsigned __int128)UINT64_MAX ? UINT64_MAX : (uint64_t)m;
+        }
+    }
     HIP_TRY(launch_radix_partition(key_type == HJ_INT64 ? 8 : 4, keys, validity, validity_offset, ids, id_base, n,
-                                   nparts, out_keys, out_key_bytes, key_offset, out_ids, id_bytes, counts, workspace,
-                                   (hipStream_t)stream));
+                                   nparts, ps, out_keys, out_key_bytes, key_offset, out_ids, id_bytes, counts,
+                                   workspace, (hipStream_t)stream));
     return HJ_OK;
 }
 

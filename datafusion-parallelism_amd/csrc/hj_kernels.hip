@@ -1641,21 +1641,24 @@ constexpr int kMaxParts = 64;
 
 template <typename K>
 __device__ __forceinline__ int part_of(const void* keys, const uint8_t* valid, int64_t voff, int64_t i, int64_t n,
-                                       int mask) {
+                                       int mask, const PartSpec& sp) {
     if (i >= n || !bit_valid(valid, voff, i)) return -1;
-    return (int)(mix64((uint64_t)ld_key<K>(keys, i)) & (uint64_t)mask);
+    const int64_t k = ld_key<K>(keys, i);
+    if (k < sp.lo || k > sp.hi) return -1;  // cannot match: dropped before the exchange
+    if (sp.by_range) return (int)__umul64hi((uint64_t)k - (uint64_t)sp.lo, sp.mul);
+    return (int)(mix64((uint64_t)k) & (uint64_t)mask);
 }
 
 template <typename K>
 __global__ void __launch_bounds__(kPartThreads)
-part_hist_kernel(const void* keys, const uint8_t* valid, int64_t voff, int64_t n, int nparts, uint32_t* hist,
-                 int64_t nblocks) {
+part_hist_kernel(const void* keys, const uint8_t* valid, int64_t voff, int64_t n, int nparts, PartSpec sp,
+                 uint32_t* hist, int64_t nblocks) {
     __shared__ unsigned s_h[kMaxParts];
     for (int p = threadIdx.x; p < nparts; p += kPartThreads) s_h[p] = 0;
     __syncthreads();
     const int64_t r0 = (int64_t)blockIdx.x * kPartChunk;
     for (int k = threadIdx.x; k < kPartChunk; k += kPartThreads) {
-        const int p = part_of<K>(keys, valid, voff, r0 + k, n, nparts - 1);
+        const int p = part_of<K>(keys, valid, voff, r0 + k, n, nparts - 1, sp);
         if (p >= 0) atomicAdd(&s_h[p], 1u);
     }
     __syncthreads();
@@ -1675,8 +1678,8 @@ __global__ void part_counts_kernel(const uint32_t* hist, int64_t nblocks, int np
 template <typename K, typename OK, typename ID>
 __global__ void __launch_bounds__(kPartThreads)
 part_scatter_kernel(const void* keys, const uint8_t* valid, int64_t voff, const uint64_t* ids, uint64_t id_base,
-                    int64_t n, int nparts, const uint32_t* hist, int64_t nblocks, OK* out_keys, int64_t key_offset,
-                    ID* out_ids) {
+                    int64_t n, int nparts, PartSpec sp, const uint32_t* hist, int64_t nblocks, OK* out_keys,
+                    int64_t key_offset, ID* out_ids) {
     __shared__ unsigned long long s_off[kMaxParts];
     __shared__ unsigned s_wc[kPartThreads / 64][kMaxParts];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -1687,7 +1690,7 @@ part_scatter_kernel(const void* keys, const uint8_t* valid, int64_t voff, const 
     const int64_t r0 = (int64_t)blockIdx.x * kPartChunk;
     for (int k0 = 0; k0 < kPartChunk; k0 += kPartThreads) {
         const int64_t i = r0 + k0 + threadIdx.x;
-        const int p = part_of<K>(keys, valid, voff, i, n, nparts - 1);
+        const int p = part_of<K>(keys, valid, voff, i, n, nparts - 1, sp);
         // lanes with the same partition: AND of per-bit ballots (multi-split)
         unsigned long long same = __ballot(p >= 0);
         for (int bt = 0; bt < bits; ++bt) {
@@ -2111,9 +2114,9 @@ int64_t radix_partition_workspace(int64_t n, int nparts) {
 }
 
 hipError_t launch_radix_partition(int key_bytes, const void* keys, const uint8_t* valid, int64_t voff,
-                                  const uint64_t* ids, uint64_t id_base, int64_t n, int nparts, void* out_keys,
-                                  int out_key_bytes, int64_t key_offset, void* out_ids, int id_bytes, int64_t* counts,
-                                  void* workspace, hipStream_t s) {
+                                  const uint64_t* ids, uint64_t id_base, int64_t n, int nparts, const PartSpec& spec,
+                                  void* out_keys, int out_key_bytes, int64_t key_offset, void* out_ids, int id_bytes,
+                                  int64_t* counts, void* workspace, hipStream_t s) {
     if (nparts < 1 || nparts > kMaxParts || (nparts & (nparts - 1))) return hipErrorInvalidValue;
     const int64_t nblocks = (n + kPartChunk - 1) / kPartChunk;
     if (nblocks == 0) return hipMemsetAsync(counts, 0, sizeof(int64_t) * nparts, s);
@@ -2124,15 +2127,17 @@ hipError_t launch_radix_partition(int key_bytes, const void* keys, const uint8_t
     const int64_t nsb = (hlen + kScanSeg - 1) / kScanSeg;
     unsigned long long* total = scratch + nsb;  // scan_top writes bsum[nblk] = grand total
     if (key_bytes == 8)
-        part_hist_kernel<int64_t><<<(unsigned)nblocks, kPartThreads, 0, s>>>(keys, valid, voff, n, nparts, hist, nblocks);
+        part_hist_kernel<int64_t><<<(unsigned)nblocks, kPartThreads, 0, s>>>(keys, valid, voff, n, nparts, spec, hist,
+                                                                            nblocks);
     else
-        part_hist_kernel<int32_t><<<(unsigned)nblocks, kPartThreads, 0, s>>>(keys, valid, voff, n, nparts, hist, nblocks);
+        part_hist_kernel<int32_t><<<(unsigned)nblocks, kPartThreads, 0, s>>>(keys, valid, voff, n, nparts, spec, hist,
+                                                                            nblocks);
     hipError_t e = launch_scan(hist, hlen, scratch, nullptr, s);
     if (e != hipSuccess) return e;
     part_counts_kernel<<<1, 64, 0, s>>>(hist, nblocks, nparts, total, counts);
 #define DFP_PS(K, OK, ID)                                                                                 \
     part_scatter_kernel<K, OK, ID><<<(unsigned)nblocks, kPartThreads, 0, s>>>(                                  \
-        keys, valid, voff, ids, id_base, n, nparts, hist, nblocks, (OK*)out_keys, key_offset, (ID*)out_ids)
+        keys, valid, voff, ids, id_base, n, nparts, spec, hist, nblocks, (OK*)out_keys, key_offset, (ID*)out_ids)
     if (key_bytes == 8 && out_key_bytes == 8) {
         if (id_bytes == 8) DFP_PS(int64_t, int64_t, uint64_t); else DFP_PS(int64_t, int64_t, uint32_t);
     } else if (key_bytes == 8) {

@@ -52,11 +52,19 @@ hipError_t launch_table_stats(const TableView& tv,
 hipError_t launch_chain_links(const TableView& tv, int64_t* prev, int64_t nrows, hipStream_t s);
 
 // ---- multi-GPU radix partition -------------------------------------------
+// Destination map of a row: keys outside [lo, hi] are dropped (runtime min/max filter);
+// by_range: part = umulhi(key - lo, mul) with mul = floor(2^64 * nparts / (hi - lo + 1))
+// (contiguous key ranges), else the low bits of mix64(key).
+struct PartSpec {
+    int64_t lo, hi;
+    uint64_t mul;
+    int by_range;
+};
 hipError_t launch_radix_partition(int key_bytes, const void* keys, const uint8_t* valid,
                                   int64_t voff, const uint64_t* ids, uint64_t id_base,
-                                  int64_t n, int nparts, void* out_keys, int out_key_bytes,
-                                  int64_t key_offset, void* out_ids, int id_bytes, int64_t* counts,
-                                  void* workspace, hipStream_t s);
+                                  int64_t n, int nparts, const PartSpec& spec, void* out_keys,
+                                  int out_key_bytes, int64_t key_offset, void* out_ids, int id_bytes,
+                                  int64_t* counts, void* workspace, hipStream_t s);
 int64_t radix_partition_workspace(int64_t n, int nparts);
 
 // in-place exclusive scan of u64 (scratch: scan_scratch_bytes(len)); *total = sum

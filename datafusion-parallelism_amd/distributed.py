@@ -15,7 +15,8 @@ only product) implementations are the HIP kernels.
 """
 from __future__ import annotations
 
-from dataclasses import dataclass
+import ctypes
+from dataclasses import dataclass, field
 from typing import Callable
 
 import torch
@@ -26,12 +27,36 @@ from ._lib import HJ_INT32, HJ_INT64, check
 from .table import HashTable
 
 
+@dataclass(frozen=True)
+class PartSpec:
+    """hj_part_spec: rows with keys outside [key_lo, key_hi] are dropped before the
+    exchange; by_range maps contiguous key ranges to ranks (else the mix64 hash)."""
+    by_range: bool = False
+    key_lo: int = -(2**63)
+    key_hi: int = 2**63 - 1
+
+    def part_of(self, keys, nparts: int):
+        """Host restatement of the device map (tests / host stand-ins): -> (dest, keep)."""
+        import numpy as np
+
+        k = np.asarray(keys).astype(np.int64)
+        keep = (k >= self.key_lo) & (k <= self.key_hi)
+        if not self.by_range:
+            return None, keep
+        rng = (self.key_hi - self.key_lo) + 1
+        mul = min((nparts << 64) // rng, 2**64 - 1)
+        off = [(int(x) - self.key_lo) % 2**64 for x in k.tolist()]
+        return np.array([(o * mul) >> 64 for o in off], dtype=np.int64), keep
+
+
 def gpu_radix_partition(keys: torch.Tensor, ids: torch.Tensor | None, id_base: int, nparts: int,
                         stream: int | None = None, id_dtype: torch.dtype = torch.int64,
-                        key_offset: int | None = None):
-    """hj_radix_partition on device tensors -> (keys grouped by destination, ids
+                        key_offset: int | None = None, spec: PartSpec | None = None):
+    """hj_partition_rows on device tensors -> (keys grouped by destination, ids
     (int64 = u64 build ids, int32 = u32 probe ids), counts[nparts] int64 device tensor).
-    key_offset (int64 keys): the keys come out as int32(key - key_offset)."""
+    key_offset (int64 keys): the keys come out as int32(key - key_offset); spec: the
+    destination map and runtime filter (default: hash map, nothing dropped). Dropped
+    rows are not written: the outputs hold counts.sum() rows."""
     L = _lib.load()
     n = keys.numel()
     kt = HJ_INT64 if keys.dtype == torch.int64 else HJ_INT32
@@ -41,10 +66,13 @@ def gpu_radix_partition(keys: torch.Tensor, ids: torch.Tensor | None, id_base: i
     counts = torch.zeros(nparts, dtype=torch.int64, device=keys.device)
     ws = torch.empty(max(L.hj_partition_workspace_bytes(n, nparts), 8), dtype=torch.uint8, device=keys.device)
     s = stream if stream is not None else torch.cuda.current_stream(keys.device).cuda_stream
-    check(L.hj_radix_partition(kt, keys.data_ptr(), None, 0, None if ids is None else ids.data_ptr(), id_base, n,
-                               nparts, out_k.data_ptr(), out_k.element_size(), key_offset if narrow else 0,
-                               out_i.data_ptr(), 8 if id_dtype == torch.int64 else 4, counts.data_ptr(),
-                               ws.data_ptr(), s))
+    sp = None
+    if spec is not None and spec != PartSpec():
+        sp = ctypes.byref(_lib.HjPartSpec(int(spec.by_range), spec.key_lo, spec.key_hi))
+    check(L.hj_partition_rows(kt, keys.data_ptr(), None, 0, None if ids is None else ids.data_ptr(), id_base, n,
+                              nparts, sp, out_k.data_ptr(), out_k.element_size(), key_offset if narrow else 0,
+                              out_i.data_ptr(), 8 if id_dtype == torch.int64 else 4, counts.data_ptr(),
+                              ws.data_ptr(), s))
     return out_k, out_i, counts
 
 
@@ -112,10 +140,13 @@ def gpu_local_join(build_keys: torch.Tensor, build_ids: torch.Tensor, probe_keys
 
 @dataclass
 class ExchangePlan:
-    """What the exchange narrows (DistributedHashJoin.prepare): keys travel as
-    int32(key - key_offset) when key_offset is set, build ids as build_id_dtype."""
+    """What the exchange narrows and filters (DistributedHashJoin.prepare): keys travel
+    as int32(key - key_offset) when key_offset is set, build ids as build_id_dtype;
+    both sides use `spec` (probe rows outside the global build key range are dropped
+    before the exchange; a dense build key domain is split into contiguous ranges)."""
     key_offset: int | None = None
     build_id_dtype: torch.dtype = torch.int64
+    spec: PartSpec = field(default_factory=PartSpec)
 
 
 @dataclass
@@ -205,7 +236,8 @@ class DistributedHashJoin:
     default to GpuLocalTable."""
 
     def __init__(self, group=None, partition_fn: Callable | None = None, local_join_fn: Callable | None = None,
-                 chunks: int = 1, local_build_fn: Callable | None = None, compress_keys: bool = True):
+                 chunks: int = 1, local_build_fn: Callable | None = None, compress_keys: bool = True,
+                 runtime_filter: bool = True):
         self.group = group
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
@@ -214,53 +246,78 @@ class DistributedHashJoin:
         self.local_build_fn = local_build_fn or GpuLocalTable
         self.chunks = max(1, int(chunks))
         self.compress_keys = compress_keys
+        self.runtime_filter = runtime_filter
 
     def prepare(self, build_keys: torch.Tensor, probe_keys: torch.Tensor, build_base: int) -> ExchangePlan:
-        """Narrow what travels: when the global key range of both sides spans < 2^32,
-        the partition writes keys as int32(key - min - 2^31) (a bijection, so equality
-        and the join are unchanged; the local tables then use int32 keys), and build ids
-        travel as u32 when the global build side has < 2^31 rows. One pass over each
-        side (aminmax), two 8-byte all-reduces and one host read."""
+        """Plan the exchange from the global key ranges (one aminmax pass over each side,
+        two 16-byte all-reduces and one host read):
+
+        * runtime filter: probe rows outside the global build key range [bmin, bmax]
+          cannot match and are dropped by the partition kernel before they travel;
+        * range map: when the build key domain is dense (bmax - bmin + 1 <= 8 x the
+          global build rows, the direct-addressed table's criterion), ranks own
+          contiguous key ranges, so every local table is direct-addressed over 1/G of
+          the domain (else the mix64 hash map);
+        * narrowing: when the travelling keys span < 2^32 values they are written as
+          int32(key - min - 2^31) (a bijection, so equality and the join are unchanged;
+          the local tables then use int32 keys); build ids travel as u32 when the
+          global build side has < 2^31 rows."""
         plan = ExchangePlan()
-        if not self.compress_keys or build_keys.dtype != torch.int64:
+        if not (self.compress_keys or self.runtime_filter):
             return plan
         dev = build_keys.device
         big, small = 2**63 - 1, -(2**63)
-        lo = torch.full((1,), big, dtype=torch.int64, device=dev)
-        hi = torch.tensor([small, build_base + build_keys.numel()], dtype=torch.int64, device=dev)
-        for k in (build_keys, probe_keys):
+        lo = torch.full((2,), big, dtype=torch.int64, device=dev)  # [build min, probe min]
+        hi = torch.tensor([small, small, build_base + build_keys.numel()], dtype=torch.int64, device=dev)
+        for j, k in enumerate((build_keys, probe_keys)):
             if k.numel():
-                mn, mx = torch.aminmax(k)
-                lo = torch.minimum(lo, mn.view(1))
-                hi[0] = torch.maximum(hi[0], mx)
+                mn, mx = torch.aminmax(k.to(torch.int64) if k.dtype != torch.int64 else k)
+                lo[j] = mn
+                hi[j] = mx
         dist.all_reduce(lo, op=dist.ReduceOp.MIN, group=self.group)
         dist.all_reduce(hi, op=dist.ReduceOp.MAX, group=self.group)
-        gmin, gmax, bend = torch.cat([lo, hi]).tolist()
+        bmin, pmin, bmax, pmax, bend = torch.cat([lo, hi]).tolist()
         if bend < 2**31:
             plan.build_id_dtype = torch.int32
-        if gmin <= gmax and gmax - gmin < 2**32:
+        if bmin > bmax:  # empty build side: nothing can match, nothing to plan
+            return plan
+        if self.runtime_filter:
+            dense = (bmax - bmin + 1) <= 8 * bend
+            plan.spec = PartSpec(bool(dense and self.world > 1), bmin, bmax)
+            gmin, gmax = bmin, bmax  # only keys in the build range travel
+        else:
+            gmin, gmax = min(bmin, pmin), max(bmax, pmax)
+        if self.compress_keys and build_keys.dtype == torch.int64 and gmax - gmin < 2**32:
             plan.key_offset = gmin + 2**31
         return plan
 
-    def _partition(self, keys: torch.Tensor, id_base: int, id_dtype: torch.dtype, key_offset: int | None):
+    def _partition(self, keys: torch.Tensor, id_base: int, id_dtype: torch.dtype, key_offset: int | None,
+                   spec: PartSpec | None = None):
         if self.partition_fn is gpu_radix_partition:
-            return gpu_radix_partition(keys, None, id_base, self.world, id_dtype=id_dtype, key_offset=key_offset)
-        if key_offset is not None and keys.dtype == torch.int64:  # host stand-ins: narrow first
-            keys = (keys - key_offset).to(torch.int32)
-        return self.partition_fn(keys, None, id_base, self.world)
+            return gpu_radix_partition(keys, None, id_base, self.world, id_dtype=id_dtype, key_offset=key_offset,
+                                       spec=spec)
+        # host stand-ins (tests): partition on the original keys, then narrow
+        if spec is not None and spec != PartSpec():
+            k, i, c = self.partition_fn(keys, None, id_base, self.world, spec=spec)
+        else:
+            k, i, c = self.partition_fn(keys, None, id_base, self.world)
+        if key_offset is not None and k.dtype == torch.int64:
+            k = (k - key_offset).to(torch.int32)
+        return k, i, c
 
     def shard(self, keys: torch.Tensor, id_base: int, id_dtype: torch.dtype = torch.int64, async_op: bool = False,
-              key_offset: int | None = None):
+              key_offset: int | None = None, spec: PartSpec | None = None):
         """Partition by destination rank and exchange: -> (keys, global ids, stats).
         Build rows carry u64 ids (int64), probe rows u32 ids (int32, the reference's
         UInt32 probe index): 16 resp. 12 bytes per int64-key row on the wire, 8 with a
         narrowing plan (prepare)."""
-        k, i, c = self._partition(keys, id_base, id_dtype, key_offset)
+        k, i, c = self._partition(keys, id_base, id_dtype, key_offset, spec)
         return all_to_all_rows(k, i, c, self.group, async_op=async_op)
 
     def shard_build(self, build_keys: torch.Tensor, build_base: int, plan: ExchangePlan):
         """The build side's exchange under `plan`: -> (keys, int64 global ids)."""
-        bk, bi, _ = self.shard(build_keys, build_base, plan.build_id_dtype, key_offset=plan.key_offset)
+        bk, bi, _ = self.shard(build_keys, build_base, plan.build_id_dtype, key_offset=plan.key_offset,
+                               spec=plan.spec)
         return bk, (bi.to(torch.int64) if bi.dtype != torch.int64 else bi)
 
     def run(self, build_keys: torch.Tensor, build_base: int, probe_keys: torch.Tensor, probe_base: int,
@@ -269,24 +326,30 @@ class DistributedHashJoin:
         plan = self.prepare(build_keys, probe_keys, build_base)
         bk, bi = self.shard_build(build_keys, build_base, plan)
         if self.chunks <= 1:
-            pk, pi, _ = self.shard(probe_keys, probe_base, torch.int32, key_offset=plan.key_offset)
+            pk, pi, _ = self.shard(probe_keys, probe_base, torch.int32, key_offset=plan.key_offset, spec=plan.spec)
             return self.local_join_fn(bk, bi, pk, pi, capacity_hint)
         outs = self.run_pipelined(bk, bi, probe_keys, probe_base, plan)
         return torch.cat([b for b, _ in outs]), torch.cat([p for _, p in outs])
 
     def run_pipelined(self, bk: torch.Tensor, bi: torch.Tensor, probe_keys: torch.Tensor, probe_base: int,
                       plan: ExchangePlan | None = None):
-        """Local build, then the probe side in `chunks` slices: exchange of slice c in
-        flight while slice c-1 is probed. -> list of per-chunk (build_idx, probe_idx)."""
+        """Local build, then the probe side in `chunks` slices. Every slice is partitioned
+        up front and their counts travel in one all_gather (one host sync); then the
+        exchange of slice c is in flight (RCCL stream) while slice c-1 is probed
+        (compute stream). -> list of per-chunk (build_idx, probe_idx)."""
+        plan = plan or ExchangePlan()
         table = self.local_build_fn(bk, bi)
         try:
             n = probe_keys.numel()
+            w = self.world
             bounds = [n * c // self.chunks for c in range(self.chunks + 1)]
+            parts = [self._partition(probe_keys[bounds[c]:bounds[c + 1]], probe_base + bounds[c], torch.int32,
+                                     plan.key_offset, plan.spec) for c in range(self.chunks)]
+            mats = _count_matrix(torch.cat([p[2] for p in parts]), self.group)  # rank s: [chunk c, dest d]
             results, pending = [], None
             for c in range(self.chunks):
-                lo, hi = bounds[c], bounds[c + 1]
-                rk, ri, _, works = self.shard(probe_keys[lo:hi], probe_base + lo, torch.int32, async_op=True,
-                                              key_offset=plan.key_offset if plan else None)
+                m = [[row[c * w + d] for d in range(w)] for row in mats]
+                (rk, ri), works = _exchange_cols([parts[c][0], parts[c][1]], m, self.group, async_op=True)
                 if pending is not None:
                     results.append(self._probe_chunk(table, *pending))
                 pending = (rk, ri, works)

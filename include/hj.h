@@ -209,6 +209,27 @@ hj_status hj_radix_partition(hj_key_type key_type, const void* keys,
                              void* out_ids, int id_bytes, int64_t* counts,
                              void* workspace, void* stream);
 
+/* Destination map and runtime filter of hj_partition_rows. Rows whose key lies outside
+ * [key_lo, key_hi] are dropped like null rows: an inner join's probe row outside the
+ * global build key range cannot match (a min/max runtime filter ahead of the exchange).
+ * by_range 1: destination = (key - key_lo) * nparts / (key_hi - key_lo + 1) (fixed point,
+ * floor(2^64 * nparts / range) multiply-high), i.e. contiguous key ranges, so a dense
+ * global key domain gives every rank a dense local one; by_range 0: the hash map of
+ * hj_radix_partition. Both sides of one join must use the same spec. */
+typedef struct hj_part_spec {
+    int by_range;
+    int64_t key_lo;
+    int64_t key_hi;
+} hj_part_spec;
+
+/* hj_radix_partition with a spec (NULL: hash map, no filter). */
+hj_status hj_partition_rows(hj_key_type key_type, const void* keys,
+                            const uint8_t* validity, int64_t validity_offset,
+                            const uint64_t* ids, uint64_t id_base, int64_t n, int nparts,
+                            const hj_part_spec* spec, void* out_keys, int out_key_bytes,
+                            int64_t key_offset, void* out_ids, int id_bytes, int64_t* counts,
+                            void* workspace, void* stream);
+
 /* ---- join types and output materialisation. Device pointers,
  *      asynchronous on `stream`. Index arrays are uint32 (idx_bytes 4) or uint64 (8);
  *      an all-ones index is a null index (the outer joins' missing side). ---------- */

@@ -72,6 +72,7 @@ def test_no_device_fails_loudly(dfp):
     x = np.zeros(4, np.int64)
     assert L.hj_gen_uniform_keys(x.ctypes.data, 4, 1, 10, None) == _lib.HJ_ERR_NO_DEVICE
     assert L.hj_radix_partition(1, None, None, 0, None, 0, 0, 2, None, 8, 0, None, 8, None, None, None) == _lib.HJ_ERR_NO_DEVICE
+    assert L.hj_partition_rows(1, None, None, 0, None, 0, 0, 2, None, None, 8, 0, None, 8, None, None, None) == _lib.HJ_ERR_NO_DEVICE
 
 
 def test_null_args_rejected(dfp):

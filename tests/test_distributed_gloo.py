@@ -27,11 +27,17 @@ def _mix64(k: np.ndarray) -> np.ndarray:
         return k
 
 
-def cpu_partition(keys, ids, id_base, nparts):
-    """Stable multi-split by the low hash bits (the semantics of hj_radix_partition)."""
+def cpu_partition(keys, ids, id_base, nparts, spec=None):
+    """Stable multi-split by the low hash bits, or by key range and dropping keys outside
+    the spec's bounds (the semantics of hj_partition_rows)."""
     k = keys.numpy()
     i = np.arange(len(k), dtype=np.int64) + id_base if ids is None else ids.numpy()
     dest = (_mix64(k) & np.uint64(nparts - 1)).astype(np.int64)
+    if spec is not None:
+        rdest, keep = spec.part_of(k, nparts)
+        if spec.by_range:
+            dest = rdest
+        k, i, dest = k[keep], i[keep], dest[keep]
     order = np.argsort(dest, kind="stable")
     counts = np.bincount(dest, minlength=nparts)
     return torch.from_numpy(k[order].copy()), torch.from_numpy(i[order].copy()), torch.from_numpy(counts)
@@ -65,7 +71,7 @@ def _canonical(b, p):
     return bool(np.all(pl[1:] >= pl[:-1]) and np.all(bl[1:][same] < bl[:-1][same]))
 
 
-def _worker(rank, world, port, bks, pks, q, chunks=1, max_bytes=None):
+def _worker(rank, world, port, bks, pks, q, chunks=1, max_bytes=None, rfilter=True):
     sys.path.insert(0, ROOT)
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -77,7 +83,7 @@ def _worker(rank, world, port, bks, pks, q, chunks=1, max_bytes=None):
         distributed.A2A_MAX_BYTES = max_bytes
 
     dj = DistributedHashJoin(partition_fn=cpu_partition, local_join_fn=oracle_local_join, chunks=chunks,
-                             local_build_fn=CpuLocalTable)
+                             local_build_fn=CpuLocalTable, runtime_filter=rfilter)
     bbase = sum(len(x) for x in bks[:rank])
     pbase = sum(len(x) for x in pks[:rank])
     if chunks == 1:
@@ -85,7 +91,11 @@ def _worker(rank, world, port, bks, pks, q, chunks=1, max_bytes=None):
         segs = [(b, p)]
     else:  # pipelined probe side: canonical per chunk
         plan = dj.prepare(torch.from_numpy(bks[rank]), torch.from_numpy(pks[rank]), bbase)
-        assert (plan.key_offset is None) == (bks[rank].max() - bks[rank].min() >= 2**32)
+        allb = np.concatenate(bks)
+        span = allb.max() - allb.min() if rfilter else max(allb.max(), max(p.max() for p in pks)) - min(
+            allb.min(), min(p.min() for p in pks))
+        assert (plan.key_offset is None) == (span >= 2**32)
+        assert plan.spec.by_range == (rfilter and allb.max() - allb.min() + 1 <= 8 * len(allb))
         bk, bi = dj.shard_build(torch.from_numpy(bks[rank]), bbase, plan)
         segs = dj.run_pipelined(bk, bi, torch.from_numpy(pks[rank]), pbase, plan)
         assert len(segs) == chunks
@@ -109,9 +119,12 @@ def _free_port():
     return port
 
 
-@pytest.mark.parametrize("world,chunks,wide,max_bytes", [(2, 1, False, None), (2, 3, False, None),
-                                                         (2, 3, True, None), (2, 1, False, 5000), (2, 3, True, 7000)])
-def test_distributed_exchange_matches_single_join(oracle_mod, world, chunks, wide, max_bytes):
+@pytest.mark.parametrize("world,chunks,wide,max_bytes,rfilter", [
+    (2, 1, False, None, True), (2, 3, False, None, True), (2, 3, True, None, True), (2, 1, False, 5000, True),
+    (2, 3, True, 7000, True), (2, 3, False, None, False), (2, 1, True, None, False)])
+def test_distributed_exchange_matches_single_join(oracle_mod, world, chunks, wide, max_bytes, rfilter):
+    """rfilter: runtime min/max filter + range map for dense build domains (the default);
+    off: every probe row travels, hash map."""
     """wide: keys spread over > 2^32 values, so they travel as full int64 (otherwise
     DistributedHashJoin.prepare narrows them to int32 offsets)."""
     rng = np.random.default_rng(9)
@@ -124,7 +137,7 @@ def test_distributed_exchange_matches_single_join(oracle_mod, world, chunks, wid
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, bks, pks, q, chunks, max_bytes)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, bks, pks, q, chunks, max_bytes, rfilter)) for r in range(world)]
     for pr in procs:
         pr.start()
     res = q.get(timeout=240)

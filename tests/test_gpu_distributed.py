@@ -45,6 +45,32 @@ def test_radix_partition_kernel(dfp, nparts, id_dtype, narrow):
     assert np.array_equal(out_i.cpu().numpy(), order + 1000)
 
 
+@pytest.mark.parametrize("nparts", [1, 2, 8, 64])
+@pytest.mark.parametrize("by_range,lo,hi", [(True, 0, 99999), (True, -(2**63), 2**63 - 1), (False, 2000, 60000),
+                                            (True, 2000, 60000), (True, -(2**40), 2**40 + 3)])
+def test_partition_spec_kernel(dfp, nparts, by_range, lo, hi):
+    """hj_partition_rows: keys outside [lo, hi] dropped, range or hash map, stable; the
+    host restatement PartSpec.part_of gives the same destinations."""
+    from datafusion_parallelism_amd.distributed import PartSpec, gpu_radix_partition
+
+    rng = np.random.default_rng(nparts + 7)
+    k = rng.integers(-(2**41), 2**41, 50007) if lo < -1000 else rng.integers(-500, 100500, 50007)
+    k[:5] = [lo, hi, max(lo - 1, -(2**63)), min(hi + 1, 2**63 - 1), (lo + hi) // 2]
+    spec = PartSpec(by_range, lo, hi)
+    out_k, out_i, counts = gpu_radix_partition(torch.from_numpy(k).cuda(), None, 0, nparts, spec=spec)
+    rdest, keep = spec.part_of(k, nparts)
+    dest = rdest if by_range else (_mix64(k) & np.uint64(nparts - 1)).astype(np.int64)
+    idx = np.nonzero(keep)[0]
+    order = idx[np.argsort(dest[idx], kind="stable")]
+    tot = int(counts.sum())
+    assert np.array_equal(counts.cpu().numpy(), np.bincount(dest[idx], minlength=nparts))
+    assert np.array_equal(out_k[:tot].cpu().numpy(), k[order])
+    assert np.array_equal(out_i[:tot].cpu().numpy(), order)
+    if by_range:  # contiguous key ranges: destination non-decreasing in the key
+        srt = idx[np.argsort(k[idx], kind="stable")]
+        assert (np.diff(dest[srt]) >= 0).all()
+
+
 @pytest.mark.parametrize("chunks", [1, 3])
 def test_distributed_join_one_rank(dfp, oracle_mod, chunks):
     """One RCCL rank (the exchange is a self-copy): pairs equal the oracle's; with
