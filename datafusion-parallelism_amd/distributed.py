@@ -180,6 +180,7 @@ def _exchange_cols(cols: list[torch.Tensor], m: list[list[int]], group=None, asy
     world = len(m)
     send = m[me]
     recv = [m[s][me] for s in range(world)]
+    cols = [c[:sum(send)] for c in cols]  # rows the partition dropped are not sent
     widest = max(c.element_size() for c in cols) if cols else 1
     peak = max(max(sum(m[r]), sum(m[s][r] for s in range(world))) for r in range(world)) * widest
     rounds = max(1, -(-peak // A2A_MAX_BYTES))

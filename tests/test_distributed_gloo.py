@@ -40,7 +40,12 @@ def cpu_partition(keys, ids, id_base, nparts, spec=None):
         k, i, dest = k[keep], i[keep], dest[keep]
     order = np.argsort(dest, kind="stable")
     counts = np.bincount(dest, minlength=nparts)
-    return torch.from_numpy(k[order].copy()), torch.from_numpy(i[order].copy()), torch.from_numpy(counts)
+    n = len(keys)  # like the device kernel: full-length outputs, the first counts.sum() rows valid
+    ok_ = np.zeros(n, dtype=k.dtype)
+    oi_ = np.zeros(n, dtype=i.dtype)
+    ok_[:len(order)] = k[order]
+    oi_[:len(order)] = i[order]
+    return torch.from_numpy(ok_), torch.from_numpy(oi_), torch.from_numpy(counts)
 
 
 def oracle_local_join(bk, bi, pk, pi, cap=None):
