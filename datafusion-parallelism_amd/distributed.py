@@ -80,14 +80,18 @@ class GpuLocalTable:
     """One rank's shard table (global build ids held in place of row numbers when they
     fit 31 bits and ascend, HJ_IDS_U31) and asynchronous probes of received chunks."""
 
-    def __init__(self, build_keys: torch.Tensor, build_ids: torch.Tensor):
+    def __init__(self, build_keys: torch.Tensor, build_ids: torch.Tensor, ids_u31: bool | None = None):
+        """ids_u31: the caller knows the ids ascend and are < 2^31 (DistributedHashJoin:
+        stable partition, ranks in order, global build side < 2^31 rows); None checks."""
         dev = build_keys.device
         kt = "int64" if build_keys.dtype == torch.int64 else "int32"
         # received build ids ascend (stable partition, ranks in order): when they also
         # fit 31 bits the table keeps them in place of row numbers (no id gather per pair)
         nbi = build_ids.numel()
-        u31 = nbi == 0 or bool(((build_ids[-1] < 2**31) & (build_ids[0] >= 0) &
-                                (nbi < 2 or bool((build_ids[1:] > build_ids[:-1]).all()))).item())
+        u31 = ids_u31
+        if u31 is None:
+            u31 = nbi == 0 or bool(((build_ids[-1] < 2**31) & (build_ids[0] >= 0) &
+                                    (nbi < 2 or bool((build_ids[1:] > build_ids[:-1]).all()))).item())
         self.table = HashTable(1, kt, dev.index or 0)
         self.table.append(0, build_keys, ids=build_ids, ids_u31=u31)
         self.table.finish(0)
@@ -113,14 +117,16 @@ class GpuLocalTable:
 
         ob, op = launch(cap)
 
-        def result():
+        def result(total: int | None = None):
+            """total: d_total already read by the caller (one host sync for many probes)."""
             nonlocal ob, op
-            total = int(d_total.item())
+            total = int(d_total.item()) if total is None else total
             if total > cap:  # rare (duplicate-heavy keys): once more with the exact size
                 ob, op = launch(total)
                 total = int(d_total.item())
             return ob[:total], op[:total]
 
+        result.d_total = d_total
         return result
 
     def close(self):
@@ -270,7 +276,9 @@ class DistributedHashJoin:
         big, small = 2**63 - 1, -(2**63)
         lo = torch.full((2,), big, dtype=torch.int64, device=dev)  # [build min, probe min]
         hi = torch.tensor([small, small, build_base + build_keys.numel()], dtype=torch.int64, device=dev)
-        for j, k in enumerate((build_keys, probe_keys)):
+        # with the runtime filter only build-range keys travel: the probe range is not needed
+        sides = (build_keys,) if self.runtime_filter else (build_keys, probe_keys)
+        for j, k in enumerate(sides):
             if k.numel():
                 mn, mx = torch.aminmax(k.to(torch.int64) if k.dtype != torch.int64 else k)
                 lo[j] = mn
@@ -339,7 +347,10 @@ class DistributedHashJoin:
         exchange of slice c is in flight (RCCL stream) while slice c-1 is probed
         (compute stream). -> list of per-chunk (build_idx, probe_idx)."""
         plan = plan or ExchangePlan()
-        table = self.local_build_fn(bk, bi)
+        if self.local_build_fn is GpuLocalTable:
+            table = GpuLocalTable(bk, bi, ids_u31=True if plan.build_id_dtype == torch.int32 else None)
+        else:
+            table = self.local_build_fn(bk, bi)
         try:
             n = probe_keys.numel()
             w = self.world
@@ -355,6 +366,9 @@ class DistributedHashJoin:
                     results.append(self._probe_chunk(table, *pending))
                 pending = (rk, ri, works)
             results.append(self._probe_chunk(table, *pending))
+            if all(hasattr(r, "d_total") for r in results):  # every chunk's match count in one host read
+                totals = torch.cat([r.d_total for r in results]).tolist()
+                return [r(t) for r, t in zip(results, totals)]
             return [r() for r in results]
         finally:
             table.close()
