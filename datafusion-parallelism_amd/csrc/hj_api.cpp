@@ -355,7 +355,12 @@ hj_status build_attempt(hj_table* t, const std::vector<Segment>& segs, double lf
     t->tbl = nullptr;
     t->dense = nullptr;
     if (dense) {
-        if ((st = dev_alloc(t, t->allocs, &p, sizeof(uint32_t) * (size_t)(nchunks << kDenseShift))) != HJ_OK) return st;
+        // the one-level build writes whole blocks of 2^kDenseBlockShift chunks
+        const uint64_t dchunks = dense_one_level((uint32_t)nchunks)
+                                     ? (uint64_t)dense_blocks((uint32_t)nchunks) << kDenseBlockShift
+                                     : nchunks;
+        if ((st = dev_alloc(t, t->allocs, &p, sizeof(uint32_t) * (size_t)(dchunks << kDenseShift))) != HJ_OK)
+            return st;
         t->dense = (uint32_t*)p;
     } else {
         if ((st = dev_alloc(t, t->allocs, &p, (size_t)(t->nb + 1) * sizeof(Bucket))) != HJ_OK) return st;
@@ -375,14 +380,14 @@ hj_status build_attempt(hj_table* t, const std::vector<Segment>& segs, double lf
     void* scan;
     if ((st = dev_alloc(t, t->scratch, &p, sizeof(uint32_t) * (size_t)std::max<int64_t>(hlen, 1))) != HJ_OK) return st;
     hist = (uint32_t*)p;
-    if ((st = dev_alloc(t, t->scratch, &p, sizeof(uint32_t) * (size_t)std::max<int64_t>(kCoarseBins * ntiles, 1))) !=
+    if ((st = dev_alloc(t, t->scratch, &p, sizeof(uint32_t) * (size_t)std::max<int64_t>(kMaxLevel1Bins * ntiles, 1))) !=
         HJ_OK)
         return st;
     hist1 = (uint32_t*)p;
     uint32_t* chunk_starts;
     if ((st = dev_alloc(t, t->scratch, &p, sizeof(uint32_t) * (size_t)(nchunks + 2))) != HJ_OK) return st;
     chunk_starts = (uint32_t*)p;
-    if ((st = dev_alloc(t, t->scratch, &p, (size_t)scan_scratch_bytes(std::max<int64_t>(hlen, kCoarseBins * ntiles)))) !=
+    if ((st = dev_alloc(t, t->scratch, &p, (size_t)scan_scratch_bytes(std::max<int64_t>(hlen, kMaxLevel1Bins * ntiles)))) !=
         HJ_OK)
         return st;
     scan = p;

@@ -148,14 +148,16 @@ __device__ __forceinline__ void load_rows(const Segment* __restrict__ segs, int 
     }
 }
 
-// level 1: rows per (group, tile); hist1[g * ntiles + tile]
-template <typename K>
+// level 1: rows per (group, tile); hist1[g * ntiles + tile]. NB bins in COPIES LDS
+// copies (per-wave copies for the 128-group level; 4 copies of 2048 bins for the
+// one-level dense partition): fewer LDS atomic collisions.
+template <typename K, int NB, int COPIES>
 __global__ void __launch_bounds__(kHistThreads)
 coarse_hist_kernel(const Segment* __restrict__ segs, int nseg, int64_t total, ChunkGeom g, uint32_t gshift, uint32_t ngroups, uint32_t* __restrict__ hist1,
                    int64_t ntiles, int64_t tile_rows) {
-    __shared__ uint32_t s_h[kHistThreads / 64][kCoarseBins];  // per-wave copies: fewer LDS atomic collisions
-    const int wave = threadIdx.x >> 6;
-    for (uint32_t k = threadIdx.x; k < (kHistThreads / 64) * kCoarseBins; k += kHistThreads) (&s_h[0][0])[k] = 0;
+    __shared__ uint32_t s_h[COPIES][NB];
+    const int wave = (threadIdx.x >> 6) % COPIES;
+    for (uint32_t k = threadIdx.x; k < (uint32_t)(COPIES * NB); k += kHistThreads) (&s_h[0][0])[k] = 0;
     __syncthreads();
     const int64_t r0 = (int64_t)blockIdx.x * tile_rows;
     const int64_t r1 = min<int64_t>(total, r0 + tile_rows);
@@ -174,7 +176,7 @@ coarse_hist_kernel(const Segment* __restrict__ segs, int nseg, int64_t total, Ch
     __syncthreads();
     for (uint32_t g = threadIdx.x; g < ngroups; g += kHistThreads) {
         uint32_t v = 0;
-        for (int w = 0; w < kHistThreads / 64; ++w) v += s_h[w][g];
+        for (int w = 0; w < COPIES; ++w) v += s_h[w][g];
         hist1[(int64_t)g * ntiles + blockIdx.x] = v;
     }
 }
@@ -300,6 +302,7 @@ scan_down_kernel(T* __restrict__ a, int64_t len, const unsigned long long* __res
 // one line per lane). s_cur[b] = next global position of bin b (advanced here).
 constexpr int kStageRows = kHistThreads * kRowBatch;  // 8192 rows: 64 KB keys + 32 KB rows
 constexpr int kStageMaxBins = 2048;
+static_assert(kStageMaxBins == kMaxLevel1Bins, "one-level dense partition bins");
 constexpr size_t kStageLds = (size_t)kStageRows * 12 + (size_t)kStageMaxBins * 12;
 
 __device__ __forceinline__ void staged_scatter_batch(const unsigned long long (&key)[kRowBatch],
@@ -707,82 +710,86 @@ chunk_build_kernel(uint32_t nb, uint32_t clog2, uint32_t nchunks, const uint32_t
 // ---------------------------------------------------------------------------
 // build 3 (dense): key ranges of at most 8 x the build rows get a direct-addressed table
 // of one u32 ref per key value (dense[key - dmin]; kMiss = absent), same ref / dup_rows
-// encoding as the buckets. One 512-thread workgroup builds 2^dshift = 2048 consecutive
-// key values: refs in LDS, the first insert of a key stores its row (atomicExch); a key
-// seen twice switches the chunk to the duplicate passes (counts, directory, canonical
-// descending segments), which cannot overflow (a chunk has at most 2048 keys).
+// encoding as the buckets. One workgroup builds GV consecutive key values (one block of
+// the partition: 2048 values, or 8192 for the one-level partition): refs in LDS, the
+// first insert of a key stores its row (atomicExch); a key seen twice switches its
+// 2048-value sub-range to the duplicate passes (counts, directory, canonical descending
+// segments), whose directory cannot overflow (a sub-range has at most 2048 keys).
 // ---------------------------------------------------------------------------
-constexpr int kDenseThreads = 512;
-constexpr int kDenseRegRows = 4;
+constexpr uint32_t kDenseSub = 1u << kDenseShift;  // values per duplicate-pass sub-range
 
-__global__ void __launch_bounds__(kDenseThreads)
+template <uint32_t GV, int T, int RR>
+__global__ void __launch_bounds__(T)
 dense_chunk_build_kernel(ChunkGeom g, const uint32_t* __restrict__ starts, const unsigned long long* __restrict__ skeys,
                          const uint32_t* __restrict__ srows, uint32_t* __restrict__ dense,
                          uint32_t* __restrict__ dup_rows, BigSeg* __restrict__ big, BuildCounters* ctr) {
-    constexpr uint32_t CV = 1u << kDenseShift;
-    __shared__ uint32_t refs[CV];
-    __shared__ uint32_t d_off[CV], d_cur[CV], d_cnt[CV];
-    __shared__ unsigned s_ndup, s_dup;
-    __shared__ unsigned long long s_w[kDenseThreads / 64];
+    constexpr uint32_t NSUB = GV / kDenseSub;
+    static_assert(GV % kDenseSub == 0, "block of whole sub-ranges");
+    __shared__ uint32_t refs[GV];
+    __shared__ uint32_t d_off[kDenseSub], d_cur[kDenseSub], d_cnt[kDenseSub];
+    __shared__ unsigned s_ndup, s_dup[NSUB];
+    __shared__ unsigned long long s_w[T / 64];
     __shared__ unsigned long long s_base;
     const uint32_t c = blockIdx.x;
     const uint32_t start = starts[c], end = starts[c + 1];
-    const uint64_t cbase = (uint64_t)c << kDenseShift;  // key index of refs[0]
-    for (uint32_t i = threadIdx.x; i < CV; i += kDenseThreads) refs[i] = kMiss;
-    if (threadIdx.x == 0) {
-        s_ndup = 0;
-        s_dup = 0;
-    }
+    const uint64_t cbase = (uint64_t)c * GV;  // key index of refs[0]
+    for (uint32_t i = threadIdx.x; i < GV; i += T) refs[i] = kMiss;
+    const bool in_regs = end - start <= (uint32_t)(T * RR);
+    if (threadIdx.x < NSUB) s_dup[threadIdx.x] = in_regs ? 0u : 1u;  // more rows than the registers hold
     __syncthreads();
-    const bool in_regs = end - start <= (uint32_t)(kDenseThreads * kDenseRegRows);
-    uint32_t rrow[kDenseRegRows];
-    int ridx[kDenseRegRows];
+    uint32_t rrow[RR];
+    int ridx[RR];
     auto index_of = [&](unsigned long long key) {
         return (int)(((uint64_t)key - (uint64_t)g.dmin) - cbase);
     };
     if (in_regs) {
 #pragma unroll
-        for (int u = 0; u < kDenseRegRows; ++u) {
-            const uint32_t r = start + u * kDenseThreads + threadIdx.x;
+        for (int u = 0; u < RR; ++u) {
+            const uint32_t r = start + u * T + threadIdx.x;
             ridx[u] = r < end ? index_of(skeys[r]) : -1;
             rrow[u] = r < end ? srows[r] : 0u;
         }
 #pragma unroll
-        for (int u = 0; u < kDenseRegRows; ++u)
-            if (ridx[u] >= 0 && atomicExch(&refs[ridx[u]], rrow[u]) != kMiss) s_dup = 1u;
-    } else if (threadIdx.x == 0) {
-        s_dup = 1u;  // more rows than key values: duplicates for sure
+        for (int u = 0; u < RR; ++u)
+            if (ridx[u] >= 0 && atomicExch(&refs[ridx[u]], rrow[u]) != kMiss) s_dup[ridx[u] / kDenseSub] = 1u;
     }
     __syncthreads();
-    if (s_dup) {
+    for (uint32_t q = 0; q < NSUB; ++q) {
+        if (!s_dup[q]) continue;  // uniform: every thread reads the same LDS word
+        const int lo = (int)(q * kDenseSub), hi = lo + (int)kDenseSub;
+        uint32_t* img = refs + lo;
+        if (threadIdx.x == 0) s_ndup = 0;
         // counts
-        for (uint32_t i = threadIdx.x; i < CV; i += kDenseThreads) refs[i] = 0;
+        for (uint32_t i = threadIdx.x; i < kDenseSub; i += T) img[i] = 0;
         __syncthreads();
         if (in_regs) {
 #pragma unroll
-            for (int u = 0; u < kDenseRegRows; ++u)
-                if (ridx[u] >= 0) atomicAdd(&refs[ridx[u]], 1u);
+            for (int u = 0; u < RR; ++u)
+                if (ridx[u] >= lo && ridx[u] < hi) atomicAdd(&refs[ridx[u]], 1u);
         } else {
-            for (uint32_t r = start + threadIdx.x; r < end; r += kDenseThreads) atomicAdd(&refs[index_of(skeys[r])], 1u);
+            for (uint32_t r = start + threadIdx.x; r < end; r += T) {
+                const int i = index_of(skeys[r]);
+                if (i >= lo && i < hi) atomicAdd(&refs[i], 1u);
+            }
         }
         __syncthreads();
         // directory of duplicated keys; absent keys become kMiss before rows are placed
-        for (uint32_t i = threadIdx.x; i < CV; i += kDenseThreads) {
-            const uint32_t cnt = refs[i];
+        for (uint32_t i = threadIdx.x; i < kDenseSub; i += T) {
+            const uint32_t cnt = img[i];
             if (cnt == 0) {
-                refs[i] = kMiss;
+                img[i] = kMiss;
             } else if (cnt > 1) {
                 const unsigned li = atomicAdd(&s_ndup, 1u);
                 d_cnt[li] = cnt;
                 d_cur[li] = 0;
-                refs[i] = kDupFlag | li;
+                img[i] = kDupFlag | li;
             }
         }
         __syncthreads();
         const unsigned ndup = s_ndup;
         unsigned long long carry = 0;
-        for (unsigned b = 0; b < ndup; b += kDenseThreads) {
-            const unsigned li = b + threadIdx.x;
+        for (unsigned b0 = 0; b0 < ndup; b0 += T) {
+            const unsigned li = b0 + threadIdx.x;
             const unsigned long long v = li < ndup ? (unsigned long long)d_cnt[li] + 1 : 0;
             unsigned long long tot;
             const unsigned long long ex = block_excl_scan<unsigned long long>(v, s_w, &tot);
@@ -791,7 +798,7 @@ dense_chunk_build_kernel(ChunkGeom g, const uint32_t* __restrict__ starts, const
         }
         if (threadIdx.x == 0) s_base = carry ? atomicAdd(&ctr->dup_used, carry) : 0;
         __syncthreads();
-        for (unsigned li = threadIdx.x; li < ndup; li += kDenseThreads) {
+        for (unsigned li = threadIdx.x; li < ndup; li += T) {
             d_off[li] += (uint32_t)s_base;
             dup_rows[d_off[li]] = d_cnt[li];
         }
@@ -807,13 +814,16 @@ dense_chunk_build_kernel(ChunkGeom g, const uint32_t* __restrict__ starts, const
         };
         if (in_regs) {
 #pragma unroll
-            for (int u = 0; u < kDenseRegRows; ++u)
-                if (ridx[u] >= 0) place(ridx[u], rrow[u]);
+            for (int u = 0; u < RR; ++u)
+                if (ridx[u] >= lo && ridx[u] < hi) place(ridx[u], rrow[u]);
         } else {
-            for (uint32_t r = start + threadIdx.x; r < end; r += kDenseThreads) place(index_of(skeys[r]), srows[r]);
+            for (uint32_t r = start + threadIdx.x; r < end; r += T) {
+                const int i = index_of(skeys[r]);
+                if (i >= lo && i < hi) place(i, srows[r]);
+            }
         }
         __syncthreads();
-        for (unsigned li = threadIdx.x; li < ndup; li += kDenseThreads) {
+        for (unsigned li = threadIdx.x; li < ndup; li += T) {
             const unsigned n = d_cnt[li], off = d_off[li];
             if (n <= (unsigned)kSmallSeg) {
                 uint32_t v[16];
@@ -825,16 +835,16 @@ dense_chunk_build_kernel(ChunkGeom g, const uint32_t* __restrict__ starts, const
                     if (i < (int)n) dup_rows[off + 1 + i] = v[i];
             }
         }
-        for (uint32_t i = threadIdx.x; i < CV; i += kDenseThreads) {
-            const uint32_t rv = refs[i];
+        for (uint32_t i = threadIdx.x; i < kDenseSub; i += T) {
+            const uint32_t rv = img[i];
             if (rv != kMiss && (rv & kDupFlag)) {
                 const unsigned li = rv & ~kDupFlag;
                 if (d_cnt[li] > (unsigned)kSmallSeg) {
                     const unsigned bi = (unsigned)atomicAdd(&ctr->n_big, 1ull);
-                    big[bi] = BigSeg{(unsigned long long)((uint64_t)g.dmin + cbase + i), d_off[li], 0u};
+                    big[bi] = BigSeg{(unsigned long long)((uint64_t)g.dmin + cbase + lo + i), d_off[li], 0u};
                 }
                 const uint32_t c4 = (g.packed && d_cnt[li] <= 15u) ? d_cnt[li] : 0u;
-                refs[i] = kDupFlag | (c4 << 27) | d_off[li];
+                img[i] = kDupFlag | (c4 << 27) | d_off[li];
             }
         }
         __syncthreads();
@@ -842,7 +852,7 @@ dense_chunk_build_kernel(ChunkGeom g, const uint32_t* __restrict__ starts, const
     // write out (coalesced)
     uint4* dst = reinterpret_cast<uint4*>(dense + cbase);
     const uint4* src = reinterpret_cast<const uint4*>(refs);
-    for (uint32_t i = threadIdx.x; i < CV / 4; i += kDenseThreads) dst[i] = src[i];
+    for (uint32_t i = threadIdx.x; i < GV / 4; i += T) dst[i] = src[i];
 }
 
 // ---------------------------------------------------------------------------
@@ -1764,6 +1774,21 @@ static hipError_t launch_scan(T* a, int64_t len, unsigned long long* bsum, unsig
     return hipGetLastError();
 }
 
+static hipError_t set_stage_lds() {
+    static const bool lds_ok = [] {
+        return hipFuncSetAttribute((const void*)coarse_scatter_staged_kernel<int64_t>,
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)kStageLds) == hipSuccess &&
+               hipFuncSetAttribute((const void*)coarse_scatter_staged_kernel<int32_t>,
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)kStageLds) == hipSuccess &&
+               hipFuncSetAttribute((const void*)fine_scatter_staged_kernel,
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)kStageLds) == hipSuccess;
+    }();
+    return lds_ok ? hipSuccess : hipErrorInvalidConfiguration;
+}
+
+uint32_t dense_blocks(uint32_t nchunks) { return (nchunks + (1u << kDenseBlockShift) - 1) >> kDenseBlockShift; }
+bool dense_one_level(uint32_t nchunks) { return dense_blocks(nchunks) <= (uint32_t)kMaxLevel1Bins; }
+
 uint32_t coarse_shift(uint32_t nchunks) {
     // smallest shift with (nchunks >> shift) + 1 <= kCoarseBins groups (side chunk included)
     uint32_t sh = 0;
@@ -1848,30 +1873,54 @@ hipError_t launch_build(int key_bytes, const Segment* d_segs, int nseg, int64_t 
                         BigSeg* big, BuildCounters* ctr, int big_grid, hipStream_t s) {
     const uint32_t nb = g.nb, clog2 = g.clog2, nchunks = g.nchunks;
     const int64_t hlen = (int64_t)(nchunks + 1) * ntiles;
+    if (g.dense && dense_one_level(nchunks)) {
+        // one partition level: rows -> blocks of kDenseBlockChunks chunks (<= 2048 blocks,
+        // LDS-staged scatter), each block built by one workgroup straight from tkeys/trows
+        const uint32_t gshift = kDenseBlockShift;
+        const uint32_t nblk = dense_blocks(nchunks);
+        if (ntiles > 0) {
+            unsigned long long* scr = (unsigned long long*)scan_scratch;
+            if (key_bytes == 8)
+                coarse_hist_kernel<int64_t, kStageMaxBins, 4><<<(unsigned)ntiles, kHistThreads, 0, s>>>(
+                    d_segs, nseg, total, g, gshift, nblk, hist1, ntiles, tile_rows);
+            else
+                coarse_hist_kernel<int32_t, kStageMaxBins, 4><<<(unsigned)ntiles, kHistThreads, 0, s>>>(
+                    d_segs, nseg, total, g, gshift, nblk, hist1, ntiles, tile_rows);
+            hipError_t e = launch_scan(hist1, (int64_t)nblk * ntiles, scr, &ctr->n_valid, s);
+            if (e != hipSuccess) return e;
+            if ((e = set_stage_lds()) != hipSuccess) return e;
+            // block starts from the scanned level-1 histogram, before the scatter consumes it
+            chunk_starts_kernel<<<(unsigned)std::min<uint32_t>((nblk + 1 + 255) / 256, 4096), 256, 0, s>>>(
+                hist1, ntiles, nblk - 1, ctr, chunk_starts);
+            if (key_bytes == 8)
+                coarse_scatter_staged_kernel<int64_t><<<(unsigned)ntiles, kHistThreads, kStageLds, s>>>(
+                    d_segs, nseg, total, g, gshift, nblk, hist1, ntiles, tkeys, trows, row_ids, ids_as_rows,
+                    tile_rows);
+            else
+                coarse_scatter_staged_kernel<int32_t><<<(unsigned)ntiles, kHistThreads, kStageLds, s>>>(
+                    d_segs, nseg, total, g, gshift, nblk, hist1, ntiles, tkeys, trows, row_ids, ids_as_rows,
+                    tile_rows);
+            dense_chunk_build_kernel<kDenseSub << kDenseBlockShift, 1024, 8><<<nblk, 1024, 0, s>>>(
+                g, chunk_starts, tkeys, trows, dense, dup_rows, big, ctr);
+            dup_sort_big_kernel<<<big_grid, kBigThreads, 0, s>>>(dup_rows, big, ctr, d_segs, nseg, total, key_bytes,
+                                                                 ids_as_rows);
+        }
+        return hipGetLastError();
+    }
     const uint32_t gshift = coarse_shift(nchunks);
     const uint32_t ngroups = (nchunks >> gshift) + 1;
     if (ntiles > 0) {
         unsigned long long* scr = (unsigned long long*)scan_scratch;
         // level 1: group order
         if (key_bytes == 8)
-            coarse_hist_kernel<int64_t><<<(unsigned)ntiles, kHistThreads, 0, s>>>(d_segs, nseg, total, g,
-                                                                                 gshift, ngroups, hist1, ntiles,
-                                                                                 tile_rows);
+            coarse_hist_kernel<int64_t, kCoarseBins, kHistThreads / 64><<<(unsigned)ntiles, kHistThreads, 0, s>>>(
+                d_segs, nseg, total, g, gshift, ngroups, hist1, ntiles, tile_rows);
         else
-            coarse_hist_kernel<int32_t><<<(unsigned)ntiles, kHistThreads, 0, s>>>(d_segs, nseg, total, g,
-                                                                                 gshift, ngroups, hist1, ntiles,
-                                                                                 tile_rows);
+            coarse_hist_kernel<int32_t, kCoarseBins, kHistThreads / 64><<<(unsigned)ntiles, kHistThreads, 0, s>>>(
+                d_segs, nseg, total, g, gshift, ngroups, hist1, ntiles, tile_rows);
         hipError_t e = launch_scan(hist1, (int64_t)ngroups * ntiles, scr, &ctr->n_valid, s);
         if (e != hipSuccess) return e;
-        static const bool lds_ok = [] {
-            return hipFuncSetAttribute((const void*)coarse_scatter_staged_kernel<int64_t>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)kStageLds) == hipSuccess &&
-                   hipFuncSetAttribute((const void*)coarse_scatter_staged_kernel<int32_t>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)kStageLds) == hipSuccess &&
-                   hipFuncSetAttribute((const void*)fine_scatter_staged_kernel,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)kStageLds) == hipSuccess;
-        }();
-        if (!lds_ok) return hipErrorInvalidConfiguration;
+        if ((e = set_stage_lds()) != hipSuccess) return e;
         if (key_bytes == 8)
             coarse_scatter_staged_kernel<int64_t><<<(unsigned)ntiles, kHistThreads, kStageLds, s>>>(
                 d_segs, nseg, total, g, gshift, ngroups, hist1, ntiles, tkeys, trows, row_ids,
@@ -1892,8 +1941,8 @@ hipError_t launch_build(int key_bytes, const Segment* d_segs, int nseg, int64_t 
     }
     if (g.dense) {
         if (ntiles > 0) {
-            dense_chunk_build_kernel<<<nchunks, kDenseThreads, 0, s>>>(g, chunk_starts, skeys, srows, dense, dup_rows,
-                                                                       big, ctr);
+            dense_chunk_build_kernel<kDenseSub, 512, 4><<<nchunks, 512, 0, s>>>(g, chunk_starts, skeys, srows, dense,
+                                                                                dup_rows, big, ctr);
             dup_sort_big_kernel<<<big_grid, kBigThreads, 0, s>>>(dup_rows, big, ctr, d_segs, nseg, total, key_bytes,
                                                                  ids_as_rows);
         }

@@ -17,6 +17,12 @@ int64_t build_tile_rows(int64_t total, int64_t ntiles);
 int64_t scan_scratch_bytes(int64_t len);
 
 constexpr int kCoarseBins = 128;     // level-1 partition groups (per-wave LDS copies)
+constexpr int kMaxLevel1Bins = 2048; // level-1 bins of the one-level dense partition
+// Dense tables whose key range spans <= 2048 blocks of 2^kDenseBlockShift chunks (2048
+// values each, i.e. <= 16.7 M values) are partitioned in one level, by block.
+constexpr uint32_t kDenseBlockShift = 2;
+uint32_t dense_blocks(uint32_t nchunks);
+bool dense_one_level(uint32_t nchunks);
 
 // scratch: hist u32[(nchunks + 1) * ntiles], hist1 u32[kCoarseBins * ntiles],
 // chunk_starts u32[nchunks + 2],

@@ -128,8 +128,11 @@ def test_chain_order_across_partitions_kat(dfp):
     (100003, 300007, 60000, 0.05, "int64"),
     (50000, 123457, 20000, 0.0, "int32"),
     (200000, 1000000, 400000, 0.01, "int64"),
+    (300000, 200000, 3000, 0.0, "int64"),  # dense, > 8192 rows per 8192-value block
 ])
 def test_random_parity(dfp, oracle_mod, probe_mode, nb, np_, krange, null_frac, key_type):
+    """Small key ranges take the direct-addressed layout's one-level build (hashed under
+    the *-hashed modes)."""
     rng = np.random.default_rng(nb * 31 + np_)
     dt = np.int64 if key_type == "int64" else np.int32
     bk = rng.integers(-krange // 2, krange, nb).astype(dt)
@@ -324,3 +327,17 @@ def test_large_build_120m_rows(dfp):
     assert bool((pl[1:] > pl[:-1]).all())  # unique build keys: one pair per matched row, ascending
     del bk, pk, b, p
     torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("nb,krange", [(2_200_000, 17_600_000), (2_000_000, 16_000_000)])
+def test_dense_build_levels(dfp, oracle_mod, nb, krange):
+    """Direct-addressed builds on both sides of the one-level limit (2048 blocks of 8192
+    key values): 17.6 M values take the two-level partition, 16 M the one-level one."""
+    rng = np.random.default_rng(nb)
+    bk = rng.integers(0, krange, nb)
+    bk[:3] = [0, krange - 1, krange - 1]
+    pk = rng.integers(-1000, krange + 1000, 1_000_000)
+    b, p, st = gpu_join(dfp, bk, pk)
+    assert st["buckets"] == 0  # direct-addressed
+    ob, op = oracle_mod.inner_join(bk, pk)
+    assert_same(b, p, ob, op)
