@@ -303,12 +303,13 @@ scan_down_kernel(T* __restrict__ a, int64_t len, const unsigned long long* __res
 constexpr int kStageRows = kHistThreads * kRowBatch;  // 8192 rows: 64 KB keys + 32 KB rows
 constexpr int kStageMaxBins = 2048;
 static_assert(kStageMaxBins == kMaxLevel1Bins, "one-level dense partition bins");
-constexpr size_t kStageLds = (size_t)kStageRows * 12 + (size_t)kStageMaxBins * 12;
+constexpr size_t kStageLds = (size_t)kStageRows * 14 + (size_t)kStageMaxBins * 12;  // + u16 bin per row
 
 __device__ __forceinline__ void staged_scatter_batch(const unsigned long long (&key)[kRowBatch],
                                                      const uint32_t (&row)[kRowBatch], const int (&bin)[kRowBatch],
                                                      uint32_t R, unsigned long long* s_k, uint32_t* s_r,
-                                                     uint32_t* s_cur, uint32_t* s_cnt, uint32_t* s_st, uint32_t* s_w,
+                                                     uint16_t* s_b, uint32_t* s_cur, uint32_t* s_cnt, uint32_t* s_st,
+                                                     uint32_t* s_w,
                                                      unsigned long long* __restrict__ out_k,
                                                      uint32_t* __restrict__ out_r) {
     for (uint32_t b = threadIdx.x; b < R; b += kHistThreads) s_cnt[b] = 0;
@@ -331,17 +332,13 @@ __device__ __forceinline__ void staged_scatter_batch(const unsigned long long (&
         const uint32_t pos = s_st[bin[u]] + lrank[u];
         s_k[pos] = key[u];
         s_r[pos] = row[u];
+        s_b[pos] = (uint16_t)bin[u];
     }
     __syncthreads();
-    // stores in bin order: the element's bin is found by a binary search of s_st
+    // stores in bin order (consecutive lanes, consecutive addresses within a bin)
     for (uint32_t i = threadIdx.x; i < nsub; i += kHistThreads) {
-        uint32_t lo = 0, hi = R - 1;
-        while (lo < hi) {
-            const uint32_t mid = (lo + hi + 1) >> 1;
-            if (s_st[mid] <= i) lo = mid; else hi = mid - 1;
-        }
-        // empty bins share their start with the next bin: take the last bin starting <= i
-        const uint32_t g = s_cur[lo] + (i - s_st[lo]);
+        const uint32_t b = s_b[i];
+        const uint32_t g = s_cur[b] + (i - s_st[b]);
         out_k[g] = s_k[i];
         out_r[g] = s_r[i];
     }
@@ -361,6 +358,7 @@ coarse_scatter_staged_kernel(const Segment* __restrict__ segs, int nseg, int64_t
     uint32_t* s_cur = s_r + kStageRows;
     uint32_t* s_cnt = s_cur + kStageMaxBins;
     uint32_t* s_st = s_cnt + kStageMaxBins;
+    uint16_t* s_b = reinterpret_cast<uint16_t*>(s_st + kStageMaxBins);
     __shared__ uint32_t s_w[kHistThreads / 64];
     __shared__ Segment s_seg[kTileSegs];
     __shared__ int s_info[2];
@@ -382,7 +380,7 @@ coarse_scatter_staged_kernel(const Segment* __restrict__ segs, int nseg, int64_t
             row[u] = (uint32_t)rr[u];
             bin[u] = ok[u] ? (int)(chunk_of(k64[u], g) >> gshift) : -1;
         }
-        staged_scatter_batch(key, row, bin, ngroups, s_k, s_r, s_cur, s_cnt, s_st, s_w, tkeys, trows);
+        staged_scatter_batch(key, row, bin, ngroups, s_k, s_r, s_b, s_cur, s_cnt, s_st, s_w, tkeys, trows);
     }
 }
 
@@ -397,6 +395,7 @@ fine_scatter_staged_kernel(const unsigned long long* __restrict__ tkeys, const u
     uint32_t* s_cur = s_r + kStageRows;
     uint32_t* s_cnt = s_cur + kStageMaxBins;
     uint32_t* s_st = s_cnt + kStageMaxBins;
+    uint16_t* s_b = reinterpret_cast<uint16_t*>(s_st + kStageMaxBins);
     __shared__ uint32_t s_w[kHistThreads / 64];
     const int64_t nvalid = (int64_t)ctr->n_valid;
     const int64_t r0 = (int64_t)blockIdx.x * tile_rows;
@@ -434,7 +433,7 @@ fine_scatter_staged_kernel(const unsigned long long* __restrict__ tkeys, const u
             const int64_t r = base + (int64_t)u * kHistThreads + threadIdx.x;
             bin[u] = r < r1 ? (int)(chunk_of((int64_t)key[u], g) - lo) : -1;
         }
-        staged_scatter_batch(key, row, bin, R, s_k, s_r, s_cur, s_cnt, s_st, s_w, skeys, srows);
+        staged_scatter_batch(key, row, bin, R, s_k, s_r, s_b, s_cur, s_cnt, s_st, s_w, skeys, srows);
     }
 }
 
