@@ -718,7 +718,7 @@ int hj_set_build_mode(int mode) {
 }
 
 int hj_set_probe_mode(int mode) {
-    if (mode < 0 || mode > 3) return -1;
+    if (mode < 0 || mode > 4) return -1;
     const int old = get_probe_mode();
     set_probe_mode(mode);
     return old;

@@ -1579,6 +1579,304 @@ __global__ void pp_count_kernel(const uint32_t* __restrict__ cnt2, uint32_t nbin
 }
 
 // ---------------------------------------------------------------------------
+// sliced probe (direct-addressed tables of <= kSlMaxSlices x 16384 key values): the
+// lookups run out of LDS instead of as random device reads. The fused probe does one
+// random 4-byte read per in-range probe row and is bound by the memory system's random
+// request rate (~57 G/s for an Infinity-Cache-resident table); LDS serves
+// random reads at >10x that. Three launches:
+//   S1 sl_partition_kernel  per 16384-row tile: counting sort of the in-range rows by
+//                           slice (16384 consecutive key values) in LDS; writes one u32
+//                           entry per row (key offset in slice << 14 | row in tile) in
+//                           slice order into the tile's region, and the tile's slice
+//                           offsets (u16, tile-major)
+//   S2 sl_lookup_kernel     per (slice, tile range): the slice's 64 KB of refs in LDS,
+//                           then every tile's segment of that slice: ref = LDS[offset],
+//                           written beside the entry (res)
+//   S3 sl_emit_kernel       per tile: scatters its (entry, ref) into an LDS image of the
+//                           tile's refs, then the fused kernel's ordered emission (counts,
+//                           decoupled look-back, LDS-staged pair windows)
+// Pairs are identical to the fused probe's (canonical order); only where the table
+// lookups happen changes.
+// ---------------------------------------------------------------------------
+constexpr int kSlThreads = 1024;
+constexpr int kSlTileLog = 14;
+constexpr int kSlTile = 1 << kSlTileLog;                // probe rows per tile
+constexpr int kSlGroups = kSlTile / (kSlThreads * 4);  // 4 groups of 4096 rows
+constexpr int kSlWidthLogMax = 15;                      // key values per slice: 2^wlog <= 32768 (128 KB of refs)
+constexpr int kSlMaxSlices = 2047;                      // key ranges up to ~2^25 values
+constexpr int kSlUnroll = 8;
+static_assert(kSlWidthLogMax + kSlTileLog <= 32, "entry = offset << tile bits | row");
+
+template <typename K, bool HAS_VALID>
+__global__ void __launch_bounds__(kSlThreads, 8)  // 8 waves per SIMD = two workgroups per CU: <= 64 VGPRs
+sl_partition_kernel(int64_t dmin, uint64_t drange, uint32_t wlog, uint32_t nslices, const void* __restrict__ keys,
+                    const uint8_t* __restrict__ valid, int64_t voff, int64_t n, bool vec,
+                    uint32_t* __restrict__ ent, uint16_t* __restrict__ rl, uint16_t* __restrict__ toff) {
+    __shared__ __attribute__((aligned(16))) uint32_t s_ent[kSlTile];
+    __shared__ uint32_t s_hist[2 * kSlThreads];  // bins 0..nslices (<= kSlMaxSlices + 1)
+    __shared__ uint32_t s_w[kSlThreads / 64];
+    const int64_t tile = blockIdx.x;
+    const int64_t tile0 = tile * kSlTile;
+    const uint32_t nbins = nslices + 1;  // bin nslices stays empty: its prefix is the total
+    for (uint32_t b = threadIdx.x; b < 2 * kSlThreads; b += kSlThreads) s_hist[b] = 0;
+    __syncthreads();
+    // per row: entry (offset << 14 | row) and (slice << 14 | rank in slice), ~0 = no entry
+    uint32_t e[kSlGroups][4], sr[kSlGroups][4];
+#pragma unroll
+    for (int g = 0; g < kSlGroups; ++g) {
+        const int loc0 = g * (kSlThreads * 4) + threadIdx.x * 4;
+        int64_t k[4];
+        load4<K>(keys, tile0 + loc0, n, vec, k);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int64_t row = tile0 + loc0 + q;
+            const uint64_t idx = (uint64_t)k[q] - (uint64_t)dmin;
+            const bool ok = row < n && (!HAS_VALID || bit_valid(valid, voff, row)) && idx < drange;
+            const uint32_t sl = (uint32_t)(idx >> wlog);
+            e[g][q] = ((uint32_t)(idx & ((1u << wlog) - 1)) << kSlTileLog) | (uint32_t)(loc0 + q);
+            sr[g][q] = ok ? (sl << kSlTileLog) | atomicAdd(&s_hist[sl], 1u) : 0xFFFFFFFFu;
+        }
+    }
+    __syncthreads();
+    // exclusive scan of the bins, two per thread
+    const uint32_t b0 = threadIdx.x * 2;
+    const uint32_t h0 = s_hist[b0], h1 = s_hist[b0 + 1];
+    uint32_t tot;
+    const uint32_t ex = block_excl_scan<uint32_t>(h0 + h1, s_w, &tot);
+    s_hist[b0] = ex;
+    s_hist[b0 + 1] = ex + h0;
+    __syncthreads();
+    uint16_t* to = toff + tile * (int64_t)nbins;
+    for (uint32_t b = threadIdx.x; b < nbins; b += kSlThreads) to[b] = (uint16_t)s_hist[b];
+#pragma unroll
+    for (int g = 0; g < kSlGroups; ++g)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            if (sr[g][q] != 0xFFFFFFFFu)
+                s_ent[s_hist[sr[g][q] >> kSlTileLog] + (sr[g][q] & (kSlTile - 1))] = e[g][q];
+    __syncthreads();
+    // entries leave split: the key offset (u32, replaced in place by its ref in S2) and
+    // the row in the tile (u16, read by S3)
+    uint32_t* dst = ent + tile0;
+    uint16_t* dsr = rl + tile0;
+    const uint32_t n4 = tot & ~3u;
+    for (uint32_t i = threadIdx.x * 4; i < n4; i += kSlThreads * 4) {
+        const uint4 v = *reinterpret_cast<const uint4*>(s_ent + i);
+        *reinterpret_cast<uint4*>(dst + i) = make_uint4(v.x >> kSlTileLog, v.y >> kSlTileLog, v.z >> kSlTileLog,
+                                                        v.w >> kSlTileLog);
+        constexpr uint32_t m = kSlTile - 1;
+        *reinterpret_cast<uint2*>(dsr + i) = make_uint2((v.x & m) | ((v.y & m) << 16), (v.z & m) | ((v.w & m) << 16));
+    }
+    if (threadIdx.x < (tot & 3u)) {
+        const uint32_t v = s_ent[n4 + threadIdx.x];
+        dst[n4 + threadIdx.x] = v >> kSlTileLog;
+        dsr[n4 + threadIdx.x] = (uint16_t)(v & (kSlTile - 1));
+    }
+}
+
+// grid = nslices x parts; block b: slice b % nslices, tiles [part range) with
+// part = b / nslices. Each wave walks runs of 64 tiles: lane l reads tile l's segment
+// bounds, a wave scan flattens the segments over the lanes (owner lane by binary search
+// over shuffles), kSlUnroll entries per lane in flight.
+__global__ void __launch_bounds__(kSlThreads)
+sl_lookup_kernel(const uint32_t* __restrict__ dense, uint64_t drange, uint32_t wlog, uint32_t nslices, int64_t ntiles,
+                 uint32_t parts,
+                 uint32_t* __restrict__ ent, const uint16_t* __restrict__ toff, int dbg) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t s_tab[];  // 2^wlog refs
+    const uint32_t s = blockIdx.x % nslices, part = blockIdx.x / nslices;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    {
+        const uint64_t base = (uint64_t)s << wlog;
+        const uint32_t len = (uint32_t)min<uint64_t>(1u << wlog, drange - base);
+        const uint32_t len4 = len & ~3u;
+        // dense is 256-byte aligned and slices start at multiples of 64 KB
+        for (uint32_t i = threadIdx.x * 4; i < len4; i += kSlThreads * 4)
+            *reinterpret_cast<uint4*>(s_tab + i) = *reinterpret_cast<const uint4*>(dense + base + i);
+        if (threadIdx.x < (len & 3u)) s_tab[len4 + threadIdx.x] = dense[base + len4 + threadIdx.x];
+    }
+    __syncthreads();
+    const int64_t ta = ntiles * part / parts, tb = ntiles * (part + 1) / parts;
+    const int64_t nbins = nslices + 1;
+    for (int64_t tc = ta + (int64_t)wave * 64; tc < tb; tc += (kSlThreads / 64) * 64) {
+        const int64_t t = tc + lane;
+        uint32_t st = 0, len = 0;
+        if (t < tb) {
+            if (dbg & 16) {
+                st = (s * 13) & 8191;
+                len = 13;
+            } else {
+                const uint16_t* to = toff + t * nbins + s;
+                st = to[0];
+                len = (uint32_t)to[1] - st;
+            }
+        }
+        const uint32_t incl = wave_incl_scan_dpp(len);
+        const uint32_t excl = incl - len;
+        const uint32_t R = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+        for (uint32_t r0 = 0; r0 < R; r0 += 64 * kSlUnroll) {
+            int64_t pos[kSlUnroll];
+            uint32_t ev[kSlUnroll];
+#pragma unroll
+            for (int u = 0; u < kSlUnroll; ++u) {
+                const uint32_t r = r0 + u * 64 + lane;
+                uint32_t j = 0;  // owner lane: number of lanes whose inclusive end is <= r
+#pragma unroll
+                for (uint32_t step = 32; step >= 1; step >>= 1) {
+                    const uint32_t eo = __shfl(incl, (int)(j + step - 1), 64);
+                    if (eo <= r) j += step;
+                }
+                j = j > 63 ? 63 : j;
+                const uint32_t sj = __shfl(st, (int)j, 64), xj = __shfl(excl, (int)j, 64);
+                pos[u] = (tc + j) * kSlTile + sj + (r - xj);
+                ev[u] = (dbg & 4) ? (uint32_t)pos[u] * 2654435761u : r < R ? ent[pos[u]] : 0u;
+            }
+#pragma unroll
+            for (int u = 0; u < kSlUnroll; ++u)
+                if (r0 + u * 64 + lane < R) {
+                    const uint32_t v = s_tab[ev[u] & ((1u << wlog) - 1)];
+                    if (!(dbg & 8)) ent[pos[u]] = v;  // in place: the line was just read
+                    else if (v == 0x12345678u) ent[0] = v;  // keep the LDS read
+                }
+        }
+    }
+}
+
+// row count behind a ref; packed dense refs carry counts <= 15 in bits 27-30
+__device__ __forceinline__ uint32_t sl_count(const TableView& tv, uint32_t r) {
+    const uint32_t c4 = tv.off_mask == kPackedMask ? ((r >> 27) & 15u) : 0u;
+    return r == kMiss ? 0u : !(r & kDupFlag) ? 1u : c4 ? c4 : tv.dup_rows[r & tv.off_mask];
+}
+
+// S3a: pairs per tile from its refs (one coalesced pass over res), scanned into the tiles'
+// output offsets before S3b. A decoupled look-back in S3b would wait on the inclusive
+// prefixes of the other ~500 tiles in flight, one 64-flag step (a memory round trip)
+// per 64 tiles: measured as ~40% of S3's time.
+__global__ void __launch_bounds__(256)
+sl_count_kernel(TableView tv, uint32_t nslices, const uint32_t* __restrict__ res, const uint16_t* __restrict__ toff,
+                unsigned long long* __restrict__ tcnt) {
+    __shared__ unsigned long long s_w[4];
+    const int64_t tile = blockIdx.x;
+    const uint32_t cnt = toff[tile * (int64_t)(nslices + 1) + nslices];
+    const uint32_t* tr = res + tile * kSlTile;
+    unsigned long long sum = 0;
+    const uint32_t c4 = cnt & ~3u;
+    for (uint32_t i = threadIdx.x * 4; i < c4; i += 256 * 4) {
+        const uint4 r4 = *reinterpret_cast<const uint4*>(tr + i);
+        sum += sl_count(tv, r4.x) + sl_count(tv, r4.y) + sl_count(tv, r4.z) + sl_count(tv, r4.w);
+    }
+    if (threadIdx.x < (cnt & 3u)) sum += sl_count(tv, tr[c4 + threadIdx.x]);
+    sum = wave_sum<unsigned long long>(sum);
+    if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = sum;
+    __syncthreads();
+    if (threadIdx.x == 0) tcnt[tile] = s_w[0] + s_w[1] + s_w[2] + s_w[3];
+}
+
+// S3b: 512 threads per tile, two workgroups per CU (64 KB of LDS and <= 128 VGPRs each).
+// Wave w owns the tile's rows [w * 2048, (w + 1) * 2048) and walks them 64 at a time,
+// lane l on row +l: pass 1 counts the wave's pairs, pass 2 writes them. Within a wave
+// step the pairs of consecutive rows are consecutive, so the stores of one instruction
+// cover one contiguous run (no LDS staging, no barriers in the emission).
+constexpr int kSlEmitThreads = 512;
+constexpr int kSlWaveRows = kSlTile / (kSlEmitThreads / 64);  // 2048
+
+template <bool HAS_ROW_IDS, bool HAS_PROBE_IDS>
+__device__ __forceinline__ void sl_put(const TableView& tv, uint32_t r, uint32_t c, uint32_t pidx,
+                                       unsigned long long pos, uint64_t* __restrict__ out_b,
+                                       uint32_t* __restrict__ out_p, int64_t cap) {
+    if (c == 1 && !(r & kDupFlag)) {
+        if (pos < (unsigned long long)cap) {
+            out_b[pos] = HAS_ROW_IDS ? tv.row_ids[r] : (uint64_t)r;
+            out_p[pos] = pidx;
+        }
+        return;
+    }
+    const uint32_t* seg = tv.dup_rows + (r & tv.off_mask) + 1;
+    for (uint32_t t = 0; t < c; ++t) {
+        if (pos + t < (unsigned long long)cap) {
+            const uint32_t br = seg[t];
+            out_b[pos + t] = HAS_ROW_IDS ? tv.row_ids[br] : (uint64_t)br;
+            out_p[pos + t] = pidx;
+        }
+    }
+}
+
+template <bool HAS_ROW_IDS, bool HAS_PROBE_IDS>
+__global__ void __launch_bounds__(kSlEmitThreads)
+sl_emit_kernel(TableView tv, uint32_t nslices, const uint16_t* __restrict__ rl, const uint32_t* __restrict__ res,
+               const uint16_t* __restrict__ toff, const uint32_t* __restrict__ probe_ids,
+               const unsigned long long* __restrict__ tofs, uint64_t* __restrict__ out_b,
+               uint32_t* __restrict__ out_p, int64_t cap, int dbg) {
+    __shared__ __attribute__((aligned(16))) uint32_t s_ref[kSlTile];  // the tile's refs, kMiss = none
+    __shared__ unsigned long long s_w[kSlEmitThreads / 64];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int64_t tile = blockIdx.x;
+    const int64_t tile0 = tile * kSlTile;
+    const unsigned long long tbase = tofs[tile];
+    const uint32_t cnt = (dbg & 2) ? 0u : toff[tile * (int64_t)(nslices + 1) + nslices];
+    for (int i = threadIdx.x * 4; i < kSlTile; i += kSlEmitThreads * 4)
+        *reinterpret_cast<uint4*>(s_ref + i) = make_uint4(kMiss, kMiss, kMiss, kMiss);
+    __syncthreads();
+    {
+        // all of the thread's entry loads in flight before the first LDS store
+        constexpr int U = kSlTile / (kSlEmitThreads * 4);  // 8 uint4 of entries + 8 of refs
+        const uint16_t* te = rl + tile0;
+        const uint32_t* tr = res + tile0;
+        uint2 e4[U];
+        uint4 r4[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t i = (u * kSlEmitThreads + threadIdx.x) * 4;
+            if (i + 4 <= cnt) {
+                e4[u] = *reinterpret_cast<const uint2*>(te + i);
+                r4[u] = *reinterpret_cast<const uint4*>(tr + i);
+            } else {
+                uint32_t a[4] = {0, 0, 0, 0}, b[4] = {kMiss, kMiss, kMiss, kMiss};
+                for (int q = 0; q < 3; ++q)
+                    if (i + q < cnt) a[q] = te[i + q], b[q] = tr[i + q];
+                e4[u] = make_uint2(a[0] | (a[1] << 16), a[2] | (a[3] << 16));
+                r4[u] = make_uint4(b[0], b[1], b[2], b[3]);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t i = (u * kSlEmitThreads + threadIdx.x) * 4;
+            if (i < cnt) s_ref[e4[u].x & 0xFFFF] = r4[u].x;
+            if (i + 1 < cnt) s_ref[e4[u].x >> 16] = r4[u].y;
+            if (i + 2 < cnt) s_ref[e4[u].y & 0xFFFF] = r4[u].z;
+            if (i + 3 < cnt) s_ref[e4[u].y >> 16] = r4[u].w;
+        }
+    }
+    __syncthreads();
+    // pass 1: this wave's pair count
+    const int row_w = wave * kSlWaveRows;
+    uint32_t lsum = 0;  // < 32 rows x < 2^26 rows each
+#pragma unroll 8
+    for (int k = 0; k < kSlWaveRows; k += 64) lsum += sl_count(tv, s_ref[row_w + k + lane]);
+    // wave total in u64: two 32-bit halves of the per-lane sums
+    const unsigned long long wsum = (unsigned long long)wave_sum_dpp(lsum & 0xFFFFu) +
+                                    ((unsigned long long)wave_sum_dpp(lsum >> 16) << 16);
+    if (lane == 0) s_w[wave] = wsum;
+    __syncthreads();
+    unsigned long long pos = tbase;
+    for (int w = 0; w < wave; ++w) pos += s_w[w];
+    if (dbg & 1) return;
+    // pass 2: write the wave's pairs, 64 rows per step
+#pragma unroll 4
+    for (int k = 0; k < kSlWaveRows; k += 64) {
+        const int loc = row_w + k + lane;
+        const uint32_t r = s_ref[loc];
+        const uint32_t c = sl_count(tv, r);
+        const uint32_t incl = wave_incl_scan_dpp(c);  // < 2^32: 64 rows of < 2^26 rows each
+        const int64_t row = tile0 + loc;
+        if (c) {
+            const uint32_t pidx = HAS_PROBE_IDS ? probe_ids[row] : (uint32_t)row;
+            sl_put<HAS_ROW_IDS, HAS_PROBE_IDS>(tv, r, c, pidx, pos + incl - c, out_b, out_p, cap);
+        }
+        pos += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+    }
+}
+
+// ---------------------------------------------------------------------------
 // table queries (not on the hot path)
 // ---------------------------------------------------------------------------
 __global__ void table_stats_kernel(TableView tv, unsigned long long* out) {
@@ -2005,12 +2303,36 @@ ProbeWs probe_ws_layout(void* base, int64_t n) {
     return w;
 }
 
-int env_probe_mode() {  // 0 auto, 1 two-pass direct, 2 partitioned, 3 fused
+// sliced probe workspace (16384-row tiles): tcnt u64[nt + 2] | bsum (scan scratch) |
+// toff u16[nt][kSlMaxSlices + 1] | ent u32[nt * kSlTile] (key offsets, then refs) | rl u16[nt * kSlTile]
+struct SlicedWs {
+    unsigned long long* tcnt;
+    unsigned long long* bsum;
+    uint16_t* toff;
+    uint32_t* ent;
+    uint16_t* rl;
+    int64_t bytes;
+};
+SlicedWs sliced_ws_layout(void* base, int64_t n) {
+    const int64_t nt = (n + kSlTile - 1) / kSlTile;
+    SlicedWs w;
+    uintptr_t p = (uintptr_t)base + 256;
+    w.tcnt = (unsigned long long*)p; p = al256(p + 8 * (nt + 2));
+    w.bsum = (unsigned long long*)p; p = al256(p + scan_scratch_bytes(nt));
+    w.toff = (uint16_t*)p;            p = al256(p + 2 * nt * (kSlMaxSlices + 1));
+    w.ent = (uint32_t*)p;             p = al256(p + 4 * nt * kSlTile);
+    w.rl = (uint16_t*)p;              p = al256(p + 2 * nt * kSlTile);
+    w.bytes = (int64_t)(p - (uintptr_t)base) + 256;
+    return w;
+}
+
+int env_probe_mode() {  // 0 auto, 1 two-pass direct, 2 partitioned, 3 fused, 4 sliced
     const char* e = getenv("DFP_HJ_PROBE_MODE");
     if (!e) return 0;
     if (e[0] == 'd' || e[0] == 't') return 1;
     if (e[0] == 'p') return 2;
     if (e[0] == 'f') return 3;
+    if (e[0] == 's') return 4;
     return 0;
 }
 std::atomic<int> g_probe_mode{-1};
@@ -2024,10 +2346,90 @@ int probe_mode() {
 }
 }  // namespace
 
-void set_probe_mode(int mode) { g_probe_mode.store(mode < 0 || mode > 3 ? 0 : mode, std::memory_order_relaxed); }
+void set_probe_mode(int mode) { g_probe_mode.store(mode < 0 || mode > 4 ? 0 : mode, std::memory_order_relaxed); }
 int get_probe_mode() { return probe_mode(); }
 
-int64_t probe_workspace(int64_t n) { return probe_ws_layout(nullptr, n).bytes; }
+int64_t probe_workspace(int64_t n) {
+    return std::max(probe_ws_layout(nullptr, n).bytes, sliced_ws_layout(nullptr, n).bytes);
+}
+
+namespace {
+// slice width: 2^14 key values (64 KB of refs, two lookup workgroups per CU). 2^15
+// (DFP_HJ_SLICE_LOG=15) halves the (tile, slice) fragments but leaves one workgroup per
+// CU, and measured slower (C2 lookups 318 vs 276 us)
+uint32_t sl_wlog() {
+    static const uint32_t w = [] {
+        const char* e = getenv("DFP_HJ_SLICE_LOG");
+        const int v = e ? atoi(e) : 14;
+        return (uint32_t)std::min(std::max(v, 10), kSlWidthLogMax);
+    }();
+    return w;
+}
+uint32_t sl_slices(const TableView& tv) {
+    const uint32_t w = sl_wlog();
+    return tv.dense ? (uint32_t)std::min<uint64_t>((tv.drange + (1u << w) - 1) >> w, 1u << 30) : 0;
+}
+// auto choice: the sliced probe pays for its two extra passes once the table is past
+// the L2s (> 1 M key values = 4 MB of refs) and the probe side outweighs the slice loads
+bool sl_auto(const TableView& tv, int64_t n) {
+    static const int64_t min_range = [] {
+        const char* e = getenv("DFP_HJ_SLICED_MIN_RANGE");
+        return e ? atoll(e) : (int64_t)1 << 20;
+    }();
+    return (int64_t)tv.drange >= min_range && n >= (int64_t)tv.drange && n >= 4 * (int64_t)kSlTile;
+}
+
+hipError_t launch_probe_sliced(int key_bytes, const TableView& tv, const void* keys, const uint8_t* valid,
+                               int64_t voff, const uint32_t* probe_ids, int64_t n, uint64_t* out_b,
+                               uint32_t* out_p, int64_t cap, int64_t* d_total, void* workspace, hipStream_t s) {
+    const int64_t nt = (n + kSlTile - 1) / kSlTile;
+    const uint32_t nsl = sl_slices(tv), wlog = sl_wlog();
+    SlicedWs w = sliced_ws_layout((void*)(((uintptr_t)workspace + 255) & ~(uintptr_t)255), n);
+    const bool vec = (reinterpret_cast<uintptr_t>(keys) & 15) == 0;
+    hipError_t e = hipSuccess;
+#define DFP_SLP(KT, HV)                                                                                      \
+    sl_partition_kernel<KT, HV><<<(unsigned)nt, kSlThreads, 0, s>>>(tv.dmin, tv.drange, wlog, nsl, keys, valid, voff, n, \
+                                                                   vec, w.ent, w.rl, w.toff)
+    if (key_bytes == 8) {
+        if (valid) DFP_SLP(int64_t, true); else DFP_SLP(int64_t, false);
+    } else {
+        if (valid) DFP_SLP(int32_t, true); else DFP_SLP(int32_t, false);
+    }
+#undef DFP_SLP
+    // (slice, tile range) work items: about 2048 of them, so that the 512 resident
+    // workgroups (2 per CU) run several rounds and the tail stays short
+    static const uint32_t target = [] {
+        const char* ev = getenv("DFP_HJ_SLICED_ITEMS");
+        return ev ? (uint32_t)std::max(1, atoi(ev)) : 2048u;
+    }();
+    uint32_t parts = std::max<uint32_t>(1, (target + nsl - 1) / nsl);
+    parts = (uint32_t)std::min<int64_t>(parts, nt);
+    // timing ablations only (wrong pairs): emit 1 no stores, 2 no entries; lookup 4 no
+    // entry loads, 8 no ref stores, 16 no segment-bound loads
+    static const int sl_dbg = [] {
+        const char* ev = getenv("DFP_HJ_SL_DBG");
+        return ev ? atoi(ev) : 0;
+    }();
+    const size_t tab_lds = sizeof(uint32_t) << wlog;
+    e = hipFuncSetAttribute((const void*)sl_lookup_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)tab_lds);
+    if (e != hipSuccess) return e;
+    sl_lookup_kernel<<<nsl * parts, kSlThreads, tab_lds, s>>>(tv.dense, tv.drange, wlog, nsl, nt, parts, w.ent, w.toff,
+                                                              sl_dbg);
+    sl_count_kernel<<<(unsigned)nt, 256, 0, s>>>(tv, nsl, w.ent, w.toff, w.tcnt);
+    e = launch_scan<unsigned long long>(w.tcnt, nt, w.bsum, (unsigned long long*)d_total, s);
+    if (e != hipSuccess) return e;
+    const bool ri = tv.row_ids != nullptr, pi = probe_ids != nullptr;
+#define DFP_SLE(RI, PI)                                                                                   \
+    sl_emit_kernel<RI, PI><<<(unsigned)nt, kSlEmitThreads, 0, s>>>(tv, nsl, w.rl, w.ent, w.toff, probe_ids, \
+                                                                  w.tcnt, out_b, out_p, cap, sl_dbg)
+    if (ri && pi) DFP_SLE(true, true);
+    else if (ri) DFP_SLE(true, false);
+    else if (pi) DFP_SLE(false, true);
+    else DFP_SLE(false, false);
+#undef DFP_SLE
+    return hipGetLastError();
+}
+}  // namespace
 
 hipError_t launch_probe(int key_bytes, const TableView& tv, const void* keys, const uint8_t* valid, int64_t voff,
                         const uint32_t* probe_ids, int64_t n, uint64_t* out_b, uint32_t* out_p, int64_t cap,
@@ -2042,8 +2444,12 @@ hipError_t launch_probe(int key_bytes, const TableView& tv, const void* keys, co
     // line accesses stay bound by the L2 request rate, and its two extra passes cost
     // more than it saves at C2 (profiles/r01_*). DESIGN.md §5.
     const int mode = probe_mode();
+    const uint32_t nsl = sl_slices(tv);
+    if (tv.dense != nullptr && nsl >= 1 && nsl <= (uint32_t)kSlMaxSlices && (mode == 4 || (mode == 0 && sl_auto(tv, n))))
+        return launch_probe_sliced(key_bytes, tv, keys, valid, voff, probe_ids, n, out_b, out_p, cap, d_total,
+                                   workspace, s);
     const bool part = mode == 2 && tv.dense == nullptr;  // dense tables: no pieces to partition by
-    if (mode == 0 || mode == 3 || (mode == 2 && !part)) {
+    if (mode == 0 || mode == 3 || mode == 4 || (mode == 2 && !part)) {
         static const int fused_nt = [] {  // 1: keys nontemporal, 2: pair stores nontemporal
             const char* e = getenv("DFP_HJ_NT");
             return e ? atoi(e) : 0;

@@ -24,6 +24,25 @@ __device__ __forceinline__ T wave_incl_scan(T v) {
     return v;
 }
 
+// Inclusive wave64 scan of u32 in DPP moves (no LDS round trips; __shfl_up is a
+// ds_bpermute per step): row_shr 1/2/4/8 scans each 16-lane row, then row_bcast:15 and
+// row_bcast:31 carry the row totals into the rows above (GFX9 DPP, gfx950 included).
+__device__ __forceinline__ uint32_t wave_incl_scan_dpp(uint32_t v) {
+    int x = (int)v;
+    x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, false);  // row_shr:1
+    x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, false);  // row_shr:2
+    x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, false);  // row_shr:4
+    x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, false);  // row_shr:8
+    x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xa, 0xf, false);  // row_bcast:15 -> rows 1, 3
+    x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xc, 0xf, false);  // row_bcast:31 -> rows 2, 3
+    return (uint32_t)x;
+}
+
+// wave64 total of u32 (scan, then lane 63 read as a scalar)
+__device__ __forceinline__ uint32_t wave_sum_dpp(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_scan_dpp(v), 63);
+}
+
 template <typename T>
 __device__ __forceinline__ T wave_sum(T v) {
 #pragma unroll

@@ -170,12 +170,15 @@ hj_status hj_probe_async_ids(const hj_table* t, const void* keys, const uint8_t*
                              uint64_t* out_build, uint32_t* out_probe, int64_t capacity,
                              int64_t* d_total, void* workspace, void* stream);
 
-/* Probe strategy for later probes of this process: 0 auto (= fused), 1 two-pass direct
- * (lookup kernel writes a 4-byte ref per row, then ordered emission), 2 partitioned
- * (rows grouped by table piece inside each tile, pieces looked up L2-resident per XCD),
- * 3 fused (lookup + emission in one launch, tile offsets by decoupled look-back).
+/* Probe strategy for later probes of this process: 0 auto (sliced for direct-addressed
+ * tables past the L2s with a probe side at least as large as the key range, else fused),
+ * 1 two-pass direct (lookup kernel writes a 4-byte ref per row, then ordered emission),
+ * 2 partitioned (rows grouped by table piece inside each tile, pieces looked up
+ * L2-resident per XCD), 3 fused (lookup + emission in one launch, tile offsets by
+ * decoupled look-back), 4 sliced (direct-addressed tables: probe rows partitioned by
+ * 16384-value key slice, lookups out of LDS, then ordered emission; other tables fused).
  * Results are identical; returns the previous mode, -1 for a bad value. Also settable
- * with DFP_HJ_PROBE_MODE=fused|two-pass|partitioned. */
+ * with DFP_HJ_PROBE_MODE=fused|two-pass|partitioned|sliced. */
 int hj_set_probe_mode(int mode);
 
 /* Table layout for later builds of this process: 0 auto (a direct-addressed table - one

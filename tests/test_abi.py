@@ -100,12 +100,12 @@ def test_product_path_does_not_import_the_oracle():
 
 
 def test_probe_mode_switch(dfp):
-    """hj_set_probe_mode: 0 auto (fused), 1 two-pass, 2 partitioned, 3 fused; bad -> -1.
+    """hj_set_probe_mode: 0 auto, 1 two-pass, 2 partitioned, 3 fused, 4 sliced; bad -> -1.
     No device work."""
     from datafusion_parallelism_amd import _lib
 
     L = _lib.load()
-    assert L.hj_set_probe_mode(4) == -1
+    assert L.hj_set_probe_mode(5) == -1
     assert L.hj_set_probe_mode(-1) == -1
     old = L.hj_set_probe_mode(3)
     assert L.hj_set_probe_mode(1) == 3

@@ -13,9 +13,10 @@ pytestmark = pytest.mark.gpu
 I64_MIN = np.iinfo(np.int64).min
 
 
-# (probe mode, table layout): hj_set_probe_mode 3 fused / 1 two-pass / 2 partitioned;
-# hj_set_build_mode 0 auto (direct-addressed for dense key ranges) / 1 hashed buckets
-MODES = {"fused": (3, 0), "fused-hashed": (3, 1), "two-pass": (1, 0), "partitioned-hashed": (2, 1)}
+# (probe mode, table layout): hj_set_probe_mode 3 fused / 1 two-pass / 2 partitioned /
+# 4 sliced; hj_set_build_mode 0 auto (direct-addressed for dense key ranges) / 1 hashed
+MODES = {"fused": (3, 0), "fused-hashed": (3, 1), "two-pass": (1, 0), "partitioned-hashed": (2, 1),
+         "sliced": (4, 0)}
 
 
 @pytest.fixture(params=list(MODES))
@@ -341,3 +342,69 @@ def test_dense_build_levels(dfp, oracle_mod, nb, krange):
     assert st["buckets"] == 0  # direct-addressed
     ob, op = oracle_mod.inner_join(bk, pk)
     assert_same(b, p, ob, op)
+
+
+# ---- sliced probe (LDS lookups, hj_set_probe_mode 4) --------------------------------
+
+@pytest.fixture
+def sliced_mode(dfp):
+    L = dfp.load()
+    old_p = L.hj_set_probe_mode(4)
+    old_b = L.hj_set_build_mode(0)
+    yield
+    L.hj_set_probe_mode(old_p)
+    L.hj_set_build_mode(old_b)
+
+
+@pytest.mark.parametrize("nb,krange,np_,null_frac,key_type", [
+    (5_000_000, 2047 * 16384, 2_000_000, 0.0, "int64"),     # 2047 slices: the largest sliced table
+    (5_000_000, 2048 * 16384, 1_000_000, 0.0, "int64"),     # 2048 slices: falls back to fused
+    (300_000, 1_000_000, 3_000_001, 0.02, "int32"),         # nulls, ragged last tile
+    (2_000_000, 600_000, 1_500_000, 0.0, "int64"),          # duplicated keys (counts <= 15 and more)
+])
+def test_sliced_probe_parity(dfp, oracle_mod, sliced_mode, nb, krange, np_, null_frac, key_type):
+    rng = np.random.default_rng(nb + np_)
+    dt = np.int64 if key_type == "int64" else np.int32
+    bk = rng.integers(0, krange, nb).astype(dt)
+    bk[:2] = [0, krange - 1]
+    if krange < nb:  # a few keys with > 15 rows (count read from dup_rows)
+        bk[2:2 + 40] = 17
+        bk[100:100 + 300] = krange // 2
+    pk = rng.integers(-1000, krange + 1000, np_).astype(dt)
+    bv = rng.random(nb) >= null_frac if null_frac else None
+    pv = rng.random(np_) >= null_frac if null_frac else None
+    b, p, st = gpu_join(dfp, bk, pk, bv, pv, key_type=key_type)
+    assert st["buckets"] == 0  # direct-addressed
+    ob, op = oracle_mod.inner_join(bk, pk, bv, pv)
+    assert_same(b, p, ob, op)
+
+
+def test_sliced_probe_ids_unaligned(dfp, oracle_mod, sliced_mode):
+    """hj_probe_async_ids (explicit probe ids, the multi-GPU path) on a key pointer that
+    is 8- but not 16-byte aligned (scalar key loads), with explicit build ids."""
+    rng = np.random.default_rng(77)
+    nb, krange, np_ = 400_000, 2_000_000, 1_000_003
+    bk = rng.integers(0, krange, nb).astype(np.int64)
+    ids = np.cumsum(rng.integers(1, 9, nb)).astype(np.int64)
+    pk = rng.integers(0, krange, np_ + 1).astype(np.int64)
+    pids = rng.integers(0, 2**32 - 1, np_, dtype=np.uint64).astype(np.uint32)
+    dev = torch.device("cuda", 0)
+    with dfp.HashTable(1, "int64", 0) as t:
+        t.append(0, torch.from_numpy(bk).to(dev), None, ids=torch.from_numpy(ids).to(dev))
+        t.finish_all()
+        pk_d = torch.from_numpy(pk).to(dev)
+        keys_ptr = pk_d.data_ptr() + 8  # rows 1..np_
+        assert keys_ptr % 16 == 8
+        pid_d = torch.from_numpy(pids.view(np.int32)).to(dev)
+        cap = 2 * np_
+        ob = torch.empty(cap, dtype=torch.int64, device=dev)
+        op = torch.empty(cap, dtype=torch.int32, device=dev)
+        dt = torch.zeros(1, dtype=torch.int64, device=dev)
+        ws = torch.empty(t.workspace_bytes(np_), dtype=torch.uint8, device=dev)
+        t.probe_async(keys_ptr, np_, ob.data_ptr(), op.data_ptr(), cap, dt.data_ptr(), ws.data_ptr(),
+                      probe_ids_ptr=pid_d.data_ptr())
+        total = int(dt.item())
+        b = ob[:total].cpu().numpy().astype(np.uint64)
+        p = op[:total].cpu().numpy().view(np.uint32)
+    xb, xp = oracle_mod.inner_join(bk, pk[1:])
+    assert_same(b, p, ids[xb.astype(np.int64)].astype(np.uint64), pids[xp.astype(np.int64)])
