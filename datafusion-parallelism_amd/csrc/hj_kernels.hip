@@ -1604,7 +1604,7 @@ constexpr int kSlTile = 1 << kSlTileLog;                // probe rows per tile
 constexpr int kSlGroups = kSlTile / (kSlThreads * 4);  // 4 groups of 4096 rows
 constexpr int kSlWidthLogMax = 15;                      // key values per slice: 2^wlog <= 32768 (128 KB of refs)
 constexpr int kSlMaxSlices = 2047;                      // key ranges up to ~2^25 values
-constexpr int kSlUnroll = 8;
+constexpr int kSlOwnWin = 512;  // flattened segment positions per owner window (8 per lane)
 static_assert(kSlWidthLogMax + kSlTileLog <= 32, "entry = offset << tile bits | row");
 
 template <typename K, bool HAS_VALID>
@@ -1674,15 +1674,43 @@ sl_partition_kernel(int64_t dmin, uint64_t drange, uint32_t wlog, uint32_t nslic
     }
 }
 
+// S1b: the tiles' segment bounds transposed into blocks of 64 tiles, toffT[b][slice][64],
+// so that a lookup wave reads the bounds of its 64 tiles with one coalesced 128-byte load
+// (tile-major, every lane's bound is its own memory request). Tiles past ntiles read as
+// empty.
+constexpr int kSlTrChunk = 64;  // slices per block: grid = tile blocks x slice chunks
+__global__ void __launch_bounds__(256)
+sl_toff_transpose_kernel(const uint16_t* __restrict__ toff, uint32_t nbins, int64_t ntiles,
+                         uint16_t* __restrict__ toffT) {
+    __shared__ uint16_t s_t[64][kSlTrChunk + 2];
+    const uint32_t nch = (nbins + kSlTrChunk - 1) / kSlTrChunk;
+    const int64_t b = blockIdx.x / nch;
+    const uint32_t c0 = (blockIdx.x % nch) * kSlTrChunk;
+    const uint32_t cw = min<uint32_t>(kSlTrChunk, nbins - c0);
+    for (uint32_t i = threadIdx.x; i < 64 * kSlTrChunk; i += 256) {
+        const uint32_t j = i / kSlTrChunk, c = i % kSlTrChunk;
+        const int64_t t = b * 64 + j;
+        if (c < cw) s_t[j][c] = t < ntiles ? toff[t * nbins + c0 + c] : (uint16_t)0;
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < 64 * kSlTrChunk; i += 256) {
+        const uint32_t c = i / 64, j = i % 64;
+        if (c < cw) toffT[(b * nbins + c0 + c) * 64 + j] = s_t[j][c];
+    }
+}
+
 // grid = nslices x parts; block b: slice b % nslices, tiles [part range) with
 // part = b / nslices. Each wave walks runs of 64 tiles: lane l reads tile l's segment
-// bounds, a wave scan flattens the segments over the lanes (owner lane by binary search
-// over shuffles), kSlUnroll entries per lane in flight.
+// bounds, a wave scan flattens the segments over the lanes, and the owner lane of each
+// flattened position comes from a max-scan (DPP) of start markers dropped in LDS — no
+// per-position search; 8 entries per lane in flight.
 __global__ void __launch_bounds__(kSlThreads)
 sl_lookup_kernel(const uint32_t* __restrict__ dense, uint64_t drange, uint32_t wlog, uint32_t nslices, int64_t ntiles,
                  uint32_t parts,
                  uint32_t* __restrict__ ent, const uint16_t* __restrict__ toff, int dbg) {
     extern __shared__ __attribute__((aligned(16))) uint32_t s_tab[];  // 2^wlog refs
+    __shared__ uint32_t s_base[kSlThreads];
+    __shared__ __attribute__((aligned(16))) uint8_t s_own[(kSlThreads / 64) * kSlOwnWin];
     const uint32_t s = blockIdx.x % nslices, part = blockIdx.x / nslices;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     {
@@ -1690,13 +1718,21 @@ sl_lookup_kernel(const uint32_t* __restrict__ dense, uint64_t drange, uint32_t w
         const uint32_t len = (uint32_t)min<uint64_t>(1u << wlog, drange - base);
         const uint32_t len4 = len & ~3u;
         // dense is 256-byte aligned and slices start at multiples of 64 KB
+        if (!(dbg & 32)) {
         for (uint32_t i = threadIdx.x * 4; i < len4; i += kSlThreads * 4)
             *reinterpret_cast<uint4*>(s_tab + i) = *reinterpret_cast<const uint4*>(dense + base + i);
         if (threadIdx.x < (len & 3u)) s_tab[len4 + threadIdx.x] = dense[base + len4 + threadIdx.x];
+        }
     }
     __syncthreads();
-    const int64_t ta = ntiles * part / parts, tb = ntiles * (part + 1) / parts;
+    // part boundaries on 64-tile blocks (the transposed bounds' granule)
+    const int64_t nblk = (ntiles + 63) / 64;
+    const int64_t ta = nblk * part / parts * 64, tb = min<int64_t>(nblk * (part + 1) / parts * 64, ntiles);
     const int64_t nbins = nslices + 1;
+    // per wave: owner markers of one 512-position window (u8: lane + 1 at the start of
+    // each non-empty segment) and each lane's segment base (tile-relative position - excl)
+    uint8_t* own = s_own + wave * kSlOwnWin;
+    uint32_t* sbase = s_base + wave * 64;
     for (int64_t tc = ta + (int64_t)wave * 64; tc < tb; tc += (kSlThreads / 64) * 64) {
         const int64_t t = tc + lane;
         uint32_t st = 0, len = 0;
@@ -1705,38 +1741,40 @@ sl_lookup_kernel(const uint32_t* __restrict__ dense, uint64_t drange, uint32_t w
                 st = (s * 13) & 8191;
                 len = 13;
             } else {
-                const uint16_t* to = toff + t * nbins + s;
+                const uint16_t* to = toff + ((tc >> 6) * nbins + s) * 64 + lane;  // toffT
                 st = to[0];
-                len = (uint32_t)to[1] - st;
+                len = (uint32_t)to[64] - st;
             }
         }
         const uint32_t incl = wave_incl_scan_dpp(len);
         const uint32_t excl = incl - len;
         const uint32_t R = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
-        for (uint32_t r0 = 0; r0 < R; r0 += 64 * kSlUnroll) {
-            int64_t pos[kSlUnroll];
-            uint32_t ev[kSlUnroll];
+        sbase[lane] = (uint32_t)lane * kSlTile + st - excl;  // >= 0: excl <= lane * kSlTile
+        const uint32_t* tent = ent + tc * kSlTile;
+        uint32_t carry = 0;  // owner (lane + 1) of the position before the window
+        for (uint32_t w0 = 0; w0 < R; w0 += kSlOwnWin) {
+            *reinterpret_cast<uint2*>(own + lane * 8) = make_uint2(0, 0);
+            __builtin_amdgcn_wave_barrier();
+            if (len != 0 && excl >= w0 && excl < w0 + kSlOwnWin) own[excl - w0] = (uint8_t)(lane + 1);
+            __builtin_amdgcn_wave_barrier();
+            uint32_t pos[kSlOwnWin / 64], ev[kSlOwnWin / 64];
 #pragma unroll
-            for (int u = 0; u < kSlUnroll; ++u) {
-                const uint32_t r = r0 + u * 64 + lane;
-                uint32_t j = 0;  // owner lane: number of lanes whose inclusive end is <= r
-#pragma unroll
-                for (uint32_t step = 32; step >= 1; step >>= 1) {
-                    const uint32_t eo = __shfl(incl, (int)(j + step - 1), 64);
-                    if (eo <= r) j += step;
-                }
-                j = j > 63 ? 63 : j;
-                const uint32_t sj = __shfl(st, (int)j, 64), xj = __shfl(excl, (int)j, 64);
-                pos[u] = (tc + j) * kSlTile + sj + (r - xj);
-                ev[u] = (dbg & 4) ? (uint32_t)pos[u] * 2654435761u : r < R ? ent[pos[u]] : 0u;
+            for (int u = 0; u < kSlOwnWin / 64; ++u) {
+                const uint32_t r = w0 + u * 64 + lane;
+                const uint32_t o = max(wave_incl_max_dpp(own[u * 64 + lane]), carry);
+                carry = (uint32_t)__builtin_amdgcn_readlane((int)o, 63);
+                pos[u] = sbase[(o - 1) & 63] + r;
+                ev[u] = (dbg & 4) ? pos[u] * 2654435761u : (r < R ? tent[pos[u]] : 0u);
             }
 #pragma unroll
-            for (int u = 0; u < kSlUnroll; ++u)
-                if (r0 + u * 64 + lane < R) {
+            for (int u = 0; u < kSlOwnWin / 64; ++u) {
+                if (w0 + u * 64 + lane < R) {
                     const uint32_t v = s_tab[ev[u] & ((1u << wlog) - 1)];
-                    if (!(dbg & 8)) ent[pos[u]] = v;  // in place: the line was just read
+                    if (!(dbg & 8)) const_cast<uint32_t*>(tent)[pos[u]] = v;  // in place: the line was just read
                     else if (v == 0x12345678u) ent[0] = v;  // keep the LDS read
                 }
+            }
+            __builtin_amdgcn_wave_barrier();
         }
     }
 }
@@ -1801,42 +1839,43 @@ __device__ __forceinline__ void sl_put(const TableView& tv, uint32_t r, uint32_t
 }
 
 template <bool HAS_ROW_IDS, bool HAS_PROBE_IDS>
-__global__ void __launch_bounds__(kSlEmitThreads)
+__global__ void __launch_bounds__(kSlEmitThreads, 4)  // two workgroups per CU: <= 128 VGPRs
 sl_emit_kernel(TableView tv, uint32_t nslices, const uint16_t* __restrict__ rl, const uint32_t* __restrict__ res,
                const uint16_t* __restrict__ toff, const uint32_t* __restrict__ probe_ids,
-               const unsigned long long* __restrict__ tofs, uint64_t* __restrict__ out_b,
+               const unsigned long long* __restrict__ tofs, int64_t ntiles, uint64_t* __restrict__ out_b,
                uint32_t* __restrict__ out_p, int64_t cap, int dbg) {
     __shared__ __attribute__((aligned(16))) uint32_t s_ref[kSlTile];  // the tile's refs, kMiss = none
     __shared__ unsigned long long s_w[kSlEmitThreads / 64];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int64_t tile = blockIdx.x;
-    const int64_t tile0 = tile * kSlTile;
-    const unsigned long long tbase = tofs[tile];
-    const uint32_t cnt = (dbg & 2) ? 0u : toff[tile * (int64_t)(nslices + 1) + nslices];
-    for (int i = threadIdx.x * 4; i < kSlTile; i += kSlEmitThreads * 4)
-        *reinterpret_cast<uint4*>(s_ref + i) = make_uint4(kMiss, kMiss, kMiss, kMiss);
-    __syncthreads();
-    {
-        // all of the thread's entry loads in flight before the first LDS store
-        constexpr int U = kSlTile / (kSlEmitThreads * 4);  // 8 uint4 of entries + 8 of refs
-        const uint16_t* te = rl + tile0;
-        const uint32_t* tr = res + tile0;
-        uint2 e4[U];
-        uint4 r4[U];
+    constexpr int U = kSlTile / (kSlEmitThreads * 4);  // 8 x (4 rows + 4 refs) per thread
+    uint2 e4[U];
+    uint4 r4[U];
+    uint32_t cnt = 0;
+    unsigned long long tbase = 0;
+    // Persistent: workgroup b takes tiles b, b + grid, ...; the next tile's entries are
+    // loaded while this tile's pairs are counted and written. All loads of a tile are
+    // issued at once, after its entry count.
+    auto fetch = [&](int64_t t) {
+        cnt = (dbg & 2) ? 0u : toff[t * (int64_t)(nslices + 1) + nslices];
+        tbase = tofs[t];
+        const uint16_t* te = rl + t * kSlTile;
+        const uint32_t* tr = res + t * kSlTile;
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const uint32_t i = (u * kSlEmitThreads + threadIdx.x) * 4;
-            if (i + 4 <= cnt) {
+            if (i < cnt) {  // whole uint4s: the region holds kSlTile entries, lanes past cnt are ignored
                 e4[u] = *reinterpret_cast<const uint2*>(te + i);
                 r4[u] = *reinterpret_cast<const uint4*>(tr + i);
-            } else {
-                uint32_t a[4] = {0, 0, 0, 0}, b[4] = {kMiss, kMiss, kMiss, kMiss};
-                for (int q = 0; q < 3; ++q)
-                    if (i + q < cnt) a[q] = te[i + q], b[q] = tr[i + q];
-                e4[u] = make_uint2(a[0] | (a[1] << 16), a[2] | (a[3] << 16));
-                r4[u] = make_uint4(b[0], b[1], b[2], b[3]);
             }
         }
+    };
+    int64_t tile = blockIdx.x;
+    if (tile < ntiles) fetch(tile);
+    for (; tile < ntiles; tile += gridDim.x) {
+        const int64_t tile0 = tile * kSlTile;
+        for (int i = threadIdx.x * 4; i < kSlTile; i += kSlEmitThreads * 4)
+            *reinterpret_cast<uint4*>(s_ref + i) = make_uint4(kMiss, kMiss, kMiss, kMiss);
+        __syncthreads();
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const uint32_t i = (u * kSlEmitThreads + threadIdx.x) * 4;
@@ -1845,34 +1884,38 @@ sl_emit_kernel(TableView tv, uint32_t nslices, const uint16_t* __restrict__ rl, 
             if (i + 2 < cnt) s_ref[e4[u].y & 0xFFFF] = r4[u].z;
             if (i + 3 < cnt) s_ref[e4[u].y >> 16] = r4[u].w;
         }
-    }
-    __syncthreads();
-    // pass 1: this wave's pair count
-    const int row_w = wave * kSlWaveRows;
-    uint32_t lsum = 0;  // < 32 rows x < 2^26 rows each
+        const unsigned long long base = tbase;
+        __syncthreads();
+        if (tile + (int64_t)gridDim.x < ntiles) fetch(tile + gridDim.x);
+        // pass 1: this wave's pair count
+        const int row_w = wave * kSlWaveRows;
+        uint32_t lsum = 0;  // < 32 rows x < 2^26 rows each
 #pragma unroll 8
-    for (int k = 0; k < kSlWaveRows; k += 64) lsum += sl_count(tv, s_ref[row_w + k + lane]);
-    // wave total in u64: two 32-bit halves of the per-lane sums
-    const unsigned long long wsum = (unsigned long long)wave_sum_dpp(lsum & 0xFFFFu) +
-                                    ((unsigned long long)wave_sum_dpp(lsum >> 16) << 16);
-    if (lane == 0) s_w[wave] = wsum;
-    __syncthreads();
-    unsigned long long pos = tbase;
-    for (int w = 0; w < wave; ++w) pos += s_w[w];
-    if (dbg & 1) return;
-    // pass 2: write the wave's pairs, 64 rows per step
+        for (int k = 0; k < kSlWaveRows; k += 64) lsum += sl_count(tv, s_ref[row_w + k + lane]);
+        // wave total in u64: two 32-bit halves of the per-lane sums
+        const unsigned long long wsum = (unsigned long long)wave_sum_dpp(lsum & 0xFFFFu) +
+                                        ((unsigned long long)wave_sum_dpp(lsum >> 16) << 16);
+        if (lane == 0) s_w[wave] = wsum;
+        __syncthreads();
+        unsigned long long pos = base;
+        for (int w = 0; w < wave; ++w) pos += s_w[w];
+        if (!(dbg & 1)) {
+            // pass 2: write the wave's pairs, 64 rows per step
 #pragma unroll 4
-    for (int k = 0; k < kSlWaveRows; k += 64) {
-        const int loc = row_w + k + lane;
-        const uint32_t r = s_ref[loc];
-        const uint32_t c = sl_count(tv, r);
-        const uint32_t incl = wave_incl_scan_dpp(c);  // < 2^32: 64 rows of < 2^26 rows each
-        const int64_t row = tile0 + loc;
-        if (c) {
-            const uint32_t pidx = HAS_PROBE_IDS ? probe_ids[row] : (uint32_t)row;
-            sl_put<HAS_ROW_IDS, HAS_PROBE_IDS>(tv, r, c, pidx, pos + incl - c, out_b, out_p, cap);
+            for (int k = 0; k < kSlWaveRows; k += 64) {
+                const int loc = row_w + k + lane;
+                const uint32_t r = s_ref[loc];
+                const uint32_t c = sl_count(tv, r);
+                const uint32_t incl = wave_incl_scan_dpp(c);  // < 2^32: 64 rows of < 2^26 rows each
+                const int64_t row = tile0 + loc;
+                if (c) {
+                    const uint32_t pidx = HAS_PROBE_IDS ? probe_ids[row] : (uint32_t)row;
+                    sl_put<HAS_ROW_IDS, HAS_PROBE_IDS>(tv, r, c, pidx, pos + incl - c, out_b, out_p, cap);
+                }
+                pos += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+            }
         }
-        pos += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+        __syncthreads();  // s_ref and s_w are rewritten for the next tile
     }
 }
 
@@ -2309,6 +2352,7 @@ struct SlicedWs {
     unsigned long long* tcnt;
     unsigned long long* bsum;
     uint16_t* toff;
+    uint16_t* toffT;
     uint32_t* ent;
     uint16_t* rl;
     int64_t bytes;
@@ -2320,6 +2364,7 @@ SlicedWs sliced_ws_layout(void* base, int64_t n) {
     w.tcnt = (unsigned long long*)p; p = al256(p + 8 * (nt + 2));
     w.bsum = (unsigned long long*)p; p = al256(p + scan_scratch_bytes(nt));
     w.toff = (uint16_t*)p;            p = al256(p + 2 * nt * (kSlMaxSlices + 1));
+    w.toffT = (uint16_t*)p;           p = al256(p + 2 * ((nt + 63) & ~(int64_t)63) * (kSlMaxSlices + 1));
     w.ent = (uint32_t*)p;             p = al256(p + 4 * nt * kSlTile);
     w.rl = (uint16_t*)p;              p = al256(p + 2 * nt * kSlTile);
     w.bytes = (int64_t)(p - (uintptr_t)base) + 256;
@@ -2365,6 +2410,26 @@ uint32_t sl_wlog() {
     }();
     return w;
 }
+int sl_num_cus() {
+    static const int c = [] {
+        int d = 0, v = 0;
+        if (hipGetDevice(&d) != hipSuccess || hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, d) !=
+                                                  hipSuccess || v < 1)
+            v = 256;
+        return v;
+    }();
+    return c;
+}
+// persistent emission grid: workgroups per CU (DFP_HJ_SL_EMIT_WGS; a large value gives
+// one workgroup per tile)
+int sl_env_int(const char* name, int dflt) {
+    const char* e = getenv(name);
+    return e ? std::max(1, atoi(e)) : dflt;
+}
+int sl_emit_wgs_per_cu() {
+    static const int v = sl_env_int("DFP_HJ_SL_EMIT_WGS", 2);
+    return v;
+}
 uint32_t sl_slices(const TableView& tv) {
     const uint32_t w = sl_wlog();
     return tv.dense ? (uint32_t)std::min<uint64_t>((tv.drange + (1u << w) - 1) >> w, 1u << 30) : 0;
@@ -2403,7 +2468,7 @@ hipError_t launch_probe_sliced(int key_bytes, const TableView& tv, const void* k
         return ev ? (uint32_t)std::max(1, atoi(ev)) : 2048u;
     }();
     uint32_t parts = std::max<uint32_t>(1, (target + nsl - 1) / nsl);
-    parts = (uint32_t)std::min<int64_t>(parts, nt);
+    parts = (uint32_t)std::min<int64_t>(parts, (nt + 63) / 64);
     // timing ablations only (wrong pairs): emit 1 no stores, 2 no entries; lookup 4 no
     // entry loads, 8 no ref stores, 16 no segment-bound loads
     static const int sl_dbg = [] {
@@ -2413,15 +2478,18 @@ hipError_t launch_probe_sliced(int key_bytes, const TableView& tv, const void* k
     const size_t tab_lds = sizeof(uint32_t) << wlog;
     e = hipFuncSetAttribute((const void*)sl_lookup_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)tab_lds);
     if (e != hipSuccess) return e;
-    sl_lookup_kernel<<<nsl * parts, kSlThreads, tab_lds, s>>>(tv.dense, tv.drange, wlog, nsl, nt, parts, w.ent, w.toff,
+    sl_toff_transpose_kernel<<<(unsigned)((nt + 63) / 64 * ((nsl + kSlTrChunk) / kSlTrChunk)), 256, 0, s>>>(
+        w.toff, nsl + 1, nt, w.toffT);
+    sl_lookup_kernel<<<nsl * parts, kSlThreads, tab_lds, s>>>(tv.dense, tv.drange, wlog, nsl, nt, parts, w.ent, w.toffT,
                                                               sl_dbg);
     sl_count_kernel<<<(unsigned)nt, 256, 0, s>>>(tv, nsl, w.ent, w.toff, w.tcnt);
     e = launch_scan<unsigned long long>(w.tcnt, nt, w.bsum, (unsigned long long*)d_total, s);
     if (e != hipSuccess) return e;
     const bool ri = tv.row_ids != nullptr, pi = probe_ids != nullptr;
+    const unsigned egrid = (unsigned)std::min<int64_t>(nt, (int64_t)sl_emit_wgs_per_cu() * sl_num_cus());
 #define DFP_SLE(RI, PI)                                                                                   \
-    sl_emit_kernel<RI, PI><<<(unsigned)nt, kSlEmitThreads, 0, s>>>(tv, nsl, w.rl, w.ent, w.toff, probe_ids, \
-                                                                  w.tcnt, out_b, out_p, cap, sl_dbg)
+    sl_emit_kernel<RI, PI><<<egrid, kSlEmitThreads, 0, s>>>(tv, nsl, w.rl, w.ent, w.toff, probe_ids, w.tcnt, nt, \
+                                                           out_b, out_p, cap, sl_dbg)
     if (ri && pi) DFP_SLE(true, true);
     else if (ri) DFP_SLE(true, false);
     else if (pi) DFP_SLE(false, true);

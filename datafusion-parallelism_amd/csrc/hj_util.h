@@ -38,6 +38,18 @@ __device__ __forceinline__ uint32_t wave_incl_scan_dpp(uint32_t v) {
     return (uint32_t)x;
 }
 
+// Inclusive wave64 max-scan of u32, same DPP pattern (0 is the identity)
+__device__ __forceinline__ uint32_t wave_incl_max_dpp(uint32_t v) {
+    uint32_t x = v;
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false));
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false));
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false));
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false));
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false));
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false));
+    return x;
+}
+
 // wave64 total of u32 (scan, then lane 63 read as a scalar)
 __device__ __forceinline__ uint32_t wave_sum_dpp(uint32_t v) {
     return (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_scan_dpp(v), 63);
