@@ -266,13 +266,14 @@ def main():
         "frac": round(achieved / HBM_PEAK_GBS, 4),
         "traffic": (traffic or {}).get("hbm_bytes_per_launch"),
         "traffic_lower": ((traffic or {}).get("probe_phase") or {}).get("hbm_bytes_lower"),
-        "kernel": "probe_fused_kernel (the whole hj_probe_async: lookup + ordered pair emission)",
+        "kernel": "the whole hj_probe_async (sliced probe: sl_partition + sl_toff_transpose + sl_lookup + "
+                  "sl_count + scan + sl_emit, DESIGN.md §4)",
         "alg_bytes_per_launch": alg_bytes,
         "alg_bytes_formula": "8*P + 16*B + 12*M (SURVEY.md §8d)",
-        # the lookup is one random 64-B bucket read per probe row; DESIGN.md §4 prices it
-        # against the measured random-line ceiling (profiles/r01_ubench_gather.txt)
-        "random_lines_per_s": round(P / (probe_ms / 1e3) / 1e9, 2),
-        "random_lines_unit": "G/s",
+        # the probe rows' lookups run out of LDS (no random device reads per row); the HBM
+        # streams of the sliced pipeline (keys, entries, refs, rows, pairs) are in DESIGN.md §4
+        "probe_rows_per_s": round(P / (probe_ms / 1e3) / 1e9, 2),
+        "probe_rows_unit": "G/s",
     }
 
     if rank == 0:

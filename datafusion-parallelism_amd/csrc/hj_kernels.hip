@@ -1818,27 +1818,6 @@ constexpr int kSlEmitThreads = 512;
 constexpr int kSlWaveRows = kSlTile / (kSlEmitThreads / 64);  // 2048
 
 template <bool HAS_ROW_IDS, bool HAS_PROBE_IDS>
-__device__ __forceinline__ void sl_put(const TableView& tv, uint32_t r, uint32_t c, uint32_t pidx,
-                                       unsigned long long pos, uint64_t* __restrict__ out_b,
-                                       uint32_t* __restrict__ out_p, int64_t cap) {
-    if (c == 1 && !(r & kDupFlag)) {
-        if (pos < (unsigned long long)cap) {
-            out_b[pos] = HAS_ROW_IDS ? tv.row_ids[r] : (uint64_t)r;
-            out_p[pos] = pidx;
-        }
-        return;
-    }
-    const uint32_t* seg = tv.dup_rows + (r & tv.off_mask) + 1;
-    for (uint32_t t = 0; t < c; ++t) {
-        if (pos + t < (unsigned long long)cap) {
-            const uint32_t br = seg[t];
-            out_b[pos + t] = HAS_ROW_IDS ? tv.row_ids[br] : (uint64_t)br;
-            out_p[pos + t] = pidx;
-        }
-    }
-}
-
-template <bool HAS_ROW_IDS, bool HAS_PROBE_IDS>
 __global__ void __launch_bounds__(kSlEmitThreads, 4)  // two workgroups per CU: <= 128 VGPRs
 sl_emit_kernel(TableView tv, uint32_t nslices, const uint16_t* __restrict__ rl, const uint32_t* __restrict__ res,
                const uint16_t* __restrict__ toff, const uint32_t* __restrict__ probe_ids,
@@ -1846,6 +1825,7 @@ sl_emit_kernel(TableView tv, uint32_t nslices, const uint16_t* __restrict__ rl, 
                uint32_t* __restrict__ out_p, int64_t cap, int dbg) {
     __shared__ __attribute__((aligned(16))) uint32_t s_ref[kSlTile];  // the tile's refs, kMiss = none
     __shared__ unsigned long long s_w[kSlEmitThreads / 64];
+    __shared__ uint32_t s_own[kSlEmitThreads / 64][64];  // per wave: owner markers of one output window
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     constexpr int U = kSlTile / (kSlEmitThreads * 4);  // 8 x (4 rows + 4 refs) per thread
     uint2 e4[U];
@@ -1900,19 +1880,53 @@ sl_emit_kernel(TableView tv, uint32_t nslices, const uint16_t* __restrict__ rl, 
         unsigned long long pos = base;
         for (int w = 0; w < wave; ++w) pos += s_w[w];
         if (!(dbg & 1)) {
-            // pass 2: write the wave's pairs, 64 rows per step
-#pragma unroll 4
+            // pass 2: write the wave's pairs, 64 rows per step. Steps whose rows all have
+            // at most one pair store them directly; a step with a duplicated key expands
+            // its pairs over the lanes, 64 output positions at a time (owner row by a
+            // max-scan of start markers), so every store instruction writes one
+            // contiguous run and the duplicate segments are read in parallel.
+            uint32_t* own = s_own[wave];
+#pragma unroll 2
             for (int k = 0; k < kSlWaveRows; k += 64) {
                 const int loc = row_w + k + lane;
                 const uint32_t r = s_ref[loc];
                 const uint32_t c = sl_count(tv, r);
                 const uint32_t incl = wave_incl_scan_dpp(c);  // < 2^32: 64 rows of < 2^26 rows each
+                const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
                 const int64_t row = tile0 + loc;
-                if (c) {
-                    const uint32_t pidx = HAS_PROBE_IDS ? probe_ids[row] : (uint32_t)row;
-                    sl_put<HAS_ROW_IDS, HAS_PROBE_IDS>(tv, r, c, pidx, pos + incl - c, out_b, out_p, cap);
+                if (__ballot(c > 1) == 0) {
+                    if (c) {
+                        const unsigned long long o = pos + incl - 1;
+                        if (o < (unsigned long long)cap) {
+                            out_b[o] = HAS_ROW_IDS ? tv.row_ids[r] : (uint64_t)r;
+                            out_p[o] = HAS_PROBE_IDS ? probe_ids[row] : (uint32_t)row;
+                        }
+                    }
+                } else {
+                    const uint32_t excl = incl - c;
+                    uint32_t carry = 0;
+                    for (uint32_t w0 = 0; w0 < total; w0 += 64) {
+                        own[lane] = 0;
+                        __builtin_amdgcn_wave_barrier();
+                        if (c && excl >= w0 && excl < w0 + 64) own[excl - w0] = (uint32_t)lane + 1;
+                        __builtin_amdgcn_wave_barrier();
+                        const uint32_t ol = max(wave_incl_max_dpp(own[lane]), carry);
+                        carry = (uint32_t)__builtin_amdgcn_readlane((int)ol, 63);
+                        const int j = (int)((ol - 1) & 63);
+                        const uint32_t xj = (uint32_t)__shfl((int)excl, j, 64);
+                        const uint32_t rj = (uint32_t)__shfl((int)r, j, 64);
+                        const uint32_t p = w0 + lane;
+                        const unsigned long long o = pos + p;
+                        if (p < total && o < (unsigned long long)cap) {
+                            const uint32_t br = (rj & kDupFlag) ? tv.dup_rows[(rj & tv.off_mask) + 1 + (p - xj)] : rj;
+                            const int64_t rowj = tile0 + row_w + k + j;
+                            out_b[o] = HAS_ROW_IDS ? tv.row_ids[br] : (uint64_t)br;
+                            out_p[o] = HAS_PROBE_IDS ? probe_ids[rowj] : (uint32_t)rowj;
+                        }
+                        __builtin_amdgcn_wave_barrier();
+                    }
                 }
-                pos += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+                pos += total;
             }
         }
         __syncthreads();  // s_ref and s_w are rewritten for the next tile

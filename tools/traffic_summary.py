@@ -21,7 +21,8 @@ import sys
 
 PROBE_KERNELS = ("probe_fused_kernel", "probe_lookup_kernel", "probe_emit_kernel", "scan_reduce_kernel<unsigned long long>",
                  "scan_down_kernel<unsigned long long>", "pp_partition_kernel", "pp_lookup_kernel",
-                 "pp_count_kernel")
+                 "pp_count_kernel", "sl_partition_kernel", "sl_toff_transpose_kernel", "sl_lookup_kernel",
+                 "sl_count_kernel", "sl_emit_kernel")
 BUILD_KERNELS = ("key_minmax_kernel", "coarse_hist_kernel", "coarse_scatter", "fine_hist_kernel", "fine_scatter",
                  "chunk_starts_kernel", "scan_reduce_kernel<unsigned int>", "scan_down_kernel<unsigned int>",
                  "chunk_build_kernel", "dup_sort_big_kernel")
@@ -69,7 +70,8 @@ def main():
         "probe_phase": probe,
         "build_phase": build,
         "kernels": kernels,
-        "note": "probe phase = the kernels of one hj_probe_async (default: probe_fused_kernel alone). "
+        "note": "probe phase = the kernels of one hj_probe_async (C2 default: the sliced probe's sl_* kernels "
+                "and the u64 scan). "
                 "Upper = 2 x FETCH_SIZE + WRITE_SIZE (guide's gfx950 correction applied to all reads); "
                 "lower = FETCH_SIZE + WRITE_SIZE (random 64-B bucket reads counted at 64 B each).",
     }
