@@ -101,8 +101,9 @@ class SingleGpuJoin:
     def step(self, record=True):
         t = HashTable(1, "int64", self.dev.index or 0)
         t.append(0, self.bk)
-        t.finish(0)  # device build; returns when the table is complete
+        t.finish(0)  # device build (runs on asynchronously for a direct-addressed table)
         s = torch.cuda.current_stream(self.dev)
+        t.stream_wait(s.cuda_stream)  # probe_ms times the probe alone
         self.ev[0].record(s)
         t.probe_async(self.pk.data_ptr(), self.pk.numel(), self.ob.data_ptr(), self.op.data_ptr(), self.cap,
                       self.d_total.data_ptr(), self.ws.data_ptr(), s.cuda_stream)

@@ -20,7 +20,7 @@ LIB_PATH = os.path.join(HERE, "lib", "libdfp_hj.so")
 
 HJ_OK, HJ_ERR_INVALID, HJ_ERR_OOM, HJ_ERR_HIP, HJ_ERR_RCCL, HJ_ERR_CAPACITY, HJ_ERR_NO_DEVICE = range(7)
 HJ_INT32, HJ_INT64 = 0, 1
-HJ_INPUT_DEVICE, HJ_BORROW, HJ_OUTPUT_HOST, HJ_IDS_U31 = 1, 2, 4, 8
+HJ_INPUT_DEVICE, HJ_BORROW, HJ_OUTPUT_HOST, HJ_IDS_U31, HJ_BORROW_KEEP = 1, 2, 4, 8, 16
 
 STATUS_NAMES = {
     HJ_OK: "HJ_OK", HJ_ERR_INVALID: "HJ_ERR_INVALID", HJ_ERR_OOM: "HJ_ERR_OOM", HJ_ERR_HIP: "HJ_ERR_HIP",

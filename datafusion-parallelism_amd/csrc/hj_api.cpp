@@ -188,15 +188,21 @@ constexpr double kDefaultLoadFactor = 0.35;
 // build rows, else hashed buckets), 1 hashed always. DFP_HJ_DENSE=0 selects 1.
 constexpr uint64_t kDenseFactor = 8;
 std::atomic<int> g_build_mode{-1};
-int build_mode() {
+int build_mode_raw() {
     int m = g_build_mode.load(std::memory_order_relaxed);
     if (m < 0) {
         const char* e = getenv("DFP_HJ_DENSE");
         m = (e && e[0] == '0') ? 1 : 0;
+        const char* f = getenv("DFP_HJ_FRAG_BUILD");
+        if (m == 0 && f && f[0] == '0') m = 2;
         g_build_mode.store(m, std::memory_order_relaxed);
     }
     return m;
 }
+// 0 and 2 both choose the direct-addressed layout for dense key ranges; 2 keeps the
+// histogram + scan + staged-scatter partition for it (the tile-local one is the default)
+int build_mode() { return build_mode_raw() == 1 ? 1 : 0; }
+bool frag_build_mode() { return build_mode_raw() == 0; }
 double load_factor() {
     const char* e = getenv("DFP_HJ_LOAD_FACTOR");
     double lf = e ? atof(e) : kDefaultLoadFactor;
@@ -228,6 +234,7 @@ struct hj_table {
     std::vector<char> finished;
     int arrived = 0;
     bool built = false;
+    bool sync_finish = false;  // some input was borrowed without HJ_BORROW_KEEP
     hj_status build_st = HJ_OK;
     std::string build_err;
     bool has_ids = false, has_no_ids = false;
@@ -347,6 +354,11 @@ hj_status build_attempt(hj_table* t, const std::vector<Segment>& segs, double lf
     t->packed = g.packed != 0;
     t->nb = g.nb;
     const uint64_t nchunks = g.nchunks;
+    // dense builds that fit the tile-local partition skip the histogram/scan/scatter path
+    std::vector<int64_t> seg_n(segs.size());
+    for (size_t i = 0; i < segs.size(); ++i) seg_n[i] = segs[i].n;
+    const int64_t ftiles = frag_build_tiles(seg_n.data(), (int)segs.size());
+    const bool frag = dense && total > 0 && frag_build_mode() && frag_build_ok(g, ftiles);
     hipDeviceProp_t* prop0 = device_props(t->device);
     const int64_t ntiles = build_tiles(total, prop0 ? prop0->multiProcessorCount : 256);
     const int64_t tile_rows = build_tile_rows(total, ntiles);
@@ -373,6 +385,41 @@ hj_status build_attempt(hj_table* t, const std::vector<Segment>& segs, double lf
         if ((st = dev_alloc(t, t->allocs, &p, sizeof(uint64_t) * (size_t)std::max<int64_t>(total, 1))) != HJ_OK)
             return st;
         t->row_ids = (uint64_t*)p;
+    }
+    if (frag) {
+        void* fscr;
+        uint32_t* d_tb;
+        uint64_t* ids32 = nullptr;
+        BigSeg* fbig;
+        if ((st = dev_alloc(t, t->scratch, &fscr, (size_t)frag_build_scratch_bytes(g, ftiles))) != HJ_OK) return st;
+        if ((st = dev_alloc(t, t->scratch, &p, sizeof(uint32_t) * (size_t)ftiles)) != HJ_OK) return st;
+        d_tb = (uint32_t*)p;
+        if ((st = dev_alloc(t, t->scratch, &p, sizeof(BigSeg) * (size_t)(total / (kSmallSeg + 1) + 2))) != HJ_OK)
+            return st;
+        fbig = (BigSeg*)p;
+        // first row of every tile (a tile never spans two appended batches)
+        std::vector<uint32_t> tb((size_t)ftiles);
+        int64_t k = 0;
+        for (const Segment& sg : segs)
+            for (int64_t j = 0; j * kFragTileRows < sg.n; ++j)
+                tb[(size_t)k++] = (uint32_t)(sg.row_base + j * kFragTileRows);
+        HIP_TRY(hipMemcpyAsync(d_tb, tb.data(), sizeof(uint32_t) * tb.size(), hipMemcpyHostToDevice, s));
+        if (t->has_ids) {  // explicit ids in row order: the table's row_ids, or scratch when held in place of rows
+            uint64_t* dst = t->row_ids;
+            if (ids_as_rows) {
+                if ((st = dev_alloc(t, t->scratch, &p, sizeof(uint64_t) * (size_t)total)) != HJ_OK) return st;
+                dst = ids32 = (uint64_t*)p;
+            }
+            for (const Segment& sg : segs)
+                HIP_TRY(hipMemcpyAsync(dst + sg.row_base, sg.ids, sizeof(uint64_t) * (size_t)sg.n, hipMemcpyDefault, s));
+        }
+        hipDeviceProp_t* prop = device_props(t->device);
+        const int cus = prop ? prop->multiProcessorCount : 256;
+        HIP_TRY(launch_build_frag(t->key_bytes, segs.data(), (int)segs.size(), g, ftiles, fscr, d_tb, ids32, t->dense,
+                                  t->dup_rows, fbig, ctr, d_segs, total, ids_as_rows, cus, s));
+        // a direct-addressed build cannot overflow (no retry): nothing to read back, the
+        // build stays asynchronous; consumers wait on its completion event
+        return HJ_OK;
     }
     uint32_t *hist, *hist1, *srows, *trows;
     unsigned long long *skeys, *tkeys;
@@ -409,6 +456,7 @@ hj_status build_attempt(hj_table* t, const std::vector<Segment>& segs, double lf
     HIP_TRY(launch_build(t->key_bytes, d_segs, (int)segs.size(), total, g, hist, hist1, chunk_starts, ntiles, tile_rows,
                          scan, tkeys, trows, skeys, srows, t->row_ids, ids_as_rows, t->tbl, t->dense, t->dup_rows, big,
                          ctr, cus, s));
+    if (dense) return HJ_OK;  // cannot overflow: asynchronous, as above
     BuildCounters hc;
     HIP_TRY(hipMemcpyAsync(&hc, ctr, sizeof(hc), hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
@@ -457,11 +505,28 @@ hj_status run_build(hj_table* t) {
         lf *= 0.5;
         HIP_TRY(hipEventRecord(t->res.ev0, s));
     }
+    // ev1 marks the table complete: probes and queries on other streams wait on it
+    // (hipStreamWaitEvent, no host synchronisation); build_ns is read when first asked
     HIP_TRY(hipEventRecord(t->res.ev1, s));
-    HIP_TRY(hipEventSynchronize(t->res.ev1));
-    float ms = 0;
-    HIP_TRY(hipEventElapsedTime(&ms, t->res.ev0, t->res.ev1));
-    t->build_ns = (int64_t)(ms * 1e6);
+    t->build_ns = -1;
+    return HJ_OK;
+}
+
+// device build time, waiting for the build if it is still running
+int64_t build_time_ns(hj_table* t) {
+    if (t->build_ns < 0) {
+        float ms = 0;
+        if (hipEventSynchronize(t->res.ev1) != hipSuccess ||
+            hipEventElapsedTime(&ms, t->res.ev0, t->res.ev1) != hipSuccess)
+            return -1;
+        t->build_ns = (int64_t)(ms * 1e6);
+    }
+    return t->build_ns;
+}
+
+// make stream s wait for the table's build
+hj_status wait_built(const hj_table* t, hipStream_t s) {
+    if (s != t->res.stream) HIP_TRY(hipStreamWaitEvent(s, t->res.ev1, 0));
     return HJ_OK;
 }
 
@@ -524,6 +589,7 @@ hj_status probe_impl(const hj_table* t, const void* keys, const uint8_t* valid, 
     if (cap < 0) return fail(HJ_ERR_INVALID, "negative capacity");
     if (reinterpret_cast<uintptr_t>(ws) & 7) return fail(HJ_ERR_INVALID, "workspace must be 8-byte aligned");
     HIP_TRY(hipMemsetAsync((char*)ws + 8, 0, 8, s));  // error word
+    if (wait_built(t, s) != HJ_OK) return HJ_ERR_HIP;
     HIP_TRY(launch_probe(t->key_bytes, view_of(t), keys, valid, voff, probe_ids, n, out_b, out_p, cap, d_total, ws,
                          s));
     return HJ_OK;
@@ -603,6 +669,10 @@ hj_status hj_build_append(hj_table* t, int partition, const void* keys, const ui
     if (dev_in && (!is_device_ptr(keys) || !is_device_ptr(validity) || !is_device_ptr(ids)))
         return fail(HJ_ERR_INVALID, "HJ_INPUT_DEVICE given but a pointer is not device memory");
     if (dev_in && (flags & HJ_BORROW)) {
+        if (!(flags & HJ_BORROW_KEEP)) {
+            std::lock_guard<std::mutex> g(t->mu);
+            t->sync_finish = true;  // the caller may drop the buffer once hj_build_finish returns
+        }
         HIP_TRY(hipEventCreateWithFlags(&hs.ready, hipEventDisableTiming));
         HIP_TRY(hipEventRecord(hs.ready, s));
         hs.keys = keys;
@@ -650,6 +720,8 @@ hj_status hj_build_finish(hj_table* t, int partition) {
     if (t->arrived == t->parallelism) {
         // last arriver finalises (InitializeLast::initialize_or_wait)
         hj_status st = run_build(t);
+        if (st == HJ_OK && t->sync_finish && hipEventSynchronize(t->res.ev1) != hipSuccess)
+            st = fail(HJ_ERR_HIP, "build failed on the device");
         t->build_st = st;
         t->build_err = st == HJ_OK ? "" : g_err;
         t->built = true;
@@ -685,6 +757,7 @@ hj_status hj_table_stats_get(const hj_table* t, hj_table_stats* out) {
     unsigned long long* d = nullptr;
     HIP_TRY(hipMallocAsync((void**)&d, 4 * sizeof(unsigned long long), s));
     HIP_TRY(hipMemsetAsync(d, 0, 4 * sizeof(unsigned long long), s));
+    if (wait_built(t, s) != HJ_OK) return HJ_ERR_HIP;
     HIP_TRY(launch_table_stats(view_of(t), d, s));
     unsigned long long h[4];
     HIP_TRY(hipMemcpyAsync(h, d, sizeof(h), hipMemcpyDeviceToHost, s));
@@ -699,20 +772,20 @@ hj_status hj_table_stats_get(const hj_table* t, hj_table_stats* out) {
     out->buckets = t->dense ? 0 : t->nb;
     out->table_bytes = t->dense ? (int64_t)sizeof(uint32_t) * ((int64_t)t->nchunks << kDenseShift)
                                 : (int64_t)(t->nb + 1) * (int64_t)sizeof(Bucket);
-    out->build_ns = t->build_ns;
+    out->build_ns = build_time_ns(const_cast<hj_table*>(t));
     return HJ_OK;
 }
 
 int64_t hj_table_build_ns(const hj_table* t) {
     if (t == nullptr || !t->built || t->build_st != HJ_OK) return -1;
-    return t->build_ns;
+    return build_time_ns(const_cast<hj_table*>(t));
 }
 
 int64_t hj_probe_workspace_bytes(int64_t n) { return probe_workspace(n); }
 
 int hj_set_build_mode(int mode) {
-    if (mode < 0 || mode > 1) return -1;
-    const int old = build_mode();
+    if (mode < 0 || mode > 2) return -1;
+    const int old = build_mode_raw();
     g_build_mode.store(mode, std::memory_order_relaxed);
     return old;
 }
@@ -867,6 +940,7 @@ hj_status hj_table_chain_links(const hj_table* t, int64_t* prev, int64_t n) {
     hipStream_t s = thread_stream(t->device);
     int64_t* d = nullptr;
     HIP_TRY(hipMallocAsync((void**)&d, (size_t)n * 8, s));
+    if (wait_built(t, s) != HJ_OK) return HJ_ERR_HIP;
     HIP_TRY(launch_chain_links(view_of(t), d, n, s));
     HIP_TRY(hipMemcpyAsync(prev, d, (size_t)n * 8, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipFreeAsync(d, s));
@@ -884,7 +958,8 @@ hj_status hj_table_stream_wait(const hj_table* t, void* stream) {
 void hj_table_free(hj_table* t) {
     if (t == nullptr) return;
     (void)hipSetDevice(t->device);
-    // stream-ordered frees on the (pooled) build stream; no host synchronisation
+    // the blocks return to the cache (reused by any stream): the build must be done
+    if (t->built) (void)hipEventSynchronize(t->res.ev1);
     free_list(t, t->allocs);
     free_list(t, t->scratch);
     for (auto& part : t->parts)

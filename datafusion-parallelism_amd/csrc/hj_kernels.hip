@@ -1611,11 +1611,13 @@ template <typename K, bool HAS_VALID>
 __global__ void __launch_bounds__(kSlThreads, 8)  // 8 waves per SIMD = two workgroups per CU: <= 64 VGPRs
 sl_partition_kernel(int64_t dmin, uint64_t drange, uint32_t wlog, uint32_t nslices, const void* __restrict__ keys,
                     const uint8_t* __restrict__ valid, int64_t voff, int64_t n, bool vec,
-                    uint32_t* __restrict__ ent, uint16_t* __restrict__ rl, uint16_t* __restrict__ toff) {
+                    uint32_t* __restrict__ ent, uint16_t* __restrict__ rl, uint16_t* __restrict__ toff, int nt,
+                    int64_t tile_off) {
     __shared__ __attribute__((aligned(16))) uint32_t s_ent[kSlTile];
     __shared__ uint32_t s_hist[2 * kSlThreads];  // bins 0..nslices (<= kSlMaxSlices + 1)
     __shared__ uint32_t s_w[kSlThreads / 64];
-    const int64_t tile = blockIdx.x;
+    const int64_t tile = blockIdx.x;          // tile of this key array
+    const int64_t gtile = tile + tile_off;    // its output region (the build partitions several arrays)
     const int64_t tile0 = tile * kSlTile;
     const uint32_t nbins = nslices + 1;  // bin nslices stays empty: its prefix is the total
     for (uint32_t b = threadIdx.x; b < 2 * kSlThreads; b += kSlThreads) s_hist[b] = 0;
@@ -1626,7 +1628,8 @@ sl_partition_kernel(int64_t dmin, uint64_t drange, uint32_t wlog, uint32_t nslic
     for (int g = 0; g < kSlGroups; ++g) {
         const int loc0 = g * (kSlThreads * 4) + threadIdx.x * 4;
         int64_t k[4];
-        load4<K>(keys, tile0 + loc0, n, vec, k);
+        if (nt & 1) load4<K, true>(keys, tile0 + loc0, n, vec, k);
+        else load4<K>(keys, tile0 + loc0, n, vec, k);
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const int64_t row = tile0 + loc0 + q;
@@ -1646,7 +1649,7 @@ sl_partition_kernel(int64_t dmin, uint64_t drange, uint32_t wlog, uint32_t nslic
     s_hist[b0] = ex;
     s_hist[b0 + 1] = ex + h0;
     __syncthreads();
-    uint16_t* to = toff + tile * (int64_t)nbins;
+    uint16_t* to = toff + gtile * (int64_t)nbins;
     for (uint32_t b = threadIdx.x; b < nbins; b += kSlThreads) to[b] = (uint16_t)s_hist[b];
 #pragma unroll
     for (int g = 0; g < kSlGroups; ++g)
@@ -1657,8 +1660,8 @@ sl_partition_kernel(int64_t dmin, uint64_t drange, uint32_t wlog, uint32_t nslic
     __syncthreads();
     // entries leave split: the key offset (u32, replaced in place by its ref in S2) and
     // the row in the tile (u16, read by S3)
-    uint32_t* dst = ent + tile0;
-    uint16_t* dsr = rl + tile0;
+    uint32_t* dst = ent + gtile * kSlTile;
+    uint16_t* dsr = rl + gtile * kSlTile;
     const uint32_t n4 = tot & ~3u;
     for (uint32_t i = threadIdx.x * 4; i < n4; i += kSlThreads * 4) {
         const uint4 v = *reinterpret_cast<const uint4*>(s_ent + i);
@@ -1697,6 +1700,196 @@ sl_toff_transpose_kernel(const uint16_t* __restrict__ toff, uint32_t nbins, int6
         const uint32_t c = i / 64, j = i % 64;
         if (c < cw) toffT[(b * nbins + c0 + c) * 64 + j] = s_t[j][c];
     }
+}
+
+// ---------------------------------------------------------------------------
+// build (dense, <= 2047 blocks of 8192 key values, <= kFragMaxTiles tiles): the probe's
+// tile-local partition (sl_partition_kernel, 8192-value slices) replaces the histogram,
+// scan and staged scatter; each block then gathers its rows from every tile's fragment
+// (bounds in the transposed layout, one block-wide scan over the tiles, owner tile of a
+// position by binary search in LDS) and builds exactly as dense_chunk_build_kernel.
+// ---------------------------------------------------------------------------
+constexpr int kFragMaxTiles = 2048;
+static_assert(kSlTile == kFragTileRows, "build tiles are the probe's tiles");
+
+template <int T, int RR>
+__global__ void __launch_bounds__(T)
+dense_frag_build_kernel(ChunkGeom g, uint32_t nblk, int64_t ntiles, const uint16_t* __restrict__ toffT,
+                        const uint32_t* __restrict__ ent, const uint16_t* __restrict__ rl,
+                        const uint32_t* __restrict__ tile_base, const uint64_t* __restrict__ ids32,
+                        uint32_t* __restrict__ dense, uint32_t* __restrict__ dup_rows, BigSeg* __restrict__ big,
+                        BuildCounters* ctr) {
+    constexpr uint32_t GV = kDenseSub << kDenseBlockShift;  // 8192 values per block
+    constexpr uint32_t NSUB = GV / kDenseSub;
+    __shared__ uint32_t refs[GV];
+    __shared__ uint32_t d_off[kDenseSub], d_cur[kDenseSub], d_cnt[kDenseSub];
+    __shared__ uint32_t s_to[kFragMaxTiles + 1];  // exclusive position of each tile's fragment
+    __shared__ uint32_t s_pb[kFragMaxTiles];      // fragment position - s_to (region offset)
+    __shared__ unsigned s_ndup, s_dup[NSUB];
+    __shared__ unsigned long long s_w[T / 64];
+    __shared__ unsigned long long s_base;
+    __shared__ uint32_t s_carry;
+    const uint32_t c = blockIdx.x;
+    const uint64_t cbase = (uint64_t)c * GV;  // key index of refs[0]
+    const uint32_t nbins = nblk + 1;
+    for (uint32_t i = threadIdx.x; i < GV; i += T) refs[i] = kMiss;
+    if (threadIdx.x == 0) s_carry = 0;
+    __syncthreads();
+    // fragment bounds of this block in every tile -> exclusive positions (block scan)
+    for (int64_t t0 = 0; t0 < ntiles; t0 += T) {
+        const int64_t t = t0 + threadIdx.x;
+        uint32_t st = 0, len = 0;
+        if (t < ntiles) {
+            const uint16_t* to = toffT + ((t >> 6) * nbins + c) * 64 + (t & 63);
+            st = to[0];
+            len = (uint32_t)to[64] - st;
+        }
+        uint32_t tot;
+        const uint32_t ex = block_excl_scan<uint32_t>(len, reinterpret_cast<uint32_t*>(s_w), &tot) + s_carry;
+        if (t < ntiles) {
+            s_to[t] = ex;
+            s_pb[t] = (uint32_t)t * kSlTile + st - ex;  // >= 0: ex <= t * kSlTile
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) s_carry += tot;
+        __syncthreads();
+    }
+    const uint32_t R = s_carry;
+    if (threadIdx.x == 0) {
+        s_to[ntiles] = R;
+        if (R) atomicAdd(&ctr->n_valid, (unsigned long long)R);
+    }
+    __syncthreads();
+    // position r -> (key index in the block, row value)
+    auto fetch = [&](uint32_t r, int* idx, uint32_t* row) {
+        int lo = 0, hi = (int)ntiles - 1;  // largest tile with s_to[tile] <= r (skips empty ones)
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (s_to[mid] <= r) lo = mid; else hi = mid - 1;
+        }
+        const uint32_t pos = s_pb[lo] + r;
+        *idx = (int)ent[pos];
+        const uint32_t rw = tile_base[lo] + rl[pos];
+        *row = ids32 ? (uint32_t)ids32[rw] : rw;
+    };
+    const bool in_regs = R <= (uint32_t)(T * RR);
+    if (threadIdx.x < NSUB) s_dup[threadIdx.x] = in_regs ? 0u : 1u;  // more rows than the registers hold
+    __syncthreads();
+    uint32_t rrow[RR];
+    int ridx[RR];
+    if (in_regs) {
+#pragma unroll
+        for (int u = 0; u < RR; ++u) {
+            const uint32_t r = u * T + threadIdx.x;
+            ridx[u] = -1;
+            rrow[u] = 0;
+            if (r < R) fetch(r, &ridx[u], &rrow[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < RR; ++u)
+            if (ridx[u] >= 0 && atomicExch(&refs[ridx[u]], rrow[u]) != kMiss) s_dup[ridx[u] / kDenseSub] = 1u;
+    }
+    __syncthreads();
+    for (uint32_t q = 0; q < NSUB; ++q) {
+        if (!s_dup[q]) continue;  // uniform: every thread reads the same LDS word
+        const int lo = (int)(q * kDenseSub), hi = lo + (int)kDenseSub;
+        uint32_t* img = refs + lo;
+        if (threadIdx.x == 0) s_ndup = 0;
+        for (uint32_t i = threadIdx.x; i < kDenseSub; i += T) img[i] = 0;
+        __syncthreads();
+        if (in_regs) {
+#pragma unroll
+            for (int u = 0; u < RR; ++u)
+                if (ridx[u] >= lo && ridx[u] < hi) atomicAdd(&refs[ridx[u]], 1u);
+        } else {
+            for (uint32_t r = threadIdx.x; r < R; r += T) {
+                int i;
+                uint32_t rw;
+                fetch(r, &i, &rw);
+                if (i >= lo && i < hi) atomicAdd(&refs[i], 1u);
+            }
+        }
+        __syncthreads();
+        for (uint32_t i = threadIdx.x; i < kDenseSub; i += T) {
+            const uint32_t cnt = img[i];
+            if (cnt == 0) {
+                img[i] = kMiss;
+            } else if (cnt > 1) {
+                const unsigned li = atomicAdd(&s_ndup, 1u);
+                d_cnt[li] = cnt;
+                d_cur[li] = 0;
+                img[i] = kDupFlag | li;
+            }
+        }
+        __syncthreads();
+        const unsigned ndup = s_ndup;
+        unsigned long long carry = 0;
+        for (unsigned b0 = 0; b0 < ndup; b0 += T) {
+            const unsigned li = b0 + threadIdx.x;
+            const unsigned long long v = li < ndup ? (unsigned long long)d_cnt[li] + 1 : 0;
+            unsigned long long tot;
+            const unsigned long long ex = block_excl_scan<unsigned long long>(v, s_w, &tot);
+            if (li < ndup) d_off[li] = (uint32_t)(carry + ex);
+            carry += tot;
+        }
+        if (threadIdx.x == 0) s_base = carry ? atomicAdd(&ctr->dup_used, carry) : 0;
+        __syncthreads();
+        for (unsigned li = threadIdx.x; li < ndup; li += T) {
+            d_off[li] += (uint32_t)s_base;
+            dup_rows[d_off[li]] = d_cnt[li];
+        }
+        __syncthreads();
+        auto place = [&](int i, uint32_t row) {
+            const uint32_t rv = refs[i];
+            if (rv & kDupFlag) {
+                const unsigned li = rv & ~kDupFlag;
+                dup_rows[d_off[li] + 1 + atomicAdd(&d_cur[li], 1u)] = row;
+            } else {
+                refs[i] = row;  // count was 1
+            }
+        };
+        if (in_regs) {
+#pragma unroll
+            for (int u = 0; u < RR; ++u)
+                if (ridx[u] >= lo && ridx[u] < hi) place(ridx[u], rrow[u]);
+        } else {
+            for (uint32_t r = threadIdx.x; r < R; r += T) {
+                int i;
+                uint32_t rw;
+                fetch(r, &i, &rw);
+                if (i >= lo && i < hi) place(i, rw);
+            }
+        }
+        __syncthreads();
+        for (unsigned li = threadIdx.x; li < ndup; li += T) {
+            const unsigned n = d_cnt[li], off = d_off[li];
+            if (n <= (unsigned)kSmallSeg) {
+                uint32_t v[16];
+#pragma unroll
+                for (int i = 0; i < 16; ++i) v[i] = (i < (int)n) ? dup_rows[off + 1 + i] : 0u;
+                sort16_desc(v);
+#pragma unroll
+                for (int i = 0; i < 16; ++i)
+                    if (i < (int)n) dup_rows[off + 1 + i] = v[i];
+            }
+        }
+        for (uint32_t i = threadIdx.x; i < kDenseSub; i += T) {
+            const uint32_t rv = img[i];
+            if (rv != kMiss && (rv & kDupFlag)) {
+                const unsigned li = rv & ~kDupFlag;
+                if (d_cnt[li] > (unsigned)kSmallSeg) {
+                    const unsigned bi = (unsigned)atomicAdd(&ctr->n_big, 1ull);
+                    big[bi] = BigSeg{(unsigned long long)((uint64_t)g.dmin + cbase + lo + i), d_off[li], 0u};
+                }
+                const uint32_t c4 = (g.packed && d_cnt[li] <= 15u) ? d_cnt[li] : 0u;
+                img[i] = kDupFlag | (c4 << 27) | d_off[li];
+            }
+        }
+        __syncthreads();
+    }
+    uint4* dst = reinterpret_cast<uint4*>(dense + cbase);
+    const uint4* src = reinterpret_cast<const uint4*>(refs);
+    for (uint32_t i = threadIdx.x; i < GV / 4; i += T) dst[i] = src[i];
 }
 
 // grid = nslices x parts; block b: slice b % nslices, tiles [part range) with
@@ -2219,6 +2412,61 @@ hipError_t launch_key_minmax(int key_bytes, const Segment* d_segs, int nseg, int
     return hipGetLastError();
 }
 
+int64_t frag_build_tiles(const int64_t* seg_n, int nseg) {
+    int64_t t = 0;
+    for (int i = 0; i < nseg; ++i) t += (seg_n[i] + kSlTile - 1) / kSlTile;
+    return t;
+}
+bool frag_build_ok(const ChunkGeom& g, int64_t ftiles) {
+    return g.dense && dense_one_level(g.nchunks) && dense_blocks(g.nchunks) <= (uint32_t)kSlMaxSlices &&
+           ftiles <= kFragMaxTiles;
+}
+int64_t frag_build_scratch_bytes(const ChunkGeom& g, int64_t ftiles) {
+    const int64_t nbins = dense_blocks(g.nchunks) + 1;
+    return 4 * ftiles * kSlTile + 2 * ftiles * kSlTile + 2 * ftiles * nbins + 2 * ((ftiles + 63) & ~(int64_t)63) * nbins +
+           4 * ftiles + 6 * 256;
+}
+
+hipError_t launch_build_frag(int key_bytes, const Segment* h_segs, int nseg, const ChunkGeom& g, int64_t ftiles,
+                             void* scratch, const uint32_t* d_tile_base, const uint64_t* ids32, uint32_t* dense,
+                             uint32_t* dup_rows, BigSeg* big, BuildCounters* ctr, const Segment* d_segs, int64_t total,
+                             bool ids_as_rows, int big_grid, hipStream_t s) {
+    const uint32_t nblk = dense_blocks(g.nchunks), nbins = nblk + 1;
+    constexpr uint32_t GV = kDenseSub << kDenseBlockShift;
+    const uint32_t wlog = 31 - __builtin_clz(GV);
+    auto a256 = [](uintptr_t x) { return (x + 255) & ~(uintptr_t)255; };
+    uintptr_t p = a256((uintptr_t)scratch);
+    uint32_t* ent = (uint32_t*)p;  p = a256(p + 4 * ftiles * kSlTile);
+    uint16_t* rl = (uint16_t*)p;   p = a256(p + 2 * ftiles * kSlTile);
+    uint16_t* toff = (uint16_t*)p; p = a256(p + 2 * ftiles * nbins);
+    uint16_t* toffT = (uint16_t*)p;
+    int64_t t0 = 0;
+    for (int i = 0; i < nseg; ++i) {
+        const Segment& sg = h_segs[i];
+        const int64_t nt = (sg.n + kSlTile - 1) / kSlTile;
+        if (nt == 0) continue;
+        const bool vec = (reinterpret_cast<uintptr_t>(sg.keys) & 15) == 0;
+        const uint64_t drange = (uint64_t)nblk * GV;
+#define DFP_BLP(KT, HV)                                                                                          \
+    sl_partition_kernel<KT, HV><<<(unsigned)nt, kSlThreads, 0, s>>>(g.dmin, drange, wlog, nblk, sg.keys, sg.valid, \
+                                                                   sg.voff, sg.n, vec, ent, rl, toff, 0, t0)
+        if (key_bytes == 8) {
+            if (sg.valid) DFP_BLP(int64_t, true); else DFP_BLP(int64_t, false);
+        } else {
+            if (sg.valid) DFP_BLP(int32_t, true); else DFP_BLP(int32_t, false);
+        }
+#undef DFP_BLP
+        t0 += nt;
+    }
+    sl_toff_transpose_kernel<<<(unsigned)((ftiles + 63) / 64 * ((nblk + kSlTrChunk) / kSlTrChunk)), 256, 0, s>>>(
+        toff, nbins, ftiles, toffT);
+    dense_frag_build_kernel<1024, 8><<<nblk, 1024, 0, s>>>(g, nblk, ftiles, toffT, ent, rl, d_tile_base,
+                                                           ids_as_rows ? ids32 : nullptr, dense, dup_rows, big, ctr);
+    dup_sort_big_kernel<<<big_grid, kBigThreads, 0, s>>>(dup_rows, big, ctr, d_segs, nseg, total, key_bytes,
+                                                         ids_as_rows);
+    return hipGetLastError();
+}
+
 hipError_t launch_build(int key_bytes, const Segment* d_segs, int nseg, int64_t total, const ChunkGeom& g,
                         uint32_t* hist, uint32_t* hist1, uint32_t* chunk_starts, int64_t ntiles,
                         int64_t tile_rows, void* scan_scratch,
@@ -2466,9 +2714,13 @@ hipError_t launch_probe_sliced(int key_bytes, const TableView& tv, const void* k
     SlicedWs w = sliced_ws_layout((void*)(((uintptr_t)workspace + 255) & ~(uintptr_t)255), n);
     const bool vec = (reinterpret_cast<uintptr_t>(keys) & 15) == 0;
     hipError_t e = hipSuccess;
+    static const int sl_nt = [] {  // 1: nontemporal probe-key loads in S1
+        const char* ev = getenv("DFP_HJ_SL_NT");
+        return ev ? atoi(ev) : 0;
+    }();
 #define DFP_SLP(KT, HV)                                                                                      \
     sl_partition_kernel<KT, HV><<<(unsigned)nt, kSlThreads, 0, s>>>(tv.dmin, tv.drange, wlog, nsl, keys, valid, voff, n, \
-                                                                   vec, w.ent, w.rl, w.toff)
+                                                                   vec, w.ent, w.rl, w.toff, sl_nt, 0)
     if (key_bytes == 8) {
         if (valid) DFP_SLP(int64_t, true); else DFP_SLP(int64_t, false);
     } else {

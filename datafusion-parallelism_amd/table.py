@@ -14,7 +14,7 @@ import numpy as np
 import torch
 
 from . import _lib
-from ._lib import HJ_BORROW, HJ_IDS_U31, HJ_INPUT_DEVICE, HJ_INT32, HJ_INT64, HJ_OUTPUT_HOST, check
+from ._lib import HJ_BORROW, HJ_BORROW_KEEP, HJ_IDS_U31, HJ_INPUT_DEVICE, HJ_INT32, HJ_INT64, HJ_OUTPUT_HOST, check
 
 try:  # pyarrow is optional for the device path
     import pyarrow as pa
@@ -106,7 +106,7 @@ class HashTable:
         h = ctypes.c_void_p()
         check(self._L.hj_build_begin(device, parallelism, kt, expected_rows, ctypes.byref(h)))
         self._h = h
-        self._keep = []  # borrowed device inputs stay alive until the barrier
+        self._keep = []  # borrowed device inputs stay alive until the table is freed
 
     # -- build --------------------------------------------------------------
     def append(self, partition: int, keys, valid=None, ids=None, borrow: bool = True, ids_u31: bool = False) -> None:
@@ -115,7 +115,9 @@ class HashTable:
         ki = as_key_input(keys, valid)
         if ki.n and ki.key_type != self.key_type:
             raise TypeError("key type of the batch differs from the table's")
-        flags = ki.flags | (HJ_BORROW if (borrow and ki.flags & HJ_INPUT_DEVICE) else 0)
+        # borrowed device inputs are kept alive (self._keep) until close(), which frees the
+        # table first: the build may run on after finish() (HJ_BORROW_KEEP)
+        flags = ki.flags | (HJ_BORROW | HJ_BORROW_KEEP if (borrow and ki.flags & HJ_INPUT_DEVICE) else 0)
         if ids is not None and ids_u31:
             flags |= HJ_IDS_U31
         ids_ptr, keep_ids = None, None
@@ -165,6 +167,11 @@ class HashTable:
         v = ctypes.c_int64()
         check(self._L.hj_build_partition_offset(self._h, partition, ctypes.byref(v)))
         return v.value
+
+    def stream_wait(self, stream: int = 0) -> None:
+        """Order `stream` (a hipStream_t, 0 = the null stream) after the device build
+        (hj_table_stream_wait; probes on any stream already wait by themselves)."""
+        check(self._L.hj_table_stream_wait(self._h, stream or None))
 
     def build_ns(self) -> int:
         """Device time of the build (HIP events), no device work."""

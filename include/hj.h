@@ -49,10 +49,14 @@ enum {
     HJ_BORROW = 1u << 1,       /* device input is not copied: caller keeps it alive until
                                   hj_build_finish returns on every partition */
     HJ_OUTPUT_HOST = 1u << 2,  /* hj_probe: return pairs in host memory (else device) */
-    HJ_IDS_U31 = 1u << 3       /* hj_build_append: the explicit ids are < 2^31 and ascend in
+    HJ_IDS_U31 = 1u << 3,      /* hj_build_append: the explicit ids are < 2^31 and ascend in
                                   canonical row order; when every id batch says so the table
                                   stores the ids in place of row numbers (pairs carry them
                                   with no id gather at probe time) */
+    HJ_BORROW_KEEP = 1u << 4   /* with HJ_BORROW: the caller keeps the buffers alive and
+                                  unmodified until hj_table_free, so hj_build_finish may return
+                                  before the device build is done (it stays ordered before
+                                  every later use of the table) */
 };
 
 typedef struct hj_table hj_table; /* opaque, device resident */
@@ -112,7 +116,10 @@ hj_status hj_build_append(hj_table* t, int partition, const void* keys,
 /* Barrier: every one of the `parallelism` partitions calls this once. The last
  * arriver runs the device build (InitializeLast::initialize_or_wait,
  * src/utils/initialize_last.rs:26-43); the others block until it is done. After it
- * returns the table is read-only and may be probed concurrently. */
+ * returns the table is read-only and may be probed concurrently. A direct-addressed
+ * build runs on asynchronously when no input was borrowed without HJ_BORROW_KEEP: every
+ * later call on the table (probe, lookup, stats) waits for it on the device, and
+ * hj_table_stream_wait orders any other stream after it. */
 hj_status hj_build_finish(hj_table* t, int partition);
 
 /* Canonical id of partition `partition`'s first row (valid after the barrier). */
@@ -184,8 +191,10 @@ int hj_set_probe_mode(int mode);
 /* Table layout for later builds of this process: 0 auto (a direct-addressed table - one
  * u32 ref per key value - when the build keys' range is at most 8x the build rows, the
  * "perfect hash" of dense integer keys; else 5-slot hashed buckets), 1 hashed buckets
- * always. Results are identical; returns the previous mode, -1 for a bad value. Also
- * settable with DFP_HJ_DENSE=0 (hashed). */
+ * always, 2 as 0 but the direct-addressed build partitions its rows by histogram + scan
+ * + scatter instead of the tile-local partition. Results are identical; returns the
+ * previous mode, -1 for a bad value. Also settable with DFP_HJ_DENSE=0 (hashed) and
+ * DFP_HJ_FRAG_BUILD=0 (mode 2). */
 int hj_set_build_mode(int mode);
 
 /* Makes `stream` wait for the build of `t` (for probes on other streams). */

@@ -127,10 +127,11 @@ def test_join_type_names():
 
 
 def test_build_mode_switch(dfp):
-    """hj_set_build_mode: 0 auto (dense layout when it pays), 1 hashed; bad -> -1."""
+    """hj_set_build_mode: 0 auto (dense layout when it pays), 1 hashed, 2 auto with the
+    histogram partition for dense builds; bad -> -1."""
     from datafusion_parallelism_amd import _lib
 
     L = _lib.load()
-    assert L.hj_set_build_mode(2) == -1
+    assert L.hj_set_build_mode(3) == -1
     old = L.hj_set_build_mode(1)
     assert L.hj_set_build_mode(old) == 1

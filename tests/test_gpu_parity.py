@@ -14,9 +14,10 @@ I64_MIN = np.iinfo(np.int64).min
 
 
 # (probe mode, table layout): hj_set_probe_mode 3 fused / 1 two-pass / 2 partitioned /
-# 4 sliced; hj_set_build_mode 0 auto (direct-addressed for dense key ranges) / 1 hashed
+# 4 sliced; hj_set_build_mode 0 auto (direct-addressed for dense key ranges, built from the
+# tile-local partition) / 1 hashed / 2 auto with the histogram partition
 MODES = {"fused": (3, 0), "fused-hashed": (3, 1), "two-pass": (1, 0), "partitioned-hashed": (2, 1),
-         "sliced": (4, 0)}
+         "sliced": (4, 0), "sliced-histbuild": (4, 2)}
 
 
 @pytest.fixture(params=list(MODES))
@@ -207,7 +208,7 @@ def test_exponential_keys_parity(dfp, oracle_mod, probe_mode):
     assert st["dup_keys"] > 0
 
 
-@pytest.mark.parametrize("layout", [0, 1])
+@pytest.mark.parametrize("layout", [0, 1, 2])
 def test_stats(dfp, layout):
     L = dfp.load()
     old = L.hj_set_build_mode(layout)
@@ -220,8 +221,8 @@ def test_stats(dfp, layout):
         L.hj_set_build_mode(old)
     assert s["build_rows"] == 6 and s["inserted_rows"] == 5
     assert s["distinct_keys"] == 3 and s["dup_keys"] == 1 and s["dup_rows"] == 3 and s["max_key_rows"] == 3
-    # layout 0 chooses the direct-addressed table for this dense range (3 values, 6 rows)
-    assert (s["buckets"] == 0) == (layout == 0)
+    # layouts 0 and 2 choose the direct-addressed table for this dense range (3 values, 6 rows)
+    assert (s["buckets"] == 0) == (layout != 1)
 
 
 # ---- full-size properties (BASELINE configs) -------------------------------------
@@ -330,10 +331,21 @@ def test_large_build_120m_rows(dfp):
     torch.cuda.empty_cache()
 
 
+@pytest.mark.parametrize("bmode", [0, 2])
 @pytest.mark.parametrize("nb,krange", [(2_200_000, 17_600_000), (2_000_000, 16_000_000)])
-def test_dense_build_levels(dfp, oracle_mod, nb, krange):
+def test_dense_build_levels(dfp, oracle_mod, nb, krange, bmode):
     """Direct-addressed builds on both sides of the one-level limit (2048 blocks of 8192
-    key values): 17.6 M values take the two-level partition, 16 M the one-level one."""
+    key values): 17.6 M values take the two-level partition, 16 M the one-level one (the
+    tile-local partition under build mode 0, histogram + scatter under mode 2)."""
+    L = dfp.load()
+    old = L.hj_set_build_mode(bmode)
+    try:
+        _dense_build_levels(dfp, oracle_mod, nb, krange)
+    finally:
+        L.hj_set_build_mode(old)
+
+
+def _dense_build_levels(dfp, oracle_mod, nb, krange):
     rng = np.random.default_rng(nb)
     bk = rng.integers(0, krange, nb)
     bk[:3] = [0, krange - 1, krange - 1]
