@@ -391,19 +391,12 @@ hj_status build_attempt(hj_table* t, const std::vector<Segment>& segs, double lf
         uint32_t* d_tb;
         uint64_t* ids32 = nullptr;
         BigSeg* fbig;
-        if ((st = dev_alloc(t, t->scratch, &fscr, (size_t)frag_build_scratch_bytes(g, ftiles))) != HJ_OK) return st;
+        if ((st = dev_alloc(t, t->scratch, &fscr, (size_t)frag_build_scratch_bytes(g, ftiles, total))) != HJ_OK) return st;
         if ((st = dev_alloc(t, t->scratch, &p, sizeof(uint32_t) * (size_t)ftiles)) != HJ_OK) return st;
         d_tb = (uint32_t*)p;
         if ((st = dev_alloc(t, t->scratch, &p, sizeof(BigSeg) * (size_t)(total / (kSmallSeg + 1) + 2))) != HJ_OK)
             return st;
         fbig = (BigSeg*)p;
-        // first row of every tile (a tile never spans two appended batches)
-        std::vector<uint32_t> tb((size_t)ftiles);
-        int64_t k = 0;
-        for (const Segment& sg : segs)
-            for (int64_t j = 0; j * kFragTileRows < sg.n; ++j)
-                tb[(size_t)k++] = (uint32_t)(sg.row_base + j * kFragTileRows);
-        HIP_TRY(hipMemcpyAsync(d_tb, tb.data(), sizeof(uint32_t) * tb.size(), hipMemcpyHostToDevice, s));
         if (t->has_ids) {  // explicit ids in row order: the table's row_ids, or scratch when held in place of rows
             uint64_t* dst = t->row_ids;
             if (ids_as_rows) {

@@ -60,6 +60,7 @@ struct BuildCounters {
     unsigned long long dup_used;     // dup_rows entries allocated
     unsigned long long n_big;        // segments > kSmallSeg
     unsigned long long err;          // bit 0: chunk full; bit 1: chunk dup-directory full
+    unsigned long long spill_used;   // fragment build: rows gathered for blocks past the registers
 };
 
 // a duplicate segment too large for one thread to sort

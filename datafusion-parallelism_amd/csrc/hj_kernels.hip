@@ -1612,7 +1612,7 @@ __global__ void __launch_bounds__(kSlThreads, 8)  // 8 waves per SIMD = two work
 sl_partition_kernel(int64_t dmin, uint64_t drange, uint32_t wlog, uint32_t nslices, const void* __restrict__ keys,
                     const uint8_t* __restrict__ valid, int64_t voff, int64_t n, bool vec,
                     uint32_t* __restrict__ ent, uint16_t* __restrict__ rl, uint16_t* __restrict__ toff, int nt,
-                    int64_t tile_off) {
+                    int64_t tile_off, int64_t row_base, uint32_t* __restrict__ tile_base) {
     __shared__ __attribute__((aligned(16))) uint32_t s_ent[kSlTile];
     __shared__ uint32_t s_hist[2 * kSlThreads];  // bins 0..nslices (<= kSlMaxSlices + 1)
     __shared__ uint32_t s_w[kSlThreads / 64];
@@ -1651,6 +1651,7 @@ sl_partition_kernel(int64_t dmin, uint64_t drange, uint32_t wlog, uint32_t nslic
     __syncthreads();
     uint16_t* to = toff + gtile * (int64_t)nbins;
     for (uint32_t b = threadIdx.x; b < nbins; b += kSlThreads) to[b] = (uint16_t)s_hist[b];
+    if (tile_base != nullptr && threadIdx.x == 0) tile_base[gtile] = (uint32_t)(row_base + tile0);  // build only
 #pragma unroll
     for (int g = 0; g < kSlGroups; ++g)
 #pragma unroll
@@ -1718,7 +1719,7 @@ dense_frag_build_kernel(ChunkGeom g, uint32_t nblk, int64_t ntiles, const uint16
                         const uint32_t* __restrict__ ent, const uint16_t* __restrict__ rl,
                         const uint32_t* __restrict__ tile_base, const uint64_t* __restrict__ ids32,
                         uint32_t* __restrict__ dense, uint32_t* __restrict__ dup_rows, BigSeg* __restrict__ big,
-                        BuildCounters* ctr) {
+                        BuildCounters* ctr, unsigned long long* __restrict__ spill) {
     constexpr uint32_t GV = kDenseSub << kDenseBlockShift;  // 8192 values per block
     constexpr uint32_t NSUB = GV / kDenseSub;
     __shared__ uint32_t refs[GV];
@@ -1727,7 +1728,7 @@ dense_frag_build_kernel(ChunkGeom g, uint32_t nblk, int64_t ntiles, const uint16
     __shared__ uint32_t s_pb[kFragMaxTiles];      // fragment position - s_to (region offset)
     __shared__ unsigned s_ndup, s_dup[NSUB];
     __shared__ unsigned long long s_w[T / 64];
-    __shared__ unsigned long long s_base;
+    __shared__ unsigned long long s_base, s_sp;
     __shared__ uint32_t s_carry;
     const uint32_t c = blockIdx.x;
     const uint64_t cbase = (uint64_t)c * GV;  // key index of refs[0]
@@ -1774,7 +1775,20 @@ dense_frag_build_kernel(ChunkGeom g, uint32_t nblk, int64_t ntiles, const uint16
     };
     const bool in_regs = R <= (uint32_t)(T * RR);
     if (threadIdx.x < NSUB) s_dup[threadIdx.x] = in_regs ? 0u : 1u;  // more rows than the registers hold
+    if (threadIdx.x == 0 && !in_regs) s_sp = atomicAdd(&ctr->spill_used, (unsigned long long)R);
     __syncthreads();
+    // a block with more rows than the registers hold gathers them once into the spill
+    // pool (key index << 32 | row); its duplicate passes then stream them from there
+    unsigned long long* sp = spill + (in_regs ? 0ull : s_sp);
+    if (!in_regs) {
+        for (uint32_t r = threadIdx.x; r < R; r += T) {
+            int i;
+            uint32_t rw;
+            fetch(r, &i, &rw);
+            sp[r] = ((unsigned long long)(uint32_t)i << 32) | rw;
+        }
+        __syncthreads();
+    }
     uint32_t rrow[RR];
     int ridx[RR];
     if (in_regs) {
@@ -1803,9 +1817,7 @@ dense_frag_build_kernel(ChunkGeom g, uint32_t nblk, int64_t ntiles, const uint16
                 if (ridx[u] >= lo && ridx[u] < hi) atomicAdd(&refs[ridx[u]], 1u);
         } else {
             for (uint32_t r = threadIdx.x; r < R; r += T) {
-                int i;
-                uint32_t rw;
-                fetch(r, &i, &rw);
+                const int i = (int)(sp[r] >> 32);
                 if (i >= lo && i < hi) atomicAdd(&refs[i], 1u);
             }
         }
@@ -1854,10 +1866,9 @@ dense_frag_build_kernel(ChunkGeom g, uint32_t nblk, int64_t ntiles, const uint16
                 if (ridx[u] >= lo && ridx[u] < hi) place(ridx[u], rrow[u]);
         } else {
             for (uint32_t r = threadIdx.x; r < R; r += T) {
-                int i;
-                uint32_t rw;
-                fetch(r, &i, &rw);
-                if (i >= lo && i < hi) place(i, rw);
+                const unsigned long long v = sp[r];
+                const int i = (int)(v >> 32);
+                if (i >= lo && i < hi) place(i, (uint32_t)v);
             }
         }
         __syncthreads();
@@ -2421,14 +2432,14 @@ bool frag_build_ok(const ChunkGeom& g, int64_t ftiles) {
     return g.dense && dense_one_level(g.nchunks) && dense_blocks(g.nchunks) <= (uint32_t)kSlMaxSlices &&
            ftiles <= kFragMaxTiles;
 }
-int64_t frag_build_scratch_bytes(const ChunkGeom& g, int64_t ftiles) {
+int64_t frag_build_scratch_bytes(const ChunkGeom& g, int64_t ftiles, int64_t total) {
     const int64_t nbins = dense_blocks(g.nchunks) + 1;
     return 4 * ftiles * kSlTile + 2 * ftiles * kSlTile + 2 * ftiles * nbins + 2 * ((ftiles + 63) & ~(int64_t)63) * nbins +
-           4 * ftiles + 6 * 256;
+           8 * total + 6 * 256;
 }
 
 hipError_t launch_build_frag(int key_bytes, const Segment* h_segs, int nseg, const ChunkGeom& g, int64_t ftiles,
-                             void* scratch, const uint32_t* d_tile_base, const uint64_t* ids32, uint32_t* dense,
+                             void* scratch, uint32_t* tile_base, const uint64_t* ids32, uint32_t* dense,
                              uint32_t* dup_rows, BigSeg* big, BuildCounters* ctr, const Segment* d_segs, int64_t total,
                              bool ids_as_rows, int big_grid, hipStream_t s) {
     const uint32_t nblk = dense_blocks(g.nchunks), nbins = nblk + 1;
@@ -2439,7 +2450,8 @@ hipError_t launch_build_frag(int key_bytes, const Segment* h_segs, int nseg, con
     uint32_t* ent = (uint32_t*)p;  p = a256(p + 4 * ftiles * kSlTile);
     uint16_t* rl = (uint16_t*)p;   p = a256(p + 2 * ftiles * kSlTile);
     uint16_t* toff = (uint16_t*)p; p = a256(p + 2 * ftiles * nbins);
-    uint16_t* toffT = (uint16_t*)p;
+    uint16_t* toffT = (uint16_t*)p; p = a256(p + 2 * ((ftiles + 63) & ~(int64_t)63) * nbins);
+    unsigned long long* spill = (unsigned long long*)p;  // total rows at most
     int64_t t0 = 0;
     for (int i = 0; i < nseg; ++i) {
         const Segment& sg = h_segs[i];
@@ -2449,7 +2461,8 @@ hipError_t launch_build_frag(int key_bytes, const Segment* h_segs, int nseg, con
         const uint64_t drange = (uint64_t)nblk * GV;
 #define DFP_BLP(KT, HV)                                                                                          \
     sl_partition_kernel<KT, HV><<<(unsigned)nt, kSlThreads, 0, s>>>(g.dmin, drange, wlog, nblk, sg.keys, sg.valid, \
-                                                                   sg.voff, sg.n, vec, ent, rl, toff, 0, t0)
+                                                                   sg.voff, sg.n, vec, ent, rl, toff, 0, t0,          \
+                                                                   sg.row_base, tile_base)
         if (key_bytes == 8) {
             if (sg.valid) DFP_BLP(int64_t, true); else DFP_BLP(int64_t, false);
         } else {
@@ -2460,8 +2473,9 @@ hipError_t launch_build_frag(int key_bytes, const Segment* h_segs, int nseg, con
     }
     sl_toff_transpose_kernel<<<(unsigned)((ftiles + 63) / 64 * ((nblk + kSlTrChunk) / kSlTrChunk)), 256, 0, s>>>(
         toff, nbins, ftiles, toffT);
-    dense_frag_build_kernel<1024, 8><<<nblk, 1024, 0, s>>>(g, nblk, ftiles, toffT, ent, rl, d_tile_base,
-                                                           ids_as_rows ? ids32 : nullptr, dense, dup_rows, big, ctr);
+    dense_frag_build_kernel<1024, 8><<<nblk, 1024, 0, s>>>(g, nblk, ftiles, toffT, ent, rl, tile_base,
+                                                           ids_as_rows ? ids32 : nullptr, dense, dup_rows, big, ctr,
+                                                           spill);
     dup_sort_big_kernel<<<big_grid, kBigThreads, 0, s>>>(dup_rows, big, ctr, d_segs, nseg, total, key_bytes,
                                                          ids_as_rows);
     return hipGetLastError();
@@ -2720,7 +2734,7 @@ hipError_t launch_probe_sliced(int key_bytes, const TableView& tv, const void* k
     }();
 #define DFP_SLP(KT, HV)                                                                                      \
     sl_partition_kernel<KT, HV><<<(unsigned)nt, kSlThreads, 0, s>>>(tv.dmin, tv.drange, wlog, nsl, keys, valid, voff, n, \
-                                                                   vec, w.ent, w.rl, w.toff, sl_nt, 0)
+                                                                   vec, w.ent, w.rl, w.toff, sl_nt, 0, 0, nullptr)
     if (key_bytes == 8) {
         if (valid) DFP_SLP(int64_t, true); else DFP_SLP(int64_t, false);
     } else {

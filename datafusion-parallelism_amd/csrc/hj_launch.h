@@ -38,14 +38,15 @@ hipError_t launch_build(int key_bytes, const Segment* d_segs, int nseg, int64_t 
 // Dense builds of <= 2047 blocks and <= 2048 tiles of 16384 rows (one tile range per
 // segment): the sliced probe's tile-local partition, then one workgroup per block gathers
 // its rows from the tiles' fragments (no histogram, scan or global scatter).
-// scratch: frag_build_scratch_bytes; d_tile_base: u32 first row of each tile; ids32: the
+// scratch: frag_build_scratch_bytes; tile_base: u32[ftiles], the first row of each tile
+// (written by the partition); ids32: the
 // explicit ids in row order (ids_as_rows) or NULL
 constexpr int64_t kFragTileRows = 16384;  // = the sliced probe's tile
 int64_t frag_build_tiles(const int64_t* seg_n, int nseg);
 bool frag_build_ok(const ChunkGeom& g, int64_t ftiles);
-int64_t frag_build_scratch_bytes(const ChunkGeom& g, int64_t ftiles);
+int64_t frag_build_scratch_bytes(const ChunkGeom& g, int64_t ftiles, int64_t total);
 hipError_t launch_build_frag(int key_bytes, const Segment* h_segs, int nseg, const ChunkGeom& g, int64_t ftiles,
-                             void* scratch, const uint32_t* d_tile_base, const uint64_t* ids32, uint32_t* dense,
+                             void* scratch, uint32_t* tile_base, const uint64_t* ids32, uint32_t* dense,
                              uint32_t* dup_rows, BigSeg* big, BuildCounters* ctr, const Segment* d_segs, int64_t total,
                              bool ids_as_rows, int big_grid, hipStream_t s);
 // min and max of the valid keys of the build segments -> out[0], out[1] (int64)
