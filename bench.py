@@ -113,13 +113,16 @@ class SingleGpuJoin:
             self._pending = True
 
     def collect(self):
-        """After a synchronize: per-step timings (outside the timed region)."""
+        """After a synchronize: per-step event timings; the pair count (identical every
+        step) is read once after the timed loop (finish())."""
         self.probe_ms.append(self.ev[0].elapsed_time(self.ev[1]))
         self.build_ms.append(self.table.build_ns() / 1e6)
+        self.table.close()
+
+    def finish(self):
         self.matches = int(self.d_total.item())
         if self.matches > self.cap:
             raise RuntimeError("output capacity too small")
-        self.table.close()
 
 
 def cpu_baseline(cfg, nthreads=8):
@@ -247,6 +250,7 @@ def main():
     torch.cuda.synchronize(dev)
     barrier()
     elapsed = time.perf_counter() - t_start
+    job.finish()
     if use_dist:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -355,6 +359,9 @@ class DistJob:
         # local build + probe as one device interval (build is synchronous inside)
         self.probe_ms.append(self._ev[0].elapsed_time(self._ev[1]))
         self.build_ms.append(0.0)
+
+    def finish(self):
+        pass
 
 
 if __name__ == "__main__":

@@ -77,6 +77,7 @@ hipStream_t thread_stream(int dev) {
 struct BuildResources {
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    int64_t* h_minmax = nullptr;  // pinned: the key range read back without a staging copy
 };
 std::mutex g_pool_mu;
 std::unordered_map<int, std::vector<BuildResources>> g_pool;
@@ -92,7 +93,8 @@ bool acquire_resources(int dev, BuildResources* r) {
         }
     }
     return hipStreamCreateWithFlags(&r->stream, hipStreamNonBlocking) == hipSuccess &&
-           hipEventCreate(&r->ev0) == hipSuccess && hipEventCreate(&r->ev1) == hipSuccess;
+           hipEventCreate(&r->ev0) == hipSuccess && hipEventCreate(&r->ev1) == hipSuccess &&
+           hipHostMalloc((void**)&r->h_minmax, 2 * sizeof(int64_t), hipHostMallocDefault) == hipSuccess;
 }
 
 void release_resources(int dev, const BuildResources& r) {
@@ -253,6 +255,11 @@ struct hj_table {
     int64_t dmin = 0;
     uint64_t drange = 0;
     BuildResources res;
+    // the stream the build runs on: the producers' stream when every append came on the
+    // same one (a probe there needs no cross-stream wait), else res.stream
+    hipStream_t bstream = nullptr;
+    hipStream_t app_stream = nullptr;
+    int app_streams = 0;  // 0 none yet, 1 one stream, 2 several
     int64_t build_ns = 0;
     std::vector<std::pair<void*, size_t>> allocs;   // live for the table's lifetime
     std::vector<std::pair<void*, size_t>> scratch;  // build-only, released after the build
@@ -294,7 +301,7 @@ hj_status build_attempt(hj_table* t, const std::vector<Segment>& segs, double lf
     const int64_t total = t->total_rows;
     hj_status st;
     void* p;
-    hipStream_t s = t->res.stream;
+    hipStream_t s = t->bstream;
     Segment* d_segs;
     BuildCounters* ctr;
     int64_t* d_minmax;
@@ -312,9 +319,9 @@ hj_status build_attempt(hj_table* t, const std::vector<Segment>& segs, double lf
     ChunkGeom g{};
     bool dense = false;
     if (total > 0 && build_mode() == 0) {
-        int64_t mm[2];
+        int64_t* mm = t->res.h_minmax;
         HIP_TRY(launch_key_minmax(t->key_bytes, d_segs, (int)segs.size(), total, d_minmax, s));
-        HIP_TRY(hipMemcpyAsync(mm, d_minmax, sizeof(mm), hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipMemcpyAsync(mm, d_minmax, 2 * sizeof(int64_t), hipMemcpyDeviceToHost, s));
         HIP_TRY(hipStreamSynchronize(s));
         if (mm[0] <= mm[1]) {
             const uint64_t range = (uint64_t)mm[1] - (uint64_t)mm[0] + 1;
@@ -481,7 +488,8 @@ hj_status run_build(hj_table* t) {
     if (row > 0x7FFFFFF0ll) return fail(HJ_ERR_INVALID, "build side exceeds 2^31-16 rows on one device; shard it");
     if (t->has_ids && t->has_no_ids)
         return fail(HJ_ERR_INVALID, "explicit build ids must be given for every batch or none");
-    hipStream_t s = t->res.stream;
+    t->bstream = t->app_streams == 1 ? t->app_stream : t->res.stream;
+    hipStream_t s = t->bstream;
     // wait for the producers of borrowed device input
     for (int p = 0; p < t->parallelism; ++p)
         for (auto& hs : t->parts[p])
@@ -519,7 +527,7 @@ int64_t build_time_ns(hj_table* t) {
 
 // make stream s wait for the table's build
 hj_status wait_built(const hj_table* t, hipStream_t s) {
-    if (s != t->res.stream) HIP_TRY(hipStreamWaitEvent(s, t->res.ev1, 0));
+    if (s != t->bstream) HIP_TRY(hipStreamWaitEvent(s, t->res.ev1, 0));
     return HJ_OK;
 }
 
@@ -656,6 +664,15 @@ hj_status hj_build_append(hj_table* t, int partition, const void* keys, const ui
     HostSeg hs;
     hs.n = n;
     if (n == 0) return HJ_OK;
+    {
+        std::lock_guard<std::mutex> g(t->mu);
+        if (t->app_streams == 0) {
+            t->app_stream = (hipStream_t)stream;
+            t->app_streams = 1;
+        } else if (t->app_stream != (hipStream_t)stream) {
+            t->app_streams = 2;
+        }
+    }
     // the producer's stream: the build waits for its work (borrow) or copies in its order
     hipStream_t s = (hipStream_t)stream;
     const bool dev_in = (flags & HJ_INPUT_DEVICE) != 0;
