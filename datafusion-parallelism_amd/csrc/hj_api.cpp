@@ -309,7 +309,7 @@ hj_status build_attempt(hj_table* t, const std::vector<Segment>& segs, double lf
     d_segs = (Segment*)p;
     if ((st = dev_alloc(t, t->scratch, &p, sizeof(BuildCounters))) != HJ_OK) return st;
     ctr = (BuildCounters*)p;
-    if ((st = dev_alloc(t, t->scratch, &p, 2 * sizeof(int64_t))) != HJ_OK) return st;
+    if ((st = dev_alloc(t, t->scratch, &p, (2 + 2 * kMinmaxMaxBlocks) * sizeof(int64_t))) != HJ_OK) return st;
     d_minmax = (int64_t*)p;
     if (!segs.empty())
         HIP_TRY(hipMemcpyAsync(d_segs, segs.data(), sizeof(Segment) * segs.size(), hipMemcpyHostToDevice, s));

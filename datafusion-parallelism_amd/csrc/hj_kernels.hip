@@ -2361,13 +2361,41 @@ hipError_t launch_scan_u64(unsigned long long* a, int64_t len, void* scratch, un
 }
 
 template <typename K>
-__global__ void __launch_bounds__(1024)
+__global__ void __launch_bounds__(256)
 key_minmax_kernel(const Segment* __restrict__ segs, int nseg, int64_t total, long long* out) {
-    __shared__ long long s_mn[16], s_mx[16];
+    __shared__ long long s_mn[4], s_mx[4];
     long long mn = LLONG_MAX, mx = LLONG_MIN;
     for (int si = 0; si < nseg; ++si) {
         const Segment sg = segs[si];
         const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+        if (sizeof(K) == 8 && sg.valid == nullptr && (reinterpret_cast<uintptr_t>(sg.keys) & 15) == 0) {
+            // no nulls, 16-byte aligned int64 keys: 16-byte loads, eight in flight per lane
+            const v2i64* kp = reinterpret_cast<const v2i64*>(sg.keys);
+            const int64_t n2 = sg.n >> 1;
+            for (int64_t j0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j0 < n2; j0 += 8 * stride) {
+                v2i64 v[8];
+                bool in[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const int64_t j = j0 + u * stride;
+                    in[u] = j < n2;
+                    v[u] = in[u] ? kp[j] : v2i64{0, 0};
+                }
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    if (!in[u]) continue;
+                    const long long a = v[u].x, b = v[u].y;
+                    mn = min(mn, min(a, b));
+                    mx = max(mx, max(a, b));
+                }
+            }
+            if ((sg.n & 1) && blockIdx.x == 0 && threadIdx.x == 0) {
+                const long long k = (long long)ld_key<K>(sg.keys, sg.n - 1);
+                mn = min(mn, k);
+                mx = max(mx, k);
+            }
+            continue;
+        }
         for (int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i0 < sg.n; i0 += 4 * stride) {
             long long k[4];
             bool ok[4];
@@ -2397,29 +2425,53 @@ key_minmax_kernel(const Segment* __restrict__ segs, int nseg, int64_t total, lon
     }
     __syncthreads();
     if (threadIdx.x == 0) {
-        for (int w = 1; w < 16; ++w) {
+        for (int w = 1; w < 4; ++w) {
             mn = s_mn[w] < mn ? s_mn[w] : mn;
             mx = s_mx[w] > mx ? s_mx[w] : mx;
         }
-        atomicMin(&out[0], mn);
-        atomicMax(&out[1], mx);
+        // per-block partials (out[2 + 2b], out[3 + 2b]), reduced by minmax_final_kernel: a
+        // single word sustains ~88 atomics/us, so 1024 blocks' atomics would cost ~12 us
+        out[2 + 2 * blockIdx.x] = mn;
+        out[3 + 2 * blockIdx.x] = mx;
     }
 }
 
-__global__ void minmax_init_kernel(long long* out) {
-    out[0] = LLONG_MAX;
-    out[1] = LLONG_MIN;
+__global__ void __launch_bounds__(1024) minmax_final_kernel(long long* out, unsigned nblk) {
+    __shared__ long long s_mn[16], s_mx[16];
+    long long mn = LLONG_MAX, mx = LLONG_MIN;
+    for (unsigned b = threadIdx.x; b < nblk; b += blockDim.x) {
+        mn = min(mn, out[2 + 2 * b]);
+        mx = max(mx, out[3 + 2 * b]);
+    }
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+        mn = min(mn, (long long)__shfl_xor(mn, d, 64));
+        mx = max(mx, (long long)__shfl_xor(mx, d, 64));
+    }
+    if ((threadIdx.x & 63) == 0) {
+        s_mn[threadIdx.x >> 6] = mn;
+        s_mx[threadIdx.x >> 6] = mx;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < (int)(blockDim.x >> 6); ++w) {
+            mn = min(mn, s_mn[w]);
+            mx = max(mx, s_mx[w]);
+        }
+        out[0] = mn;
+        out[1] = mx;
+    }
 }
 
 hipError_t launch_key_minmax(int key_bytes, const Segment* d_segs, int nseg, int64_t total, int64_t* out,
                              hipStream_t s) {
-    minmax_init_kernel<<<1, 1, 0, s>>>((long long*)out);
-    // <= 256 blocks: each ends with one atomicMin/Max on the same two words (~88/us each)
-    const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>((total + 16383) / 16384, 256));
+    const unsigned grid =
+        (unsigned)std::max<int64_t>(1, std::min<int64_t>((total + 4095) / 4096, kMinmaxMaxBlocks));
     if (key_bytes == 8)
-        key_minmax_kernel<int64_t><<<grid, 1024, 0, s>>>(d_segs, nseg, total, (long long*)out);
+        key_minmax_kernel<int64_t><<<grid, 256, 0, s>>>(d_segs, nseg, total, (long long*)out);
     else
-        key_minmax_kernel<int32_t><<<grid, 1024, 0, s>>>(d_segs, nseg, total, (long long*)out);
+        key_minmax_kernel<int32_t><<<grid, 256, 0, s>>>(d_segs, nseg, total, (long long*)out);
+    minmax_final_kernel<<<1, 1024, 0, s>>>((long long*)out, grid);
     return hipGetLastError();
 }
 

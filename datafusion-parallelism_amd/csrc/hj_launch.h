@@ -49,7 +49,9 @@ hipError_t launch_build_frag(int key_bytes, const Segment* h_segs, int nseg, con
                              void* scratch, uint32_t* tile_base, const uint64_t* ids32, uint32_t* dense,
                              uint32_t* dup_rows, BigSeg* big, BuildCounters* ctr, const Segment* d_segs, int64_t total,
                              bool ids_as_rows, int big_grid, hipStream_t s);
-// min and max of the valid keys of the build segments -> out[0], out[1] (int64)
+// min and max of the valid keys of the build segments -> out[0], out[1] (int64);
+// out holds 2 + 2 * kMinmaxMaxBlocks int64 (per-block partials behind the result)
+constexpr int kMinmaxMaxBlocks = 4096;
 hipError_t launch_key_minmax(int key_bytes, const Segment* d_segs, int nseg, int64_t total, int64_t* out,
                              hipStream_t s);
 
