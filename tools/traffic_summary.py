@@ -23,15 +23,30 @@ PROBE_KERNELS = ("probe_fused_kernel", "probe_lookup_kernel", "probe_emit_kernel
                  "scan_down_kernel<unsigned long long>", "pp_partition_kernel", "pp_lookup_kernel",
                  "pp_count_kernel", "sl_partition_kernel", "sl_toff_transpose_kernel", "sl_lookup_kernel",
                  "sl_count_kernel", "sl_emit_kernel")
-BUILD_KERNELS = ("key_minmax_kernel", "coarse_hist_kernel", "coarse_scatter", "fine_hist_kernel", "fine_scatter",
-                 "chunk_starts_kernel", "scan_reduce_kernel<unsigned int>", "scan_down_kernel<unsigned int>",
-                 "chunk_build_kernel", "dup_sort_big_kernel")
+BUILD_KERNELS = ("key_minmax_kernel", "minmax_final_kernel", "coarse_hist_kernel", "coarse_scatter", "fine_hist_kernel",
+                 "fine_scatter", "chunk_starts_kernel", "scan_reduce_kernel<unsigned int>",
+                 "scan_down_kernel<unsigned int>", "chunk_build_kernel", "dup_sort_big_kernel", "sl_partition_kernel",
+                 "sl_toff_transpose_kernel", "dense_frag_build_kernel")
+
+
+# kernels that run in both phases (the dense build reuses the sliced probe's partition):
+# in dispatch order, the launch after a key_minmax_kernel belongs to the build
+SHARED = ("sl_partition_kernel", "sl_toff_transpose_kernel")
 
 
 def per_kernel(path):
+    rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Dispatch_Id"]))
     d = collections.defaultdict(list)
-    for r in csv.DictReader(open(path)):
-        d[r["Kernel_Name"]].append(float(r["Counter_Value"]) * 1024.0)
+    in_build = False
+    for r in rows:
+        name = r["Kernel_Name"]
+        if "key_minmax_kernel" in name:
+            in_build = True
+        elif "dense_frag_build_kernel" in name or "dup_sort_big_kernel" in name:
+            in_build = False
+        if any(k in name for k in SHARED):
+            name = ("build:" if in_build else "probe:") + name
+        d[name].append(float(r["Counter_Value"]) * 1024.0)
     return {k: sum(v) / len(v) for k, v in d.items()}, {k: len(v) for k, v in d.items()}
 
 
@@ -52,15 +67,17 @@ def main():
             "write_size_bytes": round(write.get(k, 0.0)),
         }
 
-    def phase(names):
-        sel = [v for k, v in kernels.items() if any(k.startswith(n) or n in k for n in names)]
+    def phase(names, tag):
+        sel = [v for k, v in kernels.items()
+               if any(k.startswith(n) or n in k for n in names) and not (k.split(":")[0] in ("build", "probe")
+                                                                          and k.split(":")[0] != tag)]
         raw = sum(v["fetch_size_bytes_raw"] for v in sel)
         w = sum(v["write_size_bytes"] for v in sel)
         return {"fetch_raw": raw, "fetch_x2": 2 * raw, "write": w,
                 "hbm_bytes_upper": 2 * raw + w, "hbm_bytes_lower": raw + w}
 
-    probe = phase(PROBE_KERNELS)
-    build = phase(BUILD_KERNELS)
+    probe = phase(PROBE_KERNELS, "probe")
+    build = phase(BUILD_KERNELS, "build")
     res = {
         "config": cfg,
         "source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes) of "
