@@ -2727,13 +2727,13 @@ int64_t probe_workspace(int64_t n) {
 }
 
 namespace {
-// slice width: 2^14 key values (64 KB of refs, two lookup workgroups per CU). 2^15
-// (DFP_HJ_SLICE_LOG=15) halves the (tile, slice) fragments but leaves one workgroup per
-// CU, and measured slower (C2 lookups 318 vs 276 us)
+// slice width: 2^15 key values (128 KB of refs, one lookup workgroup per CU): half the
+// (tile, slice) fragments of 2^14 (64 KB, two workgroups per CU); C2 lookups 221 vs
+// 243 us (DFP_HJ_SLICE_LOG=14 for the narrower slices)
 uint32_t sl_wlog() {
     static const uint32_t w = [] {
         const char* e = getenv("DFP_HJ_SLICE_LOG");
-        const int v = e ? atoi(e) : 14;
+        const int v = e ? atoi(e) : 15;
         return (uint32_t)std::min(std::max(v, 10), kSlWidthLogMax);
     }();
     return w;
@@ -2793,11 +2793,11 @@ hipError_t launch_probe_sliced(int key_bytes, const TableView& tv, const void* k
         if (valid) DFP_SLP(int32_t, true); else DFP_SLP(int32_t, false);
     }
 #undef DFP_SLP
-    // (slice, tile range) work items: about 2048 of them, so that the 512 resident
-    // workgroups (2 per CU) run several rounds and the tail stays short
+    // (slice, tile range) work items: about 1024 of them, so that the resident workgroups
+    // (one per CU at 128 KB slices) run several rounds and the tail stays short
     static const uint32_t target = [] {
         const char* ev = getenv("DFP_HJ_SLICED_ITEMS");
-        return ev ? (uint32_t)std::max(1, atoi(ev)) : 2048u;
+        return ev ? (uint32_t)std::max(1, atoi(ev)) : 1024u;
     }();
     uint32_t parts = std::max<uint32_t>(1, (target + nsl - 1) / nsl);
     parts = (uint32_t)std::min<int64_t>(parts, (nt + 63) / 64);

@@ -369,8 +369,9 @@ def sliced_mode(dfp):
 
 
 @pytest.mark.parametrize("nb,krange,np_,null_frac,key_type", [
-    (5_000_000, 2047 * 16384, 2_000_000, 0.0, "int64"),     # 2047 slices: the largest sliced table
-    (5_000_000, 2048 * 16384, 1_000_000, 0.0, "int64"),     # 2048 slices: falls back to fused
+    (9_000_000, 2047 * 32768, 2_000_000, 0.0, "int64"),     # 2047 slices: the largest sliced table
+    (9_000_000, 2048 * 32768, 1_000_000, 0.0, "int64"),     # 2048 slices: falls back to fused
+    (5_000_000, 2047 * 16384, 2_000_000, 0.0, "int64"),     # ~1024 slices
     (300_000, 1_000_000, 3_000_001, 0.02, "int32"),         # nulls, ragged last tile
     (2_000_000, 600_000, 1_500_000, 0.0, "int64"),          # duplicated keys (counts <= 15 and more)
 ])
