@@ -1583,20 +1583,26 @@ __global__ void pp_count_kernel(const uint32_t* __restrict__ cnt2, uint32_t nbin
 // lookups run out of LDS instead of as random device reads. The fused probe does one
 // random 4-byte read per in-range probe row and is bound by the memory system's random
 // request rate (~57 G/s for an Infinity-Cache-resident table); LDS serves
-// random reads at >10x that. Three launches:
-//   S1 sl_partition_kernel  per 16384-row tile: counting sort of the in-range rows by
-//                           slice (16384 consecutive key values) in LDS; writes one u32
-//                           entry per row (key offset in slice << 14 | row in tile) in
-//                           slice order into the tile's region, and the tile's slice
-//                           offsets (u16, tile-major)
-//   S2 sl_lookup_kernel     per (slice, tile range): the slice's 64 KB of refs in LDS,
-//                           then every tile's segment of that slice: ref = LDS[offset],
-//                           written beside the entry (res)
-//   S3 sl_emit_kernel       per tile: scatters its (entry, ref) into an LDS image of the
-//                           tile's refs, then the fused kernel's ordered emission (counts,
-//                           decoupled look-back, LDS-staged pair windows)
+// random reads at >10x that. The launches:
+//   S1  sl_partition_kernel   per 16384-row tile: counting sort of the in-range rows by
+//                             slice (2^wlog consecutive key values) in LDS; writes, in
+//                             slice order into the tile's region, each row's key offset
+//                             in its slice (u32) and row in the tile (u16), and the tile's
+//                             slice bounds (u16, tile-major)
+//   S1b sl_toff_transpose     the bounds regrouped per 64-tile block (coalesced in S2)
+//   S2  sl_lookup_kernel      per (slice, tile range): the slice's refs in LDS, then every
+//                             tile's fragment of that slice: the key offset is replaced in
+//                             place by its ref
+//   S3a sl_count_kernel       pairs per tile (one pass over its refs), then an exclusive
+//                             scan: tile output offsets. Counting inside S2 instead
+//                             (segmented wave sums per fragment) measured slower.
+//   S3b sl_emit_kernel        per tile (persistent, prefetching): its (row, ref) pairs
+//                             scattered into an LDS image of the tile's refs, then ordered
+//                             emission, 64 rows per wave step, one contiguous store run
+//                             per step (duplicates expanded over the lanes)
 // Pairs are identical to the fused probe's (canonical order); only where the table
-// lookups happen changes.
+// lookups happen changes. The dense build reuses S1/S1b on the build keys (8192-value
+// slices), and dense_frag_build_kernel gathers each block's rows from the fragments.
 // ---------------------------------------------------------------------------
 constexpr int kSlThreads = 1024;
 constexpr int kSlTileLog = 14;
