@@ -1716,6 +1716,15 @@ sl_toff_transpose_kernel(const uint16_t* __restrict__ toff, uint32_t nbins, int6
 // (bounds in the transposed layout, one block-wide scan over the tiles, owner tile of a
 // position by binary search in LDS) and builds exactly as dense_chunk_build_kernel.
 // ---------------------------------------------------------------------------
+// Blocks are dispatched round-robin over the 8 XCDs (block b on XCD b % 8). Work item of
+// block b: the XCD's own contiguous range of items, so that the blocks resident on one
+// XCD at a time take consecutive slices — whose fragments of a tile are adjacent in
+// memory and share lines in that XCD's L2.
+__device__ __forceinline__ uint32_t xcd_item(uint32_t b, uint32_t grid) {
+    const uint32_t x = b & 7, local = b >> 3, q = grid >> 3, r = grid & 7;
+    return x < r ? x * (q + 1) + local : r * (q + 1) + (x - r) * q + local;
+}
+
 constexpr int kFragMaxTiles = 2048;
 static_assert(kSlTile == kFragTileRows, "build tiles are the probe's tiles");
 
@@ -1736,7 +1745,7 @@ dense_frag_build_kernel(ChunkGeom g, uint32_t nblk, int64_t ntiles, const uint16
     __shared__ unsigned long long s_w[T / 64];
     __shared__ unsigned long long s_base, s_sp;
     __shared__ uint32_t s_carry;
-    const uint32_t c = blockIdx.x;
+    const uint32_t c = xcd_item(blockIdx.x, gridDim.x);  // key block (slice)
     const uint64_t cbase = (uint64_t)c * GV;  // key index of refs[0]
     const uint32_t nbins = nblk + 1;
     for (uint32_t i = threadIdx.x; i < GV; i += T) refs[i] = kMiss;
@@ -1909,8 +1918,8 @@ dense_frag_build_kernel(ChunkGeom g, uint32_t nblk, int64_t ntiles, const uint16
     for (uint32_t i = threadIdx.x; i < GV / 4; i += T) dst[i] = src[i];
 }
 
-// grid = nslices x parts; block b: slice b % nslices, tiles [part range) with
-// part = b / nslices. Each wave walks runs of 64 tiles: lane l reads tile l's segment
+// grid = nslices x parts; item i: slice i % nslices, tiles [part range) with
+// part = i / nslices. Each wave walks runs of 64 tiles: lane l reads tile l's segment
 // bounds, a wave scan flattens the segments over the lanes, and the owner lane of each
 // flattened position comes from a max-scan (DPP) of start markers dropped in LDS — no
 // per-position search; 8 entries per lane in flight.
@@ -1921,7 +1930,8 @@ sl_lookup_kernel(const uint32_t* __restrict__ dense, uint64_t drange, uint32_t w
     extern __shared__ __attribute__((aligned(16))) uint32_t s_tab[];  // 2^wlog refs
     __shared__ uint32_t s_base[kSlThreads];
     __shared__ __attribute__((aligned(16))) uint8_t s_own[(kSlThreads / 64) * kSlOwnWin];
-    const uint32_t s = blockIdx.x % nslices, part = blockIdx.x / nslices;
+    const uint32_t item = (dbg & 128) ? blockIdx.x : xcd_item(blockIdx.x, gridDim.x);
+    const uint32_t s = item % nslices, part = item / nslices;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     {
         const uint64_t base = (uint64_t)s << wlog;
