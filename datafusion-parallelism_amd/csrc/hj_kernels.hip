@@ -1612,12 +1612,13 @@ constexpr int kSlWidthLogMax = 15;                      // key values per slice:
 constexpr int kSlMaxSlices = 2047;                      // key ranges up to ~2^25 values
 constexpr int kSlOwnWin = 512;  // flattened segment positions per owner window (8 per lane)
 static_assert(kSlWidthLogMax + kSlTileLog <= 32, "entry = offset << tile bits | row");
+static_assert(kSlWidthLogMax <= 16 && kSlTileLog <= 16, "key offsets and rows leave as u16");
 
 template <typename K, bool HAS_VALID>
 __global__ void __launch_bounds__(kSlThreads, 8)  // 8 waves per SIMD = two workgroups per CU: <= 64 VGPRs
 sl_partition_kernel(int64_t dmin, uint64_t drange, uint32_t wlog, uint32_t nslices, const void* __restrict__ keys,
                     const uint8_t* __restrict__ valid, int64_t voff, int64_t n, bool vec,
-                    uint32_t* __restrict__ ent, uint16_t* __restrict__ rl, uint16_t* __restrict__ toff, int nt,
+                    uint16_t* __restrict__ ko, uint16_t* __restrict__ rl, uint16_t* __restrict__ toff, int nt,
                     int64_t tile_off, int64_t row_base, uint32_t* __restrict__ tile_base) {
     __shared__ __attribute__((aligned(16))) uint32_t s_ent[kSlTile];
     __shared__ uint32_t s_hist[2 * kSlThreads];  // bins 0..nslices (<= kSlMaxSlices + 1)
@@ -1665,21 +1666,21 @@ sl_partition_kernel(int64_t dmin, uint64_t drange, uint32_t wlog, uint32_t nslic
             if (sr[g][q] != 0xFFFFFFFFu)
                 s_ent[s_hist[sr[g][q] >> kSlTileLog] + (sr[g][q] & (kSlTile - 1))] = e[g][q];
     __syncthreads();
-    // entries leave split: the key offset (u32, replaced in place by its ref in S2) and
-    // the row in the tile (u16, read by S3)
-    uint32_t* dst = ent + gtile * kSlTile;
+    // entries leave split: the key offset in the slice (u16, read by S2) and the row in
+    // the tile (u16, read by S3)
+    uint16_t* dst = ko + gtile * kSlTile;
     uint16_t* dsr = rl + gtile * kSlTile;
     const uint32_t n4 = tot & ~3u;
     for (uint32_t i = threadIdx.x * 4; i < n4; i += kSlThreads * 4) {
         const uint4 v = *reinterpret_cast<const uint4*>(s_ent + i);
-        *reinterpret_cast<uint4*>(dst + i) = make_uint4(v.x >> kSlTileLog, v.y >> kSlTileLog, v.z >> kSlTileLog,
-                                                        v.w >> kSlTileLog);
         constexpr uint32_t m = kSlTile - 1;
+        *reinterpret_cast<uint2*>(dst + i) = make_uint2((v.x >> kSlTileLog) | ((v.y >> kSlTileLog) << 16),
+                                                        (v.z >> kSlTileLog) | ((v.w >> kSlTileLog) << 16));
         *reinterpret_cast<uint2*>(dsr + i) = make_uint2((v.x & m) | ((v.y & m) << 16), (v.z & m) | ((v.w & m) << 16));
     }
     if (threadIdx.x < (tot & 3u)) {
         const uint32_t v = s_ent[n4 + threadIdx.x];
-        dst[n4 + threadIdx.x] = v >> kSlTileLog;
+        dst[n4 + threadIdx.x] = (uint16_t)(v >> kSlTileLog);
         dsr[n4 + threadIdx.x] = (uint16_t)(v & (kSlTile - 1));
     }
 }
@@ -1731,7 +1732,7 @@ static_assert(kSlTile == kFragTileRows, "build tiles are the probe's tiles");
 template <int T, int RR>
 __global__ void __launch_bounds__(T)
 dense_frag_build_kernel(ChunkGeom g, uint32_t nblk, int64_t ntiles, const uint16_t* __restrict__ toffT,
-                        const uint32_t* __restrict__ ent, const uint16_t* __restrict__ rl,
+                        const uint16_t* __restrict__ ko, const uint16_t* __restrict__ rl,
                         const uint32_t* __restrict__ tile_base, const uint64_t* __restrict__ ids32,
                         uint32_t* __restrict__ dense, uint32_t* __restrict__ dup_rows, BigSeg* __restrict__ big,
                         BuildCounters* ctr, unsigned long long* __restrict__ spill) {
@@ -1784,7 +1785,7 @@ dense_frag_build_kernel(ChunkGeom g, uint32_t nblk, int64_t ntiles, const uint16
             if (s_to[mid] <= r) lo = mid; else hi = mid - 1;
         }
         const uint32_t pos = s_pb[lo] + r;
-        *idx = (int)ent[pos];
+        *idx = (int)ko[pos];
         const uint32_t rw = tile_base[lo] + rl[pos];
         *row = ids32 ? (uint32_t)ids32[rw] : rw;
     };
@@ -1926,7 +1927,8 @@ dense_frag_build_kernel(ChunkGeom g, uint32_t nblk, int64_t ntiles, const uint16
 __global__ void __launch_bounds__(kSlThreads)
 sl_lookup_kernel(const uint32_t* __restrict__ dense, uint64_t drange, uint32_t wlog, uint32_t nslices, int64_t ntiles,
                  uint32_t parts,
-                 uint32_t* __restrict__ ent, const uint16_t* __restrict__ toff, int dbg) {
+                 const uint16_t* __restrict__ ko, uint32_t* __restrict__ res, const uint16_t* __restrict__ toff,
+                 int dbg) {
     extern __shared__ __attribute__((aligned(16))) uint32_t s_tab[];  // 2^wlog refs
     __shared__ uint32_t s_base[kSlThreads];
     __shared__ __attribute__((aligned(16))) uint8_t s_own[(kSlThreads / 64) * kSlOwnWin];
@@ -1970,7 +1972,8 @@ sl_lookup_kernel(const uint32_t* __restrict__ dense, uint64_t drange, uint32_t w
         const uint32_t excl = incl - len;
         const uint32_t R = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
         sbase[lane] = (uint32_t)lane * kSlTile + st - excl;  // >= 0: excl <= lane * kSlTile
-        const uint32_t* tent = ent + tc * kSlTile;
+        const uint16_t* tko = ko + tc * kSlTile;
+        uint32_t* tres = res + tc * kSlTile;
         uint32_t carry = 0;  // owner (lane + 1) of the position before the window
         for (uint32_t w0 = 0; w0 < R; w0 += kSlOwnWin) {
             *reinterpret_cast<uint2*>(own + lane * 8) = make_uint2(0, 0);
@@ -1984,14 +1987,14 @@ sl_lookup_kernel(const uint32_t* __restrict__ dense, uint64_t drange, uint32_t w
                 const uint32_t o = max(wave_incl_max_dpp(own[u * 64 + lane]), carry);
                 carry = (uint32_t)__builtin_amdgcn_readlane((int)o, 63);
                 pos[u] = sbase[(o - 1) & 63] + r;
-                ev[u] = (dbg & 4) ? pos[u] * 2654435761u : (r < R ? tent[pos[u]] : 0u);
+                ev[u] = (dbg & 4) ? pos[u] * 2654435761u : (r < R ? (uint32_t)tko[pos[u]] : 0u);
             }
 #pragma unroll
             for (int u = 0; u < kSlOwnWin / 64; ++u) {
                 if (w0 + u * 64 + lane < R) {
                     const uint32_t v = s_tab[ev[u] & ((1u << wlog) - 1)];
-                    if (!(dbg & 8)) const_cast<uint32_t*>(tent)[pos[u]] = v;  // in place: the line was just read
-                    else if (v == 0x12345678u) ent[0] = v;  // keep the LDS read
+                    if (!(dbg & 8)) tres[pos[u]] = v;
+                    else if (v == 0x12345678u) res[0] = v;  // keep the LDS read
                 }
             }
             __builtin_amdgcn_wave_barrier();
@@ -2502,7 +2505,7 @@ bool frag_build_ok(const ChunkGeom& g, int64_t ftiles) {
 }
 int64_t frag_build_scratch_bytes(const ChunkGeom& g, int64_t ftiles, int64_t total) {
     const int64_t nbins = dense_blocks(g.nchunks) + 1;
-    return 4 * ftiles * kSlTile + 2 * ftiles * kSlTile + 2 * ftiles * nbins + 2 * ((ftiles + 63) & ~(int64_t)63) * nbins +
+    return 2 * ftiles * kSlTile + 2 * ftiles * kSlTile + 2 * ftiles * nbins + 2 * ((ftiles + 63) & ~(int64_t)63) * nbins +
            8 * total + 6 * 256;
 }
 
@@ -2515,7 +2518,7 @@ hipError_t launch_build_frag(int key_bytes, const Segment* h_segs, int nseg, con
     const uint32_t wlog = 31 - __builtin_clz(GV);
     auto a256 = [](uintptr_t x) { return (x + 255) & ~(uintptr_t)255; };
     uintptr_t p = a256((uintptr_t)scratch);
-    uint32_t* ent = (uint32_t*)p;  p = a256(p + 4 * ftiles * kSlTile);
+    uint16_t* ko = (uint16_t*)p;   p = a256(p + 2 * ftiles * kSlTile);
     uint16_t* rl = (uint16_t*)p;   p = a256(p + 2 * ftiles * kSlTile);
     uint16_t* toff = (uint16_t*)p; p = a256(p + 2 * ftiles * nbins);
     uint16_t* toffT = (uint16_t*)p; p = a256(p + 2 * ((ftiles + 63) & ~(int64_t)63) * nbins);
@@ -2529,7 +2532,7 @@ hipError_t launch_build_frag(int key_bytes, const Segment* h_segs, int nseg, con
         const uint64_t drange = (uint64_t)nblk * GV;
 #define DFP_BLP(KT, HV)                                                                                          \
     sl_partition_kernel<KT, HV><<<(unsigned)nt, kSlThreads, 0, s>>>(g.dmin, drange, wlog, nblk, sg.keys, sg.valid, \
-                                                                   sg.voff, sg.n, vec, ent, rl, toff, 0, t0,          \
+                                                                   sg.voff, sg.n, vec, ko, rl, toff, 0, t0,          \
                                                                    sg.row_base, tile_base)
         if (key_bytes == 8) {
             if (sg.valid) DFP_BLP(int64_t, true); else DFP_BLP(int64_t, false);
@@ -2541,7 +2544,7 @@ hipError_t launch_build_frag(int key_bytes, const Segment* h_segs, int nseg, con
     }
     sl_toff_transpose_kernel<<<(unsigned)((ftiles + 63) / 64 * ((nblk + kSlTrChunk) / kSlTrChunk)), 256, 0, s>>>(
         toff, nbins, ftiles, toffT);
-    dense_frag_build_kernel<1024, 8><<<nblk, 1024, 0, s>>>(g, nblk, ftiles, toffT, ent, rl, tile_base,
+    dense_frag_build_kernel<1024, 8><<<nblk, 1024, 0, s>>>(g, nblk, ftiles, toffT, ko, rl, tile_base,
                                                            ids_as_rows ? ids32 : nullptr, dense, dup_rows, big, ctr,
                                                            spill);
     dup_sort_big_kernel<<<big_grid, kBigThreads, 0, s>>>(dup_rows, big, ctr, d_segs, nseg, total, key_bytes,
@@ -2691,14 +2694,16 @@ ProbeWs probe_ws_layout(void* base, int64_t n) {
 }
 
 // sliced probe workspace (16384-row tiles): tcnt u64[nt + 2] | bsum (scan scratch) |
-// toff u16[nt][kSlMaxSlices + 1] | ent u32[nt * kSlTile] (key offsets, then refs) | rl u16[nt * kSlTile]
+// toff u16[nt][kSlMaxSlices + 1] | toffT | ko u16[nt * kSlTile] (key offsets) |
+// rl u16[nt * kSlTile] (rows in tile) | res u32[nt * kSlTile] (refs)
 struct SlicedWs {
     unsigned long long* tcnt;
     unsigned long long* bsum;
     uint16_t* toff;
     uint16_t* toffT;
-    uint32_t* ent;
+    uint16_t* ko;
     uint16_t* rl;
+    uint32_t* res;
     int64_t bytes;
 };
 SlicedWs sliced_ws_layout(void* base, int64_t n) {
@@ -2709,8 +2714,9 @@ SlicedWs sliced_ws_layout(void* base, int64_t n) {
     w.bsum = (unsigned long long*)p; p = al256(p + scan_scratch_bytes(nt));
     w.toff = (uint16_t*)p;            p = al256(p + 2 * nt * (kSlMaxSlices + 1));
     w.toffT = (uint16_t*)p;           p = al256(p + 2 * ((nt + 63) & ~(int64_t)63) * (kSlMaxSlices + 1));
-    w.ent = (uint32_t*)p;             p = al256(p + 4 * nt * kSlTile);
+    w.ko = (uint16_t*)p;              p = al256(p + 2 * nt * kSlTile);
     w.rl = (uint16_t*)p;              p = al256(p + 2 * nt * kSlTile);
+    w.res = (uint32_t*)p;             p = al256(p + 4 * nt * kSlTile);
     w.bytes = (int64_t)(p - (uintptr_t)base) + 256;
     return w;
 }
@@ -2802,7 +2808,7 @@ hipError_t launch_probe_sliced(int key_bytes, const TableView& tv, const void* k
     }();
 #define DFP_SLP(KT, HV)                                                                                      \
     sl_partition_kernel<KT, HV><<<(unsigned)nt, kSlThreads, 0, s>>>(tv.dmin, tv.drange, wlog, nsl, keys, valid, voff, n, \
-                                                                   vec, w.ent, w.rl, w.toff, sl_nt, 0, 0, nullptr)
+                                                                   vec, w.ko, w.rl, w.toff, sl_nt, 0, 0, nullptr)
     if (key_bytes == 8) {
         if (valid) DFP_SLP(int64_t, true); else DFP_SLP(int64_t, false);
     } else {
@@ -2828,15 +2834,15 @@ hipError_t launch_probe_sliced(int key_bytes, const TableView& tv, const void* k
     if (e != hipSuccess) return e;
     sl_toff_transpose_kernel<<<(unsigned)((nt + 63) / 64 * ((nsl + kSlTrChunk) / kSlTrChunk)), 256, 0, s>>>(
         w.toff, nsl + 1, nt, w.toffT);
-    sl_lookup_kernel<<<nsl * parts, kSlThreads, tab_lds, s>>>(tv.dense, tv.drange, wlog, nsl, nt, parts, w.ent, w.toffT,
-                                                              sl_dbg);
-    sl_count_kernel<<<(unsigned)nt, 256, 0, s>>>(tv, nsl, w.ent, w.toff, w.tcnt);
+    sl_lookup_kernel<<<nsl * parts, kSlThreads, tab_lds, s>>>(tv.dense, tv.drange, wlog, nsl, nt, parts, w.ko, w.res,
+                                                              w.toffT, sl_dbg);
+    sl_count_kernel<<<(unsigned)nt, 256, 0, s>>>(tv, nsl, w.res, w.toff, w.tcnt);
     e = launch_scan<unsigned long long>(w.tcnt, nt, w.bsum, (unsigned long long*)d_total, s);
     if (e != hipSuccess) return e;
     const bool ri = tv.row_ids != nullptr, pi = probe_ids != nullptr;
     const unsigned egrid = (unsigned)std::min<int64_t>(nt, (int64_t)sl_emit_wgs_per_cu() * sl_num_cus());
 #define DFP_SLE(RI, PI)                                                                                   \
-    sl_emit_kernel<RI, PI><<<egrid, kSlEmitThreads, 0, s>>>(tv, nsl, w.rl, w.ent, w.toff, probe_ids, w.tcnt, nt, \
+    sl_emit_kernel<RI, PI><<<egrid, kSlEmitThreads, 0, s>>>(tv, nsl, w.rl, w.res, w.toff, probe_ids, w.tcnt, nt, \
                                                            out_b, out_p, cap, sl_dbg)
     if (ri && pi) DFP_SLE(true, true);
     else if (ri) DFP_SLE(true, false);
