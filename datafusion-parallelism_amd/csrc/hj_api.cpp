@@ -77,7 +77,12 @@ hipStream_t thread_stream(int dev) {
 struct BuildResources {
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
-    int64_t* h_minmax = nullptr;  // pinned: the key range read back without a staging copy
+    hipEvent_t evp = nullptr;  // end of the table's latest probe launch (no timing)
+    // key-range mailbox, fine-grained host memory written by the minmax kernel: min, max,
+    // sequence number (the host spins on it instead of a copy + stream synchronize)
+    int64_t* h_minmax = nullptr;
+    int64_t* d_mbox = nullptr;  // its device address
+    int64_t mb_seq = 0;
 };
 std::mutex g_pool_mu;
 std::unordered_map<int, std::vector<BuildResources>> g_pool;
@@ -94,7 +99,10 @@ bool acquire_resources(int dev, BuildResources* r) {
     }
     return hipStreamCreateWithFlags(&r->stream, hipStreamNonBlocking) == hipSuccess &&
            hipEventCreate(&r->ev0) == hipSuccess && hipEventCreate(&r->ev1) == hipSuccess &&
-           hipHostMalloc((void**)&r->h_minmax, 2 * sizeof(int64_t), hipHostMallocDefault) == hipSuccess;
+           hipEventCreateWithFlags(&r->evp, hipEventDisableTiming) == hipSuccess &&
+           hipHostMalloc((void**)&r->h_minmax, 4 * sizeof(int64_t), hipHostMallocCoherent | hipHostMallocMapped) ==
+               hipSuccess &&
+           hipHostGetDevicePointer((void**)&r->d_mbox, r->h_minmax, 0) == hipSuccess;
 }
 
 void release_resources(int dev, const BuildResources& r) {
@@ -237,6 +245,7 @@ struct hj_table {
     int arrived = 0;
     bool built = false;
     bool sync_finish = false;  // some input was borrowed without HJ_BORROW_KEEP
+    mutable bool probed = false;  // res.evp marks the end of the latest probe
     hj_status build_st = HJ_OK;
     std::string build_err;
     bool has_ids = false, has_no_ids = false;
@@ -266,6 +275,23 @@ struct hj_table {
 };
 
 namespace {
+
+// Spin until the minmax kernel's mailbox shows `seq` (a few us after the kernel ends,
+// against ~20 us for copy + stream synchronize). Every 4096 polls the stream is queried:
+// an error returns; a finished stream whose mailbox never updated falls back to a copy.
+hipError_t wait_mailbox(int64_t* mm, int64_t seq, const int64_t* d_minmax, hipStream_t s) {
+    for (uint32_t i = 1;; ++i) {
+        if (__atomic_load_n(&mm[2], __ATOMIC_ACQUIRE) == seq) return hipSuccess;
+        if ((i & 4095) == 0) {
+            const hipError_t q = hipStreamQuery(s);
+            if (q == hipErrorNotReady) continue;
+            if (q != hipSuccess) return q;
+            if (__atomic_load_n(&mm[2], __ATOMIC_ACQUIRE) == seq) return hipSuccess;
+            return hipMemcpy(mm, d_minmax, 2 * sizeof(int64_t), hipMemcpyDeviceToHost);
+        }
+        __builtin_ia32_pause();
+    }
+}
 
 hj_status dev_alloc(hj_table* t, std::vector<std::pair<void*, size_t>>& list, void** p, size_t bytes) {
     if (bytes == 0) bytes = 64;
@@ -320,9 +346,9 @@ hj_status build_attempt(hj_table* t, const std::vector<Segment>& segs, double lf
     bool dense = false;
     if (total > 0 && build_mode() == 0) {
         int64_t* mm = t->res.h_minmax;
-        HIP_TRY(launch_key_minmax(t->key_bytes, d_segs, (int)segs.size(), total, d_minmax, s));
-        HIP_TRY(hipMemcpyAsync(mm, d_minmax, 2 * sizeof(int64_t), hipMemcpyDeviceToHost, s));
-        HIP_TRY(hipStreamSynchronize(s));
+        const int64_t seq = ++t->res.mb_seq;
+        HIP_TRY(launch_key_minmax(t->key_bytes, d_segs, (int)segs.size(), total, d_minmax, t->res.d_mbox, seq, s));
+        HIP_TRY(wait_mailbox(mm, seq, d_minmax, s));
         if (mm[0] <= mm[1]) {
             const uint64_t range = (uint64_t)mm[1] - (uint64_t)mm[0] + 1;
             const uint64_t nch = (range + (1u << kDenseShift) - 1) >> kDenseShift;
@@ -593,6 +619,9 @@ hj_status probe_impl(const hj_table* t, const void* keys, const uint8_t* valid, 
     if (wait_built(t, s) != HJ_OK) return HJ_ERR_HIP;
     HIP_TRY(launch_probe(t->key_bytes, view_of(t), keys, valid, voff, probe_ids, n, out_b, out_p, cap, d_total, ws,
                          s));
+    // hj_table_free waits for it before the table's blocks return to the cache
+    HIP_TRY(hipEventRecord(t->res.evp, s));
+    t->probed = true;
     return HJ_OK;
 }
 
@@ -968,8 +997,10 @@ hj_status hj_table_stream_wait(const hj_table* t, void* stream) {
 void hj_table_free(hj_table* t) {
     if (t == nullptr) return;
     (void)hipSetDevice(t->device);
-    // the blocks return to the cache (reused by any stream): the build must be done
+    // the blocks return to the cache (reused by any stream): the build and the latest
+    // probe must be done (earlier probes on other streams are the caller's to finish)
     if (t->built) (void)hipEventSynchronize(t->res.ev1);
+    if (t->probed) (void)hipEventSynchronize(t->res.evp);
     free_list(t, t->allocs);
     free_list(t, t->scratch);
     for (auto& part : t->parts)

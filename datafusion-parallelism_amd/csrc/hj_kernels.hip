@@ -1746,7 +1746,9 @@ dense_frag_build_kernel(ChunkGeom g, uint32_t nblk, int64_t ntiles, const uint16
     __shared__ unsigned long long s_w[T / 64];
     __shared__ unsigned long long s_base, s_sp;
     __shared__ uint32_t s_carry;
-    const uint32_t c = xcd_item(blockIdx.x, gridDim.x);  // key block (slice)
+    // key block (slice): plain block order. The XCD-contiguous order of the lookups puts
+    // the skewed distributions' heavy low blocks on one XCD (C3 build 0.35 -> 0.76 ms).
+    const uint32_t c = blockIdx.x;
     const uint64_t cbase = (uint64_t)c * GV;  // key index of refs[0]
     const uint32_t nbins = nblk + 1;
     for (uint32_t i = threadIdx.x; i < GV; i += T) refs[i] = kMiss;
@@ -2455,7 +2457,8 @@ key_minmax_kernel(const Segment* __restrict__ segs, int nseg, int64_t total, lon
     }
 }
 
-__global__ void __launch_bounds__(1024) minmax_final_kernel(long long* out, unsigned nblk) {
+__global__ void __launch_bounds__(1024) minmax_final_kernel(long long* out, unsigned nblk, long long* mbox,
+                                                            long long seq) {
     __shared__ long long s_mn[16], s_mx[16];
     long long mn = LLONG_MAX, mx = LLONG_MIN;
     for (unsigned b = threadIdx.x; b < nblk; b += blockDim.x) {
@@ -2479,18 +2482,23 @@ __global__ void __launch_bounds__(1024) minmax_final_kernel(long long* out, unsi
         }
         out[0] = mn;
         out[1] = mx;
+        if (mbox != nullptr) {  // host mailbox (fine-grained): result, then the sequence number
+            mbox[0] = mn;
+            mbox[1] = mx;
+            __hip_atomic_store(&mbox[2], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
     }
 }
 
 hipError_t launch_key_minmax(int key_bytes, const Segment* d_segs, int nseg, int64_t total, int64_t* out,
-                             hipStream_t s) {
+                             int64_t* mbox, int64_t seq, hipStream_t s) {
     const unsigned grid =
         (unsigned)std::max<int64_t>(1, std::min<int64_t>((total + 4095) / 4096, kMinmaxMaxBlocks));
     if (key_bytes == 8)
         key_minmax_kernel<int64_t><<<grid, 256, 0, s>>>(d_segs, nseg, total, (long long*)out);
     else
         key_minmax_kernel<int32_t><<<grid, 256, 0, s>>>(d_segs, nseg, total, (long long*)out);
-    minmax_final_kernel<<<1, 1024, 0, s>>>((long long*)out, grid);
+    minmax_final_kernel<<<1, 1024, 0, s>>>((long long*)out, grid, (long long*)mbox, (long long)seq);
     return hipGetLastError();
 }
 

@@ -50,10 +50,12 @@ hipError_t launch_build_frag(int key_bytes, const Segment* h_segs, int nseg, con
                              uint32_t* dup_rows, BigSeg* big, BuildCounters* ctr, const Segment* d_segs, int64_t total,
                              bool ids_as_rows, int big_grid, hipStream_t s);
 // min and max of the valid keys of the build segments -> out[0], out[1] (int64);
-// out holds 2 + 2 * kMinmaxMaxBlocks int64 (per-block partials behind the result)
+// out holds 2 + 2 * kMinmaxMaxBlocks int64 (per-block partials behind the result);
+// mbox (optional, fine-grained host memory): min, max, then seq stored with system-scope
+// release once both are visible
 constexpr int kMinmaxMaxBlocks = 4096;
 hipError_t launch_key_minmax(int key_bytes, const Segment* d_segs, int nseg, int64_t total, int64_t* out,
-                             hipStream_t s);
+                             int64_t* mbox, int64_t seq, hipStream_t s);
 
 // ---- probe ---------------------------------------------------------------
 // 0 auto (= direct), 1 direct, 2 partitioned (L2-resident pieces per XCD)

@@ -143,6 +143,8 @@ hj_status hj_table_lookup(const hj_table* t, int64_t key, uint64_t* rows, int64_
  * build_rows entries. */
 hj_status hj_table_chain_links(const hj_table* t, int64_t* prev, int64_t n);
 
+/* Waits for the table's build and its latest probe launch, then releases its memory
+ * (probes still running on other streams must be finished by the caller first). */
 void hj_table_free(hj_table* t);
 
 /* ---- probe: replaces get_matching_indices + equal_rows_arr inside
