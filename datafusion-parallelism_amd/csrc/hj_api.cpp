@@ -615,7 +615,6 @@ hj_status probe_impl(const hj_table* t, const void* keys, const uint8_t* valid, 
     if (n < 0 || n > 0xFFFFFFFFll) return fail(HJ_ERR_INVALID, "probe batch must have < 2^32 rows");
     if (cap < 0) return fail(HJ_ERR_INVALID, "negative capacity");
     if (reinterpret_cast<uintptr_t>(ws) & 7) return fail(HJ_ERR_INVALID, "workspace must be 8-byte aligned");
-    HIP_TRY(hipMemsetAsync((char*)ws + 8, 0, 8, s));  // error word
     if (wait_built(t, s) != HJ_OK) return HJ_ERR_HIP;
     HIP_TRY(launch_probe(t->key_bytes, view_of(t), keys, valid, voff, probe_ids, n, out_b, out_p, cap, d_total, ws,
                          s));

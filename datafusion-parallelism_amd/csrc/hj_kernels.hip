@@ -1610,7 +1610,7 @@ constexpr int kSlTile = 1 << kSlTileLog;                // probe rows per tile
 constexpr int kSlGroups = kSlTile / (kSlThreads * 4);  // 4 groups of 4096 rows
 constexpr int kSlWidthLogMax = 15;                      // key values per slice: 2^wlog <= 32768 (128 KB of refs)
 constexpr int kSlMaxSlices = 2047;                      // key ranges up to ~2^25 values
-constexpr int kSlOwnWin = 512;  // flattened segment positions per owner window (8 per lane)
+constexpr int kSlOwnWin = 1024;  // flattened segment positions per owner window (16 per lane)
 static_assert(kSlWidthLogMax + kSlTileLog <= 32, "entry = offset << tile bits | row");
 static_assert(kSlWidthLogMax <= 16 && kSlTileLog <= 16, "key offsets and rows leave as u16");
 
@@ -1619,7 +1619,8 @@ __global__ void __launch_bounds__(kSlThreads, 8)  // 8 waves per SIMD = two work
 sl_partition_kernel(int64_t dmin, uint64_t drange, uint32_t wlog, uint32_t nslices, const void* __restrict__ keys,
                     const uint8_t* __restrict__ valid, int64_t voff, int64_t n, bool vec,
                     uint16_t* __restrict__ ko, uint16_t* __restrict__ rl, uint16_t* __restrict__ toff, int nt,
-                    int64_t tile_off, int64_t row_base, uint32_t* __restrict__ tile_base) {
+                    int64_t tile_off, int64_t row_base, uint32_t* __restrict__ tile_base,
+                    unsigned long long* __restrict__ err_word) {  // probe: the caller's error word; build: null
     __shared__ __attribute__((aligned(16))) uint32_t s_ent[kSlTile];
     __shared__ uint32_t s_hist[2 * kSlThreads];  // bins 0..nslices (<= kSlMaxSlices + 1)
     __shared__ uint32_t s_w[kSlThreads / 64];
@@ -1628,6 +1629,8 @@ sl_partition_kernel(int64_t dmin, uint64_t drange, uint32_t wlog, uint32_t nslic
     const int64_t tile0 = tile * kSlTile;
     const uint32_t nbins = nslices + 1;  // bin nslices stays empty: its prefix is the total
     for (uint32_t b = threadIdx.x; b < 2 * kSlThreads; b += kSlThreads) s_hist[b] = 0;
+    // probe: zero the caller's error word (no memset launch)
+    if (err_word != nullptr && blockIdx.x == 0 && threadIdx.x == 0) *err_word = 0;
     __syncthreads();
     // per row: entry (offset << 14 | row) and (slice << 14 | rank in slice), ~0 = no entry
     uint32_t e[kSlGroups][4], sr[kSlGroups][4];
@@ -1925,7 +1928,7 @@ dense_frag_build_kernel(ChunkGeom g, uint32_t nblk, int64_t ntiles, const uint16
 // part = i / nslices. Each wave walks runs of 64 tiles: lane l reads tile l's segment
 // bounds, a wave scan flattens the segments over the lanes, and the owner lane of each
 // flattened position comes from a max-scan (DPP) of start markers dropped in LDS — no
-// per-position search; 8 entries per lane in flight.
+// per-position search; 16 entries per lane in flight, the next block's bounds prefetched.
 __global__ void __launch_bounds__(kSlThreads)
 sl_lookup_kernel(const uint32_t* __restrict__ dense, uint64_t drange, uint32_t wlog, uint32_t nslices, int64_t ntiles,
                  uint32_t parts,
@@ -1953,23 +1956,31 @@ sl_lookup_kernel(const uint32_t* __restrict__ dense, uint64_t drange, uint32_t w
     const int64_t nblk = (ntiles + 63) / 64;
     const int64_t ta = nblk * part / parts * 64, tb = min<int64_t>(nblk * (part + 1) / parts * 64, ntiles);
     const int64_t nbins = nslices + 1;
-    // per wave: owner markers of one 512-position window (u8: lane + 1 at the start of
-    // each non-empty segment) and each lane's segment base (tile-relative position - excl)
+    // per wave: owner markers of one window (u8: lane + 1 at the start of each non-empty
+    // segment) and each lane's segment base (tile-relative position - excl)
     uint8_t* own = s_own + wave * kSlOwnWin;
     uint32_t* sbase = s_base + wave * 64;
-    for (int64_t tc = ta + (int64_t)wave * 64; tc < tb; tc += (kSlThreads / 64) * 64) {
-        const int64_t t = tc + lane;
-        uint32_t st = 0, len = 0;
-        if (t < tb) {
+    constexpr int64_t kStep = (kSlThreads / 64) * 64;  // tiles between a wave's blocks
+    // segment bounds of the lane's tile in block tc (toffT), loaded one block ahead
+    auto bounds = [&](int64_t tc, uint32_t* st, uint32_t* len) {
+        *st = 0;
+        *len = 0;
+        if (tc + lane < tb) {
             if (dbg & 16) {
-                st = (s * 13) & 8191;
-                len = 13;
+                *st = (s * 13) & 8191;
+                *len = 13;
             } else {
-                const uint16_t* to = toff + ((tc >> 6) * nbins + s) * 64 + lane;  // toffT
-                st = to[0];
-                len = (uint32_t)to[64] - st;
+                const uint16_t* to = toff + ((tc >> 6) * nbins + s) * 64 + lane;
+                *st = to[0];
+                *len = (uint32_t)to[64] - *st;
             }
         }
+    };
+    uint32_t nst, nlen;
+    bounds(ta + (int64_t)wave * 64, &nst, &nlen);
+    for (int64_t tc = ta + (int64_t)wave * 64; tc < tb; tc += kStep) {
+        const uint32_t st = nst, len = nlen;
+        bounds(tc + kStep, &nst, &nlen);
         const uint32_t incl = wave_incl_scan_dpp(len);
         const uint32_t excl = incl - len;
         const uint32_t R = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
@@ -1978,7 +1989,8 @@ sl_lookup_kernel(const uint32_t* __restrict__ dense, uint64_t drange, uint32_t w
         uint32_t* tres = res + tc * kSlTile;
         uint32_t carry = 0;  // owner (lane + 1) of the position before the window
         for (uint32_t w0 = 0; w0 < R; w0 += kSlOwnWin) {
-            *reinterpret_cast<uint2*>(own + lane * 8) = make_uint2(0, 0);
+            static_assert(kSlOwnWin == 1024, "one uint4 of markers per lane");
+            *reinterpret_cast<uint4*>(own + lane * 16) = make_uint4(0, 0, 0, 0);
             __builtin_amdgcn_wave_barrier();
             if (len != 0 && excl >= w0 && excl < w0 + kSlOwnWin) own[excl - w0] = (uint8_t)(lane + 1);
             __builtin_amdgcn_wave_barrier();
@@ -2010,10 +2022,12 @@ __device__ __forceinline__ uint32_t sl_count(const TableView& tv, uint32_t r) {
     return r == kMiss ? 0u : !(r & kDupFlag) ? 1u : c4 ? c4 : tv.dup_rows[r & tv.off_mask];
 }
 
-// S3a: pairs per tile from its refs (one coalesced pass over res), scanned into the tiles'
-// output offsets before S3b. A decoupled look-back in S3b would wait on the inclusive
-// prefixes of the other ~500 tiles in flight, one 64-flag step (a memory round trip)
-// per 64 tiles: measured as ~40% of S3's time.
+// S3a: pairs per tile from its refs (one coalesced pass over res), then one workgroup
+// scans them into the tiles' output offsets (sl_scan_kernel). A decoupled look-back in
+// S3b instead would wait on the inclusive prefixes of the other ~500 tiles in flight,
+// one 64-flag step (a memory round trip) per 64 tiles: measured as ~40% of S3's time.
+// Scanning in the count kernel's last workgroup (done counter) costs a device-scope
+// release per workgroup — an L2 writeback each: 44 -> 240 us.
 __global__ void __launch_bounds__(256)
 sl_count_kernel(TableView tv, uint32_t nslices, const uint32_t* __restrict__ res, const uint16_t* __restrict__ toff,
                 unsigned long long* __restrict__ tcnt) {
@@ -2032,6 +2046,25 @@ sl_count_kernel(TableView tv, uint32_t nslices, const uint32_t* __restrict__ res
     if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = sum;
     __syncthreads();
     if (threadIdx.x == 0) tcnt[tile] = s_w[0] + s_w[1] + s_w[2] + s_w[3];
+}
+
+// exclusive scan in place of up to kSlScanOne tile counts by one workgroup (thread j
+// takes a contiguous run), and the total: one launch instead of the three-kernel scan
+constexpr int64_t kSlScanOne = 1 << 16;
+__global__ void __launch_bounds__(1024)
+sl_scan_kernel(unsigned long long* __restrict__ tcnt, int64_t ntiles, unsigned long long* __restrict__ total) {
+    __shared__ unsigned long long s_w[16];
+    const int64_t c = (ntiles + 1023) / 1024;
+    const int64_t a = min<int64_t>((int64_t)threadIdx.x * c, ntiles), b = min<int64_t>(a + c, ntiles);
+    unsigned long long run = 0, tot;
+    for (int64_t i = a; i < b; ++i) run += tcnt[i];
+    unsigned long long ex = block_excl_scan<unsigned long long>(run, s_w, &tot);
+    for (int64_t i = a; i < b; ++i) {
+        const unsigned long long v = tcnt[i];
+        tcnt[i] = ex;
+        ex += v;
+    }
+    if (threadIdx.x == 0) *total = tot;
 }
 
 // S3b: 512 threads per tile, two workgroups per CU (64 KB of LDS and <= 128 VGPRs each).
@@ -2541,7 +2574,7 @@ hipError_t launch_build_frag(int key_bytes, const Segment* h_segs, int nseg, con
 #define DFP_BLP(KT, HV)                                                                                          \
     sl_partition_kernel<KT, HV><<<(unsigned)nt, kSlThreads, 0, s>>>(g.dmin, drange, wlog, nblk, sg.keys, sg.valid, \
                                                                    sg.voff, sg.n, vec, ko, rl, toff, 0, t0,          \
-                                                                   sg.row_base, tile_base)
+                                                                   sg.row_base, tile_base, nullptr)
         if (key_bytes == 8) {
             if (sg.valid) DFP_BLP(int64_t, true); else DFP_BLP(int64_t, false);
         } else {
@@ -2701,12 +2734,12 @@ ProbeWs probe_ws_layout(void* base, int64_t n) {
     return w;
 }
 
-// sliced probe workspace (16384-row tiles): tcnt u64[nt + 2] | bsum (scan scratch) |
+// sliced probe workspace (16384-row tiles): tcnt u64[nt + 2] (counts, then offsets) | bsum |
 // toff u16[nt][kSlMaxSlices + 1] | toffT | ko u16[nt * kSlTile] (key offsets) |
 // rl u16[nt * kSlTile] (rows in tile) | res u32[nt * kSlTile] (refs)
 struct SlicedWs {
     unsigned long long* tcnt;
-    unsigned long long* bsum;
+    unsigned long long* bsum;  // scan scratch past kSlScanOne tiles
     uint16_t* toff;
     uint16_t* toffT;
     uint16_t* ko;
@@ -2810,13 +2843,16 @@ hipError_t launch_probe_sliced(int key_bytes, const TableView& tv, const void* k
     SlicedWs w = sliced_ws_layout((void*)(((uintptr_t)workspace + 255) & ~(uintptr_t)255), n);
     const bool vec = (reinterpret_cast<uintptr_t>(keys) & 15) == 0;
     hipError_t e = hipSuccess;
+    // workspace + 8: the caller's error word, zeroed by S1 (the layout starts >= 256 bytes in)
+    unsigned long long* err_word = reinterpret_cast<unsigned long long*>((char*)workspace + 8);
     static const int sl_nt = [] {  // 1: nontemporal probe-key loads in S1
         const char* ev = getenv("DFP_HJ_SL_NT");
         return ev ? atoi(ev) : 0;
     }();
 #define DFP_SLP(KT, HV)                                                                                      \
     sl_partition_kernel<KT, HV><<<(unsigned)nt, kSlThreads, 0, s>>>(tv.dmin, tv.drange, wlog, nsl, keys, valid, voff, n, \
-                                                                   vec, w.ko, w.rl, w.toff, sl_nt, 0, 0, nullptr)
+                                                                   vec, w.ko, w.rl, w.toff, sl_nt, 0, 0, nullptr, \
+                                                                   err_word)
     if (key_bytes == 8) {
         if (valid) DFP_SLP(int64_t, true); else DFP_SLP(int64_t, false);
     } else {
@@ -2845,8 +2881,12 @@ hipError_t launch_probe_sliced(int key_bytes, const TableView& tv, const void* k
     sl_lookup_kernel<<<nsl * parts, kSlThreads, tab_lds, s>>>(tv.dense, tv.drange, wlog, nsl, nt, parts, w.ko, w.res,
                                                               w.toffT, sl_dbg);
     sl_count_kernel<<<(unsigned)nt, 256, 0, s>>>(tv, nsl, w.res, w.toff, w.tcnt);
-    e = launch_scan<unsigned long long>(w.tcnt, nt, w.bsum, (unsigned long long*)d_total, s);
-    if (e != hipSuccess) return e;
+    if (nt <= kSlScanOne) {
+        sl_scan_kernel<<<1, 1024, 0, s>>>(w.tcnt, nt, (unsigned long long*)d_total);
+    } else {
+        e = launch_scan<unsigned long long>(w.tcnt, nt, w.bsum, (unsigned long long*)d_total, s);
+        if (e != hipSuccess) return e;
+    }
     const bool ri = tv.row_ids != nullptr, pi = probe_ids != nullptr;
     const unsigned egrid = (unsigned)std::min<int64_t>(nt, (int64_t)sl_emit_wgs_per_cu() * sl_num_cus());
 #define DFP_SLE(RI, PI)                                                                                   \
@@ -2865,6 +2905,14 @@ hipError_t launch_probe(int key_bytes, const TableView& tv, const void* keys, co
                         const uint32_t* probe_ids, int64_t n, uint64_t* out_b, uint32_t* out_p, int64_t cap,
                         int64_t* d_total, void* workspace, hipStream_t s) {
     const int64_t nt = probe_tiles(n);
+    const int mode = probe_mode();
+    const uint32_t nsl = sl_slices(tv);
+    if (nt > 0 && tv.dense != nullptr && nsl >= 1 && nsl <= (uint32_t)kSlMaxSlices &&
+        (mode == 4 || (mode == 0 && sl_auto(tv, n))))
+        return launch_probe_sliced(key_bytes, tv, keys, valid, voff, probe_ids, n, out_b, out_p, cap, d_total,
+                                   workspace, s);  // S1 zeroes the error word
+    hipError_t e0 = hipMemsetAsync((char*)workspace + 8, 0, 8, s);  // error word (fused look-back)
+    if (e0 != hipSuccess) return e0;
     if (nt == 0) return hipMemsetAsync(d_total, 0, sizeof(int64_t), s);
     // align the layout on the workspace base
     ProbeWs w = probe_ws_layout((void*)(((uintptr_t)workspace + 255) & ~(uintptr_t)255), n);
@@ -2873,11 +2921,6 @@ hipError_t launch_probe(int key_bytes, const TableView& tv, const void* keys, co
     // it lifts the L2 hit rate of the lookups from ~19% to ~73% but per-lane scattered
     // line accesses stay bound by the L2 request rate, and its two extra passes cost
     // more than it saves at C2 (profiles/r01_*). DESIGN.md §5.
-    const int mode = probe_mode();
-    const uint32_t nsl = sl_slices(tv);
-    if (tv.dense != nullptr && nsl >= 1 && nsl <= (uint32_t)kSlMaxSlices && (mode == 4 || (mode == 0 && sl_auto(tv, n))))
-        return launch_probe_sliced(key_bytes, tv, keys, valid, voff, probe_ids, n, out_b, out_p, cap, d_total,
-                                   workspace, s);
     const bool part = mode == 2 && tv.dense == nullptr;  // dense tables: no pieces to partition by
     if (mode == 0 || mode == 3 || mode == 4 || (mode == 2 && !part)) {
         static const int fused_nt = [] {  // 1: keys nontemporal, 2: pair stores nontemporal
