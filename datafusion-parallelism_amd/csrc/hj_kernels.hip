@@ -1926,9 +1926,13 @@ dense_frag_build_kernel(ChunkGeom g, uint32_t nblk, int64_t ntiles, const uint16
 
 // grid = nslices x parts; item i: slice i % nslices, tiles [part range) with
 // part = i / nslices. Each wave walks runs of 64 tiles: lane l reads tile l's segment
-// bounds, a wave scan flattens the segments over the lanes, and the owner lane of each
-// flattened position comes from a max-scan (DPP) of start markers dropped in LDS — no
-// per-position search; 16 entries per lane in flight, the next block's bounds prefetched.
+// bounds (prefetched one run ahead), a wave scan flattens the segments over the lanes,
+// and the non-empty segments' bases are listed by rank. A 64-bit mask per 64 flattened
+// positions marks the segment starts (LDS atomicOr); a position's owner rank is the
+// number of starts at or before it (mbcnt) — no per-position search, no scan per row.
+// Entries and refs go through buffer descriptors: 32-bit offsets, and positions past
+// the run's total take an out-of-range offset (load 0, store dropped) instead of a
+// branch. 16 entries per lane in flight.
 __global__ void __launch_bounds__(kSlThreads)
 sl_lookup_kernel(const uint32_t* __restrict__ dense, uint64_t drange, uint32_t wlog, uint32_t nslices, int64_t ntiles,
                  uint32_t parts,
@@ -1936,7 +1940,7 @@ sl_lookup_kernel(const uint32_t* __restrict__ dense, uint64_t drange, uint32_t w
                  int dbg) {
     extern __shared__ __attribute__((aligned(16))) uint32_t s_tab[];  // 2^wlog refs
     __shared__ uint32_t s_base[kSlThreads];
-    __shared__ __attribute__((aligned(16))) uint8_t s_own[(kSlThreads / 64) * kSlOwnWin];
+    __shared__ unsigned long long s_mask[kSlThreads / 64][kSlOwnWin / 64];
     const uint32_t item = (dbg & 128) ? blockIdx.x : xcd_item(blockIdx.x, gridDim.x);
     const uint32_t s = item % nslices, part = item / nslices;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -1956,24 +1960,20 @@ sl_lookup_kernel(const uint32_t* __restrict__ dense, uint64_t drange, uint32_t w
     const int64_t nblk = (ntiles + 63) / 64;
     const int64_t ta = nblk * part / parts * 64, tb = min<int64_t>(nblk * (part + 1) / parts * 64, ntiles);
     const int64_t nbins = nslices + 1;
-    // per wave: owner markers of one window (u8: lane + 1 at the start of each non-empty
-    // segment) and each lane's segment base (tile-relative position - excl)
-    uint8_t* own = s_own + wave * kSlOwnWin;
+    // per wave: the non-empty segments' bases (tile-relative position - excl) by rank, and
+    // one 64-bit start mask per 64-position row of the window
     uint32_t* sbase = s_base + wave * 64;
+    unsigned long long* smask = s_mask[wave];
     constexpr int64_t kStep = (kSlThreads / 64) * 64;  // tiles between a wave's blocks
+    constexpr uint32_t kOob = 0x3FFFFFF0u;              // entry index past every range: load 0, no store
     // segment bounds of the lane's tile in block tc (toffT), loaded one block ahead
     auto bounds = [&](int64_t tc, uint32_t* st, uint32_t* len) {
         *st = 0;
         *len = 0;
         if (tc + lane < tb) {
-            if (dbg & 16) {
-                *st = (s * 13) & 8191;
-                *len = 13;
-            } else {
-                const uint16_t* to = toff + ((tc >> 6) * nbins + s) * 64 + lane;
-                *st = to[0];
-                *len = (uint32_t)to[64] - *st;
-            }
+            const uint16_t* to = toff + ((tc >> 6) * nbins + s) * 64 + lane;
+            *st = to[0];
+            *len = (uint32_t)to[64] - *st;
         }
     };
     uint32_t nst, nlen;
@@ -1984,34 +1984,51 @@ sl_lookup_kernel(const uint32_t* __restrict__ dense, uint64_t drange, uint32_t w
         const uint32_t incl = wave_incl_scan_dpp(len);
         const uint32_t excl = incl - len;
         const uint32_t R = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
-        sbase[lane] = (uint32_t)lane * kSlTile + st - excl;  // >= 0: excl <= lane * kSlTile
-        const uint16_t* tko = ko + tc * kSlTile;
-        uint32_t* tres = res + tc * kSlTile;
-        uint32_t carry = 0;  // owner (lane + 1) of the position before the window
+        // rank of the lane among the non-empty segments (their starts, in position order)
+        const unsigned long long ne = __ballot(len != 0);
+        const uint32_t rank =
+            __builtin_amdgcn_mbcnt_hi((uint32_t)(ne >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)ne, 0u));
+        if (len != 0) sbase[rank] = (uint32_t)lane * kSlTile + st - excl;  // >= 0: excl <= lane * kSlTile
+        // the 64 tiles' regions as buffers (wave-uniform bases): 32-bit offsets, and an
+        // out-of-range offset turns a position past R into a dropped access
+        const int64_t tcu = (int64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)tc) |
+                            ((int64_t)__builtin_amdgcn_readfirstlane((int)(tc >> 32)) << 32);
+        const __amdgpu_buffer_rsrc_t rko =
+            __builtin_amdgcn_make_buffer_rsrc((void*)(ko + tcu * kSlTile), 0, 64 * kSlTile * 2, 0x00020000);
+        const __amdgpu_buffer_rsrc_t rres =
+            __builtin_amdgcn_make_buffer_rsrc((void*)(res + tcu * kSlTile), 0, 64 * kSlTile * 4, 0x00020000);
+        uint32_t kb = 0;  // segments started before the current row
         for (uint32_t w0 = 0; w0 < R; w0 += kSlOwnWin) {
-            static_assert(kSlOwnWin == 1024, "one uint4 of markers per lane");
-            *reinterpret_cast<uint4*>(own + lane * 16) = make_uint4(0, 0, 0, 0);
+            if (lane < kSlOwnWin / 64) smask[lane] = 0;
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
             __builtin_amdgcn_wave_barrier();
-            if (len != 0 && excl >= w0 && excl < w0 + kSlOwnWin) own[excl - w0] = (uint8_t)(lane + 1);
+            if (len != 0 && excl >= w0 && excl < w0 + kSlOwnWin)
+                atomicOr(&smask[(excl - w0) >> 6], 1ull << ((excl - w0) & 63));
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
             __builtin_amdgcn_wave_barrier();
-            uint32_t pos[kSlOwnWin / 64], ev[kSlOwnWin / 64];
+            uint32_t off[kSlOwnWin / 64], ev[kSlOwnWin / 64];  // off: the entry's index or kOob
 #pragma unroll
             for (int u = 0; u < kSlOwnWin / 64; ++u) {
                 const uint32_t r = w0 + u * 64 + lane;
-                const uint32_t o = max(wave_incl_max_dpp(own[u * 64 + lane]), carry);
-                carry = (uint32_t)__builtin_amdgcn_readlane((int)o, 63);
-                pos[u] = sbase[(o - 1) & 63] + r;
-                ev[u] = (dbg & 4) ? pos[u] * 2654435761u : (r < R ? (uint32_t)tko[pos[u]] : 0u);
+                const unsigned long long m = smask[u];  // the same word for every lane
+                const uint32_t mlo = __builtin_amdgcn_readfirstlane((uint32_t)m);
+                const uint32_t mhi = __builtin_amdgcn_readfirstlane((uint32_t)(m >> 32));
+                const unsigned long long mu = ((unsigned long long)mhi << 32) | mlo;
+                // owner rank: segments started at or before this position, minus one
+                const unsigned long long m1 = mu >> 1;
+                const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m1 >> 32),
+                                                                  __builtin_amdgcn_mbcnt_lo((uint32_t)m1, 0u));
+                const uint32_t k = kb + (uint32_t)(mu & 1) + below - 1;
+                kb += (uint32_t)__builtin_popcountll(mu);
+                const uint32_t ps = sbase[k & 63] + r;
+                off[u] = r < R ? ps : kOob;
+                ev[u] = __builtin_amdgcn_raw_buffer_load_b16(rko, (int)(off[u] * 2), 0, 0);
             }
 #pragma unroll
             for (int u = 0; u < kSlOwnWin / 64; ++u) {
-                if (w0 + u * 64 + lane < R) {
-                    const uint32_t v = s_tab[ev[u] & ((1u << wlog) - 1)];
-                    if (!(dbg & 8)) tres[pos[u]] = v;
-                    else if (v == 0x12345678u) res[0] = v;  // keep the LDS read
-                }
+                const uint32_t v = s_tab[ev[u] & ((1u << wlog) - 1)];
+                __builtin_amdgcn_raw_buffer_store_b32(v, rres, (int)(off[u] * 4), 0, 0);
             }
-            __builtin_amdgcn_wave_barrier();
         }
     }
 }
