@@ -1610,7 +1610,7 @@ constexpr int kSlTile = 1 << kSlTileLog;                // probe rows per tile
 constexpr int kSlGroups = kSlTile / (kSlThreads * 4);  // 4 groups of 4096 rows
 constexpr int kSlWidthLogMax = 15;                      // key values per slice: 2^wlog <= 32768 (128 KB of refs)
 constexpr int kSlMaxSlices = 2047;                      // key ranges up to ~2^25 values
-constexpr int kSlOwnWin = 1024;  // flattened segment positions per owner window (16 per lane)
+constexpr int kSlOwnWin = 2048;  // flattened segment positions per owner window (32 per lane)
 static_assert(kSlWidthLogMax + kSlTileLog <= 32, "entry = offset << tile bits | row");
 static_assert(kSlWidthLogMax <= 16 && kSlTileLog <= 16, "key offsets and rows leave as u16");
 
@@ -1932,7 +1932,7 @@ dense_frag_build_kernel(ChunkGeom g, uint32_t nblk, int64_t ntiles, const uint16
 // number of starts at or before it (mbcnt) — no per-position search, no scan per row.
 // Entries and refs go through buffer descriptors: 32-bit offsets, and positions past
 // the run's total take an out-of-range offset (load 0, store dropped) instead of a
-// branch. 16 entries per lane in flight.
+// branch. 32 entries per lane in flight.
 __global__ void __launch_bounds__(kSlThreads)
 sl_lookup_kernel(const uint32_t* __restrict__ dense, uint64_t drange, uint32_t wlog, uint32_t nslices, int64_t ntiles,
                  uint32_t parts,
