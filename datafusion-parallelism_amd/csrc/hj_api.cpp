@@ -337,17 +337,23 @@ hj_status build_attempt(hj_table* t, const std::vector<Segment>& segs, double lf
     ctr = (BuildCounters*)p;
     if ((st = dev_alloc(t, t->scratch, &p, (2 + 2 * kMinmaxMaxBlocks) * sizeof(int64_t))) != HJ_OK) return st;
     d_minmax = (int64_t*)p;
-    if (!segs.empty())
-        HIP_TRY(hipMemcpyAsync(d_segs, segs.data(), sizeof(Segment) * segs.size(), hipMemcpyHostToDevice, s));
-    HIP_TRY(hipMemsetAsync(ctr, 0, sizeof(BuildCounters), s));
+    // few segments: the key-range kernel publishes them and zeroes the counters
+    const bool minmax = total > 0 && build_mode() == 0;
+    const bool by_arg = minmax && segs.size() <= (size_t)kArgSegs;
+    if (!by_arg) {
+        if (!segs.empty())
+            HIP_TRY(hipMemcpyAsync(d_segs, segs.data(), sizeof(Segment) * segs.size(), hipMemcpyHostToDevice, s));
+        HIP_TRY(hipMemsetAsync(ctr, 0, sizeof(BuildCounters), s));
+    }
 
     // layout: a dense key range gets the direct-addressed table (one u32 ref per key value)
     ChunkGeom g{};
     bool dense = false;
-    if (total > 0 && build_mode() == 0) {
+    if (minmax) {
         int64_t* mm = t->res.h_minmax;
         const int64_t seq = ++t->res.mb_seq;
-        HIP_TRY(launch_key_minmax(t->key_bytes, d_segs, (int)segs.size(), total, d_minmax, t->res.d_mbox, seq, s));
+        HIP_TRY(launch_key_minmax(t->key_bytes, segs.data(), d_segs, (int)segs.size(), by_arg ? ctr : nullptr, total,
+                                  d_minmax, t->res.d_mbox, seq, s));
         HIP_TRY(wait_mailbox(mm, seq, d_minmax, s));
         if (mm[0] <= mm[1]) {
             const uint64_t range = (uint64_t)mm[1] - (uint64_t)mm[0] + 1;

@@ -2433,11 +2433,17 @@ hipError_t launch_scan_u64(unsigned long long* a, int64_t len, void* scratch, un
 
 template <typename K>
 __global__ void __launch_bounds__(256)
-key_minmax_kernel(const Segment* __restrict__ segs, int nseg, int64_t total, long long* out) {
+key_minmax_kernel(const Segment* __restrict__ segs, SegArgs sa, int nseg, int64_t total, long long* out,
+                  BuildCounters* __restrict__ ctr) {
     __shared__ long long s_mn[4], s_mx[4];
     long long mn = LLONG_MAX, mx = LLONG_MIN;
+    const bool by_arg = ctr != nullptr;  // segments in the argument; block 0 publishes them
+    if (by_arg && blockIdx.x == 0) {
+        if (threadIdx.x < (unsigned)nseg) const_cast<Segment*>(segs)[threadIdx.x] = sa.s[threadIdx.x];
+        if (threadIdx.x == 0) *ctr = BuildCounters{};
+    }
     for (int si = 0; si < nseg; ++si) {
-        const Segment sg = segs[si];
+        const Segment sg = by_arg ? sa.s[si] : segs[si];
         const int64_t stride = (int64_t)gridDim.x * blockDim.x;
         if (sizeof(K) == 8 && sg.valid == nullptr && (reinterpret_cast<uintptr_t>(sg.keys) & 15) == 0) {
             // no nulls, 16-byte aligned int64 keys: 16-byte loads, eight in flight per lane
@@ -2540,14 +2546,19 @@ __global__ void __launch_bounds__(1024) minmax_final_kernel(long long* out, unsi
     }
 }
 
-hipError_t launch_key_minmax(int key_bytes, const Segment* d_segs, int nseg, int64_t total, int64_t* out,
-                             int64_t* mbox, int64_t seq, hipStream_t s) {
+hipError_t launch_key_minmax(int key_bytes, const Segment* h_segs, Segment* d_segs, int nseg, BuildCounters* ctr,
+                             int64_t total, int64_t* out, int64_t* mbox, int64_t seq, hipStream_t s) {
     const unsigned grid =
         (unsigned)std::max<int64_t>(1, std::min<int64_t>((total + 4095) / 4096, kMinmaxMaxBlocks));
+    SegArgs sa{};
+    if (ctr != nullptr) {
+        if (nseg > kArgSegs) return hipErrorInvalidValue;
+        for (int i = 0; i < nseg; ++i) sa.s[i] = h_segs[i];
+    }
     if (key_bytes == 8)
-        key_minmax_kernel<int64_t><<<grid, 256, 0, s>>>(d_segs, nseg, total, (long long*)out);
+        key_minmax_kernel<int64_t><<<grid, 256, 0, s>>>(d_segs, sa, nseg, total, (long long*)out, ctr);
     else
-        key_minmax_kernel<int32_t><<<grid, 256, 0, s>>>(d_segs, nseg, total, (long long*)out);
+        key_minmax_kernel<int32_t><<<grid, 256, 0, s>>>(d_segs, sa, nseg, total, (long long*)out, ctr);
     minmax_final_kernel<<<1, 1024, 0, s>>>((long long*)out, grid, (long long*)mbox, (long long)seq);
     return hipGetLastError();
 }

@@ -53,9 +53,16 @@ hipError_t launch_build_frag(int key_bytes, const Segment* h_segs, int nseg, con
 // out holds 2 + 2 * kMinmaxMaxBlocks int64 (per-block partials behind the result);
 // mbox (optional, fine-grained host memory): min, max, then seq stored with system-scope
 // release once both are visible
+// Up to kArgSegs segments travel as a kernel argument: the kernel's first block then
+// stores them to d_segs and zeroes *ctr (no H2D copy or memset launches before the build);
+// with more, the caller copies d_segs and zeroes ctr itself and passes ctr = nullptr.
 constexpr int kMinmaxMaxBlocks = 4096;
-hipError_t launch_key_minmax(int key_bytes, const Segment* d_segs, int nseg, int64_t total, int64_t* out,
-                             int64_t* mbox, int64_t seq, hipStream_t s);
+constexpr int kArgSegs = 16;
+struct SegArgs {
+    Segment s[kArgSegs];
+};
+hipError_t launch_key_minmax(int key_bytes, const Segment* h_segs, Segment* d_segs, int nseg, BuildCounters* ctr,
+                             int64_t total, int64_t* out, int64_t* mbox, int64_t seq, hipStream_t s);
 
 // ---- probe ---------------------------------------------------------------
 // 0 auto (= direct), 1 direct, 2 partitioned (L2-resident pieces per XCD)
