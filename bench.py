@@ -82,8 +82,11 @@ def gen_inputs(cfg, rank, world, dev):
 class SingleGpuJoin:
     """One step = build + probe on this GPU (no exchange)."""
 
-    def __init__(self, bk, pk, dev):
+    def __init__(self, bk, pk, dev, same_stream=False):
         self.bk, self.pk, self.dev = bk, pk, dev
+        # builds run on their own stream: a probe partitions its rows while its table is
+        # still being built (the library orders the first table read after the build)
+        self.bstream = None if same_stream else torch.cuda.Stream(dev)
         P = pk.numel()
         self.ws = torch.empty(HashTable.workspace_bytes(P), dtype=torch.uint8, device=dev)
         self.d_total = torch.zeros(1, dtype=torch.int64, device=dev)
@@ -102,17 +105,22 @@ class SingleGpuJoin:
         self.op = torch.empty(self.cap, dtype=torch.int32, device=self.dev)
 
     def step(self):
-        """One join: build a fresh table, probe it, all on the current stream. Returns
-        without waiting for the device; the previous step's table is then collected —
-        its probe is complete, since this step's finish() read back this build's key
-        range, which the stream orders after that probe. Steps thus overlap their host
-        work (table set-up, launches) with the previous step's device work, as a
-        pipeline of joins does."""
+        """One join: build a fresh table (on the build stream), probe it (on the current
+        stream). Returns without waiting for the device, then collects the previous step
+        (waiting for its probe). Steps thus overlap their host work (table set-up,
+        launches) with the previous step's device work, and a probe's partition with its
+        build, as a pipeline of joins does. probe_ms runs from the probe's launch to its
+        end (with the wait for the rest of the build)."""
         t = HashTable(1, "int64", self.dev.index or 0)
-        t.append(0, self.bk)
-        t.finish(0)  # device build (runs on asynchronously for a direct-addressed table)
         s = torch.cuda.current_stream(self.dev)
-        t.stream_wait(s.cuda_stream)  # probe_ms times the probe alone
+        if self.bstream is not None:
+            with torch.cuda.stream(self.bstream):
+                t.append(0, self.bk)
+                t.finish(0)  # device build (runs on asynchronously for a direct-addressed table)
+        else:
+            t.append(0, self.bk)
+            t.finish(0)
+            t.stream_wait(s.cuda_stream)  # probe_ms times the probe alone
         ev = self.evs[self.k & 1]
         self.k += 1
         ev[0].record(s)
@@ -129,7 +137,7 @@ class SingleGpuJoin:
         if self.prev is None:
             return
         t, ev = self.prev
-        ev[1].synchronize()  # already complete: no wait
+        ev[1].synchronize()
         self.probe_ms.append(ev[0].elapsed_time(ev[1]))
         self.build_ms.append(t.build_ns() / 1e6)
         t.close()
@@ -140,6 +148,25 @@ class SingleGpuJoin:
         self.matches = int(self.d_total.item())
         if self.matches > self.cap:
             raise RuntimeError("output capacity too small")
+        # after the timed loop: the probe alone on a finished table (the roofline's
+        # launch time; inside the pipeline a probe also waits for the end of its build)
+        t = HashTable(1, "int64", self.dev.index or 0)
+        t.append(0, self.bk)
+        t.finish(0)
+        s = torch.cuda.current_stream(self.dev)
+        t.stream_wait(s.cuda_stream)
+        torch.cuda.synchronize(self.dev)
+        self.probe_in_step_ms = self.probe_ms
+        self.probe_ms = []
+        for _ in range(5):
+            ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+            ev[0].record(s)
+            t.probe_async(self.pk.data_ptr(), self.pk.numel(), self.ob.data_ptr(), self.op.data_ptr(), self.cap,
+                          self.d_total.data_ptr(), self.ws.data_ptr(), s.cuda_stream)
+            ev[1].record(s)
+            ev[1].synchronize()
+            self.probe_ms.append(ev[0].elapsed_time(ev[1]))
+        t.close()
 
 
 def cpu_baseline(cfg, nthreads=8):
@@ -209,6 +236,8 @@ def main():
                     help="use the radix-exchange path even with one rank (testing)")
     ap.add_argument("--chunks", type=int, default=4,
                     help="multi-GPU: probe-side chunks whose exchange overlaps the previous chunk's probe")
+    ap.add_argument("--same-stream", action="store_true",
+                    help="run each build on the probe's stream (no build/probe overlap)")
     ap.add_argument("--sync-steps", action="store_true",
                     help="synchronize the device after every step (no host/device overlap between steps)")
     ap.add_argument("--no-compress-keys", action="store_true",
@@ -238,7 +267,7 @@ def main():
 
     use_dist = world > 1 or args.force_dist
     if not use_dist:
-        job = SingleGpuJoin(bk, pk, dev)
+        job = SingleGpuJoin(bk, pk, dev, same_stream=args.same_stream)
     else:
         from datafusion_parallelism_amd.distributed import DistributedHashJoin
 
@@ -336,6 +365,8 @@ def main():
             },
             "probe_mrows_s": round(P / (probe_ms / 1e3) / 1e6, 1),
             "probe_ms": round(probe_ms, 4),
+            "probe_ms_in_step": (round(float(np.median(job.probe_in_step_ms)), 4)
+                                 if getattr(job, "probe_in_step_ms", None) else None),
             "build_ms": round(build_ms, 4),
             # host time per step: with --sync-steps the whole step, otherwise the launch
             # interval of the pipelined steps (not a device time)

@@ -621,9 +621,9 @@ hj_status probe_impl(const hj_table* t, const void* keys, const uint8_t* valid, 
     if (n < 0 || n > 0xFFFFFFFFll) return fail(HJ_ERR_INVALID, "probe batch must have < 2^32 rows");
     if (cap < 0) return fail(HJ_ERR_INVALID, "negative capacity");
     if (reinterpret_cast<uintptr_t>(ws) & 7) return fail(HJ_ERR_INVALID, "workspace must be 8-byte aligned");
-    if (wait_built(t, s) != HJ_OK) return HJ_ERR_HIP;
+    // the probe orders itself after the build (on another stream) at its first table read
     HIP_TRY(launch_probe(t->key_bytes, view_of(t), keys, valid, voff, probe_ids, n, out_b, out_p, cap, d_total, ws,
-                         s));
+                         s != t->bstream ? t->res.ev1 : nullptr, s));
     // hj_table_free waits for it before the table's blocks return to the cache
     HIP_TRY(hipEventRecord(t->res.evp, s));
     t->probed = true;

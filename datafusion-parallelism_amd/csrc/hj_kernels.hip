@@ -2865,7 +2865,8 @@ bool sl_auto(const TableView& tv, int64_t n) {
 
 hipError_t launch_probe_sliced(int key_bytes, const TableView& tv, const void* keys, const uint8_t* valid,
                                int64_t voff, const uint32_t* probe_ids, int64_t n, uint64_t* out_b,
-                               uint32_t* out_p, int64_t cap, int64_t* d_total, void* workspace, hipStream_t s) {
+                               uint32_t* out_p, int64_t cap, int64_t* d_total, void* workspace, hipEvent_t built,
+                               hipStream_t s) {
     const int64_t nt = (n + kSlTile - 1) / kSlTile;
     const uint32_t nsl = sl_slices(tv), wlog = sl_wlog();
     SlicedWs w = sliced_ws_layout((void*)(((uintptr_t)workspace + 255) & ~(uintptr_t)255), n);
@@ -2906,6 +2907,10 @@ hipError_t launch_probe_sliced(int key_bytes, const TableView& tv, const void* k
     if (e != hipSuccess) return e;
     sl_toff_transpose_kernel<<<(unsigned)((nt + 63) / 64 * ((nsl + kSlTrChunk) / kSlTrChunk)), 256, 0, s>>>(
         w.toff, nsl + 1, nt, w.toffT);
+    if (built != nullptr) {  // S1/S1b read no table memory: the build may still be running
+        e = hipStreamWaitEvent(s, built, 0);
+        if (e != hipSuccess) return e;
+    }
     sl_lookup_kernel<<<nsl * parts, kSlThreads, tab_lds, s>>>(tv.dense, tv.drange, wlog, nsl, nt, parts, w.ko, w.res,
                                                               w.toffT, sl_dbg);
     sl_count_kernel<<<(unsigned)nt, 256, 0, s>>>(tv, nsl, w.res, w.toff, w.tcnt);
@@ -2931,14 +2936,18 @@ hipError_t launch_probe_sliced(int key_bytes, const TableView& tv, const void* k
 
 hipError_t launch_probe(int key_bytes, const TableView& tv, const void* keys, const uint8_t* valid, int64_t voff,
                         const uint32_t* probe_ids, int64_t n, uint64_t* out_b, uint32_t* out_p, int64_t cap,
-                        int64_t* d_total, void* workspace, hipStream_t s) {
+                        int64_t* d_total, void* workspace, hipEvent_t built, hipStream_t s) {
     const int64_t nt = probe_tiles(n);
     const int mode = probe_mode();
     const uint32_t nsl = sl_slices(tv);
     if (nt > 0 && tv.dense != nullptr && nsl >= 1 && nsl <= (uint32_t)kSlMaxSlices &&
         (mode == 4 || (mode == 0 && sl_auto(tv, n))))
         return launch_probe_sliced(key_bytes, tv, keys, valid, voff, probe_ids, n, out_b, out_p, cap, d_total,
-                                   workspace, s);  // S1 zeroes the error word
+                                   workspace, built, s);  // S1 zeroes the error word
+    if (built != nullptr) {
+        const hipError_t ew = hipStreamWaitEvent(s, built, 0);
+        if (ew != hipSuccess) return ew;
+    }
     hipError_t e0 = hipMemsetAsync((char*)workspace + 8, 0, 8, s);  // error word (fused look-back)
     if (e0 != hipSuccess) return e0;
     if (nt == 0) return hipMemsetAsync(d_total, 0, sizeof(int64_t), s);

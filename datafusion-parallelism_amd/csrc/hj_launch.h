@@ -71,10 +71,13 @@ int get_probe_mode();
 int64_t probe_tiles(int64_t n);
 int64_t probe_workspace(int64_t n);
 // workspace: [0,8) unused, [8,16) error word, then tile counts/offsets, then per-row refs
+// built (nullable): the table's build-complete event, waited on by `s` before the first
+// kernel that reads the table — the sliced probe partitions and regroups its rows first,
+// so a build still running on another stream overlaps them
 hipError_t launch_probe(int key_bytes, const TableView& tv, const void* keys, const uint8_t* valid,
                         int64_t voff, const uint32_t* probe_ids, int64_t n, uint64_t* out_b,
                         uint32_t* out_p, int64_t cap, int64_t* d_total, void* workspace,
-                        hipStream_t s);
+                        hipEvent_t built, hipStream_t s);
 
 // ---- table queries -------------------------------------------------------
 hipError_t launch_table_stats(const TableView& tv,
