@@ -392,6 +392,46 @@ def test_sliced_probe_parity(dfp, oracle_mod, sliced_mode, nb, krange, np_, null
     assert_same(b, p, ob, op)
 
 
+@pytest.mark.parametrize("mode", [4, 3])
+def test_probe_overlaps_build_on_other_stream(dfp, oracle_mod, mode):
+    """Build on stream A, probe launched at once on stream B (no host or stream sync in
+    between): the probe orders itself after the build only at its first table read (the
+    sliced probe's partition runs while the build may still be running). Several
+    back-to-back tables, as the bench's pipeline does."""
+    L = dfp.load()
+    old_p = L.hj_set_probe_mode(mode)
+    try:
+        rng = np.random.default_rng(5 + mode)
+        dev = torch.device("cuda", 0)
+        nb, krange, np_ = 3_000_000, 4_000_000, 4_000_000
+        sa, sb = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+        ws = torch.empty(dfp.HashTable.workspace_bytes(np_), dtype=torch.uint8, device=dev)
+        for it in range(3):
+            bk = rng.integers(0, krange, nb).astype(np.int64)
+            pk = rng.integers(-1000, krange + 1000, np_).astype(np.int64)
+            bk_d, pk_d = torch.from_numpy(bk).to(dev), torch.from_numpy(pk).to(dev)
+            torch.cuda.synchronize(dev)
+            cap = 2 * np_
+            ob = torch.empty(cap, dtype=torch.int64, device=dev)
+            op = torch.empty(cap, dtype=torch.int32, device=dev)
+            dt = torch.zeros(1, dtype=torch.int64, device=dev)
+            torch.cuda.synchronize(dev)
+            with dfp.HashTable(1, "int64", 0) as t:
+                with torch.cuda.stream(sa):
+                    t.append(0, bk_d)
+                    t.finish(0)
+                t.probe_async(pk_d.data_ptr(), np_, ob.data_ptr(), op.data_ptr(), cap, dt.data_ptr(),
+                              ws.data_ptr(), sb.cuda_stream)
+                sb.synchronize()
+                total = int(dt.item())
+                b = ob[:total].cpu().numpy().astype(np.uint64)
+                p = op[:total].cpu().numpy().view(np.uint32)
+            xb, xp = oracle_mod.inner_join(bk, pk)
+            assert_same(b, p, xb, xp)
+    finally:
+        L.hj_set_probe_mode(old_p)
+
+
 def test_sliced_probe_ids_unaligned(dfp, oracle_mod, sliced_mode):
     """hj_probe_async_ids (explicit probe ids, the multi-GPU path) on a key pointer that
     is 8- but not 16-byte aligned (scalar key loads), with explicit build ids."""
