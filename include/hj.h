@@ -165,7 +165,9 @@ void hj_pairs_free(hj_pairs* p);
  * `workspace` (device, 8-byte aligned, hj_probe_workspace_bytes(n) bytes) must not be
  * shared by concurrent calls; its bytes 8..15 (uint64) are non-zero after the call if
  * the fused probe's bounded look-back spin gave up (results invalid; never observed).
- * No host synchronisation, no allocation. */
+ * No host synchronisation, no allocation. A table built on another stream needs no
+ * wait from the caller: the probe orders itself after the build at its first table read
+ * (the sliced probe partitions its rows first, overlapping the build). */
 int64_t hj_probe_workspace_bytes(int64_t n);
 hj_status hj_probe_async(const hj_table* t, const void* keys, const uint8_t* validity,
                          int64_t validity_offset, int64_t n, uint64_t* out_build,
