@@ -2166,18 +2166,24 @@ sl_emit_kernel(TableView tv, uint32_t nslices, const uint16_t* __restrict__ rl, 
                 const int loc = row_w + k + lane;
                 const uint32_t r = s_ref[loc];
                 const uint32_t c = sl_count(tv, r);
-                const uint32_t incl = wave_incl_scan_dpp(c);  // < 2^32: 64 rows of < 2^26 rows each
-                const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
                 const int64_t row = tile0 + loc;
+                uint32_t total;
                 if (__ballot(c > 1) == 0) {
+                    // at most one pair per row: the prefix is a popcount of the hit mask
+                    const unsigned long long hit = __ballot(c != 0);
+                    total = (uint32_t)__builtin_popcountll(hit);
                     if (c) {
-                        const unsigned long long o = pos + incl - 1;
+                        const uint32_t below = __builtin_amdgcn_mbcnt_hi(
+                            (uint32_t)(hit >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)hit, 0u));
+                        const unsigned long long o = pos + below;
                         if (o < (unsigned long long)cap) {
                             out_b[o] = HAS_ROW_IDS ? tv.row_ids[r] : (uint64_t)r;
                             out_p[o] = HAS_PROBE_IDS ? probe_ids[row] : (uint32_t)row;
                         }
                     }
                 } else {
+                    const uint32_t incl = wave_incl_scan_dpp(c);  // < 2^32: 64 rows of < 2^26 rows each
+                    total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
                     const uint32_t excl = incl - c;
                     uint32_t carry = 0;
                     for (uint32_t w0 = 0; w0 < total; w0 += 64) {
