@@ -1579,7 +1579,7 @@ __global__ void pp_count_kernel(const uint32_t* __restrict__ cnt2, uint32_t nbin
 }
 
 // ---------------------------------------------------------------------------
-// sliced probe (direct-addressed tables of <= kSlMaxSlices x 16384 key values): the
+// sliced probe (direct-addressed tables of <= kSlMaxSlices x 2^wlog key values): the
 // lookups run out of LDS instead of as random device reads. The fused probe does one
 // random 4-byte read per in-range probe row and is bound by the memory system's random
 // request rate (~57 G/s for an Infinity-Cache-resident table); LDS serves
@@ -1587,15 +1587,17 @@ __global__ void pp_count_kernel(const uint32_t* __restrict__ cnt2, uint32_t nbin
 //   S1  sl_partition_kernel   per 16384-row tile: counting sort of the in-range rows by
 //                             slice (2^wlog consecutive key values) in LDS; writes, in
 //                             slice order into the tile's region, each row's key offset
-//                             in its slice (u32) and row in the tile (u16), and the tile's
+//                             in its slice (u16) and row in the tile (u16), and the tile's
 //                             slice bounds (u16, tile-major)
 //   S1b sl_toff_transpose     the bounds regrouped per 64-tile block (coalesced in S2)
-//   S2  sl_lookup_kernel      per (slice, tile range): the slice's refs in LDS, then every
-//                             tile's fragment of that slice: the key offset is replaced in
-//                             place by its ref
-//   S3a sl_count_kernel       pairs per tile (one pass over its refs), then an exclusive
-//                             scan: tile output offsets. Counting inside S2 instead
-//                             (segmented wave sums per fragment) measured slower.
+//   S2  sl_lookup_kernel      per (slice, tile range), XCD-contiguous item order: the
+//                             slice's refs in LDS, then every tile's fragment of that
+//                             slice; each entry's ref goes to the refs array (u32) at the
+//                             entry's position. The probe waits for a build on another
+//                             stream only here (S1/S1b read no table memory).
+//   S3a sl_count_kernel       pairs per tile (one pass over its refs), then sl_scan_kernel
+//                             (one workgroup): tile output offsets. Counting inside S2
+//                             instead (segmented wave sums per fragment) measured slower.
 //   S3b sl_emit_kernel        per tile (persistent, prefetching): its (row, ref) pairs
 //                             scattered into an LDS image of the tile's refs, then ordered
 //                             emission, 64 rows per wave step, one contiguous store run
