@@ -14,6 +14,7 @@ import os
 import shutil
 import subprocess
 import sys
+from concurrent.futures import ThreadPoolExecutor
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
@@ -64,17 +65,20 @@ def build(force: bool = False, verbose: bool = False) -> str:
     objdir = os.path.join(HERE, "build")
     os.makedirs(objdir, exist_ok=True)
     os.makedirs(LIBDIR, exist_ok=True)
-    objs = []
+    objs, cmds = [], []
     for src in SOURCES_HIP:
         obj = os.path.join(objdir, src + ".o")
-        _run([hipcc, f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17", "-I", INCLUDE,
-              "-c", os.path.join(CSRC, src), "-o", obj], verbose)
+        cmds.append([hipcc, f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17", "-I", INCLUDE,
+                     "-c", os.path.join(CSRC, src), "-o", obj])
         objs.append(obj)
     for src in SOURCES_CPP:
         obj = os.path.join(objdir, src + ".o")
-        _run(["g++", "-O2", "-fPIC", "-std=c++17", "-D__HIP_PLATFORM_AMD__", "-I", INCLUDE,
-              "-I", os.path.join(rocm, "include"), "-c", os.path.join(CSRC, src), "-o", obj], verbose)
+        cmds.append(["g++", "-O2", "-fPIC", "-std=c++17", "-D__HIP_PLATFORM_AMD__", "-I", INCLUDE,
+                     "-I", os.path.join(rocm, "include"), "-c", os.path.join(CSRC, src), "-o", obj])
         objs.append(obj)
+    # the translation units compile independently: in parallel
+    with ThreadPoolExecutor(max_workers=len(cmds)) as ex:
+        list(ex.map(lambda c: _run(c, verbose), cmds))
     tmp = LIB + ".tmp"
     _run(["g++", "-shared", "-o", tmp, *objs, f"-L{tlib}", "-lamdhip64", f"-Wl,-rpath,{tlib}",
           "-Wl,--no-undefined", "-lpthread"], verbose)

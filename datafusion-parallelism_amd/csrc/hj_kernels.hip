@@ -1595,9 +1595,11 @@ __global__ void pp_count_kernel(const uint32_t* __restrict__ cnt2, uint32_t nbin
 //                             slice; each entry's ref goes to the refs array (u32) at the
 //                             entry's position. The probe waits for a build on another
 //                             stream only here (S1/S1b read no table memory).
-//   S3a sl_count_kernel       pairs per tile (one pass over its refs), then sl_scan_kernel
-//                             (one workgroup): tile output offsets. Counting inside S2
-//                             instead (segmented wave sums per fragment) measured slower.
+//   S3a sl_scan_kernel        (one workgroup): tile output offsets from the tiles' pair
+//                             counts. S1 writes a tile's in-range rows as its count; S2
+//                             adds count - 1 for every entry whose key is missing or
+//                             duplicated (LDS atomics per owner tile, then one atomic per
+//                             tile and run), so no pass re-reads the refs to count them.
 //   S3b sl_emit_kernel        per tile (persistent, prefetching): its (row, ref) pairs
 //                             scattered into an LDS image of the tile's refs, then ordered
 //                             emission, 64 rows per wave step, one contiguous store run
@@ -1622,7 +1624,8 @@ sl_partition_kernel(int64_t dmin, uint64_t drange, uint32_t wlog, uint32_t nslic
                     const uint8_t* __restrict__ valid, int64_t voff, int64_t n, bool vec,
                     uint16_t* __restrict__ ko, uint16_t* __restrict__ rl, uint16_t* __restrict__ toff, int nt,
                     int64_t tile_off, int64_t row_base, uint32_t* __restrict__ tile_base,
-                    unsigned long long* __restrict__ err_word) {  // probe: the caller's error word; build: null
+                    unsigned long long* __restrict__ err_word,  // probe: the caller's error word; build: null
+                    unsigned long long* __restrict__ tcnt) {    // probe: the tile's in-range rows; build: null
     __shared__ __attribute__((aligned(16))) uint32_t s_ent[kSlTile];
     __shared__ uint32_t s_hist[2 * kSlThreads];  // bins 0..nslices (<= kSlMaxSlices + 1)
     __shared__ uint32_t s_w[kSlThreads / 64];
@@ -1664,6 +1667,9 @@ sl_partition_kernel(int64_t dmin, uint64_t drange, uint32_t wlog, uint32_t nslic
     uint16_t* to = toff + gtile * (int64_t)nbins;
     for (uint32_t b = threadIdx.x; b < nbins; b += kSlThreads) to[b] = (uint16_t)s_hist[b];
     if (tile_base != nullptr && threadIdx.x == 0) tile_base[gtile] = (uint32_t)(row_base + tile0);  // build only
+    // probe: the tile's pair count starts as its in-range rows; S2 adds count - 1 for
+    // every entry whose key is missing (-1) or duplicated (+count - 1)
+    if (tcnt != nullptr && threadIdx.x == 0) tcnt[gtile] = tot;
 #pragma unroll
     for (int g = 0; g < kSlGroups; ++g)
 #pragma unroll
@@ -1936,13 +1942,16 @@ dense_frag_build_kernel(ChunkGeom g, uint32_t nblk, int64_t ntiles, const uint16
 // the run's total take an out-of-range offset (load 0, store dropped) instead of a
 // branch. 32 entries per lane in flight.
 __global__ void __launch_bounds__(kSlThreads)
-sl_lookup_kernel(const uint32_t* __restrict__ dense, uint64_t drange, uint32_t wlog, uint32_t nslices, int64_t ntiles,
-                 uint32_t parts,
+sl_lookup_kernel(TableView tv, uint32_t wlog, uint32_t nslices, int64_t ntiles, uint32_t parts,
                  const uint16_t* __restrict__ ko, uint32_t* __restrict__ res, const uint16_t* __restrict__ toff,
-                 int dbg) {
+                 unsigned long long* __restrict__ tcnt, int dbg) {
     extern __shared__ __attribute__((aligned(16))) uint32_t s_tab[];  // 2^wlog refs
     __shared__ uint32_t s_base[kSlThreads];
+    __shared__ uint32_t s_lane[kSlThreads];   // per wave: tile lane of each non-empty segment, by rank
+    __shared__ int s_corr[kSlThreads];        // per wave: pair-count correction of each of its 64 tiles
     __shared__ unsigned long long s_mask[kSlThreads / 64][kSlOwnWin / 64];
+    const uint32_t* __restrict__ dense = tv.dense;
+    const uint64_t drange = tv.drange;
     const uint32_t item = (dbg & 128) ? blockIdx.x : xcd_item(blockIdx.x, gridDim.x);
     const uint32_t s = item % nslices, part = item / nslices;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -1965,9 +1974,13 @@ sl_lookup_kernel(const uint32_t* __restrict__ dense, uint64_t drange, uint32_t w
     // per wave: the non-empty segments' bases (tile-relative position - excl) by rank, and
     // one 64-bit start mask per 64-position row of the window
     uint32_t* sbase = s_base + wave * 64;
+    uint32_t* slane = s_lane + wave * 64;
+    int* scorr = s_corr + wave * 64;
+    scorr[lane] = 0;
     unsigned long long* smask = s_mask[wave];
     constexpr int64_t kStep = (kSlThreads / 64) * 64;  // tiles between a wave's blocks
-    constexpr uint32_t kOob = 0x3FFFFFF0u;              // entry index past every range: load 0, no store
+    constexpr uint32_t kOob = 0x3FFFFF0u;               // entry index past every range: load 0, no store
+    constexpr uint32_t kOobMask = (1u << 26) - 1;       // off[] = index | owner lane << 26
     // segment bounds of the lane's tile in block tc (toffT), loaded one block ahead
     auto bounds = [&](int64_t tc, uint32_t* st, uint32_t* len) {
         *st = 0;
@@ -1990,7 +2003,10 @@ sl_lookup_kernel(const uint32_t* __restrict__ dense, uint64_t drange, uint32_t w
         const unsigned long long ne = __ballot(len != 0);
         const uint32_t rank =
             __builtin_amdgcn_mbcnt_hi((uint32_t)(ne >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)ne, 0u));
-        if (len != 0) sbase[rank] = (uint32_t)lane * kSlTile + st - excl;  // >= 0: excl <= lane * kSlTile
+        if (len != 0) {
+            sbase[rank] = (uint32_t)lane * kSlTile + st - excl;  // >= 0: excl <= lane * kSlTile
+            slane[rank] = (uint32_t)lane;
+        }
         // the 64 tiles' regions as buffers (wave-uniform bases): 32-bit offsets, and an
         // out-of-range offset turns a position past R into a dropped access
         const int64_t tcu = (int64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)tc) |
@@ -2008,7 +2024,8 @@ sl_lookup_kernel(const uint32_t* __restrict__ dense, uint64_t drange, uint32_t w
                 atomicOr(&smask[(excl - w0) >> 6], 1ull << ((excl - w0) & 63));
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
             __builtin_amdgcn_wave_barrier();
-            uint32_t off[kSlOwnWin / 64], ev[kSlOwnWin / 64];  // off: the entry's index or kOob
+            // off: the entry's index (or kOob) | owner tile lane << 26
+            uint32_t off[kSlOwnWin / 64], ev[kSlOwnWin / 64];
 #pragma unroll
             for (int u = 0; u < kSlOwnWin / 64; ++u) {
                 const uint32_t r = w0 + u * 64 + lane;
@@ -2023,15 +2040,35 @@ sl_lookup_kernel(const uint32_t* __restrict__ dense, uint64_t drange, uint32_t w
                 const uint32_t k = kb + (uint32_t)(mu & 1) + below - 1;
                 kb += (uint32_t)__builtin_popcountll(mu);
                 const uint32_t ps = sbase[k & 63] + r;
-                off[u] = r < R ? ps : kOob;
-                ev[u] = __builtin_amdgcn_raw_buffer_load_b16(rko, (int)(off[u] * 2), 0, 0);
+                const uint32_t o = r < R ? ps : kOob;
+                ev[u] = __builtin_amdgcn_raw_buffer_load_b16(rko, (int)(o * 2), 0, 0);
+                off[u] = o | (slane[k & 63] << 26);
             }
 #pragma unroll
             for (int u = 0; u < kSlOwnWin / 64; ++u) {
                 const uint32_t v = s_tab[ev[u] & ((1u << wlog) - 1)];
-                __builtin_amdgcn_raw_buffer_store_b32(v, rres, (int)(off[u] * 4), 0, 0);
+                const uint32_t o = off[u] & kOobMask;
+                __builtin_amdgcn_raw_buffer_store_b32(v, rres, (int)(o * 4), 0, 0);
+                // pair-count correction (count - 1) of a missing or duplicated key, per
+                // owner tile; none in a window of unique hits (C2: no LDS atomics at all)
+                const bool odd = o != kOob && (v == kMiss || (v & kDupFlag));
+                if (__ballot(odd) != 0 && odd) {
+                    const uint32_t c4 = tv.off_mask == kPackedMask ? ((v >> 27) & 15u) : 0u;
+                    const uint32_t c = v == kMiss ? 0u : c4 ? c4 : tv.dup_rows[v & tv.off_mask];
+                    atomicAdd(&scorr[off[u] >> 26], (int)c - 1);
+                }
             }
         }
+        // the run's corrections: one atomic per tile that has one (64 contiguous counters)
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        const int cr = scorr[lane];
+        if (cr != 0) {
+            atomicAdd(&tcnt[tc + lane], (unsigned long long)(long long)cr);
+            scorr[lane] = 0;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
     }
 }
 
@@ -2039,32 +2076,6 @@ sl_lookup_kernel(const uint32_t* __restrict__ dense, uint64_t drange, uint32_t w
 __device__ __forceinline__ uint32_t sl_count(const TableView& tv, uint32_t r) {
     const uint32_t c4 = tv.off_mask == kPackedMask ? ((r >> 27) & 15u) : 0u;
     return r == kMiss ? 0u : !(r & kDupFlag) ? 1u : c4 ? c4 : tv.dup_rows[r & tv.off_mask];
-}
-
-// S3a: pairs per tile from its refs (one coalesced pass over res), then one workgroup
-// scans them into the tiles' output offsets (sl_scan_kernel). A decoupled look-back in
-// S3b instead would wait on the inclusive prefixes of the other ~500 tiles in flight,
-// one 64-flag step (a memory round trip) per 64 tiles: measured as ~40% of S3's time.
-// Scanning in the count kernel's last workgroup (done counter) costs a device-scope
-// release per workgroup — an L2 writeback each: 44 -> 240 us.
-__global__ void __launch_bounds__(256)
-sl_count_kernel(TableView tv, uint32_t nslices, const uint32_t* __restrict__ res, const uint16_t* __restrict__ toff,
-                unsigned long long* __restrict__ tcnt) {
-    __shared__ unsigned long long s_w[4];
-    const int64_t tile = blockIdx.x;
-    const uint32_t cnt = toff[tile * (int64_t)(nslices + 1) + nslices];
-    const uint32_t* tr = res + tile * kSlTile;
-    unsigned long long sum = 0;
-    const uint32_t c4 = cnt & ~3u;
-    for (uint32_t i = threadIdx.x * 4; i < c4; i += 256 * 4) {
-        const uint4 r4 = *reinterpret_cast<const uint4*>(tr + i);
-        sum += sl_count(tv, r4.x) + sl_count(tv, r4.y) + sl_count(tv, r4.z) + sl_count(tv, r4.w);
-    }
-    if (threadIdx.x < (cnt & 3u)) sum += sl_count(tv, tr[c4 + threadIdx.x]);
-    sum = wave_sum<unsigned long long>(sum);
-    if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = sum;
-    __syncthreads();
-    if (threadIdx.x == 0) tcnt[tile] = s_w[0] + s_w[1] + s_w[2] + s_w[3];
 }
 
 // exclusive scan in place of up to kSlScanOne tile counts by one workgroup (thread j
@@ -2610,7 +2621,7 @@ hipError_t launch_build_frag(int key_bytes, const Segment* h_segs, int nseg, con
 #define DFP_BLP(KT, HV)                                                                                          \
     sl_partition_kernel<KT, HV><<<(unsigned)nt, kSlThreads, 0, s>>>(g.dmin, drange, wlog, nblk, sg.keys, sg.valid, \
                                                                    sg.voff, sg.n, vec, ko, rl, toff, 0, t0,          \
-                                                                   sg.row_base, tile_base, nullptr)
+                                                                   sg.row_base, tile_base, nullptr, nullptr)
         if (key_bytes == 8) {
             if (sg.valid) DFP_BLP(int64_t, true); else DFP_BLP(int64_t, false);
         } else {
@@ -2889,7 +2900,7 @@ hipError_t launch_probe_sliced(int key_bytes, const TableView& tv, const void* k
 #define DFP_SLP(KT, HV)                                                                                      \
     sl_partition_kernel<KT, HV><<<(unsigned)nt, kSlThreads, 0, s>>>(tv.dmin, tv.drange, wlog, nsl, keys, valid, voff, n, \
                                                                    vec, w.ko, w.rl, w.toff, sl_nt, 0, 0, nullptr, \
-                                                                   err_word)
+                                                                   err_word, w.tcnt)
     if (key_bytes == 8) {
         if (valid) DFP_SLP(int64_t, true); else DFP_SLP(int64_t, false);
     } else {
@@ -2919,9 +2930,8 @@ hipError_t launch_probe_sliced(int key_bytes, const TableView& tv, const void* k
         e = hipStreamWaitEvent(s, built, 0);
         if (e != hipSuccess) return e;
     }
-    sl_lookup_kernel<<<nsl * parts, kSlThreads, tab_lds, s>>>(tv.dense, tv.drange, wlog, nsl, nt, parts, w.ko, w.res,
-                                                              w.toffT, sl_dbg);
-    sl_count_kernel<<<(unsigned)nt, 256, 0, s>>>(tv, nsl, w.res, w.toff, w.tcnt);
+    sl_lookup_kernel<<<nsl * parts, kSlThreads, tab_lds, s>>>(tv, wlog, nsl, nt, parts, w.ko, w.res, w.toffT,
+                                                              w.tcnt, sl_dbg);
     if (nt <= kSlScanOne) {
         sl_scan_kernel<<<1, 1024, 0, s>>>(w.tcnt, nt, (unsigned long long*)d_total);
     } else {

@@ -77,6 +77,12 @@ for s in $STEPS; do
       run timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/dist -o d --output-format csv \
         -- python3 bench.py --force-dist --no-cpu-baseline --steps 5 > $O/distprof.json 2> $O/distprof.err \
         || { tail -30 $O/distprof.err; exit 1; } ;;
+    kp)
+      # per-kernel times of one build + 5 probes (tools/probe_one.py $KP_ARGS), serialized
+      run timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/kp${KP_TAG} -o kp --output-format csv \
+        -- python3 tools/probe_one.py ${KP_ARGS} > $O/kp${KP_TAG}.log 2>&1 || { tail -30 $O/kp${KP_TAG}.log; exit 1; }
+      tail -1 $O/kp${KP_TAG}.log
+      python3 tools/kstats.py $O/kp${KP_TAG} ;;
     smoke)
       run timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 \
         || { tail -30 $O/smoke.log; exit 1; }
