@@ -37,11 +37,19 @@ from datafusion_parallelism_amd.table import HashTable  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 PERM_MUL = 7368787
+MIX_MUL = 0x9E3779B97F4A7C15  # odd: multiplication mod 2^64 is a bijection of int64
+MIX_MUL_I64 = MIX_MUL - (1 << 64)
 
 CONFIGS = {
     # BASELINE.json configs[1]: 10^8-probe x 10^7-build int64 uniform keys
     "c2": dict(workload="C2: 10^8-probe x 10^7-build int64 inner equi-join, uniform keys",
                build_rows=10**7, probe_rows=10**8, build_gen="perm", probe_range_mul=2),
+    # C2 with both sides' keys mapped by the bijection k -> k * MIX_MUL (mod 2^64): the same
+    # pairs, but the keys spread over the whole int64 domain, so the build takes the
+    # hashed (open-addressing bucket) table instead of the direct-addressed one
+    "c2h": dict(workload="C2h: C2's keys mapped onto the int64 domain by k -> k * 0x9E3779B97F4A7C15 "
+                         "(mod 2^64); hashed bucket table",
+                build_rows=10**7, probe_rows=10**8, build_gen="perm", probe_range_mul=2, mix=True),
     # BASELINE.json configs[2]: 10^8 rows with exponential/skewed build keys
     "c3": dict(workload="C3: 10^8-probe x 10^7-build int64, exponential build keys",
                build_rows=10**7, probe_rows=10**8, build_gen="exp", probe_range_mul=1),
@@ -75,6 +83,9 @@ def gen_inputs(cfg, rank, world, dev):
     pk = torch.empty(P, dtype=torch.int64, device=dev)
     prange = cfg["probe_range_mul"] * krange
     assert L.hj_gen_uniform_keys(pk.data_ptr(), P, 0xC0FFEE + rank * P, prange, s) == 0
+    if cfg.get("mix"):  # int64 multiplication wraps mod 2^64 on the device
+        bk.mul_(MIX_MUL_I64)
+        pk.mul_(MIX_MUL_I64)
     torch.cuda.synchronize(dev)
     return bk, pk
 
@@ -153,6 +164,18 @@ class SingleGpuJoin:
         t = HashTable(1, "int64", self.dev.index or 0)
         t.append(0, self.bk)
         t.finish(0)
+        st = t.stats()
+        P = self.pk.numel()
+        dense = st["buckets"] == 0
+        sliced = P >= (st["table_bytes"] // 4 if dense else st["buckets"]) and P >= 65536
+        if sliced:
+            self.kernel_desc = ("the whole hj_probe_async, sliced probe (DESIGN.md §4): " +
+                                ("sl_partition" if dense else "hs_partition") +
+                                " + sl_toff_transpose + sl_lookup + sl_emit (look-back offsets); " +
+                                ("direct-addressed table" if dense else
+                                 f"hashed table, {st['buckets']} buckets = {st['table_bytes']} B"))
+        else:
+            self.kernel_desc = "probe_fused_kernel (" + ("direct-addressed" if dense else "hashed") + " table)"
         s = torch.cuda.current_stream(self.dev)
         t.stream_wait(s.cuda_stream)
         torch.cuda.synchronize(self.dev)
@@ -182,6 +205,9 @@ def cpu_baseline(cfg, nthreads=8):
         bk = oracle.make_exponential_int_array(0, B).astype(np.int64)
     ps = min(P, 10**7)
     pk = oracle.uniform_keys(ps, 0xC0FFEE, cfg["probe_range_mul"] * B)
+    if cfg.get("mix"):
+        bk = (bk.astype(np.uint64) * np.uint64(MIX_MUL)).astype(np.int64)
+        pk = (pk.astype(np.uint64) * np.uint64(MIX_MUL)).astype(np.int64)
     t0 = time.perf_counter()
     tbl = oracle.V10Table(bk, nthreads=nthreads)
     t1 = time.perf_counter()
@@ -292,19 +318,14 @@ def main():
 
     # the local job's steps overlap one step's host work with the previous step's device
     # work (LocalJob.step); the exchange job synchronizes inside its step
-    times = []
     barrier()
     torch.cuda.synchronize(dev)
     t_start = time.perf_counter()
-    ts = t_start
     for _ in range(args.steps):
         job.step()
         if args.sync_steps or use_dist:
             torch.cuda.synchronize(dev)
             job.collect()
-        tn = time.perf_counter()
-        times.append(tn - ts)
-        ts = tn
     torch.cuda.synchronize(dev)
     barrier()
     elapsed = time.perf_counter() - t_start
@@ -329,8 +350,7 @@ def main():
         "frac": round(achieved / HBM_PEAK_GBS, 4),
         "traffic": (traffic or {}).get("hbm_bytes_per_launch"),
         "traffic_lower": ((traffic or {}).get("probe_phase") or {}).get("hbm_bytes_lower"),
-        "kernel": "the whole hj_probe_async (sliced probe: sl_partition + sl_toff_transpose + sl_lookup + "
-                  "sl_count + scan + sl_emit, DESIGN.md §4)",
+        "kernel": job.kernel_desc,
         "alg_bytes_per_launch": alg_bytes,
         "alg_bytes_formula": "8*P + 16*B + 12*M (SURVEY.md §8d)",
         # the probe rows' lookups run out of LDS (no random device reads per row); the HBM
@@ -368,9 +388,6 @@ def main():
             "probe_ms_in_step": (round(float(np.median(job.probe_in_step_ms)), 4)
                                  if getattr(job, "probe_in_step_ms", None) else None),
             "build_ms": round(build_ms, 4),
-            # host time per step: with --sync-steps the whole step, otherwise the launch
-            # interval of the pipelined steps (not a device time)
-            "step_ms_min": round(min(times) * 1e3, 4),
             "pipelined_steps": not (args.sync_steps or use_dist),
             "roofline": roofline,
             "cpu_baseline": cpu,
@@ -395,6 +412,7 @@ class DistJob:
         self.probe_ms, self.build_ms, self.exchange_ms = [], [], []
         self.matches = 0
         self.cap = pk.numel()
+        self.kernel_desc = "radix partition + RCCL all-to-all + local build + probe"
 
     def step(self):
         t0 = time.perf_counter()
@@ -410,7 +428,7 @@ class DistJob:
         else:
             from datafusion_parallelism_amd.distributed import gpu_local_join
 
-            pk, pi, _ = self.dj.shard(self.pk, self.pbase, torch.int32, key_offset=plan.key_offset)
+            pk, pi, _ = self.dj.shard(self.pk, self.pbase, torch.int32, key_offset=plan.key_offset, spec=plan.spec)
             outs = [gpu_local_join(bk, bi, pk, pi, self.cap)]
         ev[1].record()
         self._ev = ev

@@ -189,10 +189,11 @@ bool is_device_ptr(const void* p) {
     return a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged;
 }
 
-// Slots per key. 0.35 measured best for the C2 probe on MI355X (fused probe 2048 us vs
-// 2150 us at 0.5, build unchanged; profiles/r01_load_factor.txt): fewer full buckets,
-// so fewer second bucket lines on the miss path. Override with DFP_HJ_LOAD_FACTOR.
-constexpr double kDefaultLoadFactor = 0.35;
+// Keys per slot of a hashed table. 0.5 keeps a 10^7-key table within the sliced probe's
+// 2047 slices of 2048 buckets (128 KB of LDS each; C2h), where the slices are read once
+// per probe; the fused probe measured 2048 us at 0.35 and 2150 us at 0.5 on C2
+// (profiles/r01_load_factor.txt). Override with DFP_HJ_LOAD_FACTOR.
+constexpr double kDefaultLoadFactor = 0.5;
 
 // Table layout: 0 auto (direct-addressed when the key range is at most kDenseFactor x the
 // build rows, else hashed buckets), 1 hashed always. DFP_HJ_DENSE=0 selects 1.
@@ -245,7 +246,10 @@ struct hj_table {
     int arrived = 0;
     bool built = false;
     bool sync_finish = false;  // some input was borrowed without HJ_BORROW_KEEP
-    mutable bool probed = false;  // res.evp marks the end of the latest probe
+    // end of the latest probe launch on each stream that probed the table: hj_table_free
+    // waits for all of them (res.evp serves the first stream; others get their own event)
+    mutable std::mutex probe_mu;
+    mutable std::vector<std::pair<hipStream_t, hipEvent_t>> probe_evs;
     hj_status build_st = HJ_OK;
     std::string build_err;
     bool has_ids = false, has_no_ids = false;
@@ -615,6 +619,22 @@ hj_status stage_input(int key_bytes, const void* keys, const uint8_t* valid, int
     return HJ_OK;
 }
 
+// record the end of a probe on stream s (one event per probing stream, under the
+// table's probe lock: probes of one table may run concurrently from several threads)
+hj_status note_probe(const hj_table* t, hipStream_t s) {
+    std::lock_guard<std::mutex> g(t->probe_mu);
+    for (auto& se : t->probe_evs)
+        if (se.first == s) {
+            HIP_TRY(hipEventRecord(se.second, s));
+            return HJ_OK;
+        }
+    hipEvent_t ev = t->res.evp;
+    if (!t->probe_evs.empty()) HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    t->probe_evs.emplace_back(s, ev);
+    HIP_TRY(hipEventRecord(ev, s));
+    return HJ_OK;
+}
+
 hj_status probe_impl(const hj_table* t, const void* keys, const uint8_t* valid, int64_t voff,
                      const uint32_t* probe_ids, int64_t n, uint64_t* out_b, uint32_t* out_p, int64_t cap,
                      int64_t* d_total, void* ws, hipStream_t s) {
@@ -625,9 +645,7 @@ hj_status probe_impl(const hj_table* t, const void* keys, const uint8_t* valid, 
     HIP_TRY(launch_probe(t->key_bytes, view_of(t), keys, valid, voff, probe_ids, n, out_b, out_p, cap, d_total, ws,
                          s != t->bstream ? t->res.ev1 : nullptr, s));
     // hj_table_free waits for it before the table's blocks return to the cache
-    HIP_TRY(hipEventRecord(t->res.evp, s));
-    t->probed = true;
-    return HJ_OK;
+    return note_probe(t, s);
 }
 
 }  // namespace
@@ -764,6 +782,9 @@ hj_status hj_build_finish(hj_table* t, int partition) {
     if (t->arrived == t->parallelism) {
         // last arriver finalises (InitializeLast::initialize_or_wait)
         hj_status st = run_build(t);
+        // a failed build may have queued work on its stream before the error (ev1 is not
+        // recorded then): drain it, so that hj_table_free returns idle blocks to the cache
+        if (st != HJ_OK) (void)hipStreamSynchronize(t->bstream);
         if (st == HJ_OK && t->sync_finish && hipEventSynchronize(t->res.ev1) != hipSuccess)
             st = fail(HJ_ERR_HIP, "build failed on the device");
         t->build_st = st;
@@ -835,7 +856,7 @@ int hj_set_build_mode(int mode) {
 }
 
 int hj_set_probe_mode(int mode) {
-    if (mode < 0 || mode > 4) return -1;
+    if (mode != 0 && mode != 3 && mode != 4) return -1;  // 1 and 2 were retired strategies
     const int old = get_probe_mode();
     set_probe_mode(mode);
     return old;
@@ -1004,8 +1025,11 @@ void hj_table_free(hj_table* t) {
     (void)hipSetDevice(t->device);
     // the blocks return to the cache (reused by any stream): the build and the latest
     // probe must be done (earlier probes on other streams are the caller's to finish)
-    if (t->built) (void)hipEventSynchronize(t->res.ev1);
-    if (t->probed) (void)hipEventSynchronize(t->res.evp);
+    if (t->built && t->build_st == HJ_OK) (void)hipEventSynchronize(t->res.ev1);
+    for (auto& se : t->probe_evs) {
+        (void)hipEventSynchronize(se.second);
+        if (se.second != t->res.evp) (void)hipEventDestroy(se.second);
+    }
     free_list(t, t->allocs);
     free_list(t, t->scratch);
     for (auto& part : t->parts)

@@ -3,17 +3,19 @@
 //
 // Slot table in HBM:
 //   Bucket[nb + 1], one 64-byte line each, nb = nchunks << clog2:
-//     uint64 key[5]   stored key = key ^ 2^63, 0 = empty slot
+//     uint64 key[5]   stored key = mix64(key) (a bijection of the 64-bit keys, so equal
+//                     stored keys are equal keys, and the home bucket follows from the
+//                     stored key without rehashing), 0 = empty slot
 //     uint32 ref[5]   bit 31 clear: the key's only build row
 //                     bit 31 set:   offset of its duplicate segment in dup_rows
 //     uint32 meta     bit 0: an insert passed this bucket full (a lookup that misses
 //                     here continues to the next bucket only if set);
 //                     bits 1+6j..6+6j: row count of slot j's duplicated key if <= 63
 //                     (0: read it from dup_rows);
-//                     side bucket: rows of the key INT64_MIN
+//                     side bucket: rows of the key 0
 //   A key's probe sequence stays inside its chunk of 2^clog2 buckets (linear probing
 //   modulo the chunk), so one workgroup can build a whole chunk in LDS.
-//   Bucket[nb] is the side bucket for INT64_MIN, whose stored form collides with
+//   Bucket[nb] is the side bucket for key 0, whose stored form mix64(0) = 0 collides with
 //   "empty": ref[0] + meta = row count.
 //   dup_rows[]: per duplicated key a segment [count, row_0 > row_1 > ... ] — rows sorted
 //   descending = the reference's newest-first chain order at parallelism 1.
@@ -80,6 +82,26 @@ __host__ __device__ inline uint64_t mix64(uint64_t k) {
     k ^= k >> 33;
     return k;
 }
+
+// inverse of mix64 (xorshift by 33 is its own inverse on 64 bits; the multipliers' inverses
+// mod 2^64 by Newton iteration)
+__host__ __device__ constexpr uint64_t inv_odd(uint64_t a) {
+    uint64_t x = a;  // correct to 3 bits for odd a
+    for (int i = 0; i < 5; ++i) x *= 2 - a * x;
+    return x;
+}
+__host__ __device__ inline uint64_t unmix64(uint64_t k) {
+    k ^= k >> 33;
+    k *= inv_odd(0xc4ceb9fe1a85ec53ull);
+    k ^= k >> 33;
+    k *= inv_odd(0xff51afd7ed558ccdull);
+    k ^= k >> 33;
+    return k;
+}
+static_assert(inv_odd(0xff51afd7ed558ccdull) * 0xff51afd7ed558ccdull == 1, "inverse multiplier");
+
+// stored form of a key in a hashed table: mix64(key); 0 only for key 0 (the side bucket)
+__host__ __device__ inline unsigned long long stored_key(int64_t key) { return mix64((uint64_t)key); }
 
 // home bucket from the high 32 hash bits (multiply-shift range reduction); radix
 // partitioning for the multi-GPU exchange uses the LOW bits, so a shard's keys still

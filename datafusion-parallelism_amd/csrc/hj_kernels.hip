@@ -15,12 +15,12 @@
 //   probe   (replaces get_matching_indices, src/shared/shared.rs:29-47, the chain walk,
 //            src/operator/version10/lookup_implementation_3.rs:22-59, and
 //            equal_rows_arr, src/shared/datafusion_private.rs:40-80)
-//     probe_fused_kernel    (default) per probe row: hash, one 64-byte bucket line
-//                           (exact key compare, so no separate equality gather); the
-//                           tile's output offset by decoupled look-back; ordered
-//                           (probe asc, build desc) pair emission
-//     probe_lookup_kernel + scan + probe_emit_kernel: the same in two passes (4-byte
-//                           ref per row in between); partitioned variant pp_*
+//     sl_* (sliced probe)   large probes: rows partitioned by table slice, lookups out
+//                           of LDS, ordered emission per tile (see the section below)
+//     probe_fused_kernel    small probes: per probe row one table read (exact key
+//                           compare, so no separate equality gather); the tile's output
+//                           offset by decoupled look-back; ordered (probe asc, build
+//                           desc) pair emission
 //
 // No same-address global atomics on the hot loops (a single word sustains ~88
 // atomics/us, MI355X_MICROARCH.md "dequeue"). The one inter-workgroup hand-off is the
@@ -32,6 +32,7 @@
 #include <algorithm>
 #include <atomic>
 #include <climits>
+#include <type_traits>
 
 #include "hj_device.h"
 #include "hj_launch.h"
@@ -60,10 +61,12 @@ __device__ __forceinline__ int find_seg(const Segment* segs, int nseg, int64_t r
     return lo;
 }
 
-// chunk of a key: the probe sequence of a key never leaves it
+// home bucket of a key (its probe sequence never leaves the bucket's chunk), and of its
+// stored form (no rehash)
 __device__ __forceinline__ uint32_t home_bucket(int64_t key, uint32_t nb) {
     return bucket_of(mix64((uint64_t)key), nb);
 }
+__device__ __forceinline__ uint32_t stored_bucket(unsigned long long sk, uint32_t nb) { return bucket_of(sk, nb); }
 
 // ---------------------------------------------------------------------------
 // build 1: rows -> chunk order in two partition levels. A 32 K-row tile spread over all
@@ -78,7 +81,7 @@ constexpr int kFineLdsBins = 8192;  // fine histogram in LDS (32 KB) up to this 
 
 __device__ __forceinline__ uint32_t chunk_of(int64_t key, const ChunkGeom& g) {
     if (g.dense) return (uint32_t)(((uint64_t)key - (uint64_t)g.dmin) >> g.dshift);
-    return ((uint64_t)key ^ kSign) == 0 ? g.nchunks : (home_bucket(key, g.nb) >> g.clog2);
+    return key == 0 ? g.nchunks : (home_bucket(key, g.nb) >> g.clog2);  // key 0: the side bucket
 }
 
 // The segment descriptors of one tile's rows in LDS (per-row lookups in global memory
@@ -547,11 +550,11 @@ chunk_build_kernel(uint32_t nb, uint32_t clog2, uint32_t nchunks, const uint32_t
         for (int u = 0; u < kChunkRegRows; ++u) {
             rslot[u] = -1;
             if (start + u * kChunkThreads + threadIdx.x >= end) continue;
-            const unsigned long long sk = rk[u] ^ kSign;
+            const unsigned long long sk = stored_key((int64_t)rk[u]);
             int slot = 0;
             bool claimed = false;
             if (!side) {
-                const int v = chunk_slot<true>(img, cmask, home_bucket((int64_t)rk[u], nb) & cmask, sk);
+                const int v = chunk_slot<true>(img, cmask, stored_bucket(sk, nb) & cmask, sk);
                 if (v < 0) { atomicOr(&ctr->err, 1ull); continue; }  // chunk full
                 slot = v & ~kSlotNew;
                 claimed = (v & kSlotNew) != 0;
@@ -572,12 +575,12 @@ chunk_build_kernel(uint32_t nb, uint32_t clog2, uint32_t nchunks, const uint32_t
         if (threadIdx.x == 0) s_dup = 1u;
         // pass A (streamed)
         for (uint32_t r = start + threadIdx.x; r < end; r += kChunkThreads) {
-            const unsigned long long sk = skeys[r] ^ kSign;
+            const unsigned long long sk = stored_key((int64_t)skeys[r]);
             int slot;
             if (side) {
                 slot = 0;
             } else {
-                const uint32_t i0 = home_bucket((int64_t)(sk ^ kSign), nb) & cmask;
+                const uint32_t i0 = stored_bucket(sk, nb) & cmask;
                 slot = chunk_slot<true>(img, cmask, i0, sk);
                 if (slot < 0) { atomicOr(&ctr->err, 1ull); continue; }  // chunk full
                 slot &= ~kSlotNew;
@@ -646,10 +649,10 @@ chunk_build_kernel(uint32_t nb, uint32_t clog2, uint32_t nchunks, const uint32_t
                 if (rslot[u] >= 0) place(rslot[u], rrow[u]);
         } else {
             for (uint32_t r = start + threadIdx.x; r < end; r += kChunkThreads) {
-                const unsigned long long sk = skeys[r] ^ kSign;
+                const unsigned long long sk = stored_key((int64_t)skeys[r]);
                 int slot = 0;
                 if (!side) {
-                    const uint32_t i0 = home_bucket((int64_t)(sk ^ kSign), nb) & cmask;
+                    const uint32_t i0 = stored_bucket(sk, nb) & cmask;
                     slot = chunk_slot<false>(img, cmask, i0, sk);
                     if (slot < 0) continue;
                 }
@@ -678,7 +681,7 @@ chunk_build_kernel(uint32_t nb, uint32_t clog2, uint32_t nchunks, const uint32_t
                 const unsigned li = ref & ~kDupFlag;
                 if (d_cnt[li] > (unsigned)kSmallSeg) {
                     const unsigned bi = (unsigned)atomicAdd(&ctr->n_big, 1ull);  // rare: > 16 rows
-                    big[bi] = BigSeg{side ? kSign : (B.key[sl % kSlots] ^ kSign), d_off[li], 0u};
+                    big[bi] = BigSeg{side ? 0ull : unmix64(B.key[sl % kSlots]), d_off[li], 0u};
                 }
                 ref = kDupFlag | d_off[li];
                 // small row counts inline in meta (6 bits per slot): the probe's count pass
@@ -1035,8 +1038,8 @@ __device__ __forceinline__ void lookup4(const TableView& tv, const void* __restr
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
         in[q] = (row0 + q < n) && (!HAS_VALID || bit_valid(valid, voff, row0 + q));
-        sk[q] = (unsigned long long)k[q] ^ kSign;
-        b[q] = (in[q] && sk[q] != 0) ? home_bucket(k[q], tv.nb) : tv.nb;
+        sk[q] = stored_key(k[q]);
+        b[q] = (in[q] && sk[q] != 0) ? stored_bucket(sk[q], tv.nb) : tv.nb;
     }
     // issue the 64-byte bucket line of all four rows before any compare (MLP)
 #pragma unroll
@@ -1048,7 +1051,7 @@ __device__ __forceinline__ void lookup4(const TableView& tv, const void* __restr
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
         ref[q] = scan_line(L0[q], L1[q], L2[q], L3[q], sk[q], &more[q], &cnt[q]);
-        if (sk[q] == 0) {  // INT64_MIN: the side bucket (ref[0] = word 10, meta = word 15 = rows)
+        if (sk[q] == 0) {  // key 0: the side bucket (ref[0] = word 10, meta = word 15 = rows)
             ref[q] = L3[q].w ? L2[q].z : kMiss;
             cnt[q] = L3[q].w;
             more[q] = false;
@@ -1070,34 +1073,6 @@ __device__ __forceinline__ void lookup4(const TableView& tv, const void* __restr
 __device__ __forceinline__ uint32_t resolve_count(const uint32_t* dup_rows, uint32_t ref, uint32_t cnt,
                                                   uint32_t off_mask) {
     return cnt == kCountUnknown ? dup_rows[ref & off_mask] : cnt;
-}
-
-template <typename K, bool HAS_VALID>
-__global__ void __launch_bounds__(kProbeThreads)
-probe_lookup_kernel(TableView tv, const void* __restrict__ keys, const uint8_t* __restrict__ valid, int64_t voff,
-                    int64_t n, bool vec, uint32_t* __restrict__ info, unsigned long long* __restrict__ tcnt) {
-    __shared__ unsigned long long s_w[kProbeThreads / 64];
-    unsigned long long tsum = 0;
-    const int64_t tile0 = (int64_t)blockIdx.x * kProbeTile;
-#pragma unroll
-    for (int g = 0; g < kGroups; ++g) {
-        const int64_t row0 = tile0 + (int64_t)g * (kProbeThreads * 4) + (int64_t)threadIdx.x * 4;
-        if (row0 >= n) break;
-        uint32_t ref[4], cnt[4];
-        lookup4<K, HAS_VALID>(tv, keys, valid, voff, n, vec, row0, ref, cnt);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) tsum += resolve_count(tv.dup_rows, ref[q], cnt[q], tv.off_mask);
-        if (vec && row0 + 4 <= n) {
-            *reinterpret_cast<uint4*>(info + row0) = make_uint4(ref[0], ref[1], ref[2], ref[3]);
-        } else {
-#pragma unroll
-            for (int q = 0; q < 4; ++q)
-                if (row0 + q < n) info[row0 + q] = ref[q];
-        }
-    }
-    unsigned long long tot;
-    block_excl_scan<unsigned long long>(tsum, s_w, &tot);
-    if (threadIdx.x == 0) tcnt[blockIdx.x] = tot;
 }
 
 // Writes the pairs of four probe rows starting at output position `pos` (canonical:
@@ -1309,275 +1284,6 @@ probe_fused_kernel(TableView tv, const void* __restrict__ keys, const uint8_t* _
     }
 }
 
-// SORTED: `info` holds each tile's refs in the tile's partition-sorted order (the
-// partitioned probe) and perm[row] is the row's position in that order; the tile's refs
-// are staged through LDS (one coalesced 16 KB load) and read back in row order.
-template <bool SORTED, bool HAS_ROW_IDS, bool HAS_PROBE_IDS>
-__global__ void __launch_bounds__(kProbeThreads)
-probe_emit_kernel(TableView tv, const uint32_t* __restrict__ info, const uint16_t* __restrict__ perm,
-                  const uint32_t* __restrict__ probe_ids, int64_t n, const unsigned long long* __restrict__ toff,
-                  uint64_t* __restrict__ out_b, uint32_t* __restrict__ out_p, int64_t cap) {
-    __shared__ unsigned long long s_w[kGroups][kProbeThreads / 64];
-    __shared__ __attribute__((aligned(16))) uint32_t s_info[SORTED ? kProbeTile : 1];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int64_t tile0 = (int64_t)blockIdx.x * kProbeTile;
-    uint32_t ref[kGroups][4];
-    uint32_t cnt[kGroups][4];
-    unsigned long long gsum[kGroups], gincl[kGroups];
-    if constexpr (SORTED) {
-        const int64_t rows = min<int64_t>(kProbeTile, n - tile0);
-        for (int64_t i = threadIdx.x * 4; i < rows; i += kProbeThreads * 4) {
-            if (i + 4 <= rows) *reinterpret_cast<uint4*>(s_info + i) = *reinterpret_cast<const uint4*>(info + tile0 + i);
-            else for (int64_t k = i; k < rows; ++k) s_info[k] = info[tile0 + k];
-        }
-        __syncthreads();
-    }
-#pragma unroll
-    for (int g = 0; g < kGroups; ++g) {
-        const int64_t row0 = tile0 + (int64_t)g * (kProbeThreads * 4) + (int64_t)threadIdx.x * 4;
-        if constexpr (SORTED) {
-            if (row0 + 4 <= n) {
-                const uint2 pv = *reinterpret_cast<const uint2*>(perm + row0);
-                ref[g][0] = s_info[pv.x & 0xFFFF]; ref[g][1] = s_info[pv.x >> 16];
-                ref[g][2] = s_info[pv.y & 0xFFFF]; ref[g][3] = s_info[pv.y >> 16];
-            } else {
-#pragma unroll
-                for (int q = 0; q < 4; ++q) ref[g][q] = (row0 + q < n) ? s_info[perm[row0 + q]] : kMiss;
-            }
-        } else if (row0 + 4 <= n) {
-            const uint4 v = *reinterpret_cast<const uint4*>(info + row0);
-            ref[g][0] = v.x; ref[g][1] = v.y; ref[g][2] = v.z; ref[g][3] = v.w;
-        } else {
-#pragma unroll
-            for (int q = 0; q < 4; ++q) ref[g][q] = (row0 + q < n) ? info[row0 + q] : kMiss;
-        }
-        unsigned long long s = 0;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            cnt[g][q] = ref_count(tv.dup_rows, ref[g][q], tv.off_mask);
-            s += cnt[g][q];
-        }
-        gsum[g] = s;
-        gincl[g] = wave_incl_scan<unsigned long long>(s);
-        if (lane == 63) s_w[g][wave] = gincl[g];
-    }
-    __syncthreads();
-    unsigned long long gbase = toff[blockIdx.x];
-#pragma unroll
-    for (int g = 0; g < kGroups; ++g) {
-        unsigned long long pos = gbase + gincl[g] - gsum[g];
-        for (int w = 0; w < kProbeThreads / 64; ++w) {
-            if (w < wave) pos += s_w[g][w];
-            gbase += s_w[g][w];
-        }
-        const int64_t row0 = tile0 + (int64_t)g * (kProbeThreads * 4) + (int64_t)threadIdx.x * 4;
-        emit4<HAS_ROW_IDS, HAS_PROBE_IDS>(tv, probe_ids, row0, ref[g], cnt[g], pos, out_b, out_p, cap);
-    }
-}
-
-// ---------------------------------------------------------------------------
-// partitioned probe (tables much larger than L2): the table is cut into pieces of
-// `cpp` chunks (~2 MB); probe rows are grouped by piece inside each 4096-row tile, and
-// the lookups of one piece run on one XCD so that its L2 holds the piece.
-// ---------------------------------------------------------------------------
-constexpr int kMaxPieces = 255;  // + 1 direct bin (nulls, INT64_MIN) <= 256 bins
-
-struct PieceGeom {
-    uint32_t cpp;     // chunks per piece
-    uint32_t npiece;  // pieces (bin npiece = rows that need no table lookup)
-};
-
-// P1: per tile, counting sort of the rows by piece in LDS; writes the tile's keys in
-// sorted order, perm[row] = sorted position, the tile's bin offsets, and resolves the
-// direct bin (nulls -> miss, INT64_MIN -> side bucket) on the spot.
-template <typename K, bool HAS_VALID>
-__global__ void __launch_bounds__(kProbeThreads)
-pp_partition_kernel(TableView tv, PieceGeom pg, const void* __restrict__ keys, const uint8_t* __restrict__ valid,
-                    int64_t voff, int64_t n, bool vec, unsigned long long* __restrict__ skeys,
-                    uint16_t* __restrict__ perm, uint16_t* __restrict__ toff, uint32_t* __restrict__ info,
-                    uint32_t* __restrict__ cnt2) {
-    __shared__ __attribute__((aligned(16))) unsigned long long s_keys[kProbeTile];
-    __shared__ unsigned s_bin[kMaxPieces + 2];
-    __shared__ unsigned s_cur[kMaxPieces + 2];
-    __shared__ unsigned s_direct;
-    const int64_t tile = blockIdx.x;
-    const int64_t tile0 = tile * kProbeTile;
-    const uint32_t nbins = pg.npiece + 1;
-    for (uint32_t b = threadIdx.x; b < nbins; b += kProbeThreads) s_bin[b] = 0;
-    if (threadIdx.x == 0) s_direct = 0;
-    __syncthreads();
-    int64_t k[kGroups][4];
-    uint32_t bin[kGroups][4];
-#pragma unroll
-    for (int g = 0; g < kGroups; ++g) {
-        const int64_t row0 = tile0 + (int64_t)g * (kProbeThreads * 4) + (int64_t)threadIdx.x * 4;
-        load4<K>(keys, row0, n, vec, k[g]);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const bool in = row0 + q < n;
-            const bool ok = in && (!HAS_VALID || bit_valid(valid, voff, row0 + q));
-            const unsigned long long sk = (unsigned long long)k[g][q] ^ kSign;
-            bin[g][q] = (!in) ? 0xFFFFFFFFu
-                        : (ok && sk != 0) ? ((home_bucket(k[g][q], tv.nb) >> tv.clog2) / pg.cpp) : pg.npiece;
-            if (in && !ok) k[g][q] = 0, bin[g][q] |= 0x80000000u;  // null: no lookup, ref = miss
-            if (in) atomicAdd(&s_bin[bin[g][q] & 0x7FFFFFFF], 1u);
-        }
-    }
-    __syncthreads();
-    // exclusive scan of the bins (<= 256) by wave 0
-    if (threadIdx.x < 64) {
-        unsigned carry = 0;
-        for (uint32_t b0 = 0; b0 < nbins; b0 += 64) {
-            const uint32_t b = b0 + threadIdx.x;
-            const unsigned v = b < nbins ? s_bin[b] : 0u;
-            const unsigned incl = wave_incl_scan<unsigned>(v);
-            if (b < nbins) s_cur[b] = carry + incl - v;
-            carry += __shfl(incl, 63, 64);
-        }
-        if (threadIdx.x == 0) s_cur[nbins] = carry;
-    }
-    __syncthreads();
-    for (uint32_t b = threadIdx.x; b <= nbins; b += kProbeThreads) toff[tile * (kMaxPieces + 2) + b] = (uint16_t)s_cur[b];
-    __syncthreads();
-    uint32_t direct_cnt = 0;
-#pragma unroll
-    for (int g = 0; g < kGroups; ++g) {
-        const int64_t row0 = tile0 + (int64_t)g * (kProbeThreads * 4) + (int64_t)threadIdx.x * 4;
-        uint32_t pos[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            pos[q] = 0;
-            if (row0 + q < n) {
-                const uint32_t b = bin[g][q] & 0x7FFFFFFF;
-                pos[q] = atomicAdd(&s_cur[b], 1u);
-                s_keys[pos[q]] = (unsigned long long)k[g][q];
-                if (b == pg.npiece) {  // direct bin: resolve now
-                    uint32_t ref = kMiss;
-                    if (!(bin[g][q] & 0x80000000u)) {  // INT64_MIN (not null)
-                        const Bucket& S = tv.tbl[tv.nb];
-                        ref = S.meta ? S.ref[0] : kMiss;
-                    }
-                    info[tile0 + pos[q]] = ref;
-                    direct_cnt += ref_count(tv.dup_rows, ref, tv.off_mask);
-                }
-            }
-        }
-        if (row0 + 4 <= n) {
-            *reinterpret_cast<uint2*>(perm + row0) = make_uint2(pos[0] | (pos[1] << 16), pos[2] | (pos[3] << 16));
-        } else {
-#pragma unroll
-            for (int q = 0; q < 4; ++q)
-                if (row0 + q < n) perm[row0 + q] = (uint16_t)pos[q];
-        }
-    }
-    if (direct_cnt) atomicAdd(&s_direct, direct_cnt);
-    __syncthreads();
-    const int64_t rows = min<int64_t>(kProbeTile, n - tile0);
-    for (int64_t i = threadIdx.x * 2; i < rows; i += kProbeThreads * 2) {
-        if (i + 2 <= rows) *reinterpret_cast<ulonglong2*>(skeys + tile0 + i) = *reinterpret_cast<const ulonglong2*>(s_keys + i);
-        else skeys[tile0 + i] = s_keys[i];
-    }
-    if (threadIdx.x == 0) cnt2[tile * (kMaxPieces + 1) + pg.npiece] = s_direct;
-}
-
-// P2: lookups of piece p on XCD p % 8 (blocks b with b % 8 == p % 8 — the observed
-// round-robin placement; a speed heuristic only, never needed for correctness). For
-// each piece every wave of the XCD takes a contiguous range of tiles, so the XCD's
-// waves move through the pieces together and the current piece stays in its L2. A
-// wave flattens the piece's runs of 64 tiles over its 64 lanes (wave scan of the run
-// lengths, owner lane by binary search over shuffles) and keeps 4 lookups per lane in
-// flight; refs go to the rows' sorted positions, match counts to cnt2[tile][piece].
-constexpr int kP2Unroll = 4;
-
-__global__ void __launch_bounds__(kProbeThreads)
-pp_lookup_kernel(TableView tv, PieceGeom pg, int64_t n, int64_t ntiles, const unsigned long long* __restrict__ skeys,
-                 const uint16_t* __restrict__ toff, uint32_t* __restrict__ info, uint32_t* __restrict__ cnt2) {
-    __shared__ unsigned s_cnt[kProbeThreads / 64][64];
-    const Bucket* __restrict__ tbl = tv.tbl;
-    const uint32_t cmask = (1u << tv.clog2) - 1;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const uint32_t xcd = blockIdx.x & 7;
-    const uint32_t wpx = (gridDim.x >> 3) * (kProbeThreads / 64);                   // waves per XCD
-    const uint32_t wid = (blockIdx.x >> 3) * (kProbeThreads / 64) + (uint32_t)wave;  // wave index in XCD
-    const int64_t tb = ntiles * wid / wpx, te = ntiles * (wid + 1) / wpx;
-    for (uint32_t p = xcd; p < pg.npiece; p += 8) {
-        for (int64_t tc = tb; tc < te; tc += 64) {
-            const int64_t t = tc + lane;
-            const bool have = t < te;
-            uint32_t st = 0, len = 0;
-            if (have) {
-                const uint16_t* to = toff + t * (kMaxPieces + 2);
-                st = to[p];
-                len = to[p + 1] - st;
-            }
-            const uint32_t incl = wave_incl_scan<uint32_t>(len);
-            const uint32_t excl = incl - len;
-            const uint32_t R = __shfl(incl, 63, 64);
-            s_cnt[wave][lane] = 0;
-            __builtin_amdgcn_wave_barrier();
-            for (uint32_t r0 = 0; r0 < R; r0 += 64 * kP2Unroll) {
-                unsigned long long sk[kP2Unroll];
-                int64_t row[kP2Unroll];
-                uint32_t own[kP2Unroll], b0[kP2Unroll];
-                uint4 a0[kP2Unroll], a1[kP2Unroll], a2[kP2Unroll], a3[kP2Unroll];
-#pragma unroll
-                for (int u = 0; u < kP2Unroll; ++u) {
-                    const uint32_t r = r0 + u * 64 + lane;
-                    // owner lane j = number of lanes whose inclusive end is <= r
-                    uint32_t j = 0;
-#pragma unroll
-                    for (uint32_t step = 32; step >= 1; step >>= 1) {
-                        const uint32_t e = __shfl(incl, (int)(j + step - 1), 64);
-                        if (e <= r) j += step;
-                    }
-                    j = j > 63 ? 63 : j;
-                    own[u] = j;
-                    const uint32_t sj = __shfl(st, (int)j, 64), xj = __shfl(excl, (int)j, 64);
-                    row[u] = (tc + j) * kProbeTile + sj + (r - xj);
-                    sk[u] = (r < R) ? (__builtin_nontemporal_load(skeys + row[u]) ^ kSign) : 0;
-                }
-#pragma unroll
-                for (int u = 0; u < kP2Unroll; ++u) {
-                    b0[u] = home_bucket((int64_t)(sk[u] ^ kSign), tv.nb);
-                    const uint4* lp = reinterpret_cast<const uint4*>(tbl + b0[u]);
-                    a0[u] = lp[0]; a1[u] = lp[1]; a2[u] = lp[2]; a3[u] = lp[3];
-                }
-#pragma unroll
-                for (int u = 0; u < kP2Unroll; ++u) {
-                    const uint32_t r = r0 + u * 64 + lane;
-                    if (r >= R) continue;
-                    bool more;
-                    uint32_t c_unused;
-                    uint32_t ref = scan_line(a0[u], a1[u], a2[u], a3[u], sk[u], &more, &c_unused);
-                    uint32_t bb = b0[u];
-                    for (uint32_t probes = 0; more && probes < cmask; ++probes) {
-                        bb = (bb & ~cmask) | ((bb + 1) & cmask);
-                        const uint4* q = reinterpret_cast<const uint4*>(tbl + bb);
-                        ref = scan_line(q[0], q[1], q[2], q[3], sk[u], &more, &c_unused);
-                    }
-                    __builtin_nontemporal_store(ref, info + row[u]);
-                    const uint32_t c = ref_count(tv.dup_rows, ref, tv.off_mask);
-                    if (c) atomicAdd(&s_cnt[wave][own[u]], c);
-                }
-            }
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-            if (have) cnt2[t * (kMaxPieces + 1) + p] = s_cnt[wave][lane];
-            __builtin_amdgcn_wave_barrier();
-        }
-    }
-}
-
-// per-tile match totals of the partitioned probe
-__global__ void pp_count_kernel(const uint32_t* __restrict__ cnt2, uint32_t nbins, int64_t ntiles,
-                                unsigned long long* __restrict__ tcnt) {
-    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= ntiles) return;
-    unsigned long long s = 0;
-    for (uint32_t b = 0; b < nbins; ++b) s += cnt2[t * (kMaxPieces + 1) + b];
-    tcnt[t] = s;
-}
-
 // ---------------------------------------------------------------------------
 // sliced probe (direct-addressed tables of <= kSlMaxSlices x 2^wlog key values): the
 // lookups run out of LDS instead of as random device reads. The fused probe does one
@@ -1596,10 +1302,13 @@ __global__ void pp_count_kernel(const uint32_t* __restrict__ cnt2, uint32_t nbin
 //                             entry's position. The probe waits for a build on another
 //                             stream only here (S1/S1b read no table memory).
 //   S3a sl_scan_kernel        (one workgroup): tile output offsets from the tiles' pair
-//                             counts. S1 writes a tile's in-range rows as its count; S2
-//                             adds count - 1 for every entry whose key is missing or
+//                             counts. S1 writes a tile's entries as its count; S2 adds
+//                             count - 1 for every entry whose key is missing or
 //                             duplicated (LDS atomics per owner tile, then one atomic per
 //                             tile and run), so no pass re-reads the refs to count them.
+//                             (A decoupled look-back inside S3b measured slower: 350 vs
+//                             212 us at C2, a tile's offset then waits for the slowest
+//                             workgroup holding an earlier tile.)
 //   S3b sl_emit_kernel        per tile (persistent, prefetching): its (row, ref) pairs
 //                             scattered into an LDS image of the tile's refs, then ordered
 //                             emission, 64 rows per wave step, one contiguous store run
@@ -1614,7 +1323,8 @@ constexpr int kSlTile = 1 << kSlTileLog;                // probe rows per tile
 constexpr int kSlGroups = kSlTile / (kSlThreads * 4);  // 4 groups of 4096 rows
 constexpr int kSlWidthLogMax = 15;                      // key values per slice: 2^wlog <= 32768 (128 KB of refs)
 constexpr int kSlMaxSlices = 2047;                      // key ranges up to ~2^25 values
-constexpr int kSlOwnWin = 2048;  // flattened segment positions per owner window (32 per lane)
+constexpr int kSlOwnWin = 2048;        // flattened segment positions per owner window (32 per lane)
+constexpr int kSlOwnWinHashed = 1024;  // hashed slices: 16 per lane (u64 entries)
 static_assert(kSlWidthLogMax + kSlTileLog <= 32, "entry = offset << tile bits | row");
 static_assert(kSlWidthLogMax <= 16 && kSlTileLog <= 16, "key offsets and rows leave as u16");
 
@@ -1624,8 +1334,8 @@ sl_partition_kernel(int64_t dmin, uint64_t drange, uint32_t wlog, uint32_t nslic
                     const uint8_t* __restrict__ valid, int64_t voff, int64_t n, bool vec,
                     uint16_t* __restrict__ ko, uint16_t* __restrict__ rl, uint16_t* __restrict__ toff, int nt,
                     int64_t tile_off, int64_t row_base, uint32_t* __restrict__ tile_base,
-                    unsigned long long* __restrict__ err_word,  // probe: the caller's error word; build: null
-                    unsigned long long* __restrict__ tcnt) {    // probe: the tile's in-range rows; build: null
+                    unsigned long long* __restrict__ hdr,  // probe: workspace header (error word at [1]); build: null
+                    unsigned long long* __restrict__ tcnt) {    // probe: the tile's entry count; build: null
     __shared__ __attribute__((aligned(16))) uint32_t s_ent[kSlTile];
     __shared__ uint32_t s_hist[2 * kSlThreads];  // bins 0..nslices (<= kSlMaxSlices + 1)
     __shared__ uint32_t s_w[kSlThreads / 64];
@@ -1634,8 +1344,8 @@ sl_partition_kernel(int64_t dmin, uint64_t drange, uint32_t wlog, uint32_t nslic
     const int64_t tile0 = tile * kSlTile;
     const uint32_t nbins = nslices + 1;  // bin nslices stays empty: its prefix is the total
     for (uint32_t b = threadIdx.x; b < 2 * kSlThreads; b += kSlThreads) s_hist[b] = 0;
-    // probe: zero the caller's error word (no memset launch)
-    if (err_word != nullptr && blockIdx.x == 0 && threadIdx.x == 0) *err_word = 0;
+    // probe: zero the workspace header incl. the error word (no memset launch)
+    if (hdr != nullptr && blockIdx.x == 0 && threadIdx.x == 0) hdr[0] = hdr[1] = 0;
     __syncthreads();
     // per row: entry (offset << 14 | row) and (slice << 14 | rank in slice), ~0 = no entry
     uint32_t e[kSlGroups][4], sr[kSlGroups][4];
@@ -1667,8 +1377,8 @@ sl_partition_kernel(int64_t dmin, uint64_t drange, uint32_t wlog, uint32_t nslic
     uint16_t* to = toff + gtile * (int64_t)nbins;
     for (uint32_t b = threadIdx.x; b < nbins; b += kSlThreads) to[b] = (uint16_t)s_hist[b];
     if (tile_base != nullptr && threadIdx.x == 0) tile_base[gtile] = (uint32_t)(row_base + tile0);  // build only
-    // probe: the tile's pair count starts as its in-range rows; S2 adds count - 1 for
-    // every entry whose key is missing (-1) or duplicated (+count - 1)
+    // probe: the tile's pair count starts as its entries (in-range rows); S2 adds count - 1
+    // for every entry whose key is missing (-1) or duplicated (+count - 1)
     if (tcnt != nullptr && threadIdx.x == 0) tcnt[gtile] = tot;
 #pragma unroll
     for (int g = 0; g < kSlGroups; ++g)
@@ -1940,31 +1650,62 @@ dense_frag_build_kernel(ChunkGeom g, uint32_t nblk, int64_t ntiles, const uint16
 // number of starts at or before it (mbcnt) — no per-position search, no scan per row.
 // Entries and refs go through buffer descriptors: 32-bit offsets, and positions past
 // the run's total take an out-of-range offset (load 0, store dropped) instead of a
-// branch. 32 entries per lane in flight.
+// branch. W / 64 entries per lane in flight.
+//   dense  (HASHED false): the slice is 2^wlog consecutive key values of the direct-
+//          addressed table (u32 refs); an entry is the key's offset in the slice (u16),
+//          its ref one LDS read.
+//   hashed (HASHED true): the slice is 2048 consecutive buckets (128 KB, kHsSliceLog);
+//          an entry is the stored key (mix64(key), u64); its ref comes from the home
+//          bucket's line in LDS (exact compare of stored keys, linear probing inside the
+//          chunk, as lookup4); key 0 reads the side bucket.
+constexpr int kHsSliceLog = 11;  // buckets per hashed slice: 2^11 x 64 B = 128 KB of LDS
+
+// ref of stored key sk (!= 0) in the LDS image of a hashed slice whose first bucket is
+// sbase; linear probing wraps inside the key's chunk (cmask), as the table was built
+__device__ __forceinline__ uint32_t lds_bucket_ref(const uint4* __restrict__ img, uint32_t nb, uint32_t sbase,
+                                                   uint32_t cmask, unsigned long long sk, uint32_t* cnt) {
+    uint32_t b = stored_bucket(sk, nb);
+    const uint4* p = img + (size_t)(b - sbase) * 4;
+    bool more;
+    uint32_t ref = scan_line(p[0], p[1], p[2], p[3], sk, &more, cnt);
+    for (uint32_t probes = 0; more && probes < cmask; ++probes) {
+        b = (b & ~cmask) | ((b + 1) & cmask);
+        const uint4* q = img + (size_t)(b - sbase) * 4;
+        ref = scan_line(q[0], q[1], q[2], q[3], sk, &more, cnt);
+    }
+    return ref;
+}
+
+template <bool HASHED, int W>
 __global__ void __launch_bounds__(kSlThreads)
 sl_lookup_kernel(TableView tv, uint32_t wlog, uint32_t nslices, int64_t ntiles, uint32_t parts,
-                 const uint16_t* __restrict__ ko, uint32_t* __restrict__ res, const uint16_t* __restrict__ toff,
+                 const void* __restrict__ ko, uint32_t* __restrict__ res, const uint16_t* __restrict__ toff,
                  unsigned long long* __restrict__ tcnt, int dbg) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t s_tab[];  // 2^wlog refs
+    extern __shared__ __attribute__((aligned(16))) uint32_t s_tab[];  // dense: 2^wlog refs; hashed: 2048 buckets
     __shared__ uint32_t s_base[kSlThreads];
-    __shared__ uint32_t s_lane[kSlThreads];   // per wave: tile lane of each non-empty segment, by rank
-    __shared__ int s_corr[kSlThreads];        // per wave: pair-count correction of each of its 64 tiles
-    __shared__ unsigned long long s_mask[kSlThreads / 64][kSlOwnWin / 64];
-    const uint32_t* __restrict__ dense = tv.dense;
-    const uint64_t drange = tv.drange;
+    __shared__ uint32_t s_lane[kSlThreads];  // per wave: tile lane of each non-empty segment, by rank
+    __shared__ int s_corr[kSlThreads];       // per wave: pair-count correction of each of its 64 tiles
+    __shared__ uint32_t s_end[HASHED ? kSlThreads : 1];  // hashed, per wave: end position of each fragment, by rank
+    __shared__ unsigned long long s_mask[kSlThreads / 64][W / 64];
     const uint32_t item = (dbg & 128) ? blockIdx.x : xcd_item(blockIdx.x, gridDim.x);
     const uint32_t s = item % nslices, part = item / nslices;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    {
+    uint32_t sbase = 0;  // hashed: first bucket of the slice
+    if constexpr (HASHED) {
+        sbase = s << kHsSliceLog;
+        const uint32_t nbk = min<uint32_t>(1u << kHsSliceLog, tv.nb - sbase);
+        const uint4* src = reinterpret_cast<const uint4*>(tv.tbl + sbase);
+        uint4* dst = reinterpret_cast<uint4*>(s_tab);
+        for (uint32_t i = threadIdx.x; i < nbk * 4; i += kSlThreads) dst[i] = src[i];
+    } else {
         const uint64_t base = (uint64_t)s << wlog;
-        const uint32_t len = (uint32_t)min<uint64_t>(1u << wlog, drange - base);
+        const uint32_t len = (uint32_t)min<uint64_t>(1u << wlog, tv.drange - base);
         const uint32_t len4 = len & ~3u;
+        const uint32_t* __restrict__ dense = tv.dense;
         // dense is 256-byte aligned and slices start at multiples of 64 KB
-        if (!(dbg & 32)) {
         for (uint32_t i = threadIdx.x * 4; i < len4; i += kSlThreads * 4)
             *reinterpret_cast<uint4*>(s_tab + i) = *reinterpret_cast<const uint4*>(dense + base + i);
         if (threadIdx.x < (len & 3u)) s_tab[len4 + threadIdx.x] = dense[base + len4 + threadIdx.x];
-        }
     }
     __syncthreads();
     // part boundaries on 64-tile blocks (the transposed bounds' granule)
@@ -1973,14 +1714,17 @@ sl_lookup_kernel(TableView tv, uint32_t wlog, uint32_t nslices, int64_t ntiles, 
     const int64_t nbins = nslices + 1;
     // per wave: the non-empty segments' bases (tile-relative position - excl) by rank, and
     // one 64-bit start mask per 64-position row of the window
-    uint32_t* sbase = s_base + wave * 64;
+    uint32_t* sbs = s_base + wave * 64;
     uint32_t* slane = s_lane + wave * 64;
     int* scorr = s_corr + wave * 64;
     scorr[lane] = 0;
+    uint32_t* send = s_end + (HASHED ? wave * 64 : 0);
     unsigned long long* smask = s_mask[wave];
     constexpr int64_t kStep = (kSlThreads / 64) * 64;  // tiles between a wave's blocks
     constexpr uint32_t kOob = 0x3FFFFF0u;               // entry index past every range: load 0, no store
     constexpr uint32_t kOobMask = (1u << 26) - 1;       // off[] = index | owner lane << 26
+    constexpr int KB = HASHED ? 8 : 2;                  // entry bytes
+    const uint32_t cmask = (1u << tv.clog2) - 1;
     // segment bounds of the lane's tile in block tc (toffT), loaded one block ahead
     auto bounds = [&](int64_t tc, uint32_t* st, uint32_t* len) {
         *st = 0;
@@ -2004,30 +1748,39 @@ sl_lookup_kernel(TableView tv, uint32_t wlog, uint32_t nslices, int64_t ntiles, 
         const uint32_t rank =
             __builtin_amdgcn_mbcnt_hi((uint32_t)(ne >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)ne, 0u));
         if (len != 0) {
-            sbase[rank] = (uint32_t)lane * kSlTile + st - excl;  // >= 0: excl <= lane * kSlTile
+            sbs[rank] = (uint32_t)lane * kSlTile + st - excl;  // >= 0: excl <= lane * kSlTile
             slane[rank] = (uint32_t)lane;
+            if constexpr (HASHED) send[rank] = excl + len;
         }
+        // hashed: the run's corrections as a running sum over the flattened positions; the
+        // last position of each fragment records it (scorr[rank]), so a fragment's
+        // correction is the difference of its end and its predecessor's end (a segmented
+        // sum without LDS atomics: half the entries of a uniform probe side miss)
+        int run_sum = 0;
         // the 64 tiles' regions as buffers (wave-uniform bases): 32-bit offsets, and an
         // out-of-range offset turns a position past R into a dropped access
         const int64_t tcu = (int64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)tc) |
                             ((int64_t)__builtin_amdgcn_readfirstlane((int)(tc >> 32)) << 32);
-        const __amdgpu_buffer_rsrc_t rko =
-            __builtin_amdgcn_make_buffer_rsrc((void*)(ko + tcu * kSlTile), 0, 64 * kSlTile * 2, 0x00020000);
+        const __amdgpu_buffer_rsrc_t rko = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)((const char*)ko + tcu * kSlTile * KB), 0, 64 * kSlTile * KB, 0x00020000);
         const __amdgpu_buffer_rsrc_t rres =
             __builtin_amdgcn_make_buffer_rsrc((void*)(res + tcu * kSlTile), 0, 64 * kSlTile * 4, 0x00020000);
         uint32_t kb = 0;  // segments started before the current row
-        for (uint32_t w0 = 0; w0 < R; w0 += kSlOwnWin) {
-            if (lane < kSlOwnWin / 64) smask[lane] = 0;
+        for (uint32_t w0 = 0; w0 < R; w0 += W) {
+            if (lane < W / 64) smask[lane] = 0;
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
             __builtin_amdgcn_wave_barrier();
-            if (len != 0 && excl >= w0 && excl < w0 + kSlOwnWin)
-                atomicOr(&smask[(excl - w0) >> 6], 1ull << ((excl - w0) & 63));
+            if (len != 0 && excl >= w0 && excl < w0 + W) atomicOr(&smask[(excl - w0) >> 6], 1ull << ((excl - w0) & 63));
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
             __builtin_amdgcn_wave_barrier();
-            // off: the entry's index (or kOob) | owner tile lane << 26
-            uint32_t off[kSlOwnWin / 64], ev[kSlOwnWin / 64];
+            uint32_t off[W / 64];  // the entry's index (or kOob) | owner tile lane << 26
+            uint32_t off_end = 0;  // hashed: bit u = this lane's position u ends its fragment
+            using EV = typename std::conditional<HASHED, unsigned long long, uint32_t>::type;
+            EV ev[W / 64];
 #pragma unroll
-            for (int u = 0; u < kSlOwnWin / 64; ++u) {
+            for (int u = 0; u < W / 64; ++u) {
+                off[u] = kOob;
+                if (HASHED && w0 + u * 64 >= R) continue;  // uniform: past the run (small fragments)
                 const uint32_t r = w0 + u * 64 + lane;
                 const unsigned long long m = smask[u];  // the same word for every lane
                 const uint32_t mlo = __builtin_amdgcn_readfirstlane((uint32_t)m);
@@ -2039,25 +1792,70 @@ sl_lookup_kernel(TableView tv, uint32_t wlog, uint32_t nslices, int64_t ntiles, 
                                                                   __builtin_amdgcn_mbcnt_lo((uint32_t)m1, 0u));
                 const uint32_t k = kb + (uint32_t)(mu & 1) + below - 1;
                 kb += (uint32_t)__builtin_popcountll(mu);
-                const uint32_t ps = sbase[k & 63] + r;
+                const uint32_t ps = sbs[k & 63] + r;
                 const uint32_t o = r < R ? ps : kOob;
-                ev[u] = __builtin_amdgcn_raw_buffer_load_b16(rko, (int)(o * 2), 0, 0);
-                off[u] = o | (slane[k & 63] << 26);
+                if constexpr (HASHED) {
+                    if (r + 1 == send[k & 63]) off_end |= 1u << u;  // last position of its fragment
+                }
+                if constexpr (HASHED) {
+                    const uint2 v = __builtin_bit_cast(
+                        uint2, __builtin_amdgcn_raw_buffer_load_b64(rko, (int)(o * 8), 0, 0));
+                    ev[u] = ((unsigned long long)v.y << 32) | v.x;
+                } else {
+                    ev[u] = __builtin_amdgcn_raw_buffer_load_b16(rko, (int)(o * 2), 0, 0);
+                }
+                off[u] = o | ((HASHED ? (k & 63) : slane[k & 63]) << 26);  // hashed: the owner's rank
             }
 #pragma unroll
-            for (int u = 0; u < kSlOwnWin / 64; ++u) {
-                const uint32_t v = s_tab[ev[u] & ((1u << wlog) - 1)];
+            for (int u = 0; u < W / 64; ++u) {
+                if (HASHED && w0 + u * 64 >= R) continue;  // uniform: past the run
                 const uint32_t o = off[u] & kOobMask;
+                uint32_t v, c;  // ref and its row count
+                if constexpr (HASHED) {
+                    const unsigned long long sk = ev[u];
+                    if (o == kOob) {
+                        v = kMiss;  // no store, no correction
+                        c = 1;
+                    } else if (dbg & 4) {  // timing ablation: no bucket lookup (wrong pairs)
+                        v = (uint32_t)sk & 0xFFFFFFu;
+                        c = 1;
+                    } else if (sk == 0) {  // key 0: the side bucket (rare)
+                        const Bucket& S = tv.tbl[tv.nb];
+                        v = S.meta ? S.ref[0] : kMiss;
+                        c = S.meta;
+                    } else {
+                        v = lds_bucket_ref(reinterpret_cast<const uint4*>(s_tab), tv.nb, sbase, cmask, sk, &c);
+                        if (c == kCountUnknown) c = tv.dup_rows[v & tv.off_mask];
+                    }
+                } else {
+                    v = s_tab[ev[u] & ((1u << wlog) - 1)];
+                    c = 1;
+                    if (o != kOob && (v == kMiss || (v & kDupFlag))) {
+                        const uint32_t c4 = tv.off_mask == kPackedMask ? ((v >> 27) & 15u) : 0u;
+                        c = v == kMiss ? 0u : c4 ? c4 : tv.dup_rows[v & tv.off_mask];
+                    }
+                }
                 __builtin_amdgcn_raw_buffer_store_b32(v, rres, (int)(o * 4), 0, 0);
                 // pair-count correction (count - 1) of a missing or duplicated key, per
                 // owner tile; none in a window of unique hits (C2: no LDS atomics at all)
-                const bool odd = o != kOob && (v == kMiss || (v & kDupFlag));
-                if (__ballot(odd) != 0 && odd) {
-                    const uint32_t c4 = tv.off_mask == kPackedMask ? ((v >> 27) & 15u) : 0u;
-                    const uint32_t c = v == kMiss ? 0u : c4 ? c4 : tv.dup_rows[v & tv.off_mask];
+                const bool odd = c != 1;
+                if constexpr (HASHED) {
+                    const int incl = (int)wave_incl_scan_dpp((uint32_t)((int)c - 1)) + run_sum;
+                    run_sum = __builtin_amdgcn_readlane(incl, 63);
+                    if (off_end & (1u << u)) scorr[off[u] >> 26] = incl;
+                } else if (__ballot(odd) != 0 && odd) {
                     atomicAdd(&scorr[off[u] >> 26], (int)c - 1);
                 }
             }
+        }
+        if constexpr (HASHED) {  // fragment ends -> per-tile corrections (rank order = lane order)
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            int cr = 0;
+            if (len != 0) cr = scorr[rank] - (rank > 0 ? scorr[rank - 1] : 0);
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            scorr[lane] = cr;  // by tile lane, as the dense path leaves it
         }
         // the run's corrections: one atomic per tile that has one (64 contiguous counters)
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -2069,6 +1867,96 @@ sl_lookup_kernel(TableView tv, uint32_t wlog, uint32_t nslices, int64_t ntiles, 
         }
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         __builtin_amdgcn_wave_barrier();
+    }
+}
+
+// S1 of the hashed sliced probe: per 16384-row tile, the valid rows sorted by slice
+// (home bucket >> kHsSliceLog) in LDS; the tile's stored keys (u64) and rows in the
+// tile (u16) leave in slice order, with the tile's slice bounds (u16). Persistent, one
+// workgroup per CU (128 KB of staged keys): the next tile's keys load into registers
+// once this tile's keys are staged, while they and the rows are written out.
+template <typename K, bool HAS_VALID>
+__global__ void __launch_bounds__(kSlThreads, 4)  // 16 waves per CU: <= 128 VGPRs
+hs_partition_kernel(uint32_t nb, uint32_t nslices, const void* __restrict__ keys,
+                    const uint8_t* __restrict__ valid, int64_t voff, int64_t n, int64_t ntiles, bool vec,
+                    unsigned long long* __restrict__ ko, uint16_t* __restrict__ rl, uint16_t* __restrict__ toff,
+                    unsigned long long* __restrict__ hdr, unsigned long long* __restrict__ tcnt) {
+    __shared__ __attribute__((aligned(16))) unsigned long long s_key[kSlTile];  // also the rows (u16) pass
+    __shared__ uint32_t s_hist[2 * kSlThreads];
+    __shared__ uint32_t s_w[kSlThreads / 64];
+    const uint32_t nbins = nslices + 1;
+    if (blockIdx.x == 0 && threadIdx.x == 0) hdr[0] = hdr[1] = 0;  // workspace header (error word)
+    int64_t k[kSlGroups][4], nk[kSlGroups][4];
+    auto load = [&](int64_t t, int64_t (&dst)[kSlGroups][4]) {
+#pragma unroll
+        for (int g = 0; g < kSlGroups; ++g)
+            load4<K>(keys, t * kSlTile + g * (kSlThreads * 4) + threadIdx.x * 4, n, vec, dst[g]);
+    };
+    int64_t tile = blockIdx.x;
+    if (tile < ntiles) load(tile, nk);
+    for (; tile < ntiles; tile += gridDim.x) {
+        const int64_t tile0 = tile * kSlTile;
+#pragma unroll
+        for (int g = 0; g < kSlGroups; ++g)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) k[g][q] = nk[g][q];
+        for (uint32_t b = threadIdx.x; b < 2 * kSlThreads; b += kSlThreads) s_hist[b] = 0;
+        __syncthreads();
+        uint32_t sr[kSlGroups][4];  // slice << 14 | rank in slice, ~0 = no entry
+#pragma unroll
+        for (int g = 0; g < kSlGroups; ++g) {
+            const int loc0 = g * (kSlThreads * 4) + threadIdx.x * 4;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int64_t row = tile0 + loc0 + q;
+                const bool ok = row < n && (!HAS_VALID || bit_valid(valid, voff, row));
+                const unsigned long long sk = stored_key(k[g][q]);
+                const uint32_t sl = stored_bucket(sk, nb) >> kHsSliceLog;
+                sr[g][q] = ok ? (sl << kSlTileLog) | atomicAdd(&s_hist[sl], 1u) : 0xFFFFFFFFu;
+            }
+        }
+        __syncthreads();
+        const uint32_t b0 = threadIdx.x * 2;
+        const uint32_t h0 = s_hist[b0], h1 = s_hist[b0 + 1];
+        uint32_t tot;
+        const uint32_t ex = block_excl_scan<uint32_t>(h0 + h1, s_w, &tot);
+        s_hist[b0] = ex;
+        s_hist[b0 + 1] = ex + h0;
+        __syncthreads();
+        uint16_t* to = toff + tile * (int64_t)nbins;
+        for (uint32_t b = threadIdx.x; b < nbins; b += kSlThreads) to[b] = (uint16_t)s_hist[b];
+        if (threadIdx.x == 0) tcnt[tile] = tot;  // S2 corrects it to the tile's pair count
+        // pass 1: stored keys in slice order
+#pragma unroll
+        for (int g = 0; g < kSlGroups; ++g)
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                if (sr[g][q] != 0xFFFFFFFFu)
+                    s_key[s_hist[sr[g][q] >> kSlTileLog] + (sr[g][q] & (kSlTile - 1))] = stored_key(k[g][q]);
+        __syncthreads();
+        if (tile + (int64_t)gridDim.x < ntiles) load(tile + gridDim.x, nk);  // in flight during the write-out
+        unsigned long long* dk = ko + tile0;
+        for (uint32_t i = threadIdx.x * 2; i < tot; i += kSlThreads * 2) {
+            if (i + 2 <= tot) *reinterpret_cast<ulonglong2*>(dk + i) = *reinterpret_cast<const ulonglong2*>(s_key + i);
+            else dk[i] = s_key[i];
+        }
+        __syncthreads();
+        // pass 2: rows in the tile (u16), same order
+        uint16_t* s_row = reinterpret_cast<uint16_t*>(s_key);
+#pragma unroll
+        for (int g = 0; g < kSlGroups; ++g)
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                if (sr[g][q] != 0xFFFFFFFFu)
+                    s_row[s_hist[sr[g][q] >> kSlTileLog] + (sr[g][q] & (kSlTile - 1))] =
+                        (uint16_t)(g * (kSlThreads * 4) + threadIdx.x * 4 + q);
+        __syncthreads();
+        uint16_t* dr = rl + tile0;
+        for (uint32_t i = threadIdx.x * 8; i < tot; i += kSlThreads * 8) {
+            if (i + 8 <= tot) *reinterpret_cast<uint4*>(dr + i) = *reinterpret_cast<const uint4*>(s_row + i);
+            else for (uint32_t j = i; j < tot; ++j) dr[j] = s_row[j];
+        }
+        __syncthreads();  // s_key / s_hist are rewritten for the next tile
     }
 }
 
@@ -2750,46 +2638,33 @@ hipError_t launch_build(int key_bytes, const Segment* d_segs, int nseg, int64_t 
 
 int64_t probe_tiles(int64_t n) { return (n + kProbeTile - 1) / kProbeTile; }
 
-// workspace layout (all regions 256-byte aligned):
-//   [0,16) header (bytes 8..15: error word) | tcnt u64[nt+2] | bsum (scan scratch) | cnt2 u32[nt][256] |
-//   toff u16[nt][257] | skeys u64[nt*4096] | perm u16[n] | info u32[nt*4096]
+// fused probe workspace (all regions 256-byte aligned): [0,16) header (bytes 8..15:
+// error word) | tcnt u64[nt + 2] (the look-back's per-tile flags)
 namespace {
 struct ProbeWs {
     unsigned long long* tcnt;
-    unsigned long long* bsum;
-    uint32_t* cnt2;
-    uint16_t* toff;
-    unsigned long long* skeys;
-    uint16_t* perm;
-    uint32_t* info;
     int64_t bytes;
 };
 inline uintptr_t al256(uintptr_t x) { return (x + 255) & ~(uintptr_t)255; }
 ProbeWs probe_ws_layout(void* base, int64_t n) {
     const int64_t nt = probe_tiles(n > 0 ? n : 0);
-    const int64_t rows = nt * kProbeTile;
     ProbeWs w;
     uintptr_t p = (uintptr_t)base + 256;
     w.tcnt = (unsigned long long*)p; p = al256(p + 8 * (nt + 2));
-    w.bsum = (unsigned long long*)p; p = al256(p + scan_scratch_bytes(nt));
-    w.cnt2 = (uint32_t*)p;           p = al256(p + 4 * nt * (kMaxPieces + 1));
-    w.toff = (uint16_t*)p;           p = al256(p + 2 * nt * (kMaxPieces + 2));
-    w.skeys = (unsigned long long*)p; p = al256(p + 8 * rows);
-    w.perm = (uint16_t*)p;           p = al256(p + 2 * rows);
-    w.info = (uint32_t*)p;           p = al256(p + 4 * rows);
     w.bytes = (int64_t)(p - (uintptr_t)base) + 256;  // + slack for an unaligned base
     return w;
 }
 
-// sliced probe workspace (16384-row tiles): tcnt u64[nt + 2] (counts, then offsets) | bsum |
-// toff u16[nt][kSlMaxSlices + 1] | toffT | ko u16[nt * kSlTile] (key offsets) |
-// rl u16[nt * kSlTile] (rows in tile) | res u32[nt * kSlTile] (refs)
+// sliced probe workspace (16384-row tiles), after the 16-byte header (error word at
+// bytes 8..15): tcnt u64[nt + 2] (counts, then offsets) | bsum | toff u16[nt][kSlMaxSlices + 1] | toffT |
+// ko (entries: u16 key offsets in a dense slice, u64 stored keys in a hashed one; 8 B per
+// row reserved) | rl u16[nt * kSlTile] (rows in tile) | res u32[nt * kSlTile] (refs)
 struct SlicedWs {
     unsigned long long* tcnt;
     unsigned long long* bsum;  // scan scratch past kSlScanOne tiles
     uint16_t* toff;
     uint16_t* toffT;
-    uint16_t* ko;
+    void* ko;
     uint16_t* rl;
     uint32_t* res;
     int64_t bytes;
@@ -2798,22 +2673,20 @@ SlicedWs sliced_ws_layout(void* base, int64_t n) {
     const int64_t nt = (n + kSlTile - 1) / kSlTile;
     SlicedWs w;
     uintptr_t p = (uintptr_t)base + 256;
-    w.tcnt = (unsigned long long*)p; p = al256(p + 8 * (nt + 2));
-    w.bsum = (unsigned long long*)p; p = al256(p + scan_scratch_bytes(nt));
+    w.tcnt = (unsigned long long*)p;  p = al256(p + 8 * (nt + 2));
+    w.bsum = (unsigned long long*)p;  p = al256(p + scan_scratch_bytes(nt));
     w.toff = (uint16_t*)p;            p = al256(p + 2 * nt * (kSlMaxSlices + 1));
     w.toffT = (uint16_t*)p;           p = al256(p + 2 * ((nt + 63) & ~(int64_t)63) * (kSlMaxSlices + 1));
-    w.ko = (uint16_t*)p;              p = al256(p + 2 * nt * kSlTile);
+    w.ko = (void*)p;                  p = al256(p + 8 * nt * kSlTile);
     w.rl = (uint16_t*)p;              p = al256(p + 2 * nt * kSlTile);
     w.res = (uint32_t*)p;             p = al256(p + 4 * nt * kSlTile);
     w.bytes = (int64_t)(p - (uintptr_t)base) + 256;
     return w;
 }
 
-int env_probe_mode() {  // 0 auto, 1 two-pass direct, 2 partitioned, 3 fused, 4 sliced
+int env_probe_mode() {  // 0 auto, 3 fused, 4 sliced (1 and 2 were retired strategies)
     const char* e = getenv("DFP_HJ_PROBE_MODE");
     if (!e) return 0;
-    if (e[0] == 'd' || e[0] == 't') return 1;
-    if (e[0] == 'p') return 2;
     if (e[0] == 'f') return 3;
     if (e[0] == 's') return 4;
     return 0;
@@ -2829,7 +2702,9 @@ int probe_mode() {
 }
 }  // namespace
 
-void set_probe_mode(int mode) { g_probe_mode.store(mode < 0 || mode > 4 ? 0 : mode, std::memory_order_relaxed); }
+void set_probe_mode(int mode) {
+    g_probe_mode.store(mode == 3 || mode == 4 ? mode : 0, std::memory_order_relaxed);
+}
 int get_probe_mode() { return probe_mode(); }
 
 int64_t probe_workspace(int64_t n) {
@@ -2869,44 +2744,64 @@ int sl_emit_wgs_per_cu() {
     return v;
 }
 uint32_t sl_slices(const TableView& tv) {
+    if (tv.dense == nullptr) return (tv.nb + (1u << kHsSliceLog) - 1) >> kHsSliceLog;  // 128 KB bucket slices
     const uint32_t w = sl_wlog();
-    return tv.dense ? (uint32_t)std::min<uint64_t>((tv.drange + (1u << w) - 1) >> w, 1u << 30) : 0;
+    return (uint32_t)std::min<uint64_t>((tv.drange + (1u << w) - 1) >> w, 1u << 30);
 }
 // auto choice: the sliced probe pays for its two extra passes once the table is past
-// the L2s (> 1 M key values = 4 MB of refs) and the probe side outweighs the slice loads
+// the L2s (direct-addressed: > 1 M key values = 4 MB of refs; hashed: > 2^16 buckets =
+// 4 MB) and the probe side outweighs the slice loads (every slice is read once or a few
+// times per probe)
 bool sl_auto(const TableView& tv, int64_t n) {
     static const int64_t min_range = [] {
         const char* e = getenv("DFP_HJ_SLICED_MIN_RANGE");
         return e ? atoll(e) : (int64_t)1 << 20;
     }();
-    return (int64_t)tv.drange >= min_range && n >= (int64_t)tv.drange && n >= 4 * (int64_t)kSlTile;
+    if (n < 4 * (int64_t)kSlTile) return false;
+    if (tv.dense == nullptr) return (int64_t)tv.nb * 16 >= min_range && n >= (int64_t)tv.nb;
+    return (int64_t)tv.drange >= min_range && n >= (int64_t)tv.drange;
 }
 
 hipError_t launch_probe_sliced(int key_bytes, const TableView& tv, const void* keys, const uint8_t* valid,
                                int64_t voff, const uint32_t* probe_ids, int64_t n, uint64_t* out_b,
                                uint32_t* out_p, int64_t cap, int64_t* d_total, void* workspace, hipEvent_t built,
                                hipStream_t s) {
+    const bool hashed = tv.dense == nullptr;
     const int64_t nt = (n + kSlTile - 1) / kSlTile;
     const uint32_t nsl = sl_slices(tv), wlog = sl_wlog();
     SlicedWs w = sliced_ws_layout((void*)(((uintptr_t)workspace + 255) & ~(uintptr_t)255), n);
     const bool vec = (reinterpret_cast<uintptr_t>(keys) & 15) == 0;
     hipError_t e = hipSuccess;
-    // workspace + 8: the caller's error word, zeroed by S1 (the layout starts >= 256 bytes in)
-    unsigned long long* err_word = reinterpret_cast<unsigned long long*>((char*)workspace + 8);
+    // workspace [0, 16): header with the caller's error word, zeroed by S1 (the layout
+    // starts >= 256 bytes in)
+    unsigned long long* hdr = reinterpret_cast<unsigned long long*>(workspace);
     static const int sl_nt = [] {  // 1: nontemporal probe-key loads in S1
         const char* ev = getenv("DFP_HJ_SL_NT");
         return ev ? atoi(ev) : 0;
     }();
+    if (hashed) {
+        const unsigned pgrid = (unsigned)std::min<int64_t>(nt, sl_num_cus());
+#define DFP_HSP(KT, HV)                                                                                           \
+    hs_partition_kernel<KT, HV><<<pgrid, kSlThreads, 0, s>>>(tv.nb, nsl, keys, valid, voff, n, nt, vec,            \
+                                                            (unsigned long long*)w.ko, w.rl, w.toff, hdr, w.tcnt)
+        if (key_bytes == 8) {
+            if (valid) DFP_HSP(int64_t, true); else DFP_HSP(int64_t, false);
+        } else {
+            if (valid) DFP_HSP(int32_t, true); else DFP_HSP(int32_t, false);
+        }
+#undef DFP_HSP
+    } else {
 #define DFP_SLP(KT, HV)                                                                                      \
     sl_partition_kernel<KT, HV><<<(unsigned)nt, kSlThreads, 0, s>>>(tv.dmin, tv.drange, wlog, nsl, keys, valid, voff, n, \
-                                                                   vec, w.ko, w.rl, w.toff, sl_nt, 0, 0, nullptr, \
-                                                                   err_word, w.tcnt)
-    if (key_bytes == 8) {
-        if (valid) DFP_SLP(int64_t, true); else DFP_SLP(int64_t, false);
-    } else {
-        if (valid) DFP_SLP(int32_t, true); else DFP_SLP(int32_t, false);
-    }
+                                                                   vec, (uint16_t*)w.ko, w.rl, w.toff, sl_nt, 0, 0,   \
+                                                                   nullptr, hdr, w.tcnt)
+        if (key_bytes == 8) {
+            if (valid) DFP_SLP(int64_t, true); else DFP_SLP(int64_t, false);
+        } else {
+            if (valid) DFP_SLP(int32_t, true); else DFP_SLP(int32_t, false);
+        }
 #undef DFP_SLP
+    }
     // (slice, tile range) work items: about 1024 of them, so that the resident workgroups
     // (one per CU at 128 KB slices) run several rounds and the tail stays short
     static const uint32_t target = [] {
@@ -2916,13 +2811,15 @@ hipError_t launch_probe_sliced(int key_bytes, const TableView& tv, const void* k
     uint32_t parts = std::max<uint32_t>(1, (target + nsl - 1) / nsl);
     parts = (uint32_t)std::min<int64_t>(parts, (nt + 63) / 64);
     // timing ablations only (wrong pairs): emit 1 no stores, 2 no entries; lookup 4 no
-    // entry loads, 8 no ref stores, 16 no segment-bound loads
+    // bucket lookup (hashed), 128 plain item order
     static const int sl_dbg = [] {
         const char* ev = getenv("DFP_HJ_SL_DBG");
         return ev ? atoi(ev) : 0;
     }();
-    const size_t tab_lds = sizeof(uint32_t) << wlog;
-    e = hipFuncSetAttribute((const void*)sl_lookup_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)tab_lds);
+    const size_t tab_lds = hashed ? (sizeof(Bucket) << kHsSliceLog) : (sizeof(uint32_t) << wlog);
+    const void* lk = hashed ? (const void*)sl_lookup_kernel<true, kSlOwnWinHashed>
+                            : (const void*)sl_lookup_kernel<false, kSlOwnWin>;
+    e = hipFuncSetAttribute(lk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)tab_lds);
     if (e != hipSuccess) return e;
     sl_toff_transpose_kernel<<<(unsigned)((nt + 63) / 64 * ((nsl + kSlTrChunk) / kSlTrChunk)), 256, 0, s>>>(
         w.toff, nsl + 1, nt, w.toffT);
@@ -2930,8 +2827,12 @@ hipError_t launch_probe_sliced(int key_bytes, const TableView& tv, const void* k
         e = hipStreamWaitEvent(s, built, 0);
         if (e != hipSuccess) return e;
     }
-    sl_lookup_kernel<<<nsl * parts, kSlThreads, tab_lds, s>>>(tv, wlog, nsl, nt, parts, w.ko, w.res, w.toffT,
-                                                              w.tcnt, sl_dbg);
+    if (hashed)
+        sl_lookup_kernel<true, kSlOwnWinHashed><<<nsl * parts, kSlThreads, tab_lds, s>>>(tv, wlog, nsl, nt, parts, w.ko,
+                                                                                       w.res, w.toffT, w.tcnt, sl_dbg);
+    else
+        sl_lookup_kernel<false, kSlOwnWin><<<nsl * parts, kSlThreads, tab_lds, s>>>(tv, wlog, nsl, nt, parts, w.ko,
+                                                                                  w.res, w.toffT, w.tcnt, sl_dbg);
     if (nt <= kSlScanOne) {
         sl_scan_kernel<<<1, 1024, 0, s>>>(w.tcnt, nt, (unsigned long long*)d_total);
     } else {
@@ -2940,7 +2841,7 @@ hipError_t launch_probe_sliced(int key_bytes, const TableView& tv, const void* k
     }
     const bool ri = tv.row_ids != nullptr, pi = probe_ids != nullptr;
     const unsigned egrid = (unsigned)std::min<int64_t>(nt, (int64_t)sl_emit_wgs_per_cu() * sl_num_cus());
-#define DFP_SLE(RI, PI)                                                                                   \
+#define DFP_SLE(RI, PI)                                                                                           \
     sl_emit_kernel<RI, PI><<<egrid, kSlEmitThreads, 0, s>>>(tv, nsl, w.rl, w.res, w.toff, probe_ids, w.tcnt, nt, \
                                                            out_b, out_p, cap, sl_dbg)
     if (ri && pi) DFP_SLE(true, true);
@@ -2958,8 +2859,7 @@ hipError_t launch_probe(int key_bytes, const TableView& tv, const void* keys, co
     const int64_t nt = probe_tiles(n);
     const int mode = probe_mode();
     const uint32_t nsl = sl_slices(tv);
-    if (nt > 0 && tv.dense != nullptr && nsl >= 1 && nsl <= (uint32_t)kSlMaxSlices &&
-        (mode == 4 || (mode == 0 && sl_auto(tv, n))))
+    if (nt > 0 && nsl >= 1 && nsl <= (uint32_t)kSlMaxSlices && (mode == 4 || (mode == 0 && sl_auto(tv, n))))
         return launch_probe_sliced(key_bytes, tv, keys, valid, voff, probe_ids, n, out_b, out_p, cap, d_total,
                                    workspace, built, s);  // S1 zeroes the error word
     if (built != nullptr) {
@@ -2972,21 +2872,15 @@ hipError_t launch_probe(int key_bytes, const TableView& tv, const void* keys, co
     // align the layout on the workspace base
     ProbeWs w = probe_ws_layout((void*)(((uintptr_t)workspace + 255) & ~(uintptr_t)255), n);
     const bool vec = (reinterpret_cast<uintptr_t>(keys) & 15) == 0;
-    // The partitioned probe (pieces L2-resident per XCD) is opt-in: measured on MI355X
-    // it lifts the L2 hit rate of the lookups from ~19% to ~73% but per-lane scattered
-    // line accesses stay bound by the L2 request rate, and its two extra passes cost
-    // more than it saves at C2 (profiles/r01_*). DESIGN.md §5.
-    const bool part = mode == 2 && tv.dense == nullptr;  // dense tables: no pieces to partition by
-    if (mode == 0 || mode == 3 || mode == 4 || (mode == 2 && !part)) {
-        static const int fused_nt = [] {  // 1: keys nontemporal, 2: pair stores nontemporal
-            const char* e = getenv("DFP_HJ_NT");
-            return e ? atoi(e) : 0;
-        }();
-        // fused lookup + emission; tile flags live in the tile-count region
-        hipError_t e = hipMemsetAsync(w.tcnt, 0, sizeof(unsigned long long) * nt, s);
-        if (e != hipSuccess) return e;
-        unsigned long long* err = reinterpret_cast<unsigned long long*>((char*)workspace + 8);
-        const bool ri = tv.row_ids != nullptr, pi = probe_ids != nullptr;
+    static const int fused_nt = [] {  // 1: keys nontemporal, 2: pair stores nontemporal
+        const char* e = getenv("DFP_HJ_NT");
+        return e ? atoi(e) : 0;
+    }();
+    // fused lookup + emission; tile flags live in the tile-count region
+    hipError_t e = hipMemsetAsync(w.tcnt, 0, sizeof(unsigned long long) * nt, s);
+    if (e != hipSuccess) return e;
+    unsigned long long* err = reinterpret_cast<unsigned long long*>((char*)workspace + 8);
+    const bool ri = tv.row_ids != nullptr, pi = probe_ids != nullptr;
 #define DFP_FUSED(KT, HV, RI, PI)                                                                             \
     probe_fused_kernel<KT, HV, RI, PI><<<(unsigned)nt, kProbeThreads, 0, s>>>(tv, keys, valid, voff, probe_ids, n, \
                                                                              vec, w.tcnt, err, out_b, out_p, cap, \
@@ -2998,83 +2892,13 @@ hipError_t launch_probe(int key_bytes, const TableView& tv, const void* keys, co
         else if (pi) DFP_FUSED(KT, HV, false, true);     \
         else DFP_FUSED(KT, HV, false, false);            \
     } while (0)
-        if (key_bytes == 8) {
-            if (valid) DFP_FUSED_K(int64_t, true); else DFP_FUSED_K(int64_t, false);
-        } else {
-            if (valid) DFP_FUSED_K(int32_t, true); else DFP_FUSED_K(int32_t, false);
-        }
+    if (key_bytes == 8) {
+        if (valid) DFP_FUSED_K(int64_t, true); else DFP_FUSED_K(int64_t, false);
+    } else {
+        if (valid) DFP_FUSED_K(int32_t, true); else DFP_FUSED_K(int32_t, false);
+    }
 #undef DFP_FUSED_K
 #undef DFP_FUSED
-        return hipGetLastError();
-    }
-    if (part) {
-        const uint32_t chunk_bytes = (1u << tv.clog2) * (uint32_t)sizeof(Bucket);
-        const uint32_t nchunks = tv.nb >> tv.clog2;
-        PieceGeom pg;
-        static const uint32_t piece_bytes = [] {
-            const char* e = getenv("DFP_HJ_PIECE_KB");
-            const long kb = e ? atol(e) : 2048;
-            return (uint32_t)std::max<long>(64, kb) << 10;
-        }();
-        pg.cpp = std::max<uint32_t>(1, piece_bytes / chunk_bytes);
-        pg.npiece = (nchunks + pg.cpp - 1) / pg.cpp;
-        if (pg.npiece > (uint32_t)kMaxPieces) {
-            pg.cpp = (nchunks + kMaxPieces - 1) / kMaxPieces;
-            pg.npiece = (nchunks + pg.cpp - 1) / pg.cpp;
-        }
-#define DFP_PART(KT, HV)                                                                                         \
-    pp_partition_kernel<KT, HV><<<(unsigned)nt, kProbeThreads, 0, s>>>(tv, pg, keys, valid, voff, n, vec, w.skeys, \
-                                                                       w.perm, w.toff, w.info, w.cnt2)
-        if (key_bytes == 8) {
-            if (valid) DFP_PART(int64_t, true); else DFP_PART(int64_t, false);
-        } else {
-            if (valid) DFP_PART(int32_t, true); else DFP_PART(int32_t, false);
-        }
-#undef DFP_PART
-        // one resident wave set: every block must be running at once for the XCD
-        // grouping (blockIdx % 8) and the lockstep over pieces to hold
-        static const int pp_grid = [] {
-            int dev = 0, per_cu = 0;
-            hipDeviceProp_t prop;
-            if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&prop, dev) != hipSuccess) return 1024;
-            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, pp_lookup_kernel, kProbeThreads, 0) !=
-                    hipSuccess || per_cu < 1)
-                per_cu = 1;
-            const int g = per_cu * prop.multiProcessorCount;
-            return std::max(8, g & ~7);
-        }();
-        pp_lookup_kernel<<<pp_grid, kProbeThreads, 0, s>>>(tv, pg, n, nt, w.skeys, w.toff, w.info, w.cnt2);
-        pp_count_kernel<<<(unsigned)((nt + 255) / 256), 256, 0, s>>>(w.cnt2, pg.npiece + 1, nt, w.tcnt);
-    } else {
-#define DFP_LOOKUP(KT, HV) \
-    probe_lookup_kernel<KT, HV><<<(unsigned)nt, kProbeThreads, 0, s>>>(tv, keys, valid, voff, n, vec, w.info, w.tcnt)
-        if (key_bytes == 8) {
-            if (valid) DFP_LOOKUP(int64_t, true); else DFP_LOOKUP(int64_t, false);
-        } else {
-            if (valid) DFP_LOOKUP(int32_t, true); else DFP_LOOKUP(int32_t, false);
-        }
-#undef DFP_LOOKUP
-    }
-    {
-        hipError_t e = launch_scan<unsigned long long>(w.tcnt, nt, w.bsum, (unsigned long long*)d_total, s);
-        if (e != hipSuccess) return e;
-    }
-#define DFP_EMIT(SO, RI, PI)                                                                                          \
-    probe_emit_kernel<SO, RI, PI><<<(unsigned)nt, kProbeThreads, 0, s>>>(tv, w.info, w.perm, probe_ids, n, w.tcnt, \
-                                                                        out_b, out_p, cap)
-    const bool ri = tv.row_ids != nullptr, pi = probe_ids != nullptr;
-    if (part) {
-        if (ri && pi) DFP_EMIT(true, true, true);
-        else if (ri) DFP_EMIT(true, true, false);
-        else if (pi) DFP_EMIT(true, false, true);
-        else DFP_EMIT(true, false, false);
-    } else {
-        if (ri && pi) DFP_EMIT(false, true, true);
-        else if (ri) DFP_EMIT(false, true, false);
-        else if (pi) DFP_EMIT(false, false, true);
-        else DFP_EMIT(false, false, false);
-    }
-#undef DFP_EMIT
     return hipGetLastError();
 }
 

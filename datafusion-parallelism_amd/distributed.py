@@ -408,8 +408,10 @@ def all_gather_rows(cols: list[torch.Tensor], group=None) -> list[torch.Tensor]:
 
 def shuffle(keys: torch.Tensor, payload: list[torch.Tensor], group=None, partition_fn: Callable | None = None):
     """Hash-repartition exchange (DataFusion's RepartitionExec Hash, over RCCL): row i goes
-    to rank ``mix64(key) & (G-1)`` — the same map as DistributedHashJoin, so two sides
-    shuffled on the same key meet on one rank — carrying its payload columns.
+    to rank ``mix64(key) & (G-1)``, carrying its payload columns. Two sides shuffled by
+    this function on the same key meet on one rank. It is NOT the map a
+    DistributedHashJoin plan may choose (dense build domains go by key range there), so
+    do not mix shuffle() output with a side partitioned by a join plan.
 
     hj_radix_partition is run with ids = local row numbers, so its id output is the
     stable destination permutation; payload columns are gathered by it and sent with the

@@ -183,13 +183,11 @@ hj_status hj_probe_async_ids(const hj_table* t, const void* keys, const uint8_t*
 
 /* Probe strategy for later probes of this process: 0 auto (sliced for direct-addressed
  * tables past the L2s with a probe side at least as large as the key range, else fused),
- * 1 two-pass direct (lookup kernel writes a 4-byte ref per row, then ordered emission),
- * 2 partitioned (rows grouped by table piece inside each tile, pieces looked up
- * L2-resident per XCD), 3 fused (lookup + emission in one launch, tile offsets by
- * decoupled look-back), 4 sliced (direct-addressed tables: probe rows partitioned by
- * 16384-value key slice, lookups out of LDS, then ordered emission; other tables fused).
- * Results are identical; returns the previous mode, -1 for a bad value. Also settable
- * with DFP_HJ_PROBE_MODE=fused|two-pass|partitioned|sliced. */
+ * 3 fused (lookup + emission in one launch, tile offsets by decoupled look-back),
+ * 4 sliced (direct-addressed tables: probe rows partitioned by 32768-value key slice,
+ * lookups out of LDS, then ordered emission; other tables fused). Results are identical;
+ * returns the previous mode, -1 for a bad value (1 and 2 named strategies measured slower
+ * and removed). Also settable with DFP_HJ_PROBE_MODE=fused|sliced. */
 int hj_set_probe_mode(int mode);
 
 /* Table layout for later builds of this process: 0 auto (a direct-addressed table - one

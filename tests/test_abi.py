@@ -100,16 +100,16 @@ def test_product_path_does_not_import_the_oracle():
 
 
 def test_probe_mode_switch(dfp):
-    """hj_set_probe_mode: 0 auto, 1 two-pass, 2 partitioned, 3 fused, 4 sliced; bad -> -1.
+    """hj_set_probe_mode: 0 auto, 3 fused, 4 sliced; bad (incl. the retired 1 and 2) -> -1.
     No device work."""
     from datafusion_parallelism_amd import _lib
 
     L = _lib.load()
-    assert L.hj_set_probe_mode(5) == -1
-    assert L.hj_set_probe_mode(-1) == -1
+    for bad in (5, -1, 1, 2):
+        assert L.hj_set_probe_mode(bad) == -1
     old = L.hj_set_probe_mode(3)
-    assert L.hj_set_probe_mode(1) == 3
-    assert L.hj_set_probe_mode(old) == 1
+    assert L.hj_set_probe_mode(4) == 3
+    assert L.hj_set_probe_mode(old) == 4
 
 
 def test_join_type_names():

@@ -13,11 +13,11 @@ pytestmark = pytest.mark.gpu
 I64_MIN = np.iinfo(np.int64).min
 
 
-# (probe mode, table layout): hj_set_probe_mode 3 fused / 1 two-pass / 2 partitioned /
-# 4 sliced; hj_set_build_mode 0 auto (direct-addressed for dense key ranges, built from the
-# tile-local partition) / 1 hashed / 2 auto with the histogram partition
-MODES = {"fused": (3, 0), "fused-hashed": (3, 1), "two-pass": (1, 0), "partitioned-hashed": (2, 1),
-         "sliced": (4, 0), "sliced-histbuild": (4, 2)}
+# (probe mode, table layout): hj_set_probe_mode 3 fused / 4 sliced; hj_set_build_mode 0
+# auto (direct-addressed for dense key ranges, built from the tile-local partition) /
+# 1 hashed / 2 auto with the histogram partition
+MODES = {"fused": (3, 0), "fused-hashed": (3, 1), "sliced": (4, 0), "sliced-hashed": (4, 1),
+         "sliced-histbuild": (4, 2)}
 
 
 @pytest.fixture(params=list(MODES))
@@ -253,6 +253,73 @@ def test_c2_full_size_properties(dfp, oracle_mod):
     keys = pk[p[sample].long()].cpu().numpy().astype(object)
     want = np.array([(int(k) * inv) % B for k in keys], dtype=np.int64)
     assert np.array_equal(b[sample].cpu().numpy(), want)
+
+
+MIX_MUL_I64 = 0x9E3779B97F4A7C15 - (1 << 64)  # odd: k -> k * M (mod 2^64) is a bijection
+
+
+def test_c2h_full_size_equals_c2(dfp):
+    """C2h = C2 with both sides' keys mapped by the bijection k -> k * M (mod 2^64): the
+    keys spread over the int64 domain, so the build takes the hashed bucket table and
+    the probe its sliced hashed pipeline (auto choice), yet the pairs must be exactly
+    C2's (direct-addressed table, sliced probe): same count, same order, same values."""
+    B, P, R = 10**7, 10**8, 2 * 10**7
+    dev = torch.device("cuda", 0)
+    lib = dfp.load()
+    bk = torch.empty(B, dtype=torch.int64, device=dev)
+    pk = torch.empty(P, dtype=torch.int64, device=dev)
+    s = torch.cuda.current_stream().cuda_stream
+    assert lib.hj_gen_perm_keys(bk.data_ptr(), B, 7368787, B, s) == 0
+    assert lib.hj_gen_uniform_keys(pk.data_ptr(), P, 0xC0FFEE, R, s) == 0
+    with dfp.HashTable(1, "int64", 0) as t:
+        t.build(bk)
+        assert t.stats()["buckets"] == 0
+        b0, p0 = t.probe(pk, device_output=True)
+    bk.mul_(MIX_MUL_I64)
+    pk.mul_(MIX_MUL_I64)
+    with dfp.HashTable(1, "int64", 0) as t:
+        t.build(bk)
+        st = t.stats()
+        assert st["buckets"] > 0 and st["buckets"] <= 2047 * 2048  # hashed, within the sliced limit
+        b1, p1 = t.probe(pk, device_output=True)
+    assert b1.numel() == b0.numel() == 49_999_816
+    assert torch.equal(p0, p1) and torch.equal(b0, b1)
+
+
+@pytest.mark.parametrize("nb,np_,dup_frac,null_frac,key_type", [
+    (2_000_000, 3_000_001, 0.0, 0.0, "int64"),   # ~390 slices, ragged last tile
+    (1_500_000, 2_000_000, 0.3, 0.01, "int64"),  # duplicated keys (inline meta counts and more)
+    (800_000, 1_000_000, 0.1, 0.02, "int32"),    # int32 keys over the whole int32 domain
+])
+def test_hashed_sliced_auto(dfp, oracle_mod, nb, np_, dup_frac, null_frac, key_type):
+    """Keys over the whole integer domain (hashed table), probe side large enough for the
+    auto choice to take the sliced hashed pipeline; INT64_MIN / zero included."""
+    L = dfp.load()
+    old_p, old_b = L.hj_set_probe_mode(0), L.hj_set_build_mode(0)
+    try:
+        rng = np.random.default_rng(nb + np_)
+        info = np.iinfo(np.int64 if key_type == "int64" else np.int32)
+        dt = np.int64 if key_type == "int64" else np.int32
+        distinct = rng.integers(info.min, info.max, nb, dtype=np.int64).astype(dt)
+        bk = distinct.copy()
+        nd = int(nb * dup_frac)
+        if nd:
+            bk[:nd] = distinct[rng.integers(nd, nb, nd)]  # repeated keys
+            bk[nd:nd + 70] = distinct[-1]                 # one key with > 63 rows
+        bk[-2:] = [info.min, 0]
+        pk = np.concatenate([bk[rng.integers(0, nb, np_ // 2)],
+                             rng.integers(info.min, info.max, np_ - np_ // 2, dtype=np.int64).astype(dt)])
+        rng.shuffle(pk)
+        pk[:3] = [info.min, 0, info.max]
+        bv = rng.random(nb) >= null_frac if null_frac else None
+        pv = rng.random(np_) >= null_frac if null_frac else None
+        b, p, st = gpu_join(dfp, bk, pk, bv, pv, key_type=key_type)
+        assert st["buckets"] > 0
+        ob, op = oracle_mod.inner_join(bk, pk, bv, pv)
+        assert_same(b, p, ob, op)
+    finally:
+        L.hj_set_probe_mode(old_p)
+        L.hj_set_build_mode(old_b)
 
 
 def test_c3_full_size_digest(dfp, oracle_mod):

@@ -58,10 +58,32 @@ for s in $STEPS; do
           --output-format csv -- python3 tools/probe_one.py > $O/lf_$v.log 2>&1 || { tail -30 $O/lf_$v.log; exit 1; }
         unset DFP_HJ_LOAD_FACTOR
       done ;;
-    c3)
-      run timeout -k 10 400 python3 bench.py --config c3 --no-cpu-baseline > $O/bench_c3.json 2> $O/bench_c3.err \
-        || { tail -30 $O/bench_c3.err; exit 1; }
-      cat $O/bench_c3.json ;;
+    c3|c2h)
+      run timeout -k 10 400 python3 bench.py --config $s --no-cpu-baseline > $O/bench_$s.json 2> $O/bench_$s.err \
+        || { tail -30 $O/bench_$s.err; exit 1; }
+      cat $O/bench_$s.json ;;
+    ablc2h)
+      # hashed sliced probe ablations (DFP_HJ_SL_DBG bits, wrong pairs but in-range refs):
+      # 4 no bucket lookup; per-kernel times of one build + 5 probes
+      for d in 4; do
+        DFP_HJ_SL_DBG=$d run timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/abl$d -o kp --output-format csv \
+          -- python3 tools/probe_one.py 1e7 1e8 --mix > $O/abl$d.log 2>&1 || { tail -30 $O/abl$d.log; exit 1; }
+        python3 tools/kstats.py $O/abl$d | grep -E "lookup|partition|emit"
+      done
+      # hashed table load factor (keys per slot) vs the sliced probe
+      for lf in ${LFS:-0.5 0.7 0.8}; do
+        DFP_HJ_LOAD_FACTOR=$lf run timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/lf$lf -o kp \
+          --output-format csv -- python3 tools/probe_one.py 1e7 1e8 --mix > $O/lf$lf.log 2>&1 || { tail -30 $O/lf$lf.log; exit 1; }
+        echo "lf $lf: $(tail -1 $O/lf$lf.log)"
+        python3 tools/kstats.py $O/lf$lf | grep -E "lookup|partition|emit|chunk_build|transpose"
+      done ;;
+    kpc2h|kpc3)
+      # per-kernel times of the bench config (serialized steps), kernel trace
+      c=${s#kp}
+      run timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/$s -o kp --output-format csv \
+        -- python3 bench.py --config $c --no-cpu-baseline --same-stream --sync-steps --steps 5 --warmup 3 \
+        > $O/$s.json 2> $O/$s.err || { tail -30 $O/$s.err; exit 1; }
+      python3 tools/kstats.py $O/$s ;;
     dist)
       run timeout -k 10 400 python3 bench.py --force-dist --no-cpu-baseline --steps 5 > $O/bench_dist.json \
         2> $O/bench_dist.err || { tail -30 $O/bench_dist.err; exit 1; }

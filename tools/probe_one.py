@@ -9,14 +9,19 @@ import torch  # noqa: E402
 import datafusion_parallelism_amd as dfp  # noqa: E402
 from datafusion_parallelism_amd.table import HashTable  # noqa: E402
 
-B = int(float(sys.argv[1])) if len(sys.argv) > 1 else 10**7
-P = int(float(sys.argv[2])) if len(sys.argv) > 2 else 10**8
+args = [a for a in sys.argv[1:] if not a.startswith("--")]
+B = int(float(args[0])) if len(args) > 0 else 10**7
+P = int(float(args[1])) if len(args) > 1 else 10**8
+MIX = "--mix" in sys.argv  # C2h: keys mapped by k -> k * 0x9E3779B97F4A7C15 (hashed table)
 L = dfp.load()
 dev = torch.device("cuda", 0)
 bk = torch.empty(B, dtype=torch.int64, device=dev)
 pk = torch.empty(P, dtype=torch.int64, device=dev)
 assert L.hj_gen_perm_keys(bk.data_ptr(), B, 7368787, B, None) == 0
 assert L.hj_gen_uniform_keys(pk.data_ptr(), P, 0xC0FFEE, 2 * B, None) == 0
+if MIX:
+    bk.mul_(0x9E3779B97F4A7C15 - (1 << 64))
+    pk.mul_(0x9E3779B97F4A7C15 - (1 << 64))
 ob = torch.empty(P, dtype=torch.int64, device=dev)
 op = torch.empty(P, dtype=torch.int32, device=dev)
 ws = torch.empty(HashTable.workspace_bytes(P), dtype=torch.uint8, device=dev)
