@@ -60,34 +60,36 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def gen_inputs(cfg, rank, world, dev):
-    """Device-resident synthetic input of this rank (generated on the GPU)."""
+def gen_inputs(cfg, rank, world, dev, strong=True):
+    """Device-resident synthetic input of this rank (generated on the GPU).
+    strong: the config's global join (B build x P probe rows) split into `world` contiguous
+    shards, rank r holding build rows [rB/W, (r+1)B/W) and probe rows [rP/W, (r+1)P/W);
+    weak: every rank holds a whole config-sized join over a global key domain of W x B."""
     L = dfp.load()
     B, P = cfg["build_rows"], cfg["probe_rows"]
     s = torch.cuda.current_stream(dev).cuda_stream
-    bk = torch.empty(B, dtype=torch.int64, device=dev)
+    gB = B if strong else world * B  # global build rows
+    b0, b1 = (B * rank // world, B * (rank + 1) // world) if strong else (rank * B, (rank + 1) * B)
+    p0, p1 = (P * rank // world, P * (rank + 1) // world) if strong else (rank * P, (rank + 1) * P)
     if cfg["build_gen"] == "perm":
-        # global permutation of [0, world*B); rank r holds rows [r*B, (r+1)*B)
-        gB = world * B
-        tmp = torch.empty(gB if world > 1 else B, dtype=torch.int64, device=dev)
-        assert L.hj_gen_perm_keys(tmp.data_ptr(), tmp.numel(), PERM_MUL, gB, s) == 0
-        bk.copy_(tmp[rank * B:(rank + 1) * B])
+        tmp = torch.empty(gB, dtype=torch.int64, device=dev)  # permutation of [0, gB)
+        assert L.hj_gen_perm_keys(tmp.data_ptr(), gB, PERM_MUL, gB, s) == 0
+        bk = tmp[b0:b1].clone()
         del tmp
-        krange = gB
     else:
         from datafusion_parallelism_amd.api_utils import make_exponential_int_array
 
-        e = make_exponential_int_array(0, B).astype(np.int64) + rank * B
-        bk.copy_(torch.from_numpy(e))
-        krange = world * B
-    pk = torch.empty(P, dtype=torch.int64, device=dev)
-    prange = cfg["probe_range_mul"] * krange
-    assert L.hj_gen_uniform_keys(pk.data_ptr(), P, 0xC0FFEE + rank * P, prange, s) == 0
+        e = make_exponential_int_array(0, B).astype(np.int64)
+        e = e[b0:b1] if strong else e + rank * B
+        bk = torch.from_numpy(np.ascontiguousarray(e)).to(dev)
+    pk = torch.empty(p1 - p0, dtype=torch.int64, device=dev)
+    prange = cfg["probe_range_mul"] * gB
+    assert L.hj_gen_uniform_keys(pk.data_ptr(), p1 - p0, 0xC0FFEE + p0, prange, s) == 0
     if cfg.get("mix"):  # int64 multiplication wraps mod 2^64 on the device
         bk.mul_(MIX_MUL_I64)
         pk.mul_(MIX_MUL_I64)
     torch.cuda.synchronize(dev)
-    return bk, pk
+    return bk, pk, b0, p0
 
 
 class SingleGpuJoin:
@@ -192,9 +194,43 @@ class SingleGpuJoin:
         t.close()
 
 
-def cpu_baseline(cfg, nthreads=8):
-    """Oracle's multithreaded Version-10 restatement on the host: full-size build, a
-    probe sample of 10^7 rows, probe time scaled to the full probe side."""
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def _join_cpu(oracle, bk, pk, nthreads):
+    """Build + one emitting probe pass of the oracle's Version-10 restatement; -> timings."""
+    t0 = time.perf_counter()
+    tbl = oracle.V10Table(bk, nthreads=nthreads)
+    t1 = time.perf_counter()
+    b, _ = tbl.probe(pk, nthreads=nthreads, emit=True)
+    t2 = time.perf_counter()
+    tbl.close()
+    return {"threads": nthreads, "build_ms": round((t1 - t0) * 1e3, 2), "probe_ms": round((t2 - t1) * 1e3, 2),
+            "probe_mrows_s": round(len(pk) / (t2 - t1) / 1e6, 2),
+            "value": round(len(pk) / (t2 - t0) / 1e6, 3), "pairs": int(len(b))}
+
+
+def cpu_baseline(cfg):
+    """The reference's CPU join, restated in C (oracle/hj_oracle.c, reference Version 10:
+    concurrent open-addressing insert + chain walk + key re-check), timed on this host's
+    cores at the reference's PARALLELISM = 8 threads and at every core this process may
+    use, with no extrapolation:
+      * this config (build B + probe P with pair emission);
+      * C1a (benches/lookup_speed.rs:135-154, 240-246): a 4,194,304-row build (8 partitions
+        x 64 batches x 8192 Int32 rows, batch i holding keys i*8192..(i+1)*8192), then each
+        of the 8 partitions' lookup loops, get_iter of the raw values 0..8,388,607 as
+        hashes, single-threaded one after another as the reference's bench runs them; the
+        build is build_speed.rs's workload (131-213);
+      * C1b (BASELINE.json configs[0]): 2^20 unique build keys x 2^20 probe keys over 2^21,
+        full inner join with pair emission."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
 
@@ -203,38 +239,48 @@ def cpu_baseline(cfg, nthreads=8):
         bk = oracle.perm_keys(B, PERM_MUL, B)
     else:
         bk = oracle.make_exponential_int_array(0, B).astype(np.int64)
-    ps = min(P, 10**7)
-    pk = oracle.uniform_keys(ps, 0xC0FFEE, cfg["probe_range_mul"] * B)
+    pk = oracle.uniform_keys(P, 0xC0FFEE, cfg["probe_range_mul"] * B)
     if cfg.get("mix"):
         bk = (bk.astype(np.uint64) * np.uint64(MIX_MUL)).astype(np.int64)
         pk = (pk.astype(np.uint64) * np.uint64(MIX_MUL)).astype(np.int64)
+    try:
+        all_threads = len(os.sched_getaffinity(0))
+    except AttributeError:
+        all_threads = os.cpu_count() or 8
+    counts = sorted({8, all_threads})
+    main = {f"threads_{n}": _join_cpu(oracle, bk, pk, n) for n in counts}
+    del pk
+    # C1a: lookup_speed
+    c1a_keys = np.tile(np.arange(64 * 8192, dtype=np.int64), 8)
     t0 = time.perf_counter()
-    tbl = oracle.V10Table(bk, nthreads=nthreads)
+    tbl = oracle.V10Table(c1a_keys, nthreads=8)
     t1 = time.perf_counter()
-    m = tbl.probe(pk, nthreads=nthreads, emit=True)
+    rows = sum(tbl.lookup_hashes(0, 2 * 512 * 8192) for _ in range(8))
     t2 = time.perf_counter()
     tbl.close()
-    build_s, probe_s = t1 - t0, (t2 - t1) * (P / ps)
-    cpu = "unknown"
-    try:
-        with open("/proc/cpuinfo") as f:
-            for line in f:
-                if line.startswith("model name"):
-                    cpu = line.split(":", 1)[1].strip()
-                    break
-    except OSError:
-        pass
+    c1a = {"build_rows": int(len(c1a_keys)), "build_threads": 8, "build_ms": round((t1 - t0) * 1e3, 2),
+           "lookups": 8 * 2 * 512 * 8192, "lookup_threads": 1, "lookup_ms": round((t2 - t1) * 1e3, 2),
+           "mlookups_s": round(8 * 2 * 512 * 8192 / (t2 - t1) / 1e6, 2), "rows_yielded": int(rows)}
+    # C1b: 2^20 x 2^20
+    n1 = 1 << 20
+    c1b_b = oracle.perm_keys(n1, PERM_MUL, n1)
+    c1b_p = oracle.uniform_keys(n1, 0xC0FFEE, 2 * n1)
+    c1b = {f"threads_{n}": _join_cpu(oracle, c1b_b, c1b_p, n) for n in counts}
+    m8 = main["threads_8"]
     return {
-        "value": round(P / (build_s + probe_s) / 1e6, 3),
+        "value": m8["value"],
         "unit": "Mrows/s",
-        "cores": nthreads,
+        "cores": 8,
         "kind": "port",
-        "sample": f"full {B}-row build + {ps} of the {P} probe rows (probe time scaled x{P // ps}); "
-                  f"C restatement of reference Version 10 (oracle/hj_oracle.c), {nthreads} threads on {cpu}, "
-                  f"host has {os.cpu_count()} logical CPUs",
-        "build_ms": round(build_s * 1e3, 3),
-        "probe_mrows_s": round(P / probe_s / 1e6, 3),
-        "pairs_in_sample": int(len(m[0])),
+        "sample": f"full {B}-row build + {P}-row probe with pair emission (no extrapolation); C restatement of "
+                  f"reference Version 10 (oracle/hj_oracle.c) on {_cpu_model()}; value = probe rows / (build + "
+                  f"probe) at the reference's PARALLELISM = 8 threads; also at all {all_threads} usable cores "
+                  f"(host has {os.cpu_count()} logical CPUs); plus C1a (lookup_speed) and C1b (2^20 x 2^20)",
+        "build_ms": m8["build_ms"],
+        "probe_mrows_s": m8["probe_mrows_s"],
+        "this_config": main,
+        "c1a_lookup_speed": c1a,
+        "c1b_1m_x_1m": c1b,
     }
 
 
@@ -268,6 +314,10 @@ def main():
                     help="synchronize the device after every step (no host/device overlap between steps)")
     ap.add_argument("--no-compress-keys", action="store_true",
                     help="multi-GPU: exchange full int64 keys / u64 build ids even when 32 bits suffice")
+    ap.add_argument("--plan", default="auto", choices=["auto", "broadcast", "radix"],
+                    help="multi-GPU plan for the strong-scaling line (auto: broadcast when B*G < B+P)")
+    ap.add_argument("--no-weak", action="store_true",
+                    help="multi-GPU: skip the weak-scaling extra (a config-sized join per rank, radix exchange)")
     args = ap.parse_args()
     cfg = CONFIGS[args.config]
 
@@ -288,60 +338,84 @@ def main():
     if world > 1 or args.force_dist:
         dist.init_process_group("nccl", device_id=dev)
 
-    bk, pk = gen_inputs(cfg, rank, world, dev)
-    B, P = bk.numel(), pk.numel()
-
     use_dist = world > 1 or args.force_dist
+    bk, pk, bbase, pbase = gen_inputs(cfg, rank, world, dev, strong=True)
+    B, P = bk.numel(), pk.numel()
+    gB, gP = cfg["build_rows"], cfg["probe_rows"]  # the whole join (strong scaling)
+    plan = None
     if not use_dist:
         job = SingleGpuJoin(bk, pk, dev, same_stream=args.same_stream)
     else:
         from datafusion_parallelism_amd.distributed import DistributedHashJoin
 
-        job = DistJob(DistributedHashJoin(chunks=args.chunks, compress_keys=not args.no_compress_keys), bk, pk,
-                      rank, dev)
+        dj = DistributedHashJoin(chunks=args.chunks, compress_keys=not args.no_compress_keys)
+        plan = args.plan if args.plan != "auto" else DistributedHashJoin.choose_plan(gB, gP, world)
+        job = (BroadcastJob(dj, bk, pk, pbase, dev) if plan == "broadcast" else
+               DistJob(dj, bk, pk, bbase, pbase, dev))
 
     def barrier():
         if use_dist:
             dist.barrier()
 
-    # warmup runs as the timed loop does (pipelined steps hold two tables at once: the
-    # allocator's cache fills here, not inside the timed region)
-    for _ in range(args.warmup):
-        job.step()
-        if args.sync_steps or use_dist:
-            torch.cuda.synchronize(dev)
-            job.collect()
-    torch.cuda.synchronize(dev)
-    job.collect()
-    job.probe_ms.clear()
-    job.build_ms.clear()
+    def timed(job, steps, warmup):
+        """warmup untimed steps, then `steps` timed ones between barriers + device syncs;
+        -> max over ranks of the elapsed seconds"""
+        # warmup runs as the timed loop does (pipelined steps hold two tables at once: the
+        # allocator's cache fills here, not inside the timed region)
+        for _ in range(warmup):
+            job.step()
+            if args.sync_steps or use_dist:
+                torch.cuda.synchronize(dev)
+                job.collect()
+        torch.cuda.synchronize(dev)
+        job.collect()
+        job.probe_ms.clear()
+        job.build_ms.clear()
+        # the local job's steps overlap one step's host work with the previous step's
+        # device work (SingleGpuJoin.step); the exchange jobs synchronize inside a step
+        barrier()
+        torch.cuda.synchronize(dev)
+        t_start = time.perf_counter()
+        for _ in range(steps):
+            job.step()
+            if args.sync_steps or use_dist:
+                torch.cuda.synchronize(dev)
+                job.collect()
+        torch.cuda.synchronize(dev)
+        barrier()
+        elapsed = time.perf_counter() - t_start
+        job.finish()
+        if use_dist:
+            t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            elapsed = float(t.item())
+        return elapsed
 
-    # the local job's steps overlap one step's host work with the previous step's device
-    # work (LocalJob.step); the exchange job synchronizes inside its step
-    barrier()
-    torch.cuda.synchronize(dev)
-    t_start = time.perf_counter()
-    for _ in range(args.steps):
-        job.step()
-        if args.sync_steps or use_dist:
-            torch.cuda.synchronize(dev)
-            job.collect()
-    torch.cuda.synchronize(dev)
-    barrier()
-    elapsed = time.perf_counter() - t_start
-    job.finish()
-    if use_dist:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-
+    elapsed = timed(job, args.steps, args.warmup)
     ms_per_step = elapsed / args.steps * 1e3
-    total_probe_rows = P * world
+    total_probe_rows = gP  # strong scaling: the one global join, whatever the rank count
     value = total_probe_rows / (elapsed / args.steps) / 1e6
+    weak = None
+    if use_dist and world > 1 and not args.no_weak:
+        # extra: weak scaling, a config-sized join on every rank (radix all-to-all)
+        wbk, wpk, wb0, wp0 = gen_inputs(cfg, rank, world, dev, strong=False)
+        wjob = DistJob(dj, wbk, wpk, wb0, wp0, dev)
+        we = timed(wjob, max(3, args.steps // 2), max(2, args.warmup // 4))
+        wsteps = max(3, args.steps // 2)
+        weak = {"scaling": "weak", "value": round(gP * world / (we / wsteps) / 1e6, 3), "unit": "Mrows/s",
+                "ms_per_step": round(we / wsteps * 1e3, 4), "probe_rows_per_gpu": gP, "build_rows_per_gpu": gB,
+                "plan": "radix", "exchange_ms": round(float(np.median(wjob.exchange_ms)), 4)}
+        del wbk, wpk, wjob
 
     probe_ms = float(np.median(job.probe_ms))
     build_ms = float(np.median(job.build_ms))
     M = job.matches
+    if use_dist:  # pairs of the whole join (all ranks)
+        mt = torch.tensor([M], dtype=torch.int64, device=dev)
+        dist.all_reduce(mt)
+        M_all = int(mt.item())
+    else:
+        M_all = M
     alg_bytes = 8 * P + 16 * B + 12 * M
     achieved = alg_bytes / (probe_ms / 1e3) / 1e9
     traffic = load_traffic(args.config) if not use_dist else None
@@ -372,16 +446,16 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong",
             "vs_baseline": None,
             "dtype": "int64",
             "data": "synthetic (device-generated seeded keys, SURVEY.md §8d generators)",
             "config": {
                 "workload": cfg["workload"],
-                "build_rows_per_gpu": B,
-                "probe_rows_per_gpu": P,
-                "matches_per_gpu": M,
-                "parallelism": "single-gpu" if not use_dist else f"radix-a2a x{world} (RCCL)",
+                "build_rows": gB,
+                "probe_rows": gP,
+                "matches": M_all,
+                "parallelism": "single-gpu" if not use_dist else f"{plan} x{world} (RCCL)",
             },
             "probe_mrows_s": round(P / (probe_ms / 1e3) / 1e6, 1),
             "probe_ms": round(probe_ms, 4),
@@ -394,6 +468,9 @@ def main():
         }
         if use_dist:
             line["exchange_ms"] = round(float(np.median(job.exchange_ms)), 4)
+            line["plan"] = plan
+        if weak is not None:
+            line["weak"] = weak
         print(json.dumps(line), file=json_out, flush=True)
     if use_dist:
         dist.destroy_process_group()
@@ -405,14 +482,15 @@ class DistJob:
     exchange_ms = the build-side exchange; probe_ms (HIP events) = local build +
     pipelined probe-side exchange and probes."""
 
-    def __init__(self, dj, bk, pk, rank, dev):
+    def __init__(self, dj, bk, pk, bbase, pbase, dev):
         self.dj, self.bk, self.pk, self.dev = dj, bk, pk, dev
-        self.bbase = rank * bk.numel()
-        self.pbase = rank * pk.numel()
+        self.bbase = bbase
+        self.pbase = pbase
         self.probe_ms, self.build_ms, self.exchange_ms = [], [], []
         self.matches = 0
         self.cap = pk.numel()
         self.kernel_desc = "radix partition + RCCL all-to-all + local build + probe"
+        self._ev = None
 
     def step(self):
         t0 = time.perf_counter()
@@ -436,13 +514,70 @@ class DistJob:
         self.matches = sum(b.numel() for b, _ in outs)
 
     def collect(self):
+        if self._ev is None:
+            return
         torch.cuda.synchronize(self.dev)
         # local build + probe as one device interval (build is synchronous inside)
         self.probe_ms.append(self._ev[0].elapsed_time(self._ev[1]))
         self.build_ms.append(0.0)
+        self._ev = None
 
     def finish(self):
         pass
+
+
+class BroadcastJob:
+    """One step = all_gather of the build shards (RCCL), a local build of the whole build
+    side (canonical numbering = the global build ids), and the probe of this rank's own
+    probe rows: no probe-side exchange (SURVEY.md §8e broadcast build, chosen when
+    B·G < B + P). exchange_ms = the all_gather; probe_ms (HIP events) = gather + build +
+    probe."""
+
+    def __init__(self, dj, bk, pk, pbase, dev):
+        self.dj, self.bk, self.pk, self.pbase, self.dev = dj, bk, pk, pbase, dev
+        self.probe_ms, self.build_ms, self.exchange_ms = [], [], []
+        self.matches = 0
+        n = pk.numel()
+        self.ids = torch.arange(pbase, pbase + n, dtype=torch.int64, device=dev).to(torch.int32)
+        self.ws = torch.empty(HashTable.workspace_bytes(n), dtype=torch.uint8, device=dev)
+        self.d_total = torch.zeros(1, dtype=torch.int64, device=dev)
+        self.cap = n
+        self.ob = torch.empty(n, dtype=torch.int64, device=dev)
+        self.op = torch.empty(n, dtype=torch.int32, device=dev)
+        self.kernel_desc = "RCCL all_gather of the build shards + local build + sliced probe of the local rows"
+        self._t = None
+
+    def step(self):
+        from datafusion_parallelism_amd.distributed import all_gather_rows
+
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+        ev[0].record()
+        (gathered,) = all_gather_rows([self.bk], self.dj.group)
+        ev[1].record()
+        t = HashTable(1, "int64", self.dev.index or 0)
+        t.append(0, gathered)
+        t.finish(0)
+        s = torch.cuda.current_stream(self.dev).cuda_stream
+        t.probe_async(self.pk.data_ptr(), self.pk.numel(), self.ob.data_ptr(), self.op.data_ptr(), self.cap,
+                      self.d_total.data_ptr(), self.ws.data_ptr(), s, probe_ids_ptr=self.ids.data_ptr())
+        ev[2].record()
+        self._ev, self._t = ev, t
+
+    def collect(self):
+        if self._t is None:
+            return
+        torch.cuda.synchronize(self.dev)
+        self.exchange_ms.append(self._ev[0].elapsed_time(self._ev[1]))
+        self.probe_ms.append(self._ev[0].elapsed_time(self._ev[2]))
+        self.build_ms.append(self._t.build_ns() / 1e6)
+        self.matches = int(self.d_total.item())
+        if self.matches > self.cap:
+            raise RuntimeError("output capacity too small")
+        self._t.close()
+        self._t = None
+
+    def finish(self):
+        self.collect()
 
 
 if __name__ == "__main__":

@@ -21,6 +21,7 @@ LIB_PATH = os.path.join(HERE, "lib", "libdfp_hj.so")
 HJ_OK, HJ_ERR_INVALID, HJ_ERR_OOM, HJ_ERR_HIP, HJ_ERR_RCCL, HJ_ERR_CAPACITY, HJ_ERR_NO_DEVICE = range(7)
 HJ_INT32, HJ_INT64 = 0, 1
 HJ_INPUT_DEVICE, HJ_BORROW, HJ_OUTPUT_HOST, HJ_IDS_U31, HJ_BORROW_KEEP = 1, 2, 4, 8, 16
+HJ_MULTI_AUTO, HJ_MULTI_BROADCAST, HJ_MULTI_RADIX = 0, 1, 2
 
 STATUS_NAMES = {
     HJ_OK: "HJ_OK", HJ_ERR_INVALID: "HJ_ERR_INVALID", HJ_ERR_OOM: "HJ_ERR_OOM", HJ_ERR_HIP: "HJ_ERR_HIP",
@@ -47,6 +48,11 @@ class HjTableStats(ctypes.Structure):
         "table_bytes", "build_ns")]
 
 
+class HjKeyColumn(ctypes.Structure):
+    _fields_ = [("values", ctypes.c_void_p), ("offsets", ctypes.c_void_p), ("validity", ctypes.c_void_p),
+                ("validity_offset", ctypes.c_int64), ("width", ctypes.c_int), ("offset_bytes", ctypes.c_int)]
+
+
 class HjPartSpec(ctypes.Structure):
     _fields_ = [("by_range", ctypes.c_int), ("key_lo", ctypes.c_int64), ("key_hi", ctypes.c_int64)]
 
@@ -59,6 +65,7 @@ SIGNATURES = [
     ("hj_version", ctypes.c_char_p, []),
     ("hj_device_count", I32, []),
     ("hj_build_begin", I32, [I32, I32, I32, I64, PP]),
+    ("hj_build_begin_multi", I32, [I32, ctypes.POINTER(ctypes.c_int), I32, I32, I64, I32, PP]),
     ("hj_build_append", I32, [P, I32, P, P, I64, P, I64, U32, P]),
     ("hj_build_finish", I32, [P, I32]),
     ("hj_build_partition_offset", I32, [P, I32, ctypes.POINTER(ctypes.c_int64)]),
@@ -84,6 +91,10 @@ SIGNATURES = [
     ("hj_gather_fixed", I32, [P, P, I64, I32, P, I32, I64, P, P, P]),
     ("hj_gather_var_workspace_bytes", I64, [I64]),
     ("hj_gather_var", I32, [P, I32, P, P, I64, P, I32, I64, P, P, I64, P, P, P, P]),
+    ("hj_composite_keys", I32, [I32, ctypes.POINTER(HjKeyColumn), I64, P, P, P]),
+    ("hj_equal_pairs_workspace_bytes", I64, [I64]),
+    ("hj_filter_equal_pairs", I32, [I32, ctypes.POINTER(HjKeyColumn), ctypes.POINTER(HjKeyColumn), P, P, I64, P, P,
+                                    P, P, P]),
     ("hj_gen_perm_keys", I32, [P, I64, I64, I64, P]),
     ("hj_gen_uniform_keys", I32, [P, I64, U64, I64, P]),
 ]

@@ -23,7 +23,7 @@ LIB = os.path.join(LIBDIR, "libdfp_hj.so")
 INCLUDE = os.path.join(os.path.dirname(HERE), "include")
 ARCH = "gfx950"
 
-SOURCES_HIP = ["hj_kernels.hip", "hj_columns.hip"]
+SOURCES_HIP = ["hj_kernels.hip", "hj_columns.hip", "hj_keys.hip"]
 SOURCES_CPP = ["hj_api.cpp"]
 HEADERS = ["hj_device.h", "hj_launch.h", "hj_util.h"]
 

@@ -163,6 +163,55 @@ class DeviceColumn:
         return pa.Array.from_buffers(t, n, [vbuf, pa.py_buffer(raw[: n * w].tobytes())])
 
 
+def _key_column(c: DeviceColumn) -> "_lib.HjKeyColumn":
+    """hj_key_column of a device column (fixed width or Utf8 / Binary)."""
+    vptr = c.valid.data_ptr() if c.valid is not None else None
+    if _is_var(c.type):
+        return _lib.HjKeyColumn(c.values.data_ptr(), c.offsets.data_ptr(), vptr, c.voff, 0, _VAR[c.type])
+    return _lib.HjKeyColumn(c.data.data_ptr(), None, vptr, c.voff, _fixed_width(c.type), 0)
+
+
+def _key_columns(cols: list[DeviceColumn]):
+    arr = (_lib.HjKeyColumn * len(cols))()
+    for i, c in enumerate(cols):
+        arr[i] = _key_column(c)
+    return arr
+
+
+def composite_keys(cols: list[DeviceColumn]) -> tuple[torch.Tensor, torch.Tensor]:
+    """hj_composite_keys: one int64 key per row from every key column (calculate_hash over
+    all key columns, src/shared/shared.rs:11-16) and the LSB validity bitmap (uint8
+    device tensor, bit i = no key column null at row i)."""
+    L = _lib.load()
+    n = cols[0].length
+    if any(c.length != n for c in cols):
+        raise ValueError("key columns of unequal length")
+    dev = cols[0].device
+    keys = torch.empty(max(n, 1), dtype=torch.int64, device=dev)
+    valid = torch.zeros(max(_bitmap_bytes(n), 8), dtype=torch.uint8, device=dev)
+    check(L.hj_composite_keys(len(cols), _key_columns(cols), n, keys.data_ptr(), valid.data_ptr(), _stream(dev)))
+    return keys[:n], valid
+
+
+def filter_equal_pairs(build_cols: list[DeviceColumn], probe_cols: list[DeviceColumn], b: torch.Tensor,
+                       p: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
+    """hj_filter_equal_pairs (equal_rows_arr, src/shared/datafusion_private.rs:52-73): the
+    candidate pairs whose key tuples are equal in every column, order kept."""
+    L = _lib.load()
+    n = b.numel()
+    dev = b.device
+    ob = torch.empty(max(n, 1), dtype=torch.int64, device=dev)
+    op = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+    cnt = torch.zeros(1, dtype=torch.int64, device=dev)
+    ws = torch.empty(L.hj_equal_pairs_workspace_bytes(n), dtype=torch.uint8, device=dev)
+    b, p = b.contiguous(), p.contiguous()
+    check(L.hj_filter_equal_pairs(len(build_cols), _key_columns(build_cols), _key_columns(probe_cols),
+                                  b.data_ptr() if n else None, p.data_ptr() if n else None, n, ob.data_ptr(),
+                                  op.data_ptr(), cnt.data_ptr(), ws.data_ptr(), _stream(dev)))
+    m = int(cnt.item())
+    return ob[:m], op[:m]
+
+
 def mark_rows(idx: torch.Tensor, nflags: int, flags: torch.Tensor | None = None) -> torch.Tensor:
     """flags[idx[i]] = 1 (uint8 device tensor of nflags; -1 / out-of-range ignored)."""
     L = _lib.load()

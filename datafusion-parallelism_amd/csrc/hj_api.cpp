@@ -31,6 +31,7 @@
 #include <condition_variable>
 #include <mutex>
 #include <string>
+#include <tuple>
 #include <unordered_map>
 #include <vector>
 
@@ -39,6 +40,8 @@
 #include "hj_launch.h"
 
 using namespace dfp;
+
+struct MultiTable;  // hj_build_begin_multi facade (below)
 
 namespace {
 
@@ -276,6 +279,9 @@ struct hj_table {
     int64_t build_ns = 0;
     std::vector<std::pair<void*, size_t>> allocs;   // live for the table's lifetime
     std::vector<std::pair<void*, size_t>> scratch;  // build-only, released after the build
+    // multi-GPU facade: shards on several devices behind this handle (hj_build_begin_multi)
+    MultiTable* multi = nullptr;
+    std::vector<std::tuple<int, void*, size_t>> multi_bufs;  // (device, block, bytes) the shards borrow
 };
 
 namespace {
@@ -505,11 +511,14 @@ hj_status build_attempt(hj_table* t, const std::vector<Segment>& segs, double lf
     return HJ_OK;
 }
 
+hj_status run_multi_build_entry(hj_table* t, const std::vector<Segment>& segs, const std::vector<HostSeg*>& hsegs);
+
 // The device build, run once by the last partition to arrive at the barrier.
 hj_status run_build(hj_table* t) {
     HIP_TRY(hipSetDevice(t->device));
     // canonical numbering: partition 0's appends in order, then partition 1, ...
     std::vector<Segment> segs;
+    std::vector<HostSeg*> hsegs;
     t->part_off.assign(t->parallelism, 0);
     int64_t row = 0;
     for (int p = 0; p < t->parallelism; ++p) {
@@ -517,10 +526,12 @@ hj_status run_build(hj_table* t) {
         for (auto& hs : t->parts[p]) {
             if (hs.n == 0) continue;
             segs.push_back(Segment{hs.keys, hs.valid, hs.voff, hs.ids, hs.n, row});
+            hsegs.push_back(&hs);
             row += hs.n;
         }
     }
     t->total_rows = row;
+    if (t->multi) return run_multi_build_entry(t, segs, hsegs);
     if (row > 0x7FFFFFF0ll) return fail(HJ_ERR_INVALID, "build side exceeds 2^31-16 rows on one device; shard it");
     if (t->has_ids && t->has_no_ids)
         return fail(HJ_ERR_INVALID, "explicit build ids must be given for every batch or none");
@@ -650,6 +661,377 @@ hj_status probe_impl(const hj_table* t, const void* keys, const uint8_t* valid, 
 
 }  // namespace
 
+// ---- multi-GPU table (hj_build_begin_multi): one process drives several GPUs --------
+//
+// The reference runs its join in one process over `parallelism` partitions; the drop-in
+// for a node of GPUs is a table whose shards live on several devices behind the same
+// build / probe / pairs ABI (SURVEY.md §8b "hj_build_begin_multi"). Two plans (§8e):
+//   broadcast  every GPU builds the whole build side (its rows copied over xGMI); a
+//              probe batch is split into contiguous row ranges, one per GPU, and their
+//              pairs are concatenated: canonical order with no merge. Cheaper whenever
+//              B·G < B + P (C2: 8·10^7 < 1.1·10^8).
+//   radix      the build side is sharded by key hash (the low bits of mix64, the
+//              multi-GPU partition kernel's map; the reference's precedent is the shard
+//              function of src/utils/partitioned_concurrent_self_hash_join_map.rs:13-16):
+//              shard g builds only its keys, with the rows' global canonical ids; a probe
+//              batch is partitioned the same way, each piece probed by its owner, and the
+//              pieces' pairs merged back into canonical order (every probe row's pairs
+//              come from one shard). Needed once the build side outgrows one GPU.
+// Shard tables are ordinary single-device tables; the exchange is device-to-device copies
+// (peer access over xGMI), no collective. A multi table's probes are synchronous (the
+// host reads the pieces' sizes).
+struct MultiTable {
+    int plan = HJ_MULTI_AUTO;
+    std::vector<int> devices;
+    std::vector<hj_table*> shards;
+    std::vector<hipStream_t> streams;          // one per shard, on its device
+    std::mutex probe_mu;                       // a multi probe uses the shard streams
+    int64_t total_rows = 0;
+    ~MultiTable() {
+        for (size_t g = 0; g < shards.size(); ++g) hj_table_free(shards[g]);
+        for (size_t g = 0; g < streams.size(); ++g) {
+            (void)hipSetDevice(devices[g]);
+            (void)hipStreamDestroy(streams[g]);
+        }
+    }
+};
+
+namespace {
+
+int ptr_device(const void* p, int dflt) {
+    hipPointerAttribute_t a;
+    if (p == nullptr || hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return dflt;
+    }
+    return (a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged) ? a.device : dflt;
+}
+
+// device buffers of one multi operation, returned to the cache at scope exit (after the
+// caller has synchronised the streams that use them)
+struct TmpBufs {
+    std::vector<std::tuple<int, void*, size_t>> v;
+    ~TmpBufs() {
+        for (auto& b : v) cache_free(std::get<0>(b), std::get<1>(b), std::get<2>(b));
+    }
+    void* get(int dev, size_t bytes) {
+        hipError_t e;
+        (void)hipSetDevice(dev);
+        void* p = cache_alloc(dev, bytes ? bytes : 64, &e);
+        if (p) v.emplace_back(dev, p, bytes ? bytes : 64);
+        return p;
+    }
+};
+
+#define MT_ALLOC(var, type, dev, bytes)                                                   \
+    type var = (type)tmp.get((dev), (bytes));                                             \
+    if (var == nullptr) return fail(HJ_ERR_OOM, "multi-GPU table: device allocation failed")
+
+hj_status sync_streams(const MultiTable* m) {
+    for (size_t g = 0; g < m->streams.size(); ++g) {
+        HIP_TRY(hipSetDevice(m->devices[g]));
+        HIP_TRY(hipStreamSynchronize(m->streams[g]));
+    }
+    return HJ_OK;
+}
+
+// owner shard of a key under the radix plan (hj_partition_rows' hash map, G a power of two)
+int owner_of(int64_t key, int G) { return (int)(mix64((uint64_t)key) & (uint64_t)(G - 1)); }
+
+// copy `bytes` from src (on any device) to dst on device `dev`, ordered on stream s
+hipError_t copy_to(void* dst, const void* src, size_t bytes, hipStream_t s) {
+    return bytes ? hipMemcpyAsync(dst, src, bytes, hipMemcpyDefault, s) : hipSuccess;
+}
+
+hj_status run_multi_build(hj_table* t, const std::vector<Segment>& segs, const std::vector<HostSeg*>& hsegs) {
+    MultiTable* m = t->multi;
+    const int G = (int)m->devices.size();
+    const int kb = t->key_bytes;
+    const int64_t total = t->total_rows;
+    if (m->plan == HJ_MULTI_AUTO)  // replicate build sides that fit comfortably on every GPU
+        m->plan = (total <= ((int64_t)1 << 27) || (G & (G - 1)) != 0) ? HJ_MULTI_BROADCAST : HJ_MULTI_RADIX;
+    m->total_rows = total;
+    if (t->has_ids && t->has_no_ids) return fail(HJ_ERR_INVALID, "explicit build ids must be given for every batch or none");
+    hj_status st;
+    m->shards.assign(G, nullptr);
+    for (int g = 0; g < G; ++g)
+        if ((st = hj_build_begin(m->devices[g], 1, t->kt, 0, &m->shards[g])) != HJ_OK) return st;
+    TmpBufs tmp;
+    const uint32_t keep = HJ_INPUT_DEVICE | HJ_BORROW | HJ_BORROW_KEEP;
+    if (m->plan == HJ_MULTI_BROADCAST) {
+        // every shard appends every segment in canonical order (its rows keep their
+        // canonical numbers, or the caller's ids)
+        for (int g = 0; g < G; ++g) {
+            const int dev = m->devices[g];
+            hipStream_t s = m->streams[g];
+            HIP_TRY(hipSetDevice(dev));
+            for (size_t i = 0; i < segs.size(); ++i) {
+                const Segment& sg = segs[i];
+                if (hsegs[i]->ready) HIP_TRY(hipStreamWaitEvent(s, hsegs[i]->ready, 0));
+                const void* k = sg.keys;
+                const uint8_t* v = sg.valid;
+                const uint64_t* ids = sg.ids;
+                if (ptr_device(sg.keys, t->device) != dev) {  // over xGMI into this GPU's HBM
+                    MT_ALLOC(kd, void*, dev, (size_t)sg.n * kb);
+                    HIP_TRY(copy_to(kd, sg.keys, (size_t)sg.n * kb, s));
+                    k = kd;
+                    if (sg.valid) {
+                        const size_t nbytes = (size_t)(((sg.voff & 7) + sg.n + 7) >> 3);
+                        MT_ALLOC(vd, uint8_t*, dev, nbytes);
+                        HIP_TRY(copy_to(vd, sg.valid + (sg.voff >> 3), nbytes, s));
+                        v = vd;
+                    }
+                    if (sg.ids) {
+                        MT_ALLOC(id, uint64_t*, dev, (size_t)sg.n * 8);
+                        HIP_TRY(copy_to(id, sg.ids, (size_t)sg.n * 8, s));
+                        ids = id;
+                    }
+                }
+                const int64_t voff = (v == sg.valid) ? sg.voff : (sg.voff & 7);
+                if ((st = hj_build_append(m->shards[g], 0, k, v, voff, ids, sg.n,
+                                          keep | (ids && t->ids_u31 ? HJ_IDS_U31 : 0), s)) != HJ_OK)
+                    return st;
+            }
+            if ((st = hj_build_finish(m->shards[g], 0)) != HJ_OK) return st;
+        }
+        // the shards hold borrowed copies: keep them with the table
+        st = sync_streams(m);
+        if (st != HJ_OK) return st;
+        for (auto& b : tmp.v) t->multi_bufs.push_back(b);
+        tmp.v.clear();
+        return HJ_OK;
+    }
+    // radix: partition every segment on its device by owner shard (stable; global ids)
+    struct Piece {
+        int dev;
+        void* keys;
+        uint64_t* ids;
+        std::vector<int64_t> cnt;
+    };
+    std::vector<Piece> pcs(segs.size());
+    for (size_t i = 0; i < segs.size(); ++i) {
+        const Segment& sg = segs[i];
+        Piece& pc = pcs[i];
+        pc.dev = ptr_device(sg.keys, t->device);
+        HIP_TRY(hipSetDevice(pc.dev));
+        hipStream_t s = thread_stream(pc.dev);
+        if (hsegs[i]->ready) HIP_TRY(hipStreamWaitEvent(s, hsegs[i]->ready, 0));
+        MT_ALLOC(ok, void*, pc.dev, (size_t)sg.n * kb);
+        MT_ALLOC(oi, uint64_t*, pc.dev, (size_t)sg.n * 8);
+        MT_ALLOC(cn, int64_t*, pc.dev, 8 * (size_t)G);
+        MT_ALLOC(ws, void*, pc.dev, (size_t)hj_partition_workspace_bytes(sg.n, G));
+        if ((st = hj_partition_rows(t->kt, sg.keys, sg.valid, sg.voff, sg.ids, (uint64_t)sg.row_base, sg.n, G, nullptr,
+                                    ok, kb, 0, oi, 8, cn, ws, s)) != HJ_OK)
+            return st;
+        pc.keys = ok;
+        pc.ids = oi;
+        pc.cnt.assign(G, 0);
+        HIP_TRY(hipMemcpyAsync(pc.cnt.data(), cn, 8 * (size_t)G, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+    }
+    const bool u31 = t->has_ids ? t->ids_u31 : total < ((int64_t)1 << 31);
+    for (int g = 0; g < G; ++g) {
+        const int dev = m->devices[g];
+        hipStream_t s = m->streams[g];
+        HIP_TRY(hipSetDevice(dev));
+        int64_t tot = 0;
+        for (auto& pc : pcs) tot += pc.cnt[g];
+        void* rk = nullptr;
+        uint64_t* ri = nullptr;
+        if (tot > 0) {
+            rk = tmp.get(dev, (size_t)tot * kb);
+            ri = (uint64_t*)tmp.get(dev, (size_t)tot * 8);
+            if (!rk || !ri) return fail(HJ_ERR_OOM, "multi-GPU table: device allocation failed");
+        }
+        int64_t at = 0;
+        for (auto& pc : pcs) {  // segment order: the ids ascend (stable partition)
+            int64_t off = 0;
+            for (int q = 0; q < g; ++q) off += pc.cnt[q];
+            const int64_t c = pc.cnt[g];
+            HIP_TRY(copy_to((char*)rk + at * kb, (const char*)pc.keys + off * kb, (size_t)c * kb, s));
+            HIP_TRY(copy_to(ri + at, pc.ids + off, (size_t)c * 8, s));
+            at += c;
+        }
+        if (tot > 0 && (st = hj_build_append(m->shards[g], 0, rk, nullptr, 0, ri, tot, keep | (u31 ? HJ_IDS_U31 : 0),
+                                             s)) != HJ_OK)
+            return st;
+        if ((st = hj_build_finish(m->shards[g], 0)) != HJ_OK) return st;
+    }
+    if ((st = sync_streams(m)) != HJ_OK) return st;
+    // keep the shards' borrowed receive buffers; the partition scratch goes back now
+    std::vector<std::tuple<int, void*, size_t>> keep_bufs, drop;
+    for (auto& b : tmp.v) {
+        bool is_piece = false;
+        for (auto& pc : pcs) is_piece |= std::get<1>(b) == pc.keys || std::get<1>(b) == (void*)pc.ids;
+        (is_piece ? drop : keep_bufs).push_back(b);
+    }
+    tmp.v = drop;  // partition outputs, counts and workspaces: freed at scope exit
+    for (auto& b : keep_bufs) t->multi_bufs.push_back(b);
+    return HJ_OK;
+}
+
+// Probe of a multi table into caller buffers on the keys' device; synchronous.
+hj_status multi_probe(const hj_table* t, const void* keys, const uint8_t* valid, int64_t voff,
+                      const uint32_t* probe_ids, int64_t n, uint64_t* out_b, uint32_t* out_p, int64_t cap,
+                      int64_t* d_total, void* workspace, hipStream_t s) {
+    MultiTable* m = t->multi;
+    std::lock_guard<std::mutex> lk(m->probe_mu);
+    const int G = (int)m->devices.size();
+    const int kb = t->key_bytes;
+    const int d = ptr_device(keys ? (const void*)keys : (const void*)out_b, t->device);
+    TmpBufs tmp;
+    hj_status st;
+    HIP_TRY(hipSetDevice(d));
+    hipEvent_t ready;  // the caller's inputs are produced in stream s's order
+    HIP_TRY(hipEventCreateWithFlags(&ready, hipEventDisableTiming));
+    struct EvGuard {
+        hipEvent_t e;
+        ~EvGuard() { (void)hipEventDestroy(e); }
+    } evg{ready};
+    HIP_TRY(hipEventRecord(ready, s));
+    struct Part {
+        int64_t n = 0;
+        uint64_t* ob = nullptr;
+        uint32_t* op = nullptr;
+        int64_t cap = 0;
+        int64_t* dt = nullptr;
+        int64_t total = 0;
+        const void* k = nullptr;
+        const uint8_t* v = nullptr;
+        int64_t voff = 0;
+        const uint32_t* ids = nullptr;
+        void* ws = nullptr;
+    };
+    std::vector<Part> parts(G);
+    // per shard: its rows on its device
+    if (m->plan == HJ_MULTI_BROADCAST) {
+        for (int g = 0; g < G; ++g) {
+            const int dev = m->devices[g];
+            hipStream_t sg = m->streams[g];
+            Part& P = parts[g];
+            const int64_t a = n * g / G, b = n * (g + 1) / G;
+            P.n = b - a;
+            HIP_TRY(hipSetDevice(dev));
+            HIP_TRY(hipStreamWaitEvent(sg, ready, 0));
+            if (dev == d) {
+                P.k = (const char*)keys + a * kb;
+                P.v = valid;
+                P.voff = voff + a;
+            } else {
+                MT_ALLOC(kd, void*, dev, (size_t)P.n * kb);
+                HIP_TRY(copy_to(kd, (const char*)keys + a * kb, (size_t)P.n * kb, sg));
+                P.k = kd;
+                if (valid) {
+                    const int64_t b0 = (voff + a) >> 3, b1 = (voff + b + 7) >> 3;
+                    MT_ALLOC(vd, uint8_t*, dev, (size_t)(b1 - b0));
+                    HIP_TRY(copy_to(vd, valid + b0, (size_t)(b1 - b0), sg));
+                    P.v = vd;
+                    P.voff = (voff + a) & 7;
+                }
+            }
+            MT_ALLOC(ids, uint32_t*, dev, 4 * (size_t)P.n);
+            if (probe_ids) HIP_TRY(copy_to(ids, probe_ids + a, 4 * (size_t)P.n, sg));
+            else HIP_TRY(launch_iota_u32(ids, P.n, (uint32_t)a, sg));
+            P.ids = ids;
+        }
+    } else {
+        // radix: partition the batch by owner on its device; the rows travel with their
+        // row numbers (u32), the caller's ids are applied after the merge
+        HIP_TRY(hipSetDevice(d));
+        MT_ALLOC(ok, void*, d, (size_t)n * kb);
+        MT_ALLOC(oi, uint32_t*, d, (size_t)n * 4);
+        MT_ALLOC(cn, int64_t*, d, 8 * (size_t)G);
+        MT_ALLOC(ws, void*, d, (size_t)hj_partition_workspace_bytes(n, G));
+        if ((st = hj_partition_rows(t->kt, keys, valid, voff, nullptr, 0, n, G, nullptr, ok, kb, 0, oi, 4, cn, ws, s)) !=
+            HJ_OK)
+            return st;
+        std::vector<int64_t> cnt(G);
+        HIP_TRY(hipMemcpyAsync(cnt.data(), cn, 8 * (size_t)G, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        int64_t off = 0;
+        for (int g = 0; g < G; ++g) {
+            const int dev = m->devices[g];
+            hipStream_t sg = m->streams[g];
+            Part& P = parts[g];
+            P.n = cnt[g];
+            HIP_TRY(hipSetDevice(dev));
+            MT_ALLOC(kd, void*, dev, (size_t)P.n * kb);
+            MT_ALLOC(id, uint32_t*, dev, (size_t)P.n * 4);
+            HIP_TRY(copy_to(kd, (const char*)ok + off * kb, (size_t)P.n * kb, sg));
+            HIP_TRY(copy_to(id, oi + off, (size_t)P.n * 4, sg));
+            P.k = kd;
+            P.ids = id;
+            off += P.n;
+        }
+    }
+    // probe every shard (capacity: its rows; once more at the exact size if exceeded)
+    for (int pass = 0; pass < 2; ++pass) {
+        bool again = false;
+        for (int g = 0; g < G; ++g) {
+            Part& P = parts[g];
+            if (pass == 1 && P.total <= P.cap) continue;
+            const int dev = m->devices[g];
+            HIP_TRY(hipSetDevice(dev));
+            P.cap = pass == 0 ? std::max<int64_t>(P.n, 1) : P.total;
+            P.ob = (uint64_t*)tmp.get(dev, 8 * (size_t)P.cap);
+            P.op = (uint32_t*)tmp.get(dev, 4 * (size_t)P.cap);
+            if (!P.dt) P.dt = (int64_t*)tmp.get(dev, 8);
+            if (!P.ws) P.ws = tmp.get(dev, (size_t)hj_probe_workspace_bytes(P.n));
+            if (!P.ob || !P.op || !P.dt || !P.ws) return fail(HJ_ERR_OOM, "multi-GPU probe: device allocation failed");
+            if ((st = hj_probe_async_ids(m->shards[g], P.k, P.v, P.voff, P.ids, P.n, P.ob, P.op, P.cap, P.dt, P.ws,
+                                         m->streams[g])) != HJ_OK)
+                return st;
+            HIP_TRY(hipMemcpyAsync(&P.total, P.dt, 8, hipMemcpyDeviceToHost, m->streams[g]));
+            again = true;
+        }
+        if (!again) break;
+        if ((st = sync_streams(m)) != HJ_OK) return st;
+    }
+    int64_t total = 0;
+    unsigned long long err = 0;  // the shards' look-back error words, ORed into the caller's
+    for (auto& P : parts) {
+        total += P.total;
+        unsigned long long e = 0;
+        HIP_TRY(hipMemcpy(&e, (char*)P.ws + 8, 8, hipMemcpyDeviceToHost));
+        err |= e;
+    }
+    HIP_TRY(hipSetDevice(d));
+    if (workspace) HIP_TRY(hipMemcpyAsync((char*)workspace + 8, &err, 8, hipMemcpyHostToDevice, s));
+    if (m->plan == HJ_MULTI_BROADCAST) {  // contiguous row ranges: concatenation is canonical
+        int64_t at = 0;
+        for (auto& P : parts) {
+            const int64_t c = std::min<int64_t>(P.total, std::max<int64_t>(cap - at, 0));
+            HIP_TRY(copy_to(out_b + at, P.ob, 8 * (size_t)c, s));
+            HIP_TRY(copy_to(out_p + at, P.op, 4 * (size_t)c, s));
+            at += P.total;
+        }
+    } else if (total > 0) {  // gather the pieces' pairs, then the canonical merge by probe row
+        MT_ALLOC(cb, uint64_t*, d, 8 * (size_t)total);
+        MT_ALLOC(cp, uint32_t*, d, 4 * (size_t)total);
+        int64_t at = 0;
+        for (auto& P : parts) {
+            HIP_TRY(copy_to(cb + at, P.ob, 8 * (size_t)P.total, s));
+            HIP_TRY(copy_to(cp + at, P.op, 4 * (size_t)P.total, s));
+            at += P.total;
+        }
+        MT_ALLOC(mw, void*, d, (size_t)merge_pairs_workspace(n));
+        HIP_TRY(launch_merge_pairs(cb, cp, total, n, out_b, out_p, cap, mw, s));
+        if (probe_ids)  // row -> the caller's probe id, in place (each thread its own element)
+            HIP_TRY(launch_gather_fixed(probe_ids, nullptr, 0, 4, out_p, 4, std::min(total, cap), out_p, nullptr, s));
+    }
+    HIP_TRY(hipMemcpyAsync(d_total, &total, 8, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipStreamSynchronize(s));  // total lives on this frame; the scratch goes back to the cache
+    return HJ_OK;
+}
+
+}  // namespace
+
+namespace {
+hj_status run_multi_build_entry(hj_table* t, const std::vector<Segment>& segs, const std::vector<HostSeg*>& hsegs) {
+    return run_multi_build(t, segs, hsegs);
+}
+}  // namespace
+
 extern "C" {
 
 const char* hj_last_error(void) { return g_err.c_str(); }
@@ -690,6 +1072,45 @@ hj_status hj_build_begin(int device, int parallelism, hj_key_type key_type, int6
             }
         });
     *out = t;
+    return HJ_OK;
+}
+
+hj_status hj_build_begin_multi(int ngpu, const int* devices, int parallelism, hj_key_type key_type,
+                               int64_t expected_rows, int plan, hj_table** out) {
+    if (out == nullptr) return fail(HJ_ERR_INVALID, "null out");
+    *out = nullptr;
+    if (ngpu < 1 || ngpu > 64 || devices == nullptr) return fail(HJ_ERR_INVALID, "ngpu must be 1..64 with a device list");
+    if (plan != HJ_MULTI_AUTO && plan != HJ_MULTI_BROADCAST && plan != HJ_MULTI_RADIX)
+        return fail(HJ_ERR_INVALID, "unknown multi-GPU plan");
+    if (plan == HJ_MULTI_RADIX && (ngpu & (ngpu - 1)))
+        return fail(HJ_ERR_INVALID, "the radix plan shards over a power-of-two number of GPUs");
+    const int nd = device_count();
+    if (nd == 0) return fail(HJ_ERR_NO_DEVICE, "no GPU visible: the HIP path cannot run (no CPU fallback)");
+    for (int g = 0; g < ngpu; ++g)
+        if (devices[g] < 0 || devices[g] >= nd) return fail(HJ_ERR_INVALID, "bad device ordinal");
+    hj_status st = hj_build_begin(devices[0], parallelism, key_type, expected_rows, out);
+    if (st != HJ_OK) return st;
+    hj_table* t = *out;
+    MultiTable* m = new MultiTable();
+    m->plan = plan;
+    m->devices.assign(devices, devices + ngpu);
+    for (int g = 0; g < ngpu; ++g) {
+        hipStream_t s = nullptr;
+        if (hipSetDevice(devices[g]) != hipSuccess || hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) {
+            delete m;
+            hj_table_free(t);
+            *out = nullptr;
+            return fail(HJ_ERR_HIP, "multi-GPU table: stream creation failed");
+        }
+        m->streams.push_back(s);
+        for (int q = 0; q < ngpu; ++q)  // xGMI peer access for the shards' copies (already on: fine)
+            if (devices[q] != devices[g]) {
+                (void)hipDeviceEnablePeerAccess(devices[q], 0);
+                (void)hipGetLastError();
+            }
+    }
+    (void)hipSetDevice(devices[0]);
+    t->multi = m;
     return HJ_OK;
 }
 
@@ -817,6 +1238,28 @@ hj_status hj_table_stats_get(const hj_table* t, hj_table_stats* out) {
     hj_status st = check_table(t);
     if (st != HJ_OK) return st;
     if (out == nullptr) return fail(HJ_ERR_INVALID, "null out");
+    if (t->multi) {  // broadcast: every shard holds the table; radix: the shards' sums
+        const MultiTable* m = t->multi;
+        memset(out, 0, sizeof(*out));
+        for (size_t g = 0; g < m->shards.size(); ++g) {
+            hj_table_stats s;
+            if ((st = hj_table_stats_get(m->shards[g], &s)) != HJ_OK) return st;
+            if (m->plan == HJ_MULTI_BROADCAST && g > 0) {
+                out->build_ns = std::max(out->build_ns, s.build_ns);
+                continue;
+            }
+            out->inserted_rows += s.inserted_rows;
+            out->distinct_keys += s.distinct_keys;
+            out->dup_keys += s.dup_keys;
+            out->dup_rows += s.dup_rows;
+            out->max_key_rows = std::max(out->max_key_rows, s.max_key_rows);
+            out->buckets += s.buckets;
+            out->table_bytes += s.table_bytes;
+            out->build_ns = std::max(out->build_ns, s.build_ns);
+        }
+        out->build_rows = t->total_rows;
+        return HJ_OK;
+    }
     HIP_TRY(hipSetDevice(t->device));
     hipStream_t s = thread_stream(t->device);
     unsigned long long* d = nullptr;
@@ -843,6 +1286,11 @@ hj_status hj_table_stats_get(const hj_table* t, hj_table_stats* out) {
 
 int64_t hj_table_build_ns(const hj_table* t) {
     if (t == nullptr || !t->built || t->build_st != HJ_OK) return -1;
+    if (t->multi) {
+        int64_t ns = 0;
+        for (hj_table* sh : t->multi->shards) ns = std::max(ns, hj_table_build_ns(sh));
+        return ns;
+    }
     return build_time_ns(const_cast<hj_table*>(t));
 }
 
@@ -870,6 +1318,9 @@ hj_status hj_probe_async(const hj_table* t, const void* keys, const uint8_t* val
     if (d_total == nullptr || workspace == nullptr) return fail(HJ_ERR_INVALID, "null d_total/workspace");
     if (n > 0 && keys == nullptr) return fail(HJ_ERR_INVALID, "null keys");
     HIP_TRY(hipSetDevice(t->device));
+    if (t->multi)
+        return multi_probe(t, keys, validity, validity_offset, nullptr, n, out_build, out_probe, capacity, d_total,
+                           workspace, (hipStream_t)stream);
     return probe_impl(t, keys, validity, validity_offset, nullptr, n, out_build, out_probe, capacity, d_total,
                       workspace, (hipStream_t)stream /* NULL = the null stream */);
 }
@@ -881,6 +1332,9 @@ hj_status hj_probe_async_ids(const hj_table* t, const void* keys, const uint8_t*
     if (st != HJ_OK) return st;
     if (d_total == nullptr || workspace == nullptr) return fail(HJ_ERR_INVALID, "null d_total/workspace");
     HIP_TRY(hipSetDevice(t->device));
+    if (t->multi)
+        return multi_probe(t, keys, validity, validity_offset, probe_ids, n, out_build, out_probe, capacity, d_total,
+                           workspace, (hipStream_t)stream);
     return probe_impl(t, keys, validity, validity_offset, probe_ids, n, out_build, out_probe, capacity, d_total,
                       workspace, (hipStream_t)stream /* NULL = the null stream */);
 }
@@ -912,7 +1366,9 @@ hj_status hj_probe(const hj_table* t, const void* keys, const uint8_t* validity,
     for (int attempt = 0; attempt < 2; ++attempt) {
         HIP_TRY(hipMalloc((void**)&ob, (size_t)cap * 8));
         HIP_TRY(hipMalloc((void**)&op, (size_t)cap * 4));
-        if ((st = probe_impl(t, dk, dv, dvo, nullptr, n, ob, op, cap, d_total, ws, s)) != HJ_OK) break;
+        if (t->multi) st = multi_probe(t, dk, dv, dvo, nullptr, n, ob, op, cap, d_total, ws, s);
+        else st = probe_impl(t, dk, dv, dvo, nullptr, n, ob, op, cap, d_total, ws, s);
+        if (st != HJ_OK) break;
         uint64_t werr = 0;
         HIP_TRY(hipMemcpyAsync(&total, d_total, 8, hipMemcpyDeviceToHost, s));
         HIP_TRY(hipMemcpyAsync(&werr, (char*)ws + 8, 8, hipMemcpyDeviceToHost, s));
@@ -998,6 +1454,7 @@ hj_status hj_table_chain_links(const hj_table* t, int64_t* prev, int64_t n) {
     hj_status st = check_table(t);
     if (st != HJ_OK) return st;
     if (t->has_ids) return fail(HJ_ERR_INVALID, "chain links are defined for canonical row numbering (no explicit ids)");
+    if (t->multi) return fail(HJ_ERR_INVALID, "chain links are not defined for a multi-GPU table");
     if (n != t->total_rows || (n > 0 && prev == nullptr))
         return fail(HJ_ERR_INVALID, "prev must hold build_rows entries");
     if (n == 0) return HJ_OK;
@@ -1016,6 +1473,11 @@ hj_status hj_table_chain_links(const hj_table* t, int64_t* prev, int64_t n) {
 hj_status hj_table_stream_wait(const hj_table* t, void* stream) {
     hj_status st = check_table(t);
     if (st != HJ_OK) return st;
+    if (t->multi) {
+        for (hj_table* sh : t->multi->shards)
+            if ((st = hj_table_stream_wait(sh, stream)) != HJ_OK) return st;
+        return HJ_OK;
+    }
     HIP_TRY(hipStreamWaitEvent((hipStream_t)stream, t->res.ev1, 0));
     return HJ_OK;
 }
@@ -1032,6 +1494,8 @@ void hj_table_free(hj_table* t) {
     }
     free_list(t, t->allocs);
     free_list(t, t->scratch);
+    delete t->multi;  // its shards first: they borrow multi_bufs
+    for (auto& b : t->multi_bufs) cache_free(std::get<0>(b), std::get<1>(b), std::get<2>(b));
     for (auto& part : t->parts)
         for (auto& hs : part) {
             for (void* p : hs.owned) (void)hipFree(p);
@@ -1085,6 +1549,72 @@ hj_status hj_partition_rows(hj_key_type key_type, const void* keys, const uint8_
     HIP_TRY(launch_radix_partition(key_type == HJ_INT64 ? 8 : 4, keys, validity, validity_offset, ids, id_base, n,
                                    nparts, ps, out_keys, out_key_bytes, key_offset, out_ids, id_bytes, counts,
                                    workspace, (hipStream_t)stream));
+    return HJ_OK;
+}
+
+// ---- composite keys (hj_keys.hip) --------------------------------------------------
+
+namespace {
+hj_status key_cols(int ncols, const hj_key_column* cols, KeyCols* out) {
+    if (ncols < 1 || ncols > kMaxKeyCols) return fail(HJ_ERR_INVALID, "ncols must be 1..16");
+    if (cols == nullptr) return fail(HJ_ERR_INVALID, "null key columns");
+    out->n = ncols;
+    for (int j = 0; j < ncols; ++j) {
+        const hj_key_column& c = cols[j];
+        const int w = c.width;
+        if (!(w == 0 || w == 1 || w == 2 || w == 4 || w == 8 || w == 16))
+            return fail(HJ_ERR_INVALID, "key column width must be 0 (variable), 1, 2, 4, 8 or 16");
+        if (w == 0 && c.offset_bytes != 4 && c.offset_bytes != 8)
+            return fail(HJ_ERR_INVALID, "variable-width key column: offset_bytes must be 4 or 8");
+        if (c.values == nullptr || (w == 0 && c.offsets == nullptr))
+            return fail(HJ_ERR_INVALID, "null key column buffer");
+        if (c.validity_offset < 0) return fail(HJ_ERR_INVALID, "negative validity offset");
+        if (!is_device_ptr(c.values) || !is_device_ptr(c.offsets) || !is_device_ptr(c.validity))
+            return fail(HJ_ERR_INVALID, "key columns take device pointers");
+        out->c[j] = KeyCol{c.values, c.offsets, c.validity, c.validity_offset, w, c.offset_bytes};
+    }
+    return HJ_OK;
+}
+}  // namespace
+
+hj_status hj_composite_keys(int ncols, const hj_key_column* cols, int64_t n, int64_t* out_keys, uint8_t* out_valid,
+                            void* stream) {
+    if (device_count() == 0) return fail(HJ_ERR_NO_DEVICE, "no GPU visible");
+    if (n < 0) return fail(HJ_ERR_INVALID, "negative length");
+    KeyCols kc;
+    hj_status st = key_cols(ncols, cols, &kc);
+    if (st != HJ_OK) return st;
+    if (n > 0 && (out_keys == nullptr || out_valid == nullptr)) return fail(HJ_ERR_INVALID, "null output");
+    if (reinterpret_cast<uintptr_t>(out_valid) & 7) return fail(HJ_ERR_INVALID, "out_valid must be 8-byte aligned");
+    if (!is_device_ptr(out_keys) || !is_device_ptr(out_valid))
+        return fail(HJ_ERR_INVALID, "hj_composite_keys takes device pointers");
+    HIP_TRY(launch_composite_keys(kc, n, out_keys, reinterpret_cast<uint64_t*>(out_valid), (hipStream_t)stream));
+    return HJ_OK;
+}
+
+int64_t hj_equal_pairs_workspace_bytes(int64_t n) { return equal_pairs_workspace(n < 0 ? 0 : n); }
+
+hj_status hj_filter_equal_pairs(int ncols, const hj_key_column* build_cols, const hj_key_column* probe_cols,
+                                const uint64_t* build_idx, const uint32_t* probe_idx, int64_t n, uint64_t* out_build,
+                                uint32_t* out_probe, int64_t* d_count, void* workspace, void* stream) {
+    if (device_count() == 0) return fail(HJ_ERR_NO_DEVICE, "no GPU visible");
+    if (n < 0) return fail(HJ_ERR_INVALID, "negative length");
+    KeyCols bc, pc;
+    hj_status st;
+    if ((st = key_cols(ncols, build_cols, &bc)) != HJ_OK || (st = key_cols(ncols, probe_cols, &pc)) != HJ_OK) return st;
+    for (int j = 0; j < ncols; ++j)
+        if (bc.c[j].width != pc.c[j].width)
+            return fail(HJ_ERR_INVALID, "build and probe key column " + std::to_string(j) + " differ in width");
+    if (d_count == nullptr || workspace == nullptr ||
+        (n > 0 && (build_idx == nullptr || probe_idx == nullptr || out_build == nullptr || out_probe == nullptr)))
+        return fail(HJ_ERR_INVALID, "null pointer");
+    if ((const void*)out_build == (const void*)build_idx || (const void*)out_probe == (const void*)probe_idx)
+        return fail(HJ_ERR_INVALID, "outputs must not alias the candidate pairs");
+    if (!is_device_ptr(build_idx) || !is_device_ptr(probe_idx) || !is_device_ptr(out_build) ||
+        !is_device_ptr(out_probe) || !is_device_ptr(d_count) || !is_device_ptr(workspace))
+        return fail(HJ_ERR_INVALID, "hj_filter_equal_pairs takes device pointers");
+    HIP_TRY(launch_equal_pairs(bc, pc, build_idx, probe_idx, n, out_build, out_probe, d_count, workspace,
+                               (hipStream_t)stream));
     return HJ_OK;
 }
 

@@ -286,4 +286,77 @@ hipError_t launch_gather_var(const void* offsets, int offset_bytes, const uint8_
     return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------
+// multi-GPU table helpers (hj_build_begin_multi, hj_api.cpp)
+// ---------------------------------------------------------------------------
+// out[i] = base + i (u32 probe ids of a contiguous row range)
+__global__ void iota_u32_kernel(uint32_t* __restrict__ out, int64_t n, uint32_t base) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        out[i] = base + (uint32_t)i;
+}
+// out[i] = in[i] (u32 -> u64 ids for the partition kernel)
+__global__ void widen_u32_kernel(const uint32_t* __restrict__ in, int64_t n, uint64_t* __restrict__ out) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        out[i] = in[i];
+}
+// Canonical merge of the shards' pair streams: every probe row's pairs come from one shard
+// (its key's owner), contiguous and in build-descending order, and each stream ascends in
+// probe row. cnt[r] = pairs of row r, first[r] = index of its first pair; after an
+// exclusive scan of cnt, pair i goes to start[r] + (i - first[r]).
+__global__ void pairs_rank_kernel(const uint32_t* __restrict__ p, int64_t m, unsigned long long* __restrict__ cnt,
+                                  unsigned long long* __restrict__ first) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (int64_t)gridDim.x * blockDim.x) {
+        const uint32_t r = p[i];
+        atomicAdd(&cnt[r], 1ull);
+        atomicMin(&first[r], (unsigned long long)i);
+    }
+}
+__global__ void pairs_place_kernel(const uint64_t* __restrict__ b, const uint32_t* __restrict__ p, int64_t m,
+                                   const unsigned long long* __restrict__ start,
+                                   const unsigned long long* __restrict__ first, uint64_t* __restrict__ out_b,
+                                   uint32_t* __restrict__ out_p, int64_t cap) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (int64_t)gridDim.x * blockDim.x) {
+        const uint32_t r = p[i];
+        const unsigned long long pos = start[r] + ((unsigned long long)i - first[r]);
+        if (pos < (unsigned long long)cap) {
+            out_b[pos] = b[i];
+            out_p[pos] = r;
+        }
+    }
+}
+
+static unsigned grid_for(int64_t n) { return (unsigned)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 8192)); }
+
+hipError_t launch_iota_u32(uint32_t* out, int64_t n, uint32_t base, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    iota_u32_kernel<<<grid_for(n), 256, 0, s>>>(out, n, base);
+    return hipGetLastError();
+}
+
+hipError_t launch_widen_u32(const uint32_t* in, int64_t n, uint64_t* out, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    widen_u32_kernel<<<grid_for(n), 256, 0, s>>>(in, n, out);
+    return hipGetLastError();
+}
+
+int64_t merge_pairs_workspace(int64_t nrows) { return 16 * (nrows + 2) + scan_scratch_bytes(nrows + 1) + 512; }
+
+hipError_t launch_merge_pairs(const uint64_t* b, const uint32_t* p, int64_t m, int64_t nrows, uint64_t* out_b,
+                              uint32_t* out_p, int64_t cap, void* ws, hipStream_t s) {
+    if (m <= 0 || nrows <= 0) return hipSuccess;
+    uintptr_t q = ((uintptr_t)ws + 255) & ~(uintptr_t)255;
+    unsigned long long* cnt = (unsigned long long*)q;
+    q = (q + 8 * (nrows + 1) + 255) & ~(uintptr_t)255;
+    unsigned long long* first = (unsigned long long*)q;
+    q = (q + 8 * (nrows + 1) + 255) & ~(uintptr_t)255;
+    void* scr = (void*)q;
+    hipError_t e = hipMemsetAsync(cnt, 0, 8 * (size_t)nrows, s);
+    if (e == hipSuccess) e = hipMemsetAsync(first, 0xFF, 8 * (size_t)nrows, s);
+    if (e != hipSuccess) return e;
+    pairs_rank_kernel<<<grid_for(m), 256, 0, s>>>(p, m, cnt, first);
+    if ((e = launch_scan_u64(cnt, nrows, scr, nullptr, s)) != hipSuccess) return e;
+    pairs_place_kernel<<<grid_for(m), 256, 0, s>>>(b, p, m, cnt, first, out_b, out_p, cap);
+    return hipGetLastError();
+}
+
 }  // namespace dfp

@@ -65,7 +65,7 @@ hipError_t launch_key_minmax(int key_bytes, const Segment* h_segs, Segment* d_se
                              int64_t total, int64_t* out, int64_t* mbox, int64_t seq, hipStream_t s);
 
 // ---- probe ---------------------------------------------------------------
-// 0 auto (= direct), 1 direct, 2 partitioned (L2-resident pieces per XCD)
+// 0 auto, 3 fused, 4 sliced
 void set_probe_mode(int mode);
 int get_probe_mode();
 int64_t probe_tiles(int64_t n);
@@ -119,6 +119,39 @@ hipError_t launch_gather_var(const void* offsets, int offset_bytes, const uint8_
                              int64_t src_voff, const void* idx, int idx_bytes, int64_t n, void* out_offsets,
                              uint8_t* out_values, int64_t values_cap, uint8_t* dst_valid, int64_t* d_values_len,
                              void* workspace, hipStream_t s);
+
+// ---- multi-GPU table helpers (hj_columns.hip) -------------------------------
+hipError_t launch_iota_u32(uint32_t* out, int64_t n, uint32_t base, hipStream_t s);
+hipError_t launch_widen_u32(const uint32_t* in, int64_t n, uint64_t* out, hipStream_t s);
+// canonical order of shard pair streams whose probe rows are < nrows (see hj_columns.hip)
+int64_t merge_pairs_workspace(int64_t nrows);
+hipError_t launch_merge_pairs(const uint64_t* b, const uint32_t* p, int64_t m, int64_t nrows, uint64_t* out_b,
+                              uint32_t* out_p, int64_t cap, void* ws, hipStream_t s);
+
+// ---- composite keys (hj_keys.hip) -------------------------------------------
+// A key column in device memory: fixed width (width 1/2/4/8/16) or variable width (width
+// 0: int32 / int64 offsets + value bytes), optional LSB validity bitmap from bit voff.
+struct KeyCol {
+    const void* values;
+    const void* offsets;
+    const uint8_t* valid;
+    int64_t voff;
+    int width;
+    int offset_bytes;
+};
+constexpr int kMaxKeyCols = 16;
+struct KeyCols {
+    KeyCol c[kMaxKeyCols];
+    int n;
+};
+// out_keys[i] = hash of row i's key tuple; out_valid: ceil(n / 64) u64 words, bit i = no
+// key column null at row i
+hipError_t launch_composite_keys(const KeyCols& cols, int64_t n, int64_t* out_keys, uint64_t* out_valid,
+                                 hipStream_t s);
+int64_t equal_pairs_workspace(int64_t n);
+hipError_t launch_equal_pairs(const KeyCols& bc, const KeyCols& pc, const uint64_t* bidx, const uint32_t* pidx,
+                              int64_t n, uint64_t* out_b, uint32_t* out_p, int64_t* d_count, void* ws,
+                              hipStream_t s);
 
 // ---- generators ----------------------------------------------------------
 hipError_t launch_gen_perm(int64_t* out, int64_t n, int64_t mul, int64_t range, hipStream_t s);

@@ -373,6 +373,47 @@ class DistributedHashJoin:
         finally:
             table.close()
 
+    # -- broadcast-build plan ------------------------------------------
+    @staticmethod
+    def choose_plan(build_rows: int, probe_rows: int, world: int) -> str:
+        """'broadcast' when every rank receiving the whole build side moves fewer rows than
+        the radix all-to-all of both sides (B·G < B + P), else 'radix'."""
+        return "broadcast" if build_rows * world < build_rows + probe_rows else "radix"
+
+    def run_broadcast(self, build_keys: torch.Tensor, probe_keys: torch.Tensor, probe_base: int,
+                      capacity_hint: int | None = None):
+        """Broadcast-build join: every rank all-gathers the build shards (rank order = the
+        global canonical row order, so the local table's row numbers are the global build
+        ids) and probes only its own probe rows: no probe-side exchange. -> this rank's
+        pairs (global build idx int64, global probe idx int32); the ranks' outputs in rank
+        order are the global canonical output. Needs equal-typed shards on every rank."""
+        (gathered,) = all_gather_rows([build_keys], self.group)
+        dev = build_keys.device
+        n = probe_keys.numel()
+        if self.local_join_fn is not gpu_local_join:  # host stand-in (gloo tests): explicit ids
+            bi = torch.arange(gathered.numel(), dtype=torch.int64, device=dev)
+            pi = torch.arange(probe_base, probe_base + n, dtype=torch.int64, device=dev).to(torch.int32)
+            return self.local_join_fn(gathered, bi, probe_keys, pi, capacity_hint)
+        kt = "int64" if gathered.dtype == torch.int64 else "int32"
+        with HashTable(1, kt, dev.index or 0) as t:  # canonical numbering = the global build ids
+            t.append(0, gathered)
+            t.finish(0)
+            ids = torch.arange(probe_base, probe_base + n, dtype=torch.int64, device=dev).to(torch.int32)
+            ws = torch.empty(HashTable.workspace_bytes(n), dtype=torch.uint8, device=dev)
+            d_total = torch.zeros(1, dtype=torch.int64, device=dev)
+            cap = max(capacity_hint or n, 1)
+            s = torch.cuda.current_stream(dev).cuda_stream
+            for _ in range(2):
+                ob = torch.empty(cap, dtype=torch.int64, device=dev)
+                op = torch.empty(cap, dtype=torch.int32, device=dev)
+                t.probe_async(probe_keys.data_ptr(), n, ob.data_ptr(), op.data_ptr(), cap, d_total.data_ptr(),
+                              ws.data_ptr(), s, probe_ids_ptr=ids.data_ptr())
+                total = int(d_total.item())
+                if total <= cap:
+                    return ob[:total], op[:total]
+                cap = total
+        raise RuntimeError("unreachable")
+
     @staticmethod
     def _probe_chunk(table, rk, ri, works):
         for w in works:

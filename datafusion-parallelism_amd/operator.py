@@ -29,7 +29,11 @@ whose build and probe run on the gfx950 kernels through the C ABI (``include/hj.
   apply_join_filter_to_indices (src/shared/datafusion_private.rs:295-328)
                                                               JoinFilter
 
-Single Int32/Int64 equi-join key column. Output columns are materialised on the GPU
+Join keys: one Int32/Int64 column goes to the table as is (exact keys); several key
+columns, or a key of any other fixed-width or Utf8/Binary type, go through
+hj_composite_keys (one 64-bit key per row from all key columns, the reference's
+calculate_hash) and the candidate pairs through hj_filter_equal_pairs (equal_rows_arr).
+Output columns are materialised on the GPU
 (columns.DeviceColumn.take: the build side is uploaded once after the barrier, each probe
 batch once). The reference's CPU strategies (Original, New..New10) are not part of this
 package.
@@ -47,7 +51,7 @@ import pyarrow.compute as pc
 import torch
 
 from ._lib import HjError, HJ_ERR_INVALID
-from .columns import DeviceColumn, mark_rows, select_rows
+from .columns import DeviceColumn, composite_keys, filter_equal_pairs, mark_rows, select_rows
 from .table import HashTable
 
 
@@ -79,7 +83,12 @@ def _key_type(arr: pa.Array) -> str:
         return "int64"
     if pa.types.is_int32(arr.type):
         return "int32"
-    raise HjError(HJ_ERR_INVALID, f"join key type {arr.type} is not supported (Int32/Int64 only)")
+    raise HjError(HJ_ERR_INVALID, f"join key type {arr.type} is not an Int32/Int64 key")
+
+
+def _is_simple_key(arrays: Sequence[pa.Array]) -> bool:
+    """One Int32/Int64 key column: the table takes it as is; anything else is composite."""
+    return len(arrays) == 1 and (pa.types.is_int64(arrays[0].type) or pa.types.is_int32(arrays[0].type))
 
 
 class JoinType(enum.Enum):
@@ -146,9 +155,19 @@ class GpuIndexLookup:
         internal), which the equality re-check makes equivalent."""
         return iter(self.table.lookup(key))
 
-    def matching_indices_device(self, probe_keys: pa.Array) -> tuple[torch.Tensor, torch.Tensor]:
-        """get_matching_indices + equal_rows_arr, fused on the GPU: ProbeBuildIndices
-        after the equality filter as device tensors (build int64, probe int32)."""
+    def matching_indices_device(self, probe_keys: pa.Array | Sequence[pa.Array],
+                                build_side_records: pa.RecordBatch | None = None
+                                ) -> tuple[torch.Tensor, torch.Tensor]:
+        """get_matching_indices + equal_rows_arr on the GPU: ProbeBuildIndices after the
+        equality filter as device tensors (build int64, probe int32). One Int32/Int64
+        key: the table compares exact keys (fused). Composite keys: candidates of equal
+        composite key, then hj_filter_equal_pairs on the key columns."""
+        arrays = [probe_keys] if isinstance(probe_keys, (pa.Array, pa.ChunkedArray)) else list(probe_keys)
+        if self._shared is not None and (self._shared.composite or not _is_simple_key(arrays)):
+            return self._composite_matches(arrays, build_side_records)
+        if not _is_simple_key(arrays):
+            raise HjError(HJ_ERR_INVALID, "probe keys do not match the build keys (one Int32/Int64 column)")
+        probe_keys = arrays[0]
         keys = DeviceColumn.from_arrow(probe_keys, self.device)
         n = len(probe_keys)
         if n == 0:
@@ -161,6 +180,22 @@ class GpuIndexLookup:
             bits = np.unpackbits(keys.valid.cpu().numpy(), bitorder="little")[keys.voff:keys.voff + n]
             valid = bits.astype(bool)
         return self.table.probe(kt, valid, device_output=True)
+
+    def _composite_matches(self, arrays: list[pa.Array], build_side_records: pa.RecordBatch | None):
+        sh = self._shared
+        if len(arrays) != len(sh.key_exprs):
+            raise HjError(HJ_ERR_INVALID, f"{len(arrays)} probe key columns for {len(sh.key_exprs)} build key columns")
+        n = len(arrays[0])
+        if n == 0:
+            return (torch.empty(0, dtype=torch.int64, device=self.device),
+                    torch.empty(0, dtype=torch.int32, device=self.device))
+        pcols = [DeviceColumn.from_arrow(a, self.device) for a in arrays]
+        keys, valid = composite_keys(pcols)
+        b, p = self.table.probe(keys, valid, device_output=True)
+        rb = build_side_records if build_side_records is not None else sh.concatenated()
+        bcols = self.build_columns(rb)
+        kidx = [e if isinstance(e, int) else rb.schema.get_field_index(e) for e in sh.key_exprs]
+        return filter_equal_pairs([bcols[i] for i in kidx], pcols, b, p)
 
     def matching_indices(self, probe_keys: pa.Array) -> tuple[pa.UInt64Array, pa.UInt32Array]:
         """Host form of matching_indices_device (UInt64 build, UInt32 probe)."""
@@ -188,6 +223,8 @@ class _SharedBuild:
         self.record_batch: pa.RecordBatch | None = None
         self.schema: pa.Schema | None = None
         self._dev_cols: list[DeviceColumn] | None = None
+        self.composite = False          # keys through hj_composite_keys (several / non-integer columns)
+        self.key_exprs: list = []       # the build key expressions (the equality filter's columns)
 
     def table_for(self, key_type: str) -> HashTable:
         with self.lock:
@@ -246,16 +283,25 @@ class BuildImplementation:
             if sh.taken[partition]:
                 raise HjError(HJ_ERR_INVALID, f"State already consumed for partition {partition}")
             sh.taken[partition] = True
-        if len(build_expressions) != 1:
-            raise HjError(HJ_ERR_INVALID, "only single-column equi-join keys are supported")
+        if len(build_expressions) < 1:
+            raise HjError(HJ_ERR_INVALID, "an equi-join needs at least one key column")
+        with sh.lock:
+            sh.key_exprs = list(build_expressions)
         for batch in stream:
             sh.batches[partition].append(batch)
             if sh.schema is None:
                 sh.schema = batch.schema
             if batch.num_rows == 0:
                 continue
-            (keys,) = evaluate_expressions(build_expressions, batch)
-            sh.table_for(_key_type(keys)).append(partition, keys)
+            arrays = evaluate_expressions(build_expressions, batch)
+            if _is_simple_key(arrays):
+                sh.table_for(_key_type(arrays[0])).append(partition, arrays[0])
+            else:  # calculate_hash over every key column -> one int64 key per row
+                dev = torch.device("cuda", sh.device)
+                keys, valid = composite_keys([DeviceColumn.from_arrow(a, dev) for a in arrays])
+                with sh.lock:
+                    sh.composite = True
+                sh.table_for("int64").append(partition, keys, valid=valid)
         # every partition waits for every other before the table exists for all of them
         sh.ready.wait()
         table = sh.table_for(sh.key_type or "int64")
@@ -291,9 +337,9 @@ def probe_batch(join_type: JoinType, probe_expressions: Sequence[str | int], bui
     jt = JoinType.parse(join_type)
     lookup = read_only_join_map
     dev = lookup.device
-    (probe_keys,) = evaluate_expressions(probe_expressions, probe_batch)
+    probe_keys = evaluate_expressions(probe_expressions, probe_batch)
     n = probe_batch.num_rows
-    b, p = lookup.matching_indices_device(probe_keys)
+    b, p = lookup.matching_indices_device(probe_keys, build_side_records)
     build_cols = lookup.build_columns(build_side_records)
     bnames, pnames = list(build_side_records.schema.names), list(probe_batch.schema.names)
     probe_cols = [DeviceColumn.from_arrow(c, dev) for c in probe_batch.columns]
@@ -409,8 +455,8 @@ class ParallelHashJoin:
                  on: Sequence[tuple[str, str]], join_type: JoinType | str = JoinType.Inner, device: int = 0,
                  replacement: JoinReplacement = JoinReplacement.Gpu, filter: JoinFilter | None = None,
                  right_schema: pa.Schema | None = None):
-        if len(on) != 1:
-            raise HjError(HJ_ERR_INVALID, "only single-column equi-join keys are supported")
+        if len(on) < 1:
+            raise HjError(HJ_ERR_INVALID, "an equi-join needs at least one (left, right) key pair")
         self.join_type = JoinType.parse(join_type)
         n = max(len(left), len(right), 1)
         self.left = list(left) + [[] for _ in range(n - len(left))]
@@ -423,9 +469,10 @@ class ParallelHashJoin:
         self._finalizer = _Finalizer(n)
 
     def execute(self, partition: int) -> list[pa.RecordBatch]:
-        consumer = _ProbeConsumer(self.right[partition], [self.on[0][1]], [self.on[0][0]], self.join_type,
-                                  self.filter, self._finalizer, self.right_schema)
-        return self._build.build_side(partition, self.left[partition], [self.on[0][0]], consumer)
+        lkeys, rkeys = [l for l, _ in self.on], [r for _, r in self.on]
+        consumer = _ProbeConsumer(self.right[partition], rkeys, lkeys, self.join_type, self.filter, self._finalizer,
+                                  self.right_schema)
+        return self._build.build_side(partition, self.left[partition], lkeys, consumer)
 
     def collect(self) -> list[pa.RecordBatch]:
         """DataFusion `collect`: execute every partition concurrently."""

@@ -95,16 +95,25 @@ class HashTable:
     """One shared build table for `parallelism` partitions (hj_build_begin .. finish)."""
 
     def __init__(self, parallelism: int = 1, key_type: str | int = "int64", device: int = 0,
-                 expected_rows: int = 0):
+                 expected_rows: int = 0, devices: list[int] | None = None, plan: int | str = 0):
+        """devices: a multi-GPU table over these GPUs (hj_build_begin_multi; repeats
+        allowed), `plan` 0/"auto", 1/"broadcast" or 2/"radix"; else one table on `device`."""
         self._L = _lib.load()
         kt = key_type if isinstance(key_type, int) else (HJ_INT64 if key_type == "int64" else HJ_INT32)
         if key_type not in ("int64", "int32", HJ_INT32, HJ_INT64):
             raise TypeError(f"unsupported key type {key_type}")
         self.key_type = kt
         self.parallelism = parallelism
-        self.device = device
+        self.device = devices[0] if devices else device
+        self.devices = list(devices) if devices else None
         h = ctypes.c_void_p()
-        check(self._L.hj_build_begin(device, parallelism, kt, expected_rows, ctypes.byref(h)))
+        if devices is not None:
+            plan = {"auto": 0, "broadcast": 1, "radix": 2}.get(plan, plan) if isinstance(plan, str) else plan
+            arr = (ctypes.c_int * len(devices))(*devices)
+            check(self._L.hj_build_begin_multi(len(devices), arr, parallelism, kt, expected_rows, int(plan),
+                                               ctypes.byref(h)))
+        else:
+            check(self._L.hj_build_begin(device, parallelism, kt, expected_rows, ctypes.byref(h)))
         self._h = h
         self._keep = []  # borrowed device inputs stay alive until the table is freed
 

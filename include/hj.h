@@ -102,6 +102,25 @@ int hj_device_count(void);
 hj_status hj_build_begin(int device, int parallelism, hj_key_type key_type,
                          int64_t expected_rows, hj_table** out);
 
+/* Multi-GPU table plans (hj_build_begin_multi). */
+enum { HJ_MULTI_AUTO = 0, HJ_MULTI_BROADCAST = 1, HJ_MULTI_RADIX = 2 };
+
+/* A table whose shards live on the GPUs `devices[0..ngpu)` (repeats allowed), behind the
+ * same append / finish / probe / pairs / free ABI as a one-GPU table: the drop-in for a
+ * process that drives a node of GPUs, as the reference's one process drives its
+ * `parallelism` partitions. plan HJ_MULTI_BROADCAST: every GPU builds the whole build
+ * side and a probe batch is split into contiguous row ranges, one per GPU (cheaper while
+ * build rows x GPUs < build + probe rows); HJ_MULTI_RADIX (ngpu a power
+ * of two <= 64): the build side is sharded by key hash (the hj_partition_rows map), a
+ * probe batch is partitioned the same way, every piece probed by its owner over
+ * device-to-device copies, and the pieces' pairs merged back into canonical order;
+ * HJ_MULTI_AUTO: broadcast for build sides up to 2^27 rows, else radix. Pairs carry
+ * global canonical build ids exactly as a one-GPU table's. Probes of a multi table run on
+ * `stream` and the keys' device and return after the device work (the host reads the
+ * pieces' sizes). hj_table_chain_links is not defined for multi tables. */
+hj_status hj_build_begin_multi(int ngpu, const int* devices, int parallelism, hj_key_type key_type,
+                               int64_t expected_rows, int plan, hj_table** out);
+
 /* Append one build batch of partition `partition` (one RecordBatch's key column).
  * keys: int32/int64 values; validity: Arrow LSB bitmap (NULL = all valid) starting at
  * bit `validity_offset`; ids: optional explicit build ids (NULL = canonical numbering).
@@ -280,6 +299,46 @@ hj_status hj_gather_var(const void* offsets, int offset_bytes, const uint8_t* va
                         const uint8_t* src_valid, int64_t src_voff, const void* idx, int idx_bytes,
                         int64_t n, void* out_offsets, uint8_t* out_values, int64_t values_cap,
                         uint8_t* dst_valid, int64_t* d_values_len, void* workspace, void* stream);
+
+/* ---- join keys of several columns, or of non-integer types (SURVEY.md §8a a2/a12:
+ *      calculate_hash over every key column, src/shared/shared.rs:11-16, and the
+ *      equality re-check equal_rows_arr, src/shared/datafusion_private.rs:52-73). ------
+ * Flow: hj_composite_keys on each build batch -> hj_build_append(HJ_INT64 keys, the
+ * composite validity); hj_composite_keys on a probe batch -> hj_probe* -> candidate
+ * pairs -> hj_filter_equal_pairs -> the join's pairs (canonical order kept). A single
+ * Int32/Int64 key column needs none of this (the table compares exact keys). */
+
+/* One key column in device memory. Fixed width: width 1, 2, 4, 8 or 16 bytes, values
+ * row-major. Variable width (Utf8 / Binary / LargeUtf8 / LargeBinary): width 0, offsets
+ * (offset_bytes 4 or 8, n + 1 entries) into the value bytes. validity: Arrow LSB bitmap
+ * (NULL = all valid) from bit validity_offset. Values compare byte-exactly (arrow's eq;
+ * for floats its total order, i.e. equal bits). */
+typedef struct hj_key_column {
+    const void* values;
+    const void* offsets;
+    const uint8_t* validity;
+    int64_t validity_offset;
+    int width;
+    int offset_bytes;
+} hj_key_column;
+
+/* out_keys[i] (device int64) = a 64-bit hash of row i's key tuple over the `ncols`
+ * (<= 16) columns; out_valid (device, 8-byte aligned, ceil(n / 64) * 8 bytes) bit i = no
+ * key column is null at row i (a null key never matches). Asynchronous on `stream`. */
+hj_status hj_composite_keys(int ncols, const hj_key_column* cols, int64_t n, int64_t* out_keys,
+                            uint8_t* out_valid, void* stream);
+
+/* Keep the candidate pairs (build_idx[i], probe_idx[i]) whose key tuples are equal in
+ * every column, in order: out_build / out_probe (capacity n, distinct from the inputs)
+ * receive them and *d_count (device int64) their number. build_cols index the build
+ * side's concatenated rows, probe_cols the probe batch's rows. workspace:
+ * hj_equal_pairs_workspace_bytes(n). Asynchronous on `stream`. */
+int64_t hj_equal_pairs_workspace_bytes(int64_t n);
+hj_status hj_filter_equal_pairs(int ncols, const hj_key_column* build_cols,
+                                const hj_key_column* probe_cols, const uint64_t* build_idx,
+                                const uint32_t* probe_idx, int64_t n, uint64_t* out_build,
+                                uint32_t* out_probe, int64_t* d_count, void* workspace,
+                                void* stream);
 
 /* ---- synthetic generators of SURVEY.md §8(d) on the device (bench inputs) ----- */
 /* out[i] = (i * mul) mod range  (unique build keys when gcd(mul, range) = 1);

@@ -299,13 +299,23 @@ static void* v10_probe_worker(void* arg) {
     V10Work* w = (V10Work*)arg;
     const V10Table* t = w->t;
     int64_t c = 0;
+    const int emit = w->cap > 0;
     for (int64_t j = w->begin; j < w->end; ++j) {
         const int vp = valid_bit(w->valid, j);
         uint64_t idx = v10_get(t, key_hash(w->keys[j], vp, 0));
         while (idx != 0) {
             const int64_t b = (int64_t)idx - 1;
             if (vp && t->bkeys[b] == w->keys[j]) {
-                if (c < w->cap) {
+                if (emit) {  /* ProbeBuildIndices grow as the reference's Vec builders do */
+                    if (c == w->cap) {
+                        w->cap *= 2;
+                        w->out_b = (uint64_t*)realloc(w->out_b, (size_t)w->cap * 8);
+                        w->out_p = (uint32_t*)realloc(w->out_p, (size_t)w->cap * 4);
+                        if (!w->out_b || !w->out_p) {
+                            w->fail = 1;
+                            return NULL;
+                        }
+                    }
                     w->out_b[c] = (uint64_t)b;
                     w->out_p[c] = (uint32_t)j;
                 }
@@ -377,17 +387,15 @@ int64_t ora_v10_probe(void* table, const int64_t* pkeys, const uint8_t* pvalid, 
         w[i].begin = n * i / nthreads;
         w[i].end = n * (i + 1) / nthreads;
         const int64_t len = w[i].end - w[i].begin;
-        w[i].cap = cap > 0 ? len * 8 + 64 : 0;
+        /* per-thread pair buffers start at the chunk's rows and double when full */
+        w[i].cap = cap > 0 ? len + 64 : 0;
         w[i].out_b = w[i].cap ? (uint64_t*)malloc((size_t)w[i].cap * 8) : NULL;
         w[i].out_p = w[i].cap ? (uint32_t*)malloc((size_t)w[i].cap * 4) : NULL;
-        if (w[i].cap == 0) {
-            /* count-only: use a tiny scratch so the worker never writes */
-            w[i].cap = 0;
-        }
     }
     run_threads(v10_probe_worker, w, nthreads);
     int64_t total = 0;
     for (int i = 0; i < nthreads; ++i) {
+        if (w[i].fail) total = INT64_MIN / 2; /* allocation failure: report a negative count */
         if (cap > 0) {
             const int64_t c = w[i].count < w[i].cap ? w[i].count : w[i].cap;
             for (int64_t k = 0; k < c && total + k < cap; ++k) {
@@ -401,6 +409,74 @@ int64_t ora_v10_probe(void* table, const int64_t* pkeys, const uint8_t* pvalid, 
     }
     free(w);
     return total;
+}
+
+/* One probe pass that emits: the per-thread pair buffers concatenated in chunk order into
+ * malloc'd arrays (*out_b, *out_p; release with ora_free). Returns the pair count, < 0 on
+ * allocation failure. */
+int64_t ora_v10_probe_emit(void* table, const int64_t* pkeys, const uint8_t* pvalid, int64_t n, int nthreads,
+                           uint64_t** out_b, uint32_t** out_p) {
+    if (nthreads < 1) nthreads = 1;
+    V10Table* t = (V10Table*)table;
+    V10Work* w = (V10Work*)calloc((size_t)nthreads, sizeof(V10Work));
+    for (int i = 0; i < nthreads; ++i) {
+        w[i].t = t;
+        w[i].keys = pkeys;
+        w[i].valid = pvalid;
+        w[i].begin = n * i / nthreads;
+        w[i].end = n * (i + 1) / nthreads;
+        w[i].cap = (w[i].end - w[i].begin) + 64;
+        w[i].out_b = (uint64_t*)malloc((size_t)w[i].cap * 8);
+        w[i].out_p = (uint32_t*)malloc((size_t)w[i].cap * 4);
+    }
+    run_threads(v10_probe_worker, w, nthreads);
+    int64_t total = 0;
+    int fail = 0;
+    for (int i = 0; i < nthreads; ++i) {
+        total += w[i].count;
+        fail |= w[i].fail;
+    }
+    uint64_t* ob = fail ? NULL : (uint64_t*)malloc((size_t)(total > 0 ? total : 1) * 8);
+    uint32_t* op = fail ? NULL : (uint32_t*)malloc((size_t)(total > 0 ? total : 1) * 4);
+    int64_t pos = 0;
+    for (int i = 0; i < nthreads; ++i) {
+        if (ob && op) {
+            memcpy(ob + pos, w[i].out_b, (size_t)w[i].count * 8);
+            memcpy(op + pos, w[i].out_p, (size_t)w[i].count * 4);
+        }
+        pos += w[i].count;
+        free(w[i].out_b);
+        free(w[i].out_p);
+    }
+    free(w);
+    if (!ob || !op) {
+        free(ob);
+        free(op);
+        return -1;
+    }
+    *out_b = ob;
+    *out_p = op;
+    return total;
+}
+
+void ora_free(void* p) { free(p); }
+
+/* The lookup_speed bench's timed loop (benches/lookup_speed.rs:240-246): get_iter(&i) for
+ * the raw values i in [start, start + count) used as hashes (IndexLookup<u64> is keyed by
+ * hash, version10/lookup_implementation_3.rs:46-59), each chain walked to the end as
+ * .collect() does. Single thread, as the reference calls the partitions' lookup
+ * functions one after another. Returns the number of rows the chains yielded. */
+int64_t ora_v10_lookup_hashes(void* table, uint64_t start, int64_t count) {
+    const V10Table* t = (const V10Table*)table;
+    int64_t rows = 0;
+    for (int64_t k = 0; k < count; ++k) {
+        uint64_t idx = v10_get(t, start + (uint64_t)k);
+        while (idx != 0) {
+            ++rows;
+            idx = t->overflow[idx];
+        }
+    }
+    return rows;
 }
 
 void ora_v10_free(void* table) {

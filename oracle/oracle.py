@@ -57,6 +57,13 @@ def lib() -> ctypes.CDLL:
         L.ora_v10_build.argtypes = [P, P, I64, ctypes.c_int]
         L.ora_v10_probe.restype = I64
         L.ora_v10_probe.argtypes = [P, P, P, I64, ctypes.c_int, P, P, I64]
+        L.ora_v10_probe_emit.restype = I64
+        L.ora_v10_probe_emit.argtypes = [P, P, P, I64, ctypes.c_int, ctypes.POINTER(ctypes.POINTER(ctypes.c_uint64)),
+                                         ctypes.POINTER(ctypes.POINTER(ctypes.c_uint32))]
+        L.ora_free.restype = None
+        L.ora_free.argtypes = [P]
+        L.ora_v10_lookup_hashes.restype = I64
+        L.ora_v10_lookup_hashes.argtypes = [P, ctypes.c_uint64, I64]
         L.ora_v10_free.restype = None
         L.ora_v10_free.argtypes = [P]
         L.ora_splitmix64.restype = ctypes.c_uint64
@@ -119,15 +126,29 @@ class V10Table:
             raise MemoryError("v10 build failed")
 
     def probe(self, probe_keys, probe_valid=None, nthreads: int = 8, emit: bool = True):
+        """One probe pass; emit=True returns the pairs (uint64 build, uint32 probe),
+        emit=False the pair count only."""
         pk = _keys64(probe_keys)
         pv = _valid_bits(probe_valid)
         if not emit:
             return lib().ora_v10_probe(self._h, _ptr(pk), _ptr(pv), len(pk), nthreads, None, None, 0)
-        n = lib().ora_v10_probe(self._h, _ptr(pk), _ptr(pv), len(pk), nthreads, None, None, 0)
-        ob = np.empty(max(n, 1), dtype=np.uint64)
-        op = np.empty(max(n, 1), dtype=np.uint32)
-        lib().ora_v10_probe(self._h, _ptr(pk), _ptr(pv), len(pk), nthreads, _ptr(ob), _ptr(op), n)
-        return ob[:n], op[:n]
+        pb, pp = ctypes.POINTER(ctypes.c_uint64)(), ctypes.POINTER(ctypes.c_uint32)()
+        n = lib().ora_v10_probe_emit(self._h, _ptr(pk), _ptr(pv), len(pk), nthreads, ctypes.byref(pb),
+                                     ctypes.byref(pp))
+        if n < 0:
+            raise MemoryError("v10 probe: allocation failed")
+        try:
+            ob = np.ctypeslib.as_array(pb, shape=(n,)).copy() if n else np.empty(0, np.uint64)
+            op = np.ctypeslib.as_array(pp, shape=(n,)).copy() if n else np.empty(0, np.uint32)
+        finally:
+            lib().ora_free(ctypes.cast(pb, ctypes.c_void_p))
+            lib().ora_free(ctypes.cast(pp, ctypes.c_void_p))
+        return ob, op
+
+    def lookup_hashes(self, start: int, count: int) -> int:
+        """benches/lookup_speed.rs:240-246: get_iter(&i) for raw i in [start, start+count)
+        used as hashes, chains walked; single thread. Returns the rows yielded."""
+        return lib().ora_v10_lookup_hashes(self._h, start, count)
 
     def close(self):
         if self._h:

@@ -76,7 +76,7 @@ def _canonical(b, p):
     return bool(np.all(pl[1:] >= pl[:-1]) and np.all(bl[1:][same] < bl[:-1][same]))
 
 
-def _worker(rank, world, port, bks, pks, q, chunks=1, max_bytes=None, rfilter=True):
+def _worker(rank, world, port, bks, pks, q, chunks=1, max_bytes=None, rfilter=True, plan="radix"):
     sys.path.insert(0, ROOT)
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -91,7 +91,10 @@ def _worker(rank, world, port, bks, pks, q, chunks=1, max_bytes=None, rfilter=Tr
                              local_build_fn=CpuLocalTable, runtime_filter=rfilter)
     bbase = sum(len(x) for x in bks[:rank])
     pbase = sum(len(x) for x in pks[:rank])
-    if chunks == 1:
+    if plan == "broadcast":  # all_gather of the build shards, no probe exchange
+        b, p = dj.run_broadcast(torch.from_numpy(bks[rank]), torch.from_numpy(pks[rank]), pbase)
+        segs = [(b, p)]
+    elif chunks == 1:
         b, p = dj.run(torch.from_numpy(bks[rank]), bbase, torch.from_numpy(pks[rank]), pbase)
         segs = [(b, p)]
     else:  # pipelined probe side: canonical per chunk
@@ -155,3 +158,40 @@ def test_distributed_exchange_matches_single_join(oracle_mod, world, chunks, wid
     cb, cp = oracle_mod.canonical_pairs(allb, allp)
     ob, op = oracle_mod.inner_join(bk, pk)
     assert np.array_equal(cb, ob) and np.array_equal(cp.astype(np.uint32), op)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_broadcast_plan_is_canonical(oracle_mod, world):
+    """Broadcast-build plan: the ranks' outputs, concatenated in rank
+    order, ARE the single-process canonical output (no sort): the gathered build shards
+    are the global row order and every rank probes a contiguous probe range."""
+    rng = np.random.default_rng(21)
+    bk = rng.integers(0, 2500, 7001).astype(np.int64)
+    pk = rng.integers(-50, 4000, 12003).astype(np.int64)
+    bb = np.linspace(0, len(bk), world + 1).astype(int)
+    pb = np.linspace(0, len(pk), world + 1).astype(int)
+    bks = [bk[bb[r]:bb[r + 1]] for r in range(world)]
+    pks = [pk[pb[r]:pb[r + 1]] for r in range(world)]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, bks, pks, q, 1, None, True, "broadcast"))
+             for r in range(world)]
+    for pr in procs:
+        pr.start()
+    res = q.get(timeout=240)
+    for pr in procs:
+        pr.join(timeout=60)
+        assert pr.exitcode == 0
+    allb = np.concatenate([np.array(r[0], np.int64) for r in res]).astype(np.uint64)
+    allp = np.concatenate([np.array(r[1], np.int64) for r in res]).astype(np.uint32)
+    ob, op = oracle_mod.inner_join(bk, pk)
+    assert np.array_equal(allb, ob) and np.array_equal(allp, op)
+
+
+def test_choose_plan():
+    from datafusion_parallelism_amd.distributed import DistributedHashJoin
+
+    assert DistributedHashJoin.choose_plan(10**7, 10**8, 8) == "broadcast"   # C2: 8e7 < 1.1e8
+    assert DistributedHashJoin.choose_plan(10**8, 10**8, 8) == "radix"
+    assert DistributedHashJoin.choose_plan(10**7, 10**8, 1) == "broadcast"

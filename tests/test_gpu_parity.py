@@ -255,6 +255,24 @@ def test_c2_full_size_properties(dfp, oracle_mod):
     assert np.array_equal(b[sample].cpu().numpy(), want)
 
 
+@pytest.mark.parametrize("layout", [0, 1])
+def test_c1b_full_pairs(dfp, oracle_mod, layout):
+    """C1b (BASELINE.json configs[0] shape): 2^20 unique build keys x 2^20 probe keys over
+    2^21, every pair against the oracle, in both table layouts (auto probe strategy)."""
+    L = dfp.load()
+    old = L.hj_set_build_mode(layout)
+    try:
+        n = 1 << 20
+        bk = oracle_mod.perm_keys(n, 7368787, n)
+        pk = oracle_mod.uniform_keys(n, 0xC0FFEE, 2 * n)
+        b, p, st = gpu_join(dfp, bk, pk)
+        assert (st["buckets"] == 0) == (layout == 0)
+        ob, op = oracle_mod.inner_join(bk, pk)
+        assert_same(b, p, ob, op)
+    finally:
+        L.hj_set_build_mode(old)
+
+
 MIX_MUL_I64 = 0x9E3779B97F4A7C15 - (1 << 64)  # odd: k -> k * M (mod 2^64) is a bijection
 
 

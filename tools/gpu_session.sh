@@ -85,9 +85,11 @@ for s in $STEPS; do
         > $O/$s.json 2> $O/$s.err || { tail -30 $O/$s.err; exit 1; }
       python3 tools/kstats.py $O/$s ;;
     dist)
-      run timeout -k 10 400 python3 bench.py --force-dist --no-cpu-baseline --steps 5 > $O/bench_dist.json \
-        2> $O/bench_dist.err || { tail -30 $O/bench_dist.err; exit 1; }
-      cat $O/bench_dist.json
+      for pl in broadcast radix; do
+        run timeout -k 10 400 python3 bench.py --force-dist --plan $pl --no-cpu-baseline --steps 5 > $O/bench_dist_$pl.json \
+          2> $O/bench_dist_$pl.err || { tail -30 $O/bench_dist_$pl.err; exit 1; }
+        cat $O/bench_dist_$pl.json
+      done
       run timeout -k 10 400 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 \
         --master-port 29533 bench.py --gpus 1 --steps 5 --warmup 2 --no-cpu-baseline > $O/bench_trun.json \
         2> $O/bench_trun.err || { tail -30 $O/bench_trun.err; exit 1; }
