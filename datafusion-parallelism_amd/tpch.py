@@ -334,7 +334,7 @@ def q3_dist(t: Tables, segment: str = "BUILDING", date: str = "1995-03-15", limi
     join (the stand-in hook exists only for the CPU gloo tests)."""
     import torch.distributed as dist
 
-    from .distributed import all_gather_rows, shuffle
+    from .distributed import all_gather_rows, check_ids, shuffle
 
     join = join_fn or _join
     seg = SEGMENTS.index(segment)
@@ -348,6 +348,7 @@ def q3_dist(t: Tables, segment: str = "BUILDING", date: str = "1995-03-15", limi
     rev = t.l_extendedprice[l_rows] * (100 - t.l_discount[l_rows].to(torch.int64))
     lk, (lrev,) = shuffle(t.l_orderkey[l_rows], [rev], group, partition_fn)
     bo, pl = join(ok, lk)
+    check_ids(bo, ok.numel(), "q3_dist order rows")
     sums = torch.zeros(ok.numel(), dtype=torch.int64, device=ok.device).index_add_(0, bo, lrev[pl])
     has = torch.zeros(ok.numel(), dtype=torch.bool, device=ok.device)
     has[bo] = True
@@ -369,7 +370,7 @@ def q9_dist(t: Tables, group=None, join_fn=None, partition_fn=None) -> list[tupl
     orderkey; the (nation, year) sums merge with one int64 all-reduce."""
     import torch.distributed as dist
 
-    from .distributed import all_gather_rows, shuffle
+    from .distributed import all_gather_rows, check_ids, shuffle
 
     if t.l_partkey is None:
         raise ValueError("generate(..., q9=True) tables are needed")
@@ -392,8 +393,7 @@ def q9_dist(t: Tables, group=None, join_fn=None, partition_fn=None) -> list[tupl
     lk2, (nat2, amt2) = shuffle(lok, [nation, amount], group, partition_fn)
     b_o, p_l = join(ok, lk2)
     gid = nat2[p_l] * 8 + (year[b_o] - 1992)
-    if gid.numel() and bool(((gid < 0) | (gid >= 25 * 8)).any()):  # exchanged payload must be intact
-        raise RuntimeError("q9_dist: (nation, year) group id out of range after the exchange")
+    check_ids(gid, 25 * 8, "q9_dist (nation, year) group ids")  # exchanged payload indexes the sums
     sums = torch.zeros(25 * 8, dtype=torch.int64, device=dev).index_add_(0, gid, amt2[p_l])
     cnt = torch.zeros(25 * 8, dtype=torch.int64, device=dev).index_add_(0, gid, torch.ones_like(gid))
     dist.all_reduce(sums, group=group)

@@ -26,16 +26,34 @@ def main():
         torch.cuda.synchronize()
         ok_part = (int(counts[0]) == n, bool(torch.equal(k, keys)),
                    bool(torch.equal(perm, torch.arange(n, device=dev))))
-        out = torch.empty_like(keys)
-        w = dist.all_to_all_single(out, keys, output_split_sizes=[n], input_split_sizes=[n], async_op=True)
-        w.wait()
+        res = []
+        # the same self-copy three ways: async + wait (as _exchange_cols), synchronous, and
+        # synchronous after a full device sync (input surely complete): a mismatch in all
+        # three points at the collective, not at stream ordering or buffer lifetime
+        for mode in ("async_wait", "sync", "sync_after_devsync"):
+            out = torch.full_like(keys, -1)
+            if mode == "sync_after_devsync":
+                torch.cuda.synchronize()
+            w = dist.all_to_all_single(out, keys, output_split_sizes=[n], input_split_sizes=[n],
+                                       async_op=(mode == "async_wait"))
+            if w is not None:
+                w.wait()
+            torch.cuda.synchronize()
+            ok_a2a = bool(torch.equal(out, keys))
+            mism = int((out != keys).sum()) if not ok_a2a else 0
+            first = int(torch.nonzero(out != keys)[0]) if mism else -1
+            untouched = int((out == -1).sum()) if mism else 0
+            res.append(f"{mode}: exact={ok_a2a} mismatches={mism} first_bad={first} untouched={untouched}")
+            del out
+        # and in rounds of <= A2A_MAX_BYTES (the fix in distributed._exchange_cols)
+        from datafusion_parallelism_amd import distributed as D
+
+        (o2,), _ = D._exchange_cols([keys], [[n]])
         torch.cuda.synchronize()
-        ok_a2a = bool(torch.equal(out, keys))
-        mism = int((out != keys).sum()) if not ok_a2a else 0
-        first = int(torch.nonzero(out != keys)[0]) if mism else -1
-        print(f"n={n} bytes={8 * n} partition(count,keys,perm)={ok_part} a2a_exact={ok_a2a} mismatches={mism} "
-              f"first_bad={first}", flush=True)
-        del keys, k, perm, out
+        res.append(f"rounds_of_{D.A2A_MAX_BYTES >> 20}MiB: exact={bool(torch.equal(o2, keys))}")
+        del o2
+        print(f"n={n} bytes={8 * n} partition(count,keys,perm)={ok_part} " + " | ".join(res), flush=True)
+        del keys, k, perm
         torch.cuda.empty_cache()
     dist.destroy_process_group()
 
