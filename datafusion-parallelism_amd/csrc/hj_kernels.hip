@@ -1295,20 +1295,19 @@ probe_fused_kernel(TableView tv, const void* __restrict__ keys, const uint8_t* _
 //                             slice order into the tile's region, each row's key offset
 //                             in its slice (u16) and row in the tile (u16), and the tile's
 //                             slice bounds (u16, tile-major)
-//   S1b sl_toff_transpose     the bounds regrouped per 64-tile block (coalesced in S2)
 //   S2  sl_lookup_kernel      per (slice, tile range), XCD-contiguous item order: the
 //                             slice's refs in LDS, then every tile's fragment of that
 //                             slice; each entry's ref goes to the refs array (u32) at the
 //                             entry's position. The probe waits for a build on another
 //                             stream only here (S1/S1b read no table memory).
-//   S3a sl_scan_kernel        (one workgroup): tile output offsets from the tiles' pair
-//                             counts. S1 writes a tile's entries as its count; S2 adds
+//   (counts)                  S1 writes a tile's entries as its pair count; S2 adds
 //                             count - 1 for every entry whose key is missing or
 //                             duplicated (LDS atomics per owner tile, then one atomic per
 //                             tile and run), so no pass re-reads the refs to count them.
-//                             (A decoupled look-back inside S3b measured slower: 350 vs
-//                             212 us at C2, a tile's offset then waits for the slowest
-//                             workgroup holding an earlier tile.)
+//                             S3 sums the counts below its tiles itself (no scan launch;
+//                             a decoupled look-back inside S3 measured slower: 350 vs 212
+//                             us at C2, a tile's offset then waits for the slowest
+//                             workgroup holding an earlier tile).
 //   S3b sl_emit_kernel        per tile (persistent, prefetching): its (row, ref) pairs
 //                             scattered into an LDS image of the tile's refs, then ordered
 //                             emission, 64 rows per wave step, one contiguous store run
@@ -1406,7 +1405,7 @@ sl_partition_kernel(int64_t dmin, uint64_t drange, uint32_t wlog, uint32_t nslic
     }
 }
 
-// S1b: the tiles' segment bounds transposed into blocks of 64 tiles, toffT[b][slice][64],
+// Build (S1b): the tiles' segment bounds transposed into blocks of 64 tiles, toffT[b][slice][64],
 // so that a lookup wave reads the bounds of its 64 tiles with one coalesced 128-byte load
 // (tile-major, every lane's bound is its own memory request). Tiles past ntiles read as
 // empty.
@@ -1722,17 +1721,17 @@ sl_lookup_kernel(TableView tv, uint32_t wlog, uint32_t nslices, int64_t ntiles, 
     unsigned long long* smask = s_mask[wave];
     constexpr int64_t kStep = (kSlThreads / 64) * 64;  // tiles between a wave's blocks
     constexpr uint32_t kOob = 0x3FFFFF0u;               // entry index past every range: load 0, no store
-    constexpr uint32_t kOobMask = (1u << 26) - 1;       // off[] = index | owner lane << 26
+    constexpr uint32_t kOobMask = (1u << 26) - 1;       // off[] = index | owner rank << 26
     constexpr int KB = HASHED ? 8 : 2;                  // entry bytes
     const uint32_t cmask = (1u << tv.clog2) - 1;
-    // segment bounds of the lane's tile in block tc (toffT), loaded one block ahead
+    // segment bounds of the lane's tile in block tc (tile-major toff), loaded one block ahead
     auto bounds = [&](int64_t tc, uint32_t* st, uint32_t* len) {
         *st = 0;
         *len = 0;
-        if (tc + lane < tb) {
-            const uint16_t* to = toff + ((tc >> 6) * nbins + s) * 64 + lane;
+        if (tc + lane < tb) {  // tile-major bounds: consecutive slices (one XCD's items) share lines in its L2
+            const uint16_t* to = toff + (tc + lane) * nbins + s;
             *st = to[0];
-            *len = (uint32_t)to[64] - *st;
+            *len = (uint32_t)to[1] - *st;
         }
     };
     uint32_t nst, nlen;
@@ -1773,14 +1772,14 @@ sl_lookup_kernel(TableView tv, uint32_t wlog, uint32_t nslices, int64_t ntiles, 
             if (len != 0 && excl >= w0 && excl < w0 + W) atomicOr(&smask[(excl - w0) >> 6], 1ull << ((excl - w0) & 63));
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
             __builtin_amdgcn_wave_barrier();
-            uint32_t off[W / 64];  // the entry's index (or kOob) | owner tile lane << 26
+            uint32_t off[W / 64];  // the entry's index (or kOob) | owner rank << 26
             uint32_t off_end = 0;  // hashed: bit u = this lane's position u ends its fragment
             using EV = typename std::conditional<HASHED, unsigned long long, uint32_t>::type;
             EV ev[W / 64];
 #pragma unroll
             for (int u = 0; u < W / 64; ++u) {
                 off[u] = kOob;
-                if (HASHED && w0 + u * 64 >= R) continue;  // uniform: past the run (small fragments)
+                if (w0 + u * 64 >= R) continue;  // uniform: past the run
                 const uint32_t r = w0 + u * 64 + lane;
                 const unsigned long long m = smask[u];  // the same word for every lane
                 const uint32_t mlo = __builtin_amdgcn_readfirstlane((uint32_t)m);
@@ -1804,11 +1803,11 @@ sl_lookup_kernel(TableView tv, uint32_t wlog, uint32_t nslices, int64_t ntiles, 
                 } else {
                     ev[u] = __builtin_amdgcn_raw_buffer_load_b16(rko, (int)(o * 2), 0, 0);
                 }
-                off[u] = o | ((HASHED ? (k & 63) : slane[k & 63]) << 26);  // hashed: the owner's rank
+                off[u] = o | ((k & 63) << 26);  // the owner's rank (its tile lane: slane, read only for a correction)
             }
 #pragma unroll
             for (int u = 0; u < W / 64; ++u) {
-                if (HASHED && w0 + u * 64 >= R) continue;  // uniform: past the run
+                if (w0 + u * 64 >= R) continue;  // uniform: past the run
                 const uint32_t o = off[u] & kOobMask;
                 uint32_t v, c;  // ref and its row count
                 if constexpr (HASHED) {
@@ -1844,7 +1843,7 @@ sl_lookup_kernel(TableView tv, uint32_t wlog, uint32_t nslices, int64_t ntiles, 
                     run_sum = __builtin_amdgcn_readlane(incl, 63);
                     if (off_end & (1u << u)) scorr[off[u] >> 26] = incl;
                 } else if (__ballot(odd) != 0 && odd) {
-                    atomicAdd(&scorr[off[u] >> 26], (int)c - 1);
+                    atomicAdd(&scorr[slane[off[u] >> 26]], (int)c - 1);
                 }
             }
         }
@@ -1966,25 +1965,6 @@ __device__ __forceinline__ uint32_t sl_count(const TableView& tv, uint32_t r) {
     return r == kMiss ? 0u : !(r & kDupFlag) ? 1u : c4 ? c4 : tv.dup_rows[r & tv.off_mask];
 }
 
-// exclusive scan in place of up to kSlScanOne tile counts by one workgroup (thread j
-// takes a contiguous run), and the total: one launch instead of the three-kernel scan
-constexpr int64_t kSlScanOne = 1 << 16;
-__global__ void __launch_bounds__(1024)
-sl_scan_kernel(unsigned long long* __restrict__ tcnt, int64_t ntiles, unsigned long long* __restrict__ total) {
-    __shared__ unsigned long long s_w[16];
-    const int64_t c = (ntiles + 1023) / 1024;
-    const int64_t a = min<int64_t>((int64_t)threadIdx.x * c, ntiles), b = min<int64_t>(a + c, ntiles);
-    unsigned long long run = 0, tot;
-    for (int64_t i = a; i < b; ++i) run += tcnt[i];
-    unsigned long long ex = block_excl_scan<unsigned long long>(run, s_w, &tot);
-    for (int64_t i = a; i < b; ++i) {
-        const unsigned long long v = tcnt[i];
-        tcnt[i] = ex;
-        ex += v;
-    }
-    if (threadIdx.x == 0) *total = tot;
-}
-
 // S3b: 512 threads per tile, two workgroups per CU (64 KB of LDS and <= 128 VGPRs each).
 // Wave w owns the tile's rows [w * 2048, (w + 1) * 2048) and walks them 64 at a time,
 // lane l on row +l: pass 1 counts the wave's pairs, pass 2 writes them. Within a wave
@@ -1997,23 +1977,30 @@ template <bool HAS_ROW_IDS, bool HAS_PROBE_IDS>
 __global__ void __launch_bounds__(kSlEmitThreads, 4)  // two workgroups per CU: <= 128 VGPRs
 sl_emit_kernel(TableView tv, uint32_t nslices, const uint16_t* __restrict__ rl, const uint32_t* __restrict__ res,
                const uint16_t* __restrict__ toff, const uint32_t* __restrict__ probe_ids,
-               const unsigned long long* __restrict__ tofs, int64_t ntiles, uint64_t* __restrict__ out_b,
-               uint32_t* __restrict__ out_p, int64_t cap, int dbg) {
+               const unsigned long long* __restrict__ tcnt, int64_t ntiles, uint64_t* __restrict__ out_b,
+               uint32_t* __restrict__ out_p, int64_t cap, int64_t* __restrict__ d_total, int dbg) {
     __shared__ __attribute__((aligned(16))) uint32_t s_ref[kSlTile];  // the tile's refs, kMiss = none
     __shared__ unsigned long long s_w[kSlEmitThreads / 64];
+    __shared__ unsigned long long s_pre[kSlEmitThreads / 64];
     __shared__ uint32_t s_own[kSlEmitThreads / 64][64];  // per wave: owner markers of one output window
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     constexpr int U = kSlTile / (kSlEmitThreads * 4);  // 8 x (4 rows + 4 refs) per thread
     uint2 e4[U];
     uint4 r4[U];
     uint32_t cnt = 0;
-    unsigned long long tbase = 0;
     // Persistent: workgroup b takes tiles b, b + grid, ...; the next tile's entries are
     // loaded while this tile's pairs are counted and written. All loads of a tile are
-    // issued at once, after its entry count.
+    // issued at once, after its entry count. A tile's output offset is the sum of the
+    // pair counts (tcnt, final once S2 is done) of the tiles below it: the first tile's
+    // from scratch, each next one's as this one's plus the grid's counts in between (one
+    // load per thread), so no scan launch runs between S2 and S3.
+    auto count_sum = [&](int64_t lo, int64_t hi) -> unsigned long long {  // this thread's share
+        unsigned long long v = 0;
+        for (int64_t j = lo + threadIdx.x; j < hi; j += kSlEmitThreads) v += tcnt[j];
+        return v;
+    };
     auto fetch = [&](int64_t t) {
         cnt = (dbg & 2) ? 0u : toff[t * (int64_t)(nslices + 1) + nslices];
-        tbase = tofs[t];
         const uint16_t* te = rl + t * kSlTile;
         const uint32_t* tr = res + t * kSlTile;
 #pragma unroll
@@ -2027,6 +2014,14 @@ sl_emit_kernel(TableView tv, uint32_t nslices, const uint16_t* __restrict__ rl, 
     };
     int64_t tile = blockIdx.x;
     if (tile < ntiles) fetch(tile);
+    unsigned long long base = 0;  // the current tile's output offset
+    {
+        const unsigned long long v = wave_sum<unsigned long long>(count_sum(0, min<int64_t>(tile, ntiles)));
+        if (lane == 0) s_pre[wave] = v;
+        __syncthreads();
+        for (int w = 0; w < kSlEmitThreads / 64; ++w) base += s_pre[w];
+        __syncthreads();
+    }
     for (; tile < ntiles; tile += gridDim.x) {
         const int64_t tile0 = tile * kSlTile;
         for (int i = threadIdx.x * 4; i < kSlTile; i += kSlEmitThreads * 4)
@@ -2040,9 +2035,9 @@ sl_emit_kernel(TableView tv, uint32_t nslices, const uint16_t* __restrict__ rl, 
             if (i + 2 < cnt) s_ref[e4[u].y & 0xFFFF] = r4[u].z;
             if (i + 3 < cnt) s_ref[e4[u].y >> 16] = r4[u].w;
         }
-        const unsigned long long base = tbase;
         __syncthreads();
-        if (tile + (int64_t)gridDim.x < ntiles) fetch(tile + gridDim.x);
+        const int64_t next = tile + gridDim.x;
+        if (next < ntiles) fetch(next);
         // pass 1: this wave's pair count
         const int row_w = wave * kSlWaveRows;
         uint32_t lsum = 0;  // < 32 rows x < 2^26 rows each
@@ -2053,8 +2048,12 @@ sl_emit_kernel(TableView tv, uint32_t nslices, const uint16_t* __restrict__ rl, 
                                         ((unsigned long long)wave_sum_dpp(lsum >> 16) << 16);
         if (lane == 0) s_w[wave] = wsum;
         __syncthreads();
-        unsigned long long pos = base;
-        for (int w = 0; w < wave; ++w) pos += s_w[w];
+        unsigned long long pos = base, tile_total = 0;
+        for (int w = 0; w < kSlEmitThreads / 64; ++w) {
+            if (w < wave) pos += s_w[w];
+            tile_total += s_w[w];
+        }
+        if (tile == ntiles - 1 && threadIdx.x == 0) *d_total = (int64_t)(base + tile_total);
         if (!(dbg & 1)) {
             // pass 2: write the wave's pairs, 64 rows per step. Steps whose rows all have
             // at most one pair store them directly; a step with a duplicated key expands
@@ -2111,7 +2110,12 @@ sl_emit_kernel(TableView tv, uint32_t nslices, const uint16_t* __restrict__ rl, 
                 pos += total;
             }
         }
-        __syncthreads();  // s_ref and s_w are rewritten for the next tile
+        // the next tile's offset: this one's plus the counts of the tiles in between (loaded
+        // only now: a wait on them would also wait for the next tile's entries in flight)
+        const unsigned long long pre = wave_sum<unsigned long long>(next < ntiles ? count_sum(tile, next) : 0ull);
+        if (lane == 0) s_pre[wave] = pre;
+        __syncthreads();  // s_ref, s_w and s_pre are rewritten for the next tile
+        for (int w = 0; w < kSlEmitThreads / 64; ++w) base += s_pre[w];
     }
 }
 
@@ -2656,14 +2660,12 @@ ProbeWs probe_ws_layout(void* base, int64_t n) {
 }
 
 // sliced probe workspace (16384-row tiles), after the 16-byte header (error word at
-// bytes 8..15): tcnt u64[nt + 2] (counts, then offsets) | bsum | toff u16[nt][kSlMaxSlices + 1] | toffT |
+// bytes 8..15): tcnt u64[nt + 2] (pair counts) | toff u16[nt][kSlMaxSlices + 1] | toffT |
 // ko (entries: u16 key offsets in a dense slice, u64 stored keys in a hashed one; 8 B per
 // row reserved) | rl u16[nt * kSlTile] (rows in tile) | res u32[nt * kSlTile] (refs)
 struct SlicedWs {
     unsigned long long* tcnt;
-    unsigned long long* bsum;  // scan scratch past kSlScanOne tiles
     uint16_t* toff;
-    uint16_t* toffT;
     void* ko;
     uint16_t* rl;
     uint32_t* res;
@@ -2674,9 +2676,7 @@ SlicedWs sliced_ws_layout(void* base, int64_t n) {
     SlicedWs w;
     uintptr_t p = (uintptr_t)base + 256;
     w.tcnt = (unsigned long long*)p;  p = al256(p + 8 * (nt + 2));
-    w.bsum = (unsigned long long*)p;  p = al256(p + scan_scratch_bytes(nt));
     w.toff = (uint16_t*)p;            p = al256(p + 2 * nt * (kSlMaxSlices + 1));
-    w.toffT = (uint16_t*)p;           p = al256(p + 2 * ((nt + 63) & ~(int64_t)63) * (kSlMaxSlices + 1));
     w.ko = (void*)p;                  p = al256(p + 8 * nt * kSlTile);
     w.rl = (uint16_t*)p;              p = al256(p + 2 * nt * kSlTile);
     w.res = (uint32_t*)p;             p = al256(p + 4 * nt * kSlTile);
@@ -2821,29 +2821,21 @@ hipError_t launch_probe_sliced(int key_bytes, const TableView& tv, const void* k
                             : (const void*)sl_lookup_kernel<false, kSlOwnWin>;
     e = hipFuncSetAttribute(lk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)tab_lds);
     if (e != hipSuccess) return e;
-    sl_toff_transpose_kernel<<<(unsigned)((nt + 63) / 64 * ((nsl + kSlTrChunk) / kSlTrChunk)), 256, 0, s>>>(
-        w.toff, nsl + 1, nt, w.toffT);
-    if (built != nullptr) {  // S1/S1b read no table memory: the build may still be running
+    if (built != nullptr) {  // S1 reads no table memory: the build may still be running
         e = hipStreamWaitEvent(s, built, 0);
         if (e != hipSuccess) return e;
     }
     if (hashed)
         sl_lookup_kernel<true, kSlOwnWinHashed><<<nsl * parts, kSlThreads, tab_lds, s>>>(tv, wlog, nsl, nt, parts, w.ko,
-                                                                                       w.res, w.toffT, w.tcnt, sl_dbg);
+                                                                                       w.res, w.toff, w.tcnt, sl_dbg);
     else
         sl_lookup_kernel<false, kSlOwnWin><<<nsl * parts, kSlThreads, tab_lds, s>>>(tv, wlog, nsl, nt, parts, w.ko,
-                                                                                  w.res, w.toffT, w.tcnt, sl_dbg);
-    if (nt <= kSlScanOne) {
-        sl_scan_kernel<<<1, 1024, 0, s>>>(w.tcnt, nt, (unsigned long long*)d_total);
-    } else {
-        e = launch_scan<unsigned long long>(w.tcnt, nt, w.bsum, (unsigned long long*)d_total, s);
-        if (e != hipSuccess) return e;
-    }
+                                                                                  w.res, w.toff, w.tcnt, sl_dbg);
     const bool ri = tv.row_ids != nullptr, pi = probe_ids != nullptr;
     const unsigned egrid = (unsigned)std::min<int64_t>(nt, (int64_t)sl_emit_wgs_per_cu() * sl_num_cus());
 #define DFP_SLE(RI, PI)                                                                                           \
     sl_emit_kernel<RI, PI><<<egrid, kSlEmitThreads, 0, s>>>(tv, nsl, w.rl, w.res, w.toff, probe_ids, w.tcnt, nt, \
-                                                           out_b, out_p, cap, sl_dbg)
+                                                           out_b, out_p, cap, d_total, sl_dbg)
     if (ri && pi) DFP_SLE(true, true);
     else if (ri) DFP_SLE(true, false);
     else if (pi) DFP_SLE(false, true);
