@@ -24,10 +24,12 @@ for s in $STEPS; do
         -- python3 bench.py > $O/prof_bench.json 2> $O/prof_bench.err || { tail -30 $O/prof_bench.err; exit 1; }
       cat $O/prof_bench.json ;;
     pmc)
+      # HBM traffic counters of the bench config $CFG (default c2), one counter per pass
+      CFG=${CFG:-c2}
       for c in FETCH_SIZE WRITE_SIZE; do
-        run timeout -k 10 400 rocprofv3 --pmc $c -d $O/pmc_$c -o pmc --output-format csv \
-          -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline > $O/pmc_$c.json 2> $O/pmc_$c.err \
-          || { tail -30 $O/pmc_$c.err; exit 1; }
+        run timeout -k 10 400 rocprofv3 --pmc $c -d $O/$CFG/pmc_$c -o pmc --output-format csv \
+          -- python3 bench.py --config $CFG --steps 3 --warmup 1 --no-cpu-baseline > $O/pmc_${CFG}_$c.json \
+          2> $O/pmc_${CFG}_$c.err || { tail -30 $O/pmc_${CFG}_$c.err; exit 1; }
       done ;;
     cal)
       run timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE -d $O/cal -o cal --output-format csv \
@@ -76,6 +78,13 @@ for s in $STEPS; do
           --output-format csv -- python3 tools/probe_one.py 1e7 1e8 --mix > $O/lf$lf.log 2>&1 || { tail -30 $O/lf$lf.log; exit 1; }
         echo "lf $lf: $(tail -1 $O/lf$lf.log)"
         python3 tools/kstats.py $O/lf$lf | grep -E "lookup|partition|emit|chunk_build|transpose"
+      done ;;
+    emitwgs)
+      # persistent emission grid (workgroups per CU) vs one workgroup per tile (1000)
+      for v in 2 1000; do
+        DFP_HJ_SL_EMIT_WGS=$v run timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/ew$v -o kp --output-format csv \
+          -- python3 tools/probe_one.py > $O/ew$v.log 2>&1 || { tail -30 $O/ew$v.log; exit 1; }
+        echo "emit wgs $v"; python3 tools/kstats.py $O/ew$v | grep -E "sl_"
       done ;;
     kpc2h|kpc3)
       # per-kernel times of the bench config (serialized steps), kernel trace

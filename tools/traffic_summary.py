@@ -21,7 +21,7 @@ import sys
 
 PROBE_KERNELS = ("probe_fused_kernel", "probe_lookup_kernel", "probe_emit_kernel", "scan_reduce_kernel<unsigned long long>",
                  "scan_down_kernel<unsigned long long>", "pp_partition_kernel", "pp_lookup_kernel",
-                 "pp_count_kernel", "sl_partition_kernel", "sl_toff_transpose_kernel", "sl_lookup_kernel",
+                 "pp_count_kernel", "sl_partition_kernel", "hs_partition_kernel", "sl_toff_transpose_kernel", "sl_lookup_kernel",
                  "sl_count_kernel", "sl_emit_kernel")
 BUILD_KERNELS = ("key_minmax_kernel", "minmax_final_kernel", "coarse_hist_kernel", "coarse_scatter", "fine_hist_kernel",
                  "fine_scatter", "chunk_starts_kernel", "scan_reduce_kernel<unsigned int>",
