@@ -1675,6 +1675,8 @@ __device__ __forceinline__ uint32_t lds_bucket_ref(const uint4* __restrict__ img
     return ref;
 }
 
+constexpr uint32_t kBigCorr = 1u << 16;  // counts - 1 from here on correct the tile count directly
+
 template <bool HASHED, int W>
 __global__ void __launch_bounds__(kSlThreads)
 sl_lookup_kernel(TableView tv, uint32_t wlog, uint32_t nslices, int64_t ntiles, uint32_t parts,
@@ -1683,7 +1685,9 @@ sl_lookup_kernel(TableView tv, uint32_t wlog, uint32_t nslices, int64_t ntiles, 
     extern __shared__ __attribute__((aligned(16))) uint32_t s_tab[];  // dense: 2^wlog refs; hashed: 2048 buckets
     __shared__ uint32_t s_base[kSlThreads];
     __shared__ uint32_t s_lane[kSlThreads];  // per wave: tile lane of each non-empty segment, by rank
-    __shared__ int s_corr[kSlThreads];       // per wave: pair-count correction of each of its 64 tiles
+    // per wave, by rank: dense, the correction running sum at each fragment's start;
+    // hashed, at each fragment's end
+    __shared__ uint32_t s_cst[kSlThreads];
     __shared__ uint32_t s_end[HASHED ? kSlThreads : 1];  // hashed, per wave: end position of each fragment, by rank
     __shared__ unsigned long long s_mask[kSlThreads / 64][W / 64];
     const uint32_t item = (dbg & 128) ? blockIdx.x : xcd_item(blockIdx.x, gridDim.x);
@@ -1715,8 +1719,7 @@ sl_lookup_kernel(TableView tv, uint32_t wlog, uint32_t nslices, int64_t ntiles, 
     // one 64-bit start mask per 64-position row of the window
     uint32_t* sbs = s_base + wave * 64;
     uint32_t* slane = s_lane + wave * 64;
-    int* scorr = s_corr + wave * 64;
-    scorr[lane] = 0;
+    uint32_t* scst = s_cst + wave * 64;
     uint32_t* send = s_end + (HASHED ? wave * 64 : 0);
     unsigned long long* smask = s_mask[wave];
     constexpr int64_t kStep = (kSlThreads / 64) * 64;  // tiles between a wave's blocks
@@ -1746,16 +1749,22 @@ sl_lookup_kernel(TableView tv, uint32_t wlog, uint32_t nslices, int64_t ntiles, 
         const unsigned long long ne = __ballot(len != 0);
         const uint32_t rank =
             __builtin_amdgcn_mbcnt_hi((uint32_t)(ne >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)ne, 0u));
+        const uint32_t nranks = (uint32_t)__builtin_popcountll(ne);
         if (len != 0) {
             sbs[rank] = (uint32_t)lane * kSlTile + st - excl;  // >= 0: excl <= lane * kSlTile
             slane[rank] = (uint32_t)lane;
             if constexpr (HASHED) send[rank] = excl + len;
         }
-        // hashed: the run's corrections as a running sum over the flattened positions; the
-        // last position of each fragment records it (scorr[rank]), so a fragment's
-        // correction is the difference of its end and its predecessor's end (a segmented
-        // sum without LDS atomics: half the entries of a uniform probe side miss)
-        int run_sum = 0;
+        // the run's corrections (count - 1 of a missing or duplicated key) as a running sum
+        // over the flattened positions, recorded at each fragment's first position: a
+        // fragment's correction is its successor's record minus its own (the last one's:
+        // the final sum). A segmented sum without LDS atomics, and a row of unique hits
+        // costs one ballot. Sums are mod 2^32: a fragment's true correction lies in
+        // (-2^14, 2^30) since counts of kBigCorr or more go to the tile count directly.
+        // Hashed (half the entries of a uniform probe side miss): the running sum of every
+        // row, recorded at each fragment's last position instead.
+        scst[lane] = 0;
+        uint32_t corr_run = 0;
         // the 64 tiles' regions as buffers (wave-uniform bases): 32-bit offsets, and an
         // out-of-range offset turns a position past R into a dropped access
         const int64_t tcu = (int64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)tc) |
@@ -1835,34 +1844,45 @@ sl_lookup_kernel(TableView tv, uint32_t wlog, uint32_t nslices, int64_t ntiles, 
                     }
                 }
                 __builtin_amdgcn_raw_buffer_store_b32(v, rres, (int)(o * 4), 0, 0);
-                // pair-count correction (count - 1) of a missing or duplicated key, per
-                // owner tile; none in a window of unique hits (C2: no LDS atomics at all)
-                const bool odd = c != 1;
                 if constexpr (HASHED) {
-                    const int incl = (int)wave_incl_scan_dpp((uint32_t)((int)c - 1)) + run_sum;
-                    run_sum = __builtin_amdgcn_readlane(incl, 63);
-                    if (off_end & (1u << u)) scorr[off[u] >> 26] = incl;
-                } else if (__ballot(odd) != 0 && odd) {
-                    atomicAdd(&scorr[slane[off[u] >> 26]], (int)c - 1);
+                    uint32_t d = c - 1u;  // kOob: c = 1
+                    if (d != 0xFFFFFFFFu && d >= kBigCorr) {
+                        atomicAdd(&tcnt[tc + slane[off[u] >> 26]], (unsigned long long)d);
+                        d = 0;
+                    }
+                    corr_run += wave_incl_scan_dpp(d);
+                    if (off_end & (1u << u)) scst[off[u] >> 26] = corr_run;
+                    corr_run = (uint32_t)__builtin_amdgcn_readlane((int)corr_run, 63);
+                    continue;
+                }
+                // a fragment start (start mask bit) records the running sum before it
+                const bool odd = o != kOob && c != 1;
+                if (__ballot(odd) != 0) {
+                    uint32_t d = odd ? c - 1u : 0u;
+                    if (d != 0xFFFFFFFFu && d >= kBigCorr) {  // a huge duplicate: straight to its tile
+                        atomicAdd(&tcnt[tc + slane[off[u] >> 26]], (unsigned long long)d);
+                        d = 0;
+                    }
+                    const uint32_t ci = wave_incl_scan_dpp(d) + corr_run;
+                    if ((smask[u] >> lane) & 1ull) scst[off[u] >> 26] = ci - d;
+                    corr_run = (uint32_t)__builtin_amdgcn_readlane((int)ci, 63);
+                } else if (corr_run != 0) {  // uniform
+                    if ((smask[u] >> lane) & 1ull) scst[off[u] >> 26] = corr_run;
                 }
             }
         }
-        if constexpr (HASHED) {  // fragment ends -> per-tile corrections (rank order = lane order)
-            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            int cr = 0;
-            if (len != 0) cr = scorr[rank] - (rank > 0 ? scorr[rank - 1] : 0);
-            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            scorr[lane] = cr;  // by tile lane, as the dense path leaves it
-        }
-        // the run's corrections: one atomic per tile that has one (64 contiguous counters)
+        // one atomic per tile that has a correction (64 contiguous counters)
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         __builtin_amdgcn_wave_barrier();
-        const int cr = scorr[lane];
-        if (cr != 0) {
-            atomicAdd(&tcnt[tc + lane], (unsigned long long)(long long)cr);
-            scorr[lane] = 0;
+        if (len != 0) {
+            int cr;
+            if constexpr (HASHED) {  // end records: a fragment's minus its predecessor's
+                cr = (int)(scst[rank] - (rank > 0 ? scst[rank - 1] : 0u));
+            } else {  // start records: the successor's minus its own
+                const uint32_t nxt = rank + 1 < nranks ? scst[rank + 1] : corr_run;
+                cr = (int)(nxt - scst[rank]);
+            }
+            if (cr != 0) atomicAdd(&tcnt[tc + lane], (unsigned long long)(long long)cr);
         }
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         __builtin_amdgcn_wave_barrier();
@@ -2099,7 +2119,9 @@ sl_emit_kernel(TableView tv, uint32_t nslices, const uint16_t* __restrict__ rl, 
                         const uint32_t p = w0 + lane;
                         const unsigned long long o = pos + p;
                         if (p < total && o < (unsigned long long)cap) {
-                            const uint32_t br = (rj & kDupFlag) ? tv.dup_rows[(rj & tv.off_mask) + 1 + (p - xj)] : rj;
+                            const uint32_t br = !(rj & kDupFlag) ? rj
+                                                : (dbg & 8) ? (rj & tv.off_mask) + (p - xj)  // ablation: no segment reads
+                                                            : tv.dup_rows[(rj & tv.off_mask) + 1 + (p - xj)];
                             const int64_t rowj = tile0 + row_w + k + j;
                             out_b[o] = HAS_ROW_IDS ? tv.row_ids[br] : (uint64_t)br;
                             out_p[o] = HAS_PROBE_IDS ? probe_ids[rowj] : (uint32_t)rowj;
@@ -2810,8 +2832,8 @@ hipError_t launch_probe_sliced(int key_bytes, const TableView& tv, const void* k
     }();
     uint32_t parts = std::max<uint32_t>(1, (target + nsl - 1) / nsl);
     parts = (uint32_t)std::min<int64_t>(parts, (nt + 63) / 64);
-    // timing ablations only (wrong pairs): emit 1 no stores, 2 no entries; lookup 4 no
-    // bucket lookup (hashed), 128 plain item order
+    // timing ablations only (wrong pairs): emit 1 no stores, 2 no entries, 8 no duplicate
+    // segment reads; lookup 4 no bucket lookup (hashed), 128 plain item order
     static const int sl_dbg = [] {
         const char* ev = getenv("DFP_HJ_SL_DBG");
         return ev ? atoi(ev) : 0;

@@ -116,6 +116,20 @@ for s in $STEPS; do
         -- python3 tools/probe_one.py ${KP_ARGS} > $O/kp${KP_TAG}.log 2>&1 || { tail -30 $O/kp${KP_TAG}.log; exit 1; }
       tail -1 $O/kp${KP_TAG}.log
       python3 tools/kstats.py $O/kp${KP_TAG} ;;
+    abl)
+      # ablations of one config's probe ($ABL_ARGS for probe_one.py): DFP_HJ_SL_DBG values
+      for d in ${ABL_DBG:-0 1 8}; do
+        DFP_HJ_SL_DBG=$d run timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/abl$d -o kp --output-format csv \
+          -- python3 tools/probe_one.py ${ABL_ARGS} > $O/abl$d.log 2>&1 || { tail -30 $O/abl$d.log; exit 1; }
+        echo "DFP_HJ_SL_DBG=$d"; python3 tools/kstats.py $O/abl$d | grep -E "sl_|hs_"
+      done ;;
+    chunk)
+      # the sliced probe in K chunks (tools/chunk_probe.py), auto strategy and forced sliced
+      run timeout -k 10 200 python3 tools/chunk_probe.py > $O/chunk.log 2>&1 || { tail -30 $O/chunk.log; exit 1; }
+      cat $O/chunk.log
+      DFP_HJ_PROBE_MODE=sliced run timeout -k 10 200 python3 tools/chunk_probe.py > $O/chunk_sl.log 2>&1 \
+        || { tail -30 $O/chunk_sl.log; exit 1; }
+      cat $O/chunk_sl.log ;;
     smoke)
       run timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 \
         || { tail -30 $O/smoke.log; exit 1; }
