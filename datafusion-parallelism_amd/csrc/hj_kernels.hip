@@ -1979,10 +1979,20 @@ hs_partition_kernel(uint32_t nb, uint32_t nslices, const void* __restrict__ keys
     }
 }
 
-// row count behind a ref; packed dense refs carry counts <= 15 in bits 27-30
+// row count behind a ref; packed dense refs carry counts <= 15 in bits 27-30. Other
+// duplicated keys read the count from their segment header, in a wave-uniform branch
+// that also waits for it there: merged into the common path, that load's wait would be
+// an s_waitcnt vmcnt(0) on every step for every ref (loads and stores share vmcnt) —
+// waiting for the next tile's prefetch in the emission's count pass and for the
+// previous step's stores in its write pass (C2 emit 222 -> ? us).
 __device__ __forceinline__ uint32_t sl_count(const TableView& tv, uint32_t r) {
     const uint32_t c4 = tv.off_mask == kPackedMask ? ((r >> 27) & 15u) : 0u;
-    return r == kMiss ? 0u : !(r & kDupFlag) ? 1u : c4 ? c4 : tv.dup_rows[r & tv.off_mask];
+    uint32_t c = r == kMiss ? 0u : !(r & kDupFlag) ? 1u : c4 ? c4 : kCountUnknown;
+    if (__ballot(c == kCountUnknown) != 0) {
+        if (c == kCountUnknown) c = tv.dup_rows[r & tv.off_mask];
+        asm volatile("" : "+v"(c));  // the wait stays in this branch
+    }
+    return c;
 }
 
 // S3b: 512 threads per tile, two workgroups per CU (64 KB of LDS and <= 128 VGPRs each).
