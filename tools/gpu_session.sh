@@ -123,6 +123,12 @@ for s in $STEPS; do
           -- python3 tools/probe_one.py ${ABL_ARGS} > $O/abl$d.log 2>&1 || { tail -30 $O/abl$d.log; exit 1; }
         echo "DFP_HJ_SL_DBG=$d"; python3 tools/kstats.py $O/abl$d | grep -E "sl_|hs_"
       done ;;
+    sqpmc)
+      # SQ counters of one build + 5 probes (tools/probe_one.py $KP_ARGS): where the waves wait
+      run timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY \
+        SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_INSTS_VALU -d $O/sq${KP_TAG} -o sq --output-format csv \
+        -- python3 tools/probe_one.py ${KP_ARGS} > $O/sq${KP_TAG}.log 2>&1 || { tail -30 $O/sq${KP_TAG}.log; exit 1; }
+      python3 tools/sq_summary.py $O/sq${KP_TAG} ;;
     chunk)
       # the sliced probe in K chunks (tools/chunk_probe.py), auto strategy and forced sliced
       run timeout -k 10 200 python3 tools/chunk_probe.py > $O/chunk.log 2>&1 || { tail -30 $O/chunk.log; exit 1; }
