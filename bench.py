@@ -218,6 +218,26 @@ def _join_cpu(oracle, bk, pk, nthreads):
             "value": round(len(pk) / (t2 - t0) / 1e6, 3), "pairs": int(len(b))}
 
 
+def _cpu_quota():
+    """CPUs granted by the cgroup CPU quota (v2 cpu.max or v1 cfs quota), None if unlimited."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        if q != "max":
+            return max(1, -(-int(q) // int(per)))
+        return None
+    except (OSError, ValueError):
+        pass
+    try:
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+            q = int(f.read())
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+            per = int(f.read())
+        return max(1, -(-q // per)) if q > 0 else None
+    except (OSError, ValueError):
+        return None
+
+
 def cpu_baseline(cfg):
     """The reference's CPU join, restated in C (oracle/hj_oracle.c, reference Version 10:
     concurrent open-addressing insert + chain walk + key re-check), timed on this host's
@@ -244,10 +264,16 @@ def cpu_baseline(cfg):
         bk = (bk.astype(np.uint64) * np.uint64(MIX_MUL)).astype(np.int64)
         pk = (pk.astype(np.uint64) * np.uint64(MIX_MUL)).astype(np.int64)
     try:
-        all_threads = len(os.sched_getaffinity(0))
+        affinity = len(os.sched_getaffinity(0))
     except AttributeError:
-        all_threads = os.cpu_count() or 8
-    counts = sorted({8, all_threads})
+        affinity = os.cpu_count() or 8
+    quota = _cpu_quota()
+    # the cores this process may actually run on: the affinity mask, capped by a cgroup
+    # CPU quota (a GPU box shares its host: nproc shows every CPU, the quota its share)
+    all_threads = min(affinity, quota) if quota else affinity
+    # 16: a one-GPU box's share of its host's CPUs (the pool gives 16 per GPU; the quota
+    # is not always visible from inside)
+    counts = sorted({8, min(16, all_threads), all_threads})
     main = {f"threads_{n}": _join_cpu(oracle, bk, pk, n) for n in counts}
     del pk
     # C1a: lookup_speed
@@ -275,7 +301,8 @@ def cpu_baseline(cfg):
         "sample": f"full {B}-row build + {P}-row probe with pair emission (no extrapolation); C restatement of "
                   f"reference Version 10 (oracle/hj_oracle.c) on {_cpu_model()}; value = probe rows / (build + "
                   f"probe) at the reference's PARALLELISM = 8 threads; also at all {all_threads} usable cores "
-                  f"(host has {os.cpu_count()} logical CPUs); plus C1a (lookup_speed) and C1b (2^20 x 2^20)",
+                  f"(affinity {affinity} of the host's {os.cpu_count()} logical CPUs, cgroup quota "
+                  f"{quota if quota else 'none'}); plus C1a (lookup_speed) and C1b (2^20 x 2^20)",
         "build_ms": m8["build_ms"],
         "probe_mrows_s": m8["probe_mrows_s"],
         "this_config": main,
