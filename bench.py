@@ -173,7 +173,7 @@ class SingleGpuJoin:
         if sliced:
             self.kernel_desc = ("the whole hj_probe_async, sliced probe (DESIGN.md §4): " +
                                 ("sl_partition" if dense else "hs_partition") +
-                                " + sl_toff_transpose + sl_lookup + sl_emit (look-back offsets); " +
+                                " + sl_lookup + sl_emit (tile offsets from the lookup's tile counts); " +
                                 ("direct-addressed table" if dense else
                                  f"hashed table, {st['buckets']} buckets = {st['table_bytes']} B"))
         else:
@@ -389,9 +389,10 @@ def main():
         -> max over ranks of the elapsed seconds"""
         # warmup runs as the timed loop does (pipelined steps hold two tables at once: the
         # allocator's cache fills here, not inside the timed region)
+        per_step_sync = args.sync_steps or (use_dist and not getattr(job, "pipelined", False))
         for _ in range(warmup):
             job.step()
-            if args.sync_steps or use_dist:
+            if per_step_sync:
                 torch.cuda.synchronize(dev)
                 job.collect()
         torch.cuda.synchronize(dev)
@@ -405,7 +406,7 @@ def main():
         t_start = time.perf_counter()
         for _ in range(steps):
             job.step()
-            if args.sync_steps or use_dist:
+            if per_step_sync:
                 torch.cuda.synchronize(dev)
                 job.collect()
         torch.cuda.synchronize(dev)
@@ -489,7 +490,7 @@ def main():
             "probe_ms_in_step": (round(float(np.median(job.probe_in_step_ms)), 4)
                                  if getattr(job, "probe_in_step_ms", None) else None),
             "build_ms": round(build_ms, 4),
-            "pipelined_steps": not (args.sync_steps or use_dist),
+            "pipelined_steps": not (args.sync_steps or (use_dist and not getattr(job, "pipelined", False))),
             "roofline": roofline,
             "cpu_baseline": cpu,
         }
@@ -557,15 +558,20 @@ class BroadcastJob:
     """One step = all_gather of the build shards (RCCL), a local build of the whole build
     side (canonical numbering = the global build ids), and the probe of this rank's own
     probe rows: no probe-side exchange (SURVEY.md §8e broadcast build, chosen when
-    B·G < B + P). exchange_ms = the all_gather; probe_ms (HIP events) = gather + build +
-    probe."""
+    B·G < B + P). Steps are pipelined like SingleGpuJoin's: the gather runs on its own
+    stream (into one of two buffers), the build on another, the probe on the current
+    stream, so step k's gather and build overlap step k - 1's probe; step k - 1 is
+    collected after step k is enqueued. exchange_ms = the all_gather (events on the
+    gather stream); probe_ms = the probe, from its launch to its end (with the wait for
+    its build)."""
+
+    pipelined = True
 
     def __init__(self, dj, bk, pk, pbase, dev):
         self.dj, self.bk, self.pk, self.pbase, self.dev = dj, bk, pk, pbase, dev
         self.probe_ms, self.build_ms, self.exchange_ms = [], [], []
         self.matches = 0
         n = pk.numel()
-        self.ids = torch.arange(pbase, pbase + n, dtype=torch.int64, device=dev).to(torch.int32)
         self.ws = torch.empty(HashTable.workspace_bytes(n), dtype=torch.uint8, device=dev)
         self.d_total = torch.zeros(1, dtype=torch.int64, device=dev)
         self.cap = n
@@ -577,44 +583,59 @@ class BroadcastJob:
         allb = [torch.empty_like(nb) for _ in range(W)]
         dist.all_gather(allb, nb, group=dj.group)
         self.sizes = [int(x) for x in torch.cat(allb).tolist()]  # known before the timed steps
-        self._t = None
-        # the build runs on a side stream: the probe's partition (no table reads) overlaps it
-        self.bstream = torch.cuda.Stream(dev)
+        # two gather buffers: step k + 2 reuses step k's once step k is collected
+        self.gbuf = [torch.empty(sum(self.sizes), dtype=bk.dtype, device=dev) for _ in range(2)]
+        self.cstream = torch.cuda.Stream(dev)  # the gathers
+        self.bstream = torch.cuda.Stream(dev)  # the builds
+        self.evs = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(2)]
+        self.k = 0
+        self.prev = None
+
+    def _gather(self, out):
+        if len(set(self.sizes)) == 1:
+            return dist.all_gather_into_tensor(out, self.bk, group=self.dj.group, async_op=True)
+        parts = list(torch.split(out, self.sizes))
+        return dist.all_gather(parts, self.bk, group=self.dj.group, async_op=True)
 
     def step(self):
-        from datafusion_parallelism_amd.distributed import all_gather_rows
-
-        ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
-        ev[0].record()
-        (gathered,) = all_gather_rows([self.bk], self.dj.group, sizes=self.sizes)
-        ev[1].record()
+        ev = self.evs[self.k & 1]
+        g = self.gbuf[self.k & 1]
+        self.k += 1
+        with torch.cuda.stream(self.cstream):
+            ev[0].record(self.cstream)
+            work = self._gather(g)
+            work.wait()  # the gather stream waits for the collective
+            ev[1].record(self.cstream)
+        self.bstream.wait_stream(self.cstream)
         t = HashTable(1, "int64", self.dev.index or 0)
-        cur = torch.cuda.current_stream(self.dev)
-        self.bstream.wait_stream(cur)
         with torch.cuda.stream(self.bstream):
-            t.append(0, gathered)
+            t.append(0, g)
             t.finish(0)
-        s = cur.cuda_stream
+        cur = torch.cuda.current_stream(self.dev)
+        ev[2].record(cur)
         t.probe_async(self.pk.data_ptr(), self.pk.numel(), self.ob.data_ptr(), self.op.data_ptr(), self.cap,
-                      self.d_total.data_ptr(), self.ws.data_ptr(), s, probe_ids_ptr=self.ids.data_ptr())
-        ev[2].record()
-        self._ev, self._t = ev, t
+                      self.d_total.data_ptr(), self.ws.data_ptr(), cur.cuda_stream, probe_base=self.pbase)
+        ev[3].record(cur)
+        self.collect()
+        self.prev = (t, ev)
 
     def collect(self):
-        if self._t is None:
+        if self.prev is None:
             return
-        torch.cuda.synchronize(self.dev)
-        self.exchange_ms.append(self._ev[0].elapsed_time(self._ev[1]))
-        self.probe_ms.append(self._ev[0].elapsed_time(self._ev[2]))
-        self.build_ms.append(self._t.build_ns() / 1e6)
-        self.matches = int(self.d_total.item())
-        if self.matches > self.cap:
-            raise RuntimeError("output capacity too small")
-        self._t.close()
-        self._t = None
+        t, ev = self.prev
+        ev[3].synchronize()
+        self.exchange_ms.append(ev[0].elapsed_time(ev[1]))
+        self.probe_ms.append(ev[2].elapsed_time(ev[3]))
+        self.build_ms.append(t.build_ns() / 1e6)
+        t.close()
+        self.prev = None
 
     def finish(self):
         self.collect()
+        torch.cuda.synchronize(self.dev)
+        self.matches = int(self.d_total.item())
+        if self.matches > self.cap:
+            raise RuntimeError("output capacity too small")
 
 
 if __name__ == "__main__":

@@ -81,6 +81,7 @@ SIGNATURES = [
     ("hj_set_build_mode", I32, [I32]),
     ("hj_probe_async", I32, [P, P, P, I64, I64, P, P, I64, P, P, P]),
     ("hj_probe_async_ids", I32, [P, P, P, I64, P, I64, P, P, I64, P, P, P]),
+    ("hj_probe_async_base", I32, [P, P, P, I64, I64, U32, P, P, I64, P, P, P]),
     ("hj_table_stream_wait", I32, [P, P]),
     ("hj_partition_workspace_bytes", I64, [I64, I32]),
     ("hj_radix_partition", I32, [I32, P, P, I64, P, U64, I64, I32, P, I32, I64, P, I32, P, P, P]),

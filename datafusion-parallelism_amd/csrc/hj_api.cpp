@@ -647,13 +647,14 @@ hj_status note_probe(const hj_table* t, hipStream_t s) {
 }
 
 hj_status probe_impl(const hj_table* t, const void* keys, const uint8_t* valid, int64_t voff,
-                     const uint32_t* probe_ids, int64_t n, uint64_t* out_b, uint32_t* out_p, int64_t cap,
-                     int64_t* d_total, void* ws, hipStream_t s) {
+                     const uint32_t* probe_ids, uint32_t pbase, int64_t n, uint64_t* out_b, uint32_t* out_p,
+                     int64_t cap, int64_t* d_total, void* ws, hipStream_t s) {
     if (n < 0 || n > 0xFFFFFFFFll) return fail(HJ_ERR_INVALID, "probe batch must have < 2^32 rows");
+    if ((int64_t)pbase + n > 0x100000000ll) return fail(HJ_ERR_INVALID, "probe_base + rows exceeds 2^32");
     if (cap < 0) return fail(HJ_ERR_INVALID, "negative capacity");
     if (reinterpret_cast<uintptr_t>(ws) & 7) return fail(HJ_ERR_INVALID, "workspace must be 8-byte aligned");
     // the probe orders itself after the build (on another stream) at its first table read
-    HIP_TRY(launch_probe(t->key_bytes, view_of(t), keys, valid, voff, probe_ids, n, out_b, out_p, cap, d_total, ws,
+    HIP_TRY(launch_probe(t->key_bytes, view_of(t), keys, valid, voff, probe_ids, pbase, n, out_b, out_p, cap, d_total, ws,
                          s != t->bstream ? t->res.ev1 : nullptr, s));
     // hj_table_free waits for it before the table's blocks return to the cache
     return note_probe(t, s);
@@ -872,8 +873,8 @@ hj_status run_multi_build(hj_table* t, const std::vector<Segment>& segs, const s
 
 // Probe of a multi table into caller buffers on the keys' device; synchronous.
 hj_status multi_probe(const hj_table* t, const void* keys, const uint8_t* valid, int64_t voff,
-                      const uint32_t* probe_ids, int64_t n, uint64_t* out_b, uint32_t* out_p, int64_t cap,
-                      int64_t* d_total, void* workspace, hipStream_t s) {
+                      const uint32_t* probe_ids, uint32_t pbase, int64_t n, uint64_t* out_b, uint32_t* out_p,
+                      int64_t cap, int64_t* d_total, void* workspace, hipStream_t s) {
     MultiTable* m = t->multi;
     std::lock_guard<std::mutex> lk(m->probe_mu);
     const int G = (int)m->devices.size();
@@ -900,6 +901,7 @@ hj_status multi_probe(const hj_table* t, const void* keys, const uint8_t* valid,
         const uint8_t* v = nullptr;
         int64_t voff = 0;
         const uint32_t* ids = nullptr;
+        uint32_t base = 0;  // probe_idx = base + row when ids is null
         void* ws = nullptr;
     };
     std::vector<Part> parts(G);
@@ -929,10 +931,13 @@ hj_status multi_probe(const hj_table* t, const void* keys, const uint8_t* valid,
                     P.voff = (voff + a) & 7;
                 }
             }
-            MT_ALLOC(ids, uint32_t*, dev, 4 * (size_t)P.n);
-            if (probe_ids) HIP_TRY(copy_to(ids, probe_ids + a, 4 * (size_t)P.n, sg));
-            else HIP_TRY(launch_iota_u32(ids, P.n, (uint32_t)a, sg));
-            P.ids = ids;
+            if (probe_ids) {
+                MT_ALLOC(ids, uint32_t*, dev, 4 * (size_t)P.n);
+                HIP_TRY(copy_to(ids, probe_ids + a, 4 * (size_t)P.n, sg));
+                P.ids = ids;
+            } else {
+                P.base = pbase + (uint32_t)a;  // contiguous rows: no id array
+            }
         }
     } else {
         // radix: partition the batch by owner on its device; the rows travel with their
@@ -978,9 +983,11 @@ hj_status multi_probe(const hj_table* t, const void* keys, const uint8_t* valid,
             if (!P.dt) P.dt = (int64_t*)tmp.get(dev, 8);
             if (!P.ws) P.ws = tmp.get(dev, (size_t)hj_probe_workspace_bytes(P.n));
             if (!P.ob || !P.op || !P.dt || !P.ws) return fail(HJ_ERR_OOM, "multi-GPU probe: device allocation failed");
-            if ((st = hj_probe_async_ids(m->shards[g], P.k, P.v, P.voff, P.ids, P.n, P.ob, P.op, P.cap, P.dt, P.ws,
-                                         m->streams[g])) != HJ_OK)
-                return st;
+            st = P.ids ? hj_probe_async_ids(m->shards[g], P.k, P.v, P.voff, P.ids, P.n, P.ob, P.op, P.cap, P.dt, P.ws,
+                                            m->streams[g])
+                       : hj_probe_async_base(m->shards[g], P.k, P.v, P.voff, P.n, P.base, P.ob, P.op, P.cap, P.dt,
+                                             P.ws, m->streams[g]);
+            if (st != HJ_OK) return st;
             HIP_TRY(hipMemcpyAsync(&P.total, P.dt, 8, hipMemcpyDeviceToHost, m->streams[g]));
             again = true;
         }
@@ -1018,6 +1025,8 @@ hj_status multi_probe(const hj_table* t, const void* keys, const uint8_t* valid,
         HIP_TRY(launch_merge_pairs(cb, cp, total, n, out_b, out_p, cap, mw, s));
         if (probe_ids)  // row -> the caller's probe id, in place (each thread its own element)
             HIP_TRY(launch_gather_fixed(probe_ids, nullptr, 0, 4, out_p, 4, std::min(total, cap), out_p, nullptr, s));
+        else if (pbase)  // row -> base + row
+            HIP_TRY(launch_add_u32(out_p, std::min(total, cap), pbase, s));
     }
     HIP_TRY(hipMemcpyAsync(d_total, &total, 8, hipMemcpyHostToDevice, s));
     HIP_TRY(hipStreamSynchronize(s));  // total lives on this frame; the scratch goes back to the cache
@@ -1319,10 +1328,25 @@ hj_status hj_probe_async(const hj_table* t, const void* keys, const uint8_t* val
     if (n > 0 && keys == nullptr) return fail(HJ_ERR_INVALID, "null keys");
     HIP_TRY(hipSetDevice(t->device));
     if (t->multi)
-        return multi_probe(t, keys, validity, validity_offset, nullptr, n, out_build, out_probe, capacity, d_total,
+        return multi_probe(t, keys, validity, validity_offset, nullptr, 0, n, out_build, out_probe, capacity, d_total,
                            workspace, (hipStream_t)stream);
-    return probe_impl(t, keys, validity, validity_offset, nullptr, n, out_build, out_probe, capacity, d_total,
+    return probe_impl(t, keys, validity, validity_offset, nullptr, 0, n, out_build, out_probe, capacity, d_total,
                       workspace, (hipStream_t)stream /* NULL = the null stream */);
+}
+
+hj_status hj_probe_async_base(const hj_table* t, const void* keys, const uint8_t* validity, int64_t validity_offset,
+                              int64_t n, uint32_t probe_base, uint64_t* out_build, uint32_t* out_probe,
+                              int64_t capacity, int64_t* d_total, void* workspace, void* stream) {
+    hj_status st = check_table(t);
+    if (st != HJ_OK) return st;
+    if (d_total == nullptr || workspace == nullptr) return fail(HJ_ERR_INVALID, "null d_total/workspace");
+    if (n > 0 && keys == nullptr) return fail(HJ_ERR_INVALID, "null keys");
+    HIP_TRY(hipSetDevice(t->device));
+    if (t->multi)
+        return multi_probe(t, keys, validity, validity_offset, nullptr, probe_base, n, out_build, out_probe, capacity,
+                           d_total, workspace, (hipStream_t)stream);
+    return probe_impl(t, keys, validity, validity_offset, nullptr, probe_base, n, out_build, out_probe, capacity,
+                      d_total, workspace, (hipStream_t)stream);
 }
 
 hj_status hj_probe_async_ids(const hj_table* t, const void* keys, const uint8_t* validity, int64_t validity_offset,
@@ -1333,9 +1357,9 @@ hj_status hj_probe_async_ids(const hj_table* t, const void* keys, const uint8_t*
     if (d_total == nullptr || workspace == nullptr) return fail(HJ_ERR_INVALID, "null d_total/workspace");
     HIP_TRY(hipSetDevice(t->device));
     if (t->multi)
-        return multi_probe(t, keys, validity, validity_offset, probe_ids, n, out_build, out_probe, capacity, d_total,
-                           workspace, (hipStream_t)stream);
-    return probe_impl(t, keys, validity, validity_offset, probe_ids, n, out_build, out_probe, capacity, d_total,
+        return multi_probe(t, keys, validity, validity_offset, probe_ids, 0, n, out_build, out_probe, capacity,
+                           d_total, workspace, (hipStream_t)stream);
+    return probe_impl(t, keys, validity, validity_offset, probe_ids, 0, n, out_build, out_probe, capacity, d_total,
                       workspace, (hipStream_t)stream /* NULL = the null stream */);
 }
 
@@ -1366,8 +1390,8 @@ hj_status hj_probe(const hj_table* t, const void* keys, const uint8_t* validity,
     for (int attempt = 0; attempt < 2; ++attempt) {
         HIP_TRY(hipMalloc((void**)&ob, (size_t)cap * 8));
         HIP_TRY(hipMalloc((void**)&op, (size_t)cap * 4));
-        if (t->multi) st = multi_probe(t, dk, dv, dvo, nullptr, n, ob, op, cap, d_total, ws, s);
-        else st = probe_impl(t, dk, dv, dvo, nullptr, n, ob, op, cap, d_total, ws, s);
+        if (t->multi) st = multi_probe(t, dk, dv, dvo, nullptr, 0, n, ob, op, cap, d_total, ws, s);
+        else st = probe_impl(t, dk, dv, dvo, nullptr, 0, n, ob, op, cap, d_total, ws, s);
         if (st != HJ_OK) break;
         uint64_t werr = 0;
         HIP_TRY(hipMemcpyAsync(&total, d_total, 8, hipMemcpyDeviceToHost, s));

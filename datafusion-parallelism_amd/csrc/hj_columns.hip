@@ -294,6 +294,11 @@ __global__ void iota_u32_kernel(uint32_t* __restrict__ out, int64_t n, uint32_t 
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
         out[i] = base + (uint32_t)i;
 }
+// a[i] += base (merged probe rows -> the caller's probe row base)
+__global__ void add_u32_kernel(uint32_t* __restrict__ a, int64_t n, uint32_t base) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        a[i] += base;
+}
 // out[i] = in[i] (u32 -> u64 ids for the partition kernel)
 __global__ void widen_u32_kernel(const uint32_t* __restrict__ in, int64_t n, uint64_t* __restrict__ out) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
@@ -330,6 +335,12 @@ static unsigned grid_for(int64_t n) { return (unsigned)std::max<int64_t>(1, std:
 hipError_t launch_iota_u32(uint32_t* out, int64_t n, uint32_t base, hipStream_t s) {
     if (n <= 0) return hipSuccess;
     iota_u32_kernel<<<grid_for(n), 256, 0, s>>>(out, n, base);
+    return hipGetLastError();
+}
+
+hipError_t launch_add_u32(uint32_t* a, int64_t n, uint32_t base, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    add_u32_kernel<<<grid_for(n), 256, 0, s>>>(a, n, base);
     return hipGetLastError();
 }
 

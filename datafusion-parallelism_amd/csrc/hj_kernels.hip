@@ -1078,7 +1078,8 @@ __device__ __forceinline__ uint32_t resolve_count(const uint32_t* dup_rows, uint
 // Writes the pairs of four probe rows starting at output position `pos` (canonical:
 // rows ascending, each row's build rows descending = the order of its dup segment).
 template <bool HAS_ROW_IDS, bool HAS_PROBE_IDS>
-__device__ __forceinline__ void emit4(const TableView& tv, const uint32_t* __restrict__ probe_ids, int64_t row0,
+__device__ __forceinline__ void emit4(const TableView& tv, const uint32_t* __restrict__ probe_ids, uint32_t pbase,
+                                      int64_t row0,
                                       const uint32_t (&ref)[4], const uint32_t (&cnt)[4], unsigned long long pos,
                                       uint64_t* __restrict__ out_b, uint32_t* __restrict__ out_p, int64_t cap) {
 #pragma unroll
@@ -1086,7 +1087,7 @@ __device__ __forceinline__ void emit4(const TableView& tv, const uint32_t* __res
         const uint32_t c = cnt[q];
         if (c == 0) continue;
         const int64_t prow = row0 + q;
-        const uint32_t pidx = HAS_PROBE_IDS ? probe_ids[prow] : (uint32_t)prow;
+        const uint32_t pidx = HAS_PROBE_IDS ? probe_ids[prow] : (uint32_t)prow + pbase;
         const uint32_t r = ref[q];
         if (c == 1) {
             if (pos < (unsigned long long)cap) {
@@ -1162,9 +1163,9 @@ __device__ unsigned long long lookback(unsigned long long* flags, int64_t t, uns
 template <typename K, bool HAS_VALID, bool HAS_ROW_IDS, bool HAS_PROBE_IDS>
 __global__ void __launch_bounds__(kProbeThreads)
 probe_fused_kernel(TableView tv, const void* __restrict__ keys, const uint8_t* __restrict__ valid, int64_t voff,
-                   const uint32_t* __restrict__ probe_ids, int64_t n, bool vec, unsigned long long* flags,
-                   unsigned long long* err, uint64_t* __restrict__ out_b, uint32_t* __restrict__ out_p,
-                   int64_t cap, int64_t* __restrict__ d_total, int nt) {
+                   const uint32_t* __restrict__ probe_ids, uint32_t pbase, int64_t n, bool vec,
+                   unsigned long long* flags, unsigned long long* err, uint64_t* __restrict__ out_b,
+                   uint32_t* __restrict__ out_p, int64_t cap, int64_t* __restrict__ d_total, int nt) {
     // the tile's refs wait in LDS across the look-back (registers stay free for the
     // lookups' line loads: occupancy is what keeps enough random reads in flight)
     __shared__ __attribute__((aligned(16))) uint32_t s_ref[kProbeTile];
@@ -1241,7 +1242,7 @@ probe_fused_kernel(TableView tv, const void* __restrict__ keys, const uint8_t* _
         }
         if (gt > (unsigned long long)kStage * kStageMaxWindows) {
             if (row0 < n)
-                emit4<HAS_ROW_IDS, HAS_PROBE_IDS>(tv, probe_ids, row0, ref[g], cnt, gbase + lpos, out_b, out_p, cap);
+                emit4<HAS_ROW_IDS, HAS_PROBE_IDS>(tv, probe_ids, pbase, row0, ref[g], cnt, gbase + lpos, out_b, out_p, cap);
         } else {
             for (unsigned long long w0 = 0; w0 < gt; w0 += kStage) {
                 const unsigned long long w1 = w0 + kStage;
@@ -1253,7 +1254,7 @@ probe_fused_kernel(TableView tv, const void* __restrict__ keys, const uint8_t* _
                     const unsigned long long b = (p + c) < w1 ? (p + c) : w1;
                     if (a < b) {
                         const uint32_t r = ref[g][q];
-                        const uint32_t pidx = HAS_PROBE_IDS ? probe_ids[row0 + q] : (uint32_t)(row0 + q);
+                        const uint32_t pidx = HAS_PROBE_IDS ? probe_ids[row0 + q] : (uint32_t)(row0 + q) + pbase;
                         const uint32_t* seg = (r & kDupFlag) ? tv.dup_rows + (r & tv.off_mask) + 1 : nullptr;
                         for (unsigned long long t = a; t < b; ++t) {
                             const uint32_t br = seg ? seg[t - p] : r;
@@ -2006,7 +2007,7 @@ constexpr int kSlWaveRows = kSlTile / (kSlEmitThreads / 64);  // 2048
 template <bool HAS_ROW_IDS, bool HAS_PROBE_IDS>
 __global__ void __launch_bounds__(kSlEmitThreads, 4)  // two workgroups per CU: <= 128 VGPRs
 sl_emit_kernel(TableView tv, uint32_t nslices, const uint16_t* __restrict__ rl, const uint32_t* __restrict__ res,
-               const uint16_t* __restrict__ toff, const uint32_t* __restrict__ probe_ids,
+               const uint16_t* __restrict__ toff, const uint32_t* __restrict__ probe_ids, uint32_t pbase,
                const unsigned long long* __restrict__ tcnt, int64_t ntiles, uint64_t* __restrict__ out_b,
                uint32_t* __restrict__ out_p, int64_t cap, int64_t* __restrict__ d_total, int dbg) {
     __shared__ __attribute__((aligned(16))) uint32_t s_ref[kSlTile];  // the tile's refs, kMiss = none
@@ -2108,7 +2109,7 @@ sl_emit_kernel(TableView tv, uint32_t nslices, const uint16_t* __restrict__ rl, 
                         const unsigned long long o = pos + below;
                         if (o < (unsigned long long)cap) {
                             out_b[o] = HAS_ROW_IDS ? tv.row_ids[r] : (uint64_t)r;
-                            out_p[o] = HAS_PROBE_IDS ? probe_ids[row] : (uint32_t)row;
+                            out_p[o] = HAS_PROBE_IDS ? probe_ids[row] : (uint32_t)row + pbase;
                         }
                     }
                 } else {
@@ -2134,7 +2135,7 @@ sl_emit_kernel(TableView tv, uint32_t nslices, const uint16_t* __restrict__ rl, 
                                                             : tv.dup_rows[(rj & tv.off_mask) + 1 + (p - xj)];
                             const int64_t rowj = tile0 + row_w + k + j;
                             out_b[o] = HAS_ROW_IDS ? tv.row_ids[br] : (uint64_t)br;
-                            out_p[o] = HAS_PROBE_IDS ? probe_ids[rowj] : (uint32_t)rowj;
+                            out_p[o] = HAS_PROBE_IDS ? probe_ids[rowj] : (uint32_t)rowj + pbase;
                         }
                         __builtin_amdgcn_wave_barrier();
                     }
@@ -2795,7 +2796,7 @@ bool sl_auto(const TableView& tv, int64_t n) {
 }
 
 hipError_t launch_probe_sliced(int key_bytes, const TableView& tv, const void* keys, const uint8_t* valid,
-                               int64_t voff, const uint32_t* probe_ids, int64_t n, uint64_t* out_b,
+                               int64_t voff, const uint32_t* probe_ids, uint32_t pbase, int64_t n, uint64_t* out_b,
                                uint32_t* out_p, int64_t cap, int64_t* d_total, void* workspace, hipEvent_t built,
                                hipStream_t s) {
     const bool hashed = tv.dense == nullptr;
@@ -2866,7 +2867,7 @@ hipError_t launch_probe_sliced(int key_bytes, const TableView& tv, const void* k
     const bool ri = tv.row_ids != nullptr, pi = probe_ids != nullptr;
     const unsigned egrid = (unsigned)std::min<int64_t>(nt, (int64_t)sl_emit_wgs_per_cu() * sl_num_cus());
 #define DFP_SLE(RI, PI)                                                                                           \
-    sl_emit_kernel<RI, PI><<<egrid, kSlEmitThreads, 0, s>>>(tv, nsl, w.rl, w.res, w.toff, probe_ids, w.tcnt, nt, \
+    sl_emit_kernel<RI, PI><<<egrid, kSlEmitThreads, 0, s>>>(tv, nsl, w.rl, w.res, w.toff, probe_ids, pbase, w.tcnt, nt, \
                                                            out_b, out_p, cap, d_total, sl_dbg)
     if (ri && pi) DFP_SLE(true, true);
     else if (ri) DFP_SLE(true, false);
@@ -2878,13 +2879,13 @@ hipError_t launch_probe_sliced(int key_bytes, const TableView& tv, const void* k
 }  // namespace
 
 hipError_t launch_probe(int key_bytes, const TableView& tv, const void* keys, const uint8_t* valid, int64_t voff,
-                        const uint32_t* probe_ids, int64_t n, uint64_t* out_b, uint32_t* out_p, int64_t cap,
+                        const uint32_t* probe_ids, uint32_t pbase, int64_t n, uint64_t* out_b, uint32_t* out_p, int64_t cap,
                         int64_t* d_total, void* workspace, hipEvent_t built, hipStream_t s) {
     const int64_t nt = probe_tiles(n);
     const int mode = probe_mode();
     const uint32_t nsl = sl_slices(tv);
     if (nt > 0 && nsl >= 1 && nsl <= (uint32_t)kSlMaxSlices && (mode == 4 || (mode == 0 && sl_auto(tv, n))))
-        return launch_probe_sliced(key_bytes, tv, keys, valid, voff, probe_ids, n, out_b, out_p, cap, d_total,
+        return launch_probe_sliced(key_bytes, tv, keys, valid, voff, probe_ids, pbase, n, out_b, out_p, cap, d_total,
                                    workspace, built, s);  // S1 zeroes the error word
     if (built != nullptr) {
         const hipError_t ew = hipStreamWaitEvent(s, built, 0);
@@ -2906,7 +2907,7 @@ hipError_t launch_probe(int key_bytes, const TableView& tv, const void* keys, co
     unsigned long long* err = reinterpret_cast<unsigned long long*>((char*)workspace + 8);
     const bool ri = tv.row_ids != nullptr, pi = probe_ids != nullptr;
 #define DFP_FUSED(KT, HV, RI, PI)                                                                             \
-    probe_fused_kernel<KT, HV, RI, PI><<<(unsigned)nt, kProbeThreads, 0, s>>>(tv, keys, valid, voff, probe_ids, n, \
+    probe_fused_kernel<KT, HV, RI, PI><<<(unsigned)nt, kProbeThreads, 0, s>>>(tv, keys, valid, voff, probe_ids, pbase, n, \
                                                                              vec, w.tcnt, err, out_b, out_p, cap, \
                                                                              d_total, fused_nt)
 #define DFP_FUSED_K(KT, HV)                              \

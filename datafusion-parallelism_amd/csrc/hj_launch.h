@@ -75,7 +75,7 @@ int64_t probe_workspace(int64_t n);
 // kernel that reads the table — the sliced probe partitions and regroups its rows first,
 // so a build still running on another stream overlaps them
 hipError_t launch_probe(int key_bytes, const TableView& tv, const void* keys, const uint8_t* valid,
-                        int64_t voff, const uint32_t* probe_ids, int64_t n, uint64_t* out_b,
+                        int64_t voff, const uint32_t* probe_ids, uint32_t probe_base, int64_t n, uint64_t* out_b,
                         uint32_t* out_p, int64_t cap, int64_t* d_total, void* workspace,
                         hipEvent_t built, hipStream_t s);
 
@@ -122,6 +122,7 @@ hipError_t launch_gather_var(const void* offsets, int offset_bytes, const uint8_
 
 // ---- multi-GPU table helpers (hj_columns.hip) -------------------------------
 hipError_t launch_iota_u32(uint32_t* out, int64_t n, uint32_t base, hipStream_t s);
+hipError_t launch_add_u32(uint32_t* a, int64_t n, uint32_t base, hipStream_t s);
 hipError_t launch_widen_u32(const uint32_t* in, int64_t n, uint64_t* out, hipStream_t s);
 // canonical order of shard pair streams whose probe rows are < nrows (see hj_columns.hip)
 int64_t merge_pairs_workspace(int64_t nrows);

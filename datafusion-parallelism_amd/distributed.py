@@ -418,7 +418,6 @@ class DistributedHashJoin:
         with HashTable(1, kt, dev.index or 0) as t:  # canonical numbering = the global build ids
             t.append(0, gathered)
             t.finish(0)
-            ids = torch.arange(probe_base, probe_base + n, dtype=torch.int64, device=dev).to(torch.int32)
             ws = torch.empty(HashTable.workspace_bytes(n), dtype=torch.uint8, device=dev)
             d_total = torch.zeros(1, dtype=torch.int64, device=dev)
             cap = max(capacity_hint or n, 1)
@@ -427,7 +426,7 @@ class DistributedHashJoin:
                 ob = torch.empty(cap, dtype=torch.int64, device=dev)
                 op = torch.empty(cap, dtype=torch.int32, device=dev)
                 t.probe_async(probe_keys.data_ptr(), n, ob.data_ptr(), op.data_ptr(), cap, d_total.data_ptr(),
-                              ws.data_ptr(), s, probe_ids_ptr=ids.data_ptr())
+                              ws.data_ptr(), s, probe_base=probe_base)  # global probe ids: base + row
                 total = int(d_total.item())
                 if total <= cap:
                     return ob[:total], op[:total]

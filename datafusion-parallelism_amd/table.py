@@ -253,9 +253,13 @@ class HashTable:
 
     def probe_async(self, keys_ptr: int, n: int, out_build_ptr: int, out_probe_ptr: int, capacity: int,
                     d_total_ptr: int, workspace_ptr: int, stream: int = 0, valid_ptr: int | None = None,
-                    voff: int = 0, probe_ids_ptr: int | None = None) -> None:
-        """hj_probe_async(_ids) on raw device pointers (no sync, no allocation)."""
-        if probe_ids_ptr is None:
+                    voff: int = 0, probe_ids_ptr: int | None = None, probe_base: int = 0) -> None:
+        """hj_probe_async(_ids, _base) on raw device pointers (no sync, no allocation):
+        probe_idx = row, probe_ids[row], or probe_base + row."""
+        if probe_ids_ptr is None and probe_base:
+            check(self._L.hj_probe_async_base(self._h, keys_ptr, valid_ptr, voff, n, probe_base, out_build_ptr,
+                                              out_probe_ptr, capacity, d_total_ptr, workspace_ptr, stream or None))
+        elif probe_ids_ptr is None:
             check(self._L.hj_probe_async(self._h, keys_ptr, valid_ptr, voff, n, out_build_ptr, out_probe_ptr,
                                          capacity, d_total_ptr, workspace_ptr, stream or None))
         else:

@@ -200,6 +200,17 @@ hj_status hj_probe_async_ids(const hj_table* t, const void* keys, const uint8_t*
                              uint64_t* out_build, uint32_t* out_probe, int64_t capacity,
                              int64_t* d_total, void* workspace, void* stream);
 
+/* As hj_probe_async, but probe_idx of a match is probe_base + row: the batch's rows are
+ * rows probe_base .. probe_base + n - 1 of a longer probe stream (replaces the caller-side
+ * offset of the batch-relative indices of ProbeBuildIndices, src/shared/shared.rs:29-47,
+ * when a partition's batches or a rank's share of one batch are numbered globally - the
+ * broadcast-build plan's contiguous probe ranges need no id array). probe_base + n must
+ * not exceed 2^32. */
+hj_status hj_probe_async_base(const hj_table* t, const void* keys, const uint8_t* validity,
+                              int64_t validity_offset, int64_t n, uint32_t probe_base,
+                              uint64_t* out_build, uint32_t* out_probe, int64_t capacity,
+                              int64_t* d_total, void* workspace, void* stream);
+
 /* Probe strategy for later probes of this process: 0 auto (sliced for direct-addressed
  * tables past the L2s with a probe side at least as large as the key range, else fused),
  * 3 fused (lookup + emission in one launch, tile offsets by decoupled look-back),

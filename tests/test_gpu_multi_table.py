@@ -59,3 +59,29 @@ def test_multi_table_host_probe_int32(dfp, oracle_mod, plan):
     b, p, _, _ = _multi_join(dfp, [0, 0], plan, bk, pk, key_type="int32", host_probe=True)
     ob, op = oracle_mod.inner_join(bk, pk)
     assert np.array_equal(p, op) and np.array_equal(b, ob)
+
+
+@pytest.mark.parametrize("plan", ["broadcast", "radix"])
+def test_multi_table_probe_base(dfp, oracle_mod, plan):
+    """hj_probe_async_base on a multi table: the broadcast plan's shards take their row
+    ranges' bases (no id arrays); the radix plan adds the base after the merge."""
+    rng = np.random.default_rng(17)
+    bk = rng.integers(0, 100_000, 80_000).astype(np.int64)
+    pk = rng.integers(0, 120_000, 250_001).astype(np.int64)
+    base = 123_456_789
+    ob, op = oracle_mod.inner_join(bk, pk)
+    with dfp.HashTable(1, "int64", devices=[0, 0, 0, 0], plan=plan) as t:
+        t.append(0, torch.from_numpy(bk).cuda())
+        t.finish_all()
+        n = len(pk)
+        keys = torch.from_numpy(pk).cuda()
+        cap = 4 * n
+        b = torch.empty(cap, dtype=torch.int64, device="cuda")
+        p = torch.empty(cap, dtype=torch.int32, device="cuda")
+        ws = torch.empty(dfp.HashTable.workspace_bytes(n), dtype=torch.uint8, device="cuda")
+        dt = torch.zeros(1, dtype=torch.int64, device="cuda")
+        t.probe_async(keys.data_ptr(), n, b.data_ptr(), p.data_ptr(), cap, dt.data_ptr(), ws.data_ptr(),
+                      torch.cuda.current_stream().cuda_stream, probe_base=base)
+        m = int(dt.item())
+        assert np.array_equal(b[:m].cpu().numpy().astype(np.uint64), ob)
+        assert np.array_equal(p[:m].cpu().numpy().view(np.uint32), (op.astype(np.uint64) + base).astype(np.uint32))

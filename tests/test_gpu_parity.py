@@ -546,3 +546,38 @@ def test_sliced_probe_ids_unaligned(dfp, oracle_mod, sliced_mode):
         p = op[:total].cpu().numpy().view(np.uint32)
     xb, xp = oracle_mod.inner_join(bk, pk[1:])
     assert_same(b, p, ids[xb.astype(np.int64)].astype(np.uint64), pids[xp.astype(np.int64)])
+
+
+def _probe_async_base(dfp, t, pk, base):
+    """hj_probe_async_base on device buffers -> (build idx, probe idx) as numpy."""
+    n = len(pk)
+    keys = torch.from_numpy(np.ascontiguousarray(pk)).cuda()
+    cap = max(4 * n, 16)
+    ob = torch.empty(cap, dtype=torch.int64, device="cuda")
+    op = torch.empty(cap, dtype=torch.int32, device="cuda")
+    ws = torch.empty(dfp.HashTable.workspace_bytes(n), dtype=torch.uint8, device="cuda")
+    dt = torch.zeros(1, dtype=torch.int64, device="cuda")
+    s = torch.cuda.current_stream().cuda_stream
+    t.probe_async(keys.data_ptr(), n, ob.data_ptr(), op.data_ptr(), cap, dt.data_ptr(), ws.data_ptr(), s,
+                  probe_base=base)
+    m = int(dt.item())
+    assert m <= cap
+    return ob[:m].cpu().numpy().astype(np.uint64), op[:m].cpu().numpy().view(np.uint32)
+
+
+@pytest.mark.parametrize("base", [1, 3_000_000_000])
+def test_probe_base(dfp, oracle_mod, probe_mode, base):
+    """hj_probe_async_base: probe_idx = probe_base + row (a rank's or a batch's rows of a
+    longer probe stream), identical pairs otherwise; a base past 2^32 - n is refused."""
+    rng = np.random.default_rng(base % 1000)
+    bk = rng.integers(0, 400_000, 300_000).astype(np.int64)
+    pk = rng.integers(-1000, 450_000, 1_000_003).astype(np.int64)
+    ob, op = oracle_mod.inner_join(bk, pk)
+    with dfp.HashTable(1, "int64", 0) as t:
+        t.append(0, torch.from_numpy(bk).cuda())
+        t.finish(0)
+        b, p = _probe_async_base(dfp, t, pk, base)
+        assert np.array_equal(b, ob)
+        assert np.array_equal(p, (op.astype(np.uint64) + base).astype(np.uint32))
+        with pytest.raises(dfp.HjError):
+            _probe_async_base(dfp, t, pk, 2**32 - 10)
