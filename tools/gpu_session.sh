@@ -129,6 +129,15 @@ for s in $STEPS; do
         SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_INSTS_VALU -d $O/sq${KP_TAG} -o sq --output-format csv \
         -- python3 tools/probe_one.py ${KP_ARGS} > $O/sq${KP_TAG}.log 2>&1 || { tail -30 $O/sq${KP_TAG}.log; exit 1; }
       python3 tools/sq_summary.py $O/sq${KP_TAG} ;;
+    envsweep)
+      # one env knob over values (ENV_NAME, ENV_VALS): kernel stats of tools/probe_one.py ${KP_ARGS}
+      for v in ${ENV_VALS}; do
+        export ${ENV_NAME}=$v
+        timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/ev_$v -o kp --output-format csv \
+          -- python3 tools/probe_one.py ${KP_ARGS} > $O/ev_$v.log 2>&1 || { tail -30 $O/ev_$v.log; exit 1; }
+        unset ${ENV_NAME}
+        echo "${ENV_NAME}=$v"; python3 tools/kstats.py $O/ev_$v | grep -E "${ENV_GREP:-.}"
+      done ;;
     chunk)
       # the sliced probe in K chunks (tools/chunk_probe.py), auto strategy and forced sliced
       run timeout -k 10 200 python3 tools/chunk_probe.py > $O/chunk.log 2>&1 || { tail -30 $O/chunk.log; exit 1; }
