@@ -1728,6 +1728,11 @@ sl_lookup_kernel(TableView tv, uint32_t wlog, uint32_t nslices, int64_t ntiles, 
     constexpr uint32_t kOobMask = (1u << 26) - 1;       // off[] = index | owner rank << 26
     constexpr int KB = HASHED ? 8 : 2;                  // entry bytes
     const uint32_t cmask = (1u << tv.clog2) - 1;
+    uint32_t side_meta = 0, side_ref = kMiss;  // hashed: the side bucket (key 0), read once
+    if constexpr (HASHED) {
+        side_meta = tv.tbl[tv.nb].meta;
+        side_ref = tv.tbl[tv.nb].ref[0];
+    }
     // segment bounds of the lane's tile in block tc (tile-major toff), loaded one block ahead
     auto bounds = [&](int64_t tc, uint32_t* st, uint32_t* len) {
         *st = 0;
@@ -1819,7 +1824,7 @@ sl_lookup_kernel(TableView tv, uint32_t wlog, uint32_t nslices, int64_t ntiles, 
             for (int u = 0; u < W / 64; ++u) {
                 if (w0 + u * 64 >= R) continue;  // uniform: past the run
                 const uint32_t o = off[u] & kOobMask;
-                uint32_t v, c;  // ref and its row count
+                uint32_t v, c;  // ref and its row count (kCountUnknown: in its segment header)
                 if constexpr (HASHED) {
                     const unsigned long long sk = ev[u];
                     if (o == kOob) {
@@ -1828,21 +1833,27 @@ sl_lookup_kernel(TableView tv, uint32_t wlog, uint32_t nslices, int64_t ntiles, 
                     } else if (dbg & 4) {  // timing ablation: no bucket lookup (wrong pairs)
                         v = (uint32_t)sk & 0xFFFFFFu;
                         c = 1;
-                    } else if (sk == 0) {  // key 0: the side bucket (rare)
-                        const Bucket& S = tv.tbl[tv.nb];
-                        v = S.meta ? S.ref[0] : kMiss;
-                        c = S.meta;
+                    } else if (sk == 0) {  // key 0: the side bucket (rare; loaded at the start)
+                        v = side_meta ? side_ref : kMiss;
+                        c = side_meta;
                     } else {
                         v = lds_bucket_ref(reinterpret_cast<const uint4*>(s_tab), tv.nb, sbase, cmask, sk, &c);
-                        if (c == kCountUnknown) c = tv.dup_rows[v & tv.off_mask];
                     }
                 } else {
                     v = s_tab[ev[u] & ((1u << wlog) - 1)];
                     c = 1;
                     if (o != kOob && (v == kMiss || (v & kDupFlag))) {
                         const uint32_t c4 = tv.off_mask == kPackedMask ? ((v >> 27) & 15u) : 0u;
-                        c = v == kMiss ? 0u : c4 ? c4 : tv.dup_rows[v & tv.off_mask];
+                        c = v == kMiss ? 0u : c4 ? c4 : kCountUnknown;
                     }
+                }
+                // counts not inline: read from the segment header in a wave-uniform branch
+                // that waits there. Merged into the common path, that load's wait was an
+                // s_waitcnt vmcnt(0) on every row — for the previous rows' ref stores (loads
+                // and stores share vmcnt): one store round trip per 64 entries.
+                if (__ballot(c == kCountUnknown) != 0) {
+                    if (c == kCountUnknown) c = tv.dup_rows[v & tv.off_mask];
+                    asm volatile("" : "+v"(c));
                 }
                 __builtin_amdgcn_raw_buffer_store_b32(v, rres, (int)(o * 4), 0, 0);
                 if constexpr (HASHED) {
