@@ -211,11 +211,13 @@ hj_status hj_probe_async_base(const hj_table* t, const void* keys, const uint8_t
                               uint64_t* out_build, uint32_t* out_probe, int64_t capacity,
                               int64_t* d_total, void* workspace, void* stream);
 
-/* Probe strategy for later probes of this process: 0 auto (sliced for direct-addressed
- * tables past the L2s with a probe side at least as large as the key range, else fused),
+/* Probe strategy for later probes of this process: 0 auto (sliced for tables past the L2s
+ * - more than 2^20 key values or 2^16 buckets, at most 2047 slices - with a probe side at
+ * least as large as the key range / bucket count, else fused),
  * 3 fused (lookup + emission in one launch, tile offsets by decoupled look-back),
- * 4 sliced (direct-addressed tables: probe rows partitioned by 32768-value key slice,
- * lookups out of LDS, then ordered emission; other tables fused). Results are identical;
+ * 4 sliced (probe rows partitioned by slice - 32768 key values of a direct-addressed table
+ * or 2048 buckets of a hashed one - lookups out of LDS, then ordered emission; tables of
+ * more than 2047 slices fused). Results are identical;
  * returns the previous mode, -1 for a bad value (1 and 2 named strategies measured slower
  * and removed). Also settable with DFP_HJ_PROBE_MODE=fused|sliced. */
 int hj_set_probe_mode(int mode);
