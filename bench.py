@@ -92,6 +92,22 @@ def gen_inputs(cfg, rank, world, dev, strong=True):
     return bk, pk, b0, p0
 
 
+def local_reference_count(cfg, rank, world, dev):
+    """Pairs of this rank's probe rows against the whole build side, on this GPU with no
+    exchange (outside the timed region): summed over the ranks, the count the exchange
+    plan must reproduce."""
+    bk, pk, _, _ = gen_inputs(cfg, 0, 1, dev, strong=True)  # the whole join
+    P = pk.numel()
+    p0, p1 = P * rank // world, P * (rank + 1) // world
+    with HashTable(1, "int64", dev.index or 0) as t:
+        t.append(0, bk)
+        t.finish(0)
+        b, _ = t.probe(pk[p0:p1], device_output=True)
+        n = int(b.numel())
+    del bk, pk
+    return n
+
+
 class SingleGpuJoin:
     """One step = build + probe on this GPU (no exchange)."""
 
@@ -439,9 +455,11 @@ def main():
     build_ms = float(np.median(job.build_ms))
     M = job.matches
     if use_dist:  # pairs of the whole join (all ranks)
-        mt = torch.tensor([M], dtype=torch.int64, device=dev)
+        mt = torch.tensor([M, local_reference_count(cfg, rank, world, dev)], dtype=torch.int64, device=dev)
         dist.all_reduce(mt)
-        M_all = int(mt.item())
+        M_all, M_ref = int(mt[0].item()), int(mt[1].item())
+        if M_all != M_ref:  # the exchange plan lost or invented pairs
+            raise RuntimeError(f"multi-GPU pair count {M_all} != {M_ref} of the same join without exchange")
     else:
         M_all = M
     alg_bytes = 8 * P + 16 * B + 12 * M
