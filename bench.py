@@ -111,11 +111,16 @@ def local_reference_count(cfg, rank, world, dev):
 class SingleGpuJoin:
     """One step = build + probe on this GPU (no exchange)."""
 
-    def __init__(self, bk, pk, dev, same_stream=False):
+    def __init__(self, bk, pk, dev, same_stream=False, priority="none"):
         self.bk, self.pk, self.dev = bk, pk, dev
         # builds run on their own stream: a probe partitions its rows while its table is
-        # still being built (the library orders the first table read after the build)
-        self.bstream = None if same_stream else torch.cuda.Stream(dev)
+        # still being built (the library orders the first table read after the build).
+        # priority: "probe-high" runs the probes on a high-priority stream, "build-low" the
+        # builds on a low-priority one (HIP stream priorities order the dispatch of
+        # workgroups from concurrent kernels)
+        bprio = 1 if priority == "build-low" else 0
+        self.bstream = None if same_stream else torch.cuda.Stream(dev, priority=bprio)
+        self.pstream = torch.cuda.Stream(dev, priority=-1) if priority == "probe-high" else None
         P = pk.numel()
         self.ws = torch.empty(HashTable.workspace_bytes(P), dtype=torch.uint8, device=dev)
         self.d_total = torch.zeros(1, dtype=torch.int64, device=dev)
@@ -141,7 +146,7 @@ class SingleGpuJoin:
         build, as a pipeline of joins does. probe_ms runs from the probe's launch to its
         end (with the wait for the rest of the build)."""
         t = HashTable(1, "int64", self.dev.index or 0)
-        s = torch.cuda.current_stream(self.dev)
+        s = self.pstream or torch.cuda.current_stream(self.dev)
         if self.bstream is not None:
             with torch.cuda.stream(self.bstream):
                 t.append(0, self.bk)
@@ -194,7 +199,7 @@ class SingleGpuJoin:
                                  f"hashed table, {st['buckets']} buckets = {st['table_bytes']} B"))
         else:
             self.kernel_desc = "probe_fused_kernel (" + ("direct-addressed" if dense else "hashed") + " table)"
-        s = torch.cuda.current_stream(self.dev)
+        s = self.pstream or torch.cuda.current_stream(self.dev)
         t.stream_wait(s.cuda_stream)
         torch.cuda.synchronize(self.dev)
         self.probe_in_step_ms = self.probe_ms
@@ -347,6 +352,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--stream-priority", default="none", choices=["none", "probe-high", "build-low"],
+                    help="single GPU: HIP stream priorities of the probe / build streams")
     ap.add_argument("--force-dist", action="store_true",
                     help="use the radix-exchange path even with one rank (testing)")
     ap.add_argument("--chunks", type=int, default=4,
@@ -387,7 +394,7 @@ def main():
     gB, gP = cfg["build_rows"], cfg["probe_rows"]  # the whole join (strong scaling)
     plan = None
     if not use_dist:
-        job = SingleGpuJoin(bk, pk, dev, same_stream=args.same_stream)
+        job = SingleGpuJoin(bk, pk, dev, same_stream=args.same_stream, priority=args.stream_priority)
     else:
         from datafusion_parallelism_amd.distributed import DistributedHashJoin
 

@@ -103,6 +103,14 @@ for s in $STEPS; do
         --master-port 29533 bench.py --gpus 1 --steps 5 --warmup 2 --no-cpu-baseline > $O/bench_trun.json \
         2> $O/bench_trun.err || { tail -30 $O/bench_trun.err; exit 1; }
       cat $O/bench_trun.json ;;
+    prio)
+      # HIP stream priorities of the pipelined single-GPU bench (probe high / build low)
+      python3 -c "import torch; print('priority range', torch.cuda.Stream.priority_range())"
+      for pr in none probe-high build-low none probe-high; do
+        run timeout -k 10 300 python3 bench.py --config ${CFG:-c2} --no-cpu-baseline --stream-priority $pr \
+          > $O/prio_$pr.json 2> $O/prio_$pr.err || { tail -30 $O/prio_$pr.err; exit 1; }
+        echo "$pr: $(python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(d['value'], d['ms_per_step'], d['probe_ms'], d['probe_ms_in_step'], d['build_ms'])" $O/prio_$pr.json)"
+      done ;;
     pcie)
       run timeout -k 10 400 python3 tools/pcie_rate.py > $O/pcie.json 2> $O/pcie.err || { tail -30 $O/pcie.err; exit 1; }
       cat $O/pcie.json ;;
