@@ -1456,7 +1456,7 @@ dense_frag_build_kernel(ChunkGeom g, uint32_t nblk, int64_t ntiles, const uint16
                         const uint16_t* __restrict__ ko, const uint16_t* __restrict__ rl,
                         const uint32_t* __restrict__ tile_base, const uint64_t* __restrict__ ids32,
                         uint32_t* __restrict__ dense, uint32_t* __restrict__ dup_rows, BigSeg* __restrict__ big,
-                        BuildCounters* ctr, unsigned long long* __restrict__ spill) {
+                        BuildCounters* ctr, unsigned long long* __restrict__ spill, uint32_t run) {
     constexpr uint32_t GV = kDenseSub << kDenseBlockShift;  // 8192 values per block
     constexpr uint32_t NSUB = GV / kDenseSub;
     __shared__ uint32_t refs[GV];
@@ -1467,9 +1467,18 @@ dense_frag_build_kernel(ChunkGeom g, uint32_t nblk, int64_t ntiles, const uint16
     __shared__ unsigned long long s_w[T / 64];
     __shared__ unsigned long long s_base, s_sp;
     __shared__ uint32_t s_carry;
-    // key block (slice): plain block order. The XCD-contiguous order of the lookups puts
-    // the skewed distributions' heavy low blocks on one XCD (C3 build 0.35 -> 0.76 ms).
-    const uint32_t c = blockIdx.x;
+    // key block (slice): runs of `run` consecutive blocks per XCD (blocks are dispatched
+    // round-robin over the 8 XCDs), so that the blocks resident on one XCD at once read
+    // adjacent fragments of each tile (shared lines in that XCD's L2) while the runs still
+    // interleave over the XCDs. A whole XCD-contiguous order puts the skewed distributions'
+    // heavy low blocks on one XCD (C3 build 0.35 -> 0.76 ms). The last partial group of
+    // 8 * run blocks keeps the plain order.
+    const uint32_t c = [&] {
+        const uint32_t b = blockIdx.x, grp = 8u * run;
+        if (run <= 1 || b >= nblk / grp * grp) return b;
+        const uint32_t l = b >> 3;
+        return (l / run) * grp + (b & 7u) * run + l % run;
+    }();
     const uint64_t cbase = (uint64_t)c * GV;  // key index of refs[0]
     const uint32_t nbins = nblk + 1;
     for (uint32_t i = threadIdx.x; i < GV; i += T) refs[i] = kMiss;
@@ -2533,6 +2542,14 @@ int64_t frag_build_scratch_bytes(const ChunkGeom& g, int64_t ftiles, int64_t tot
            8 * total + 6 * 256;
 }
 
+// dense frag build: consecutive key blocks per XCD run (DFP_HJ_FRAG_RUN; 1 = plain order)
+uint32_t frag_run() {
+    static const uint32_t v = [] {
+        const char* e = getenv("DFP_HJ_FRAG_RUN");
+        return e ? (uint32_t)std::max(1, atoi(e)) : 4u;
+    }();
+    return v;
+}
 hipError_t launch_build_frag(int key_bytes, const Segment* h_segs, int nseg, const ChunkGeom& g, int64_t ftiles,
                              void* scratch, uint32_t* tile_base, const uint64_t* ids32, uint32_t* dense,
                              uint32_t* dup_rows, BigSeg* big, BuildCounters* ctr, const Segment* d_segs, int64_t total,
@@ -2570,7 +2587,7 @@ hipError_t launch_build_frag(int key_bytes, const Segment* h_segs, int nseg, con
         toff, nbins, ftiles, toffT);
     dense_frag_build_kernel<1024, 8><<<nblk, 1024, 0, s>>>(g, nblk, ftiles, toffT, ko, rl, tile_base,
                                                            ids_as_rows ? ids32 : nullptr, dense, dup_rows, big, ctr,
-                                                           spill);
+                                                           spill, frag_run());
     dup_sort_big_kernel<<<big_grid, kBigThreads, 0, s>>>(dup_rows, big, ctr, d_segs, nseg, total, key_bytes,
                                                          ids_as_rows);
     return hipGetLastError();
