@@ -98,6 +98,7 @@ SIGNATURES = [
                                     P, P, P]),
     ("hj_gen_perm_keys", I32, [P, I64, I64, I64, P]),
     ("hj_gen_uniform_keys", I32, [P, I64, U64, I64, P]),
+    ("hj_gen_exponential_keys", I32, [P, I32, I32]),
 ]
 
 _lib = None

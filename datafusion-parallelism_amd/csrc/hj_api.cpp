@@ -20,6 +20,7 @@
 // There is no CPU code path: without a GPU every entry point fails with
 // HJ_ERR_NO_DEVICE.
 #include <hip/hip_runtime.h>
+#include <math.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -1653,6 +1654,21 @@ hj_status hj_gen_uniform_keys(int64_t* out, int64_t n, uint64_t seed, int64_t ra
     if (device_count() == 0) return fail(HJ_ERR_NO_DEVICE, "no GPU visible");
     if (range <= 0 || n < 0) return fail(HJ_ERR_INVALID, "bad range");
     HIP_TRY(launch_gen_uniform(out, n, seed, range, (hipStream_t)stream));
+    return HJ_OK;
+}
+
+// host buffer: src/api_utils.rs:15-23 in f32; f32::powf is libm powf, called through a
+// volatile pointer so that it is neither folded nor vectorized (libmvec differs)
+hj_status hj_gen_exponential_keys(int32_t* out, int32_t lo, int32_t hi) {
+    if (hi < lo || (hi > lo && out == nullptr)) return fail(HJ_ERR_INVALID, "bad range");
+    float (*volatile pw)(float, float) = powf;
+    const int32_t diff = hi - lo;
+    const float base = 16.0f;
+    for (int32_t n = 0; n < diff; ++n) {
+        const float x = (float)n / (float)diff;
+        const float y = (pw(base, x) - 1.0f) / (base - 1.0f);
+        out[n] = lo + (int32_t)(y * (float)diff);
+    }
     return HJ_OK;
 }
 

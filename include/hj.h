@@ -361,6 +361,9 @@ hj_status hj_gen_perm_keys(int64_t* out, int64_t n, int64_t mul, int64_t range,
 /* out[i] = splitmix64(seed + i) mod range */
 hj_status hj_gen_uniform_keys(int64_t* out, int64_t n, uint64_t seed, int64_t range,
                               void* stream);
+/* HOST buffer out[0 .. hi - lo): make_exponential_int_array(lo, hi) of
+ * src/api_utils.rs:15-23 (f32, libm powf as f32::powf); needs no GPU */
+hj_status hj_gen_exponential_keys(int32_t* out, int32_t lo, int32_t hi);
 
 #ifdef __cplusplus
 }

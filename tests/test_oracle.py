@@ -2,6 +2,7 @@
 the reference holds for this path (tests/golden/reference_kats.json, transcribed from
 the reference's own assertions), and cross-check its two restatements (reference
 semantics vs the multithreaded Version 10 table) against each other."""
+import ctypes
 import json
 import os
 
@@ -24,10 +25,40 @@ def test_exponential_generator_kat(oracle_mod):
 
 
 def test_exponential_generator_c3_shape(oracle_mod):
-    """10^7 exponential keys -> 6,602,610 distinct, max multiplicity 6."""
+    """C3's 10^7 exponential keys with libm powf (f32::powf): 6,603,254 distinct, max
+    multiplicity 6. (SURVEY.md §8(d)'s 6,602,610 came from numpy's float32 power.)"""
     e = oracle_mod.make_exponential_int_array(0, 10**7)
     vals, cnt = np.unique(e, return_counts=True)
-    assert len(vals) == 6602610 and cnt.max() == 6 and (e == 0).sum() == 6
+    assert len(vals) == 6603254 and cnt.max() == 6 and (e == 0).sum() == 6
+
+
+def test_exponential_generator_is_libm_powf(oracle_mod):
+    """src/api_utils.rs:15-23 computes 16f32.pow(x) with f32::powf, i.e. libm powf. The
+    restatement calls powf; numpy's float32 power is another approximation, which
+    this pins as different (so the C3 input is not numpy's)."""
+    import ctypes.util
+
+    libm = ctypes.CDLL(ctypes.util.find_library("m"))
+    libm.powf.restype = ctypes.c_float
+    libm.powf.argtypes = [ctypes.c_float, ctypes.c_float]
+    diff = 10**7
+    n = np.arange(0, diff, 997, dtype=np.float32)
+    x = n / np.float32(diff)
+    y = np.array([libm.powf(16.0, float(v)) for v in x], dtype=np.float32)
+    v = (((y - np.float32(1.0)) / np.float32(15.0)).astype(np.float32) * np.float32(diff)).astype(np.float32)
+    want = np.trunc(v).astype(np.int32)
+    got = oracle_mod.make_exponential_int_array(0, diff)[::997]
+    assert np.array_equal(got, want)
+    assert not np.array_equal(np.power(np.float32(16.0), x).astype(np.float32), y)
+
+
+def test_exponential_generator_product_equals_oracle(oracle_mod):
+    """The product-side generator (hj_gen_exponential_keys, a host function of the HIP
+    library; bench.py's C3 input) reproduces the oracle's keys."""
+    from datafusion_parallelism_amd.api_utils import make_exponential_int_array
+
+    for lo, hi in [(0, 10), (-50, 4000), (0, 10**6)]:
+        assert np.array_equal(make_exponential_int_array(lo, hi), oracle_mod.make_exponential_int_array(lo, hi))
 
 
 def test_v10_build_lookup_kat(oracle_mod):
