@@ -2550,6 +2550,19 @@ uint32_t frag_run() {
     }();
     return v;
 }
+// dense frag build workgroup size (DFP_HJ_FRAG_T): 512 threads x 16 rows (default) or
+// 1024 x 8. Alone the 1024-thread form is faster (C2 70 vs 74 us, C3 234 vs 309 us); beside
+// a probe on another stream the 8-wave workgroups (110 VGPRs, 74 KB LDS) fit on CUs that a
+// probe kernel's workgroup half fills, where a 16-wave one does not: the pipelined bench's
+// build span 0.36 -> 0.26 ms, C2 142.0K -> 146.2K Mrows/s, C3 66.2K -> 67.5K
+// (profiles/r02_frag_threads.txt)
+uint32_t frag_threads() {
+    static const uint32_t v = [] {
+        const char* e = getenv("DFP_HJ_FRAG_T");
+        return e ? (uint32_t)atoi(e) : 512u;
+    }();
+    return v;
+}
 hipError_t launch_build_frag(int key_bytes, const Segment* h_segs, int nseg, const ChunkGeom& g, int64_t ftiles,
                              void* scratch, uint32_t* tile_base, const uint64_t* ids32, uint32_t* dense,
                              uint32_t* dup_rows, BigSeg* big, BuildCounters* ctr, const Segment* d_segs, int64_t total,
@@ -2585,9 +2598,14 @@ hipError_t launch_build_frag(int key_bytes, const Segment* h_segs, int nseg, con
     }
     sl_toff_transpose_kernel<<<(unsigned)((ftiles + 63) / 64 * ((nblk + kSlTrChunk) / kSlTrChunk)), 256, 0, s>>>(
         toff, nbins, ftiles, toffT);
-    dense_frag_build_kernel<1024, 8><<<nblk, 1024, 0, s>>>(g, nblk, ftiles, toffT, ko, rl, tile_base,
-                                                           ids_as_rows ? ids32 : nullptr, dense, dup_rows, big, ctr,
-                                                           spill, frag_run());
+    if (frag_threads() != 1024)
+        dense_frag_build_kernel<512, 16><<<nblk, 512, 0, s>>>(g, nblk, ftiles, toffT, ko, rl, tile_base,
+                                                             ids_as_rows ? ids32 : nullptr, dense, dup_rows, big, ctr,
+                                                             spill, frag_run());
+    else
+        dense_frag_build_kernel<1024, 8><<<nblk, 1024, 0, s>>>(g, nblk, ftiles, toffT, ko, rl, tile_base,
+                                                               ids_as_rows ? ids32 : nullptr, dense, dup_rows, big, ctr,
+                                                               spill, frag_run());
     dup_sort_big_kernel<<<big_grid, kBigThreads, 0, s>>>(dup_rows, big, ctr, d_segs, nseg, total, key_bytes,
                                                          ids_as_rows);
     return hipGetLastError();

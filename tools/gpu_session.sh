@@ -111,6 +111,15 @@ for s in $STEPS; do
           > $O/prio_$pr.json 2> $O/prio_$pr.err || { tail -30 $O/prio_$pr.err; exit 1; }
         echo "$pr: $(python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(d['value'], d['ms_per_step'], d['probe_ms'], d['probe_ms_in_step'], d['build_ms'])" $O/prio_$pr.json)"
       done ;;
+    envbench)
+      # one env knob over values (ENV_NAME, ENV_VALS), the pipelined bench of ${CFG:-c2} per value
+      for v in ${ENV_VALS}; do
+        export ${ENV_NAME}=$v
+        run timeout -k 10 300 python3 bench.py --config ${CFG:-c2} --no-cpu-baseline > $O/eb_$v.json 2> $O/eb_$v.err \
+          || { tail -30 $O/eb_$v.err; exit 1; }
+        unset ${ENV_NAME}
+        echo "${ENV_NAME}=$v: $(python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(d['value'], d['ms_per_step'], d['probe_ms'], d['probe_ms_in_step'], d['build_ms'])" $O/eb_$v.json)"
+      done ;;
     pcie)
       run timeout -k 10 400 python3 tools/pcie_rate.py > $O/pcie.json 2> $O/pcie.err || { tail -30 $O/pcie.err; exit 1; }
       cat $O/pcie.json ;;
