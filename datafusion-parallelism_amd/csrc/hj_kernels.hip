@@ -2556,12 +2556,9 @@ uint32_t frag_run() {
 // probe kernel's workgroup half fills, where a 16-wave one does not: the pipelined bench's
 // build span 0.36 -> 0.26 ms, C2 142.0K -> 146.2K Mrows/s, C3 66.2K -> 67.5K
 // (profiles/r02_frag_threads.txt)
-uint32_t frag_threads() {
-    static const uint32_t v = [] {
-        const char* e = getenv("DFP_HJ_FRAG_T");
-        return e ? (uint32_t)atoi(e) : 512u;
-    }();
-    return v;
+uint32_t frag_threads() {  // read per build, so that tests can run both forms in one process
+    const char* e = getenv("DFP_HJ_FRAG_T");
+    return e && atoi(e) == 1024 ? 1024u : 512u;
 }
 hipError_t launch_build_frag(int key_bytes, const Segment* h_segs, int nseg, const ChunkGeom& g, int64_t ftiles,
                              void* scratch, uint32_t* tile_base, const uint64_t* ids32, uint32_t* dense,

@@ -208,6 +208,25 @@ def test_exponential_keys_parity(dfp, oracle_mod, probe_mode):
     assert st["dup_keys"] > 0
 
 
+@pytest.mark.parametrize("frag_t", ["512", "1024"])
+def test_frag_build_workgroup_sizes(dfp, oracle_mod, monkeypatch, frag_t):
+    """Both forms of the dense frag build (DFP_HJ_FRAG_T: 512 threads x 16 rows, the
+    default, or 1024 x 8): exponential keys (duplicate passes in most blocks), a block
+    with more rows than the registers hold (the spill path) and nulls, against the oracle."""
+    monkeypatch.setenv("DFP_HJ_FRAG_T", frag_t)
+    rng = np.random.default_rng(int(frag_t))
+    bk = np.concatenate([oracle_mod.make_exponential_int_array(0, 300000).astype(np.int64),
+                         np.full(20000, 123457, np.int64)])
+    rng.shuffle(bk)
+    bv = rng.random(len(bk)) > 0.02
+    pk = oracle_mod.uniform_keys(400000, 0xBEEF, 320000)
+    pk[::1000] = 123457
+    b, p, st = gpu_join(dfp, bk, pk, bvalid=bv)
+    ob, op = oracle_mod.inner_join(bk, pk, bv, None)
+    assert_same(b, p, ob, op)
+    assert st["buckets"] == 0 and st["dup_keys"] > 0 and st["max_key_rows"] >= 19000
+
+
 @pytest.mark.parametrize("layout", [0, 1, 2])
 def test_stats(dfp, layout):
     L = dfp.load()
