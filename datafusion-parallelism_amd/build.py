@@ -38,10 +38,10 @@ def torch_lib_dir() -> str:
     return d
 
 
-def _stale() -> bool:
-    if not os.path.exists(LIB):
+def _stale(lib: str = LIB) -> bool:
+    if not os.path.exists(lib):
         return True
-    t = os.path.getmtime(LIB)
+    t = os.path.getmtime(lib)
     deps = [os.path.join(CSRC, f) for f in SOURCES_HIP + SOURCES_CPP + HEADERS]
     deps += [os.path.join(INCLUDE, "hj.h"), __file__]
     return any(os.path.getmtime(d) > t for d in deps)
@@ -55,20 +55,23 @@ def _run(cmd: list[str], verbose: bool) -> None:
         raise RuntimeError(f"command failed ({r.returncode}): {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
-    """Compile the HIP kernels + C-ABI host layer; returns the library path."""
-    if not force and not _stale():
-        return LIB
+def build(force: bool = False, verbose: bool = False, defines: tuple[str, ...] = (), out: str = LIB) -> str:
+    """Compile the HIP kernels + C-ABI host layer; returns the library path. `defines` and
+    `out` serve diagnostic builds only (tools/build_ablation.py); the product library is
+    built without defines into lib/libdfp_hj.so."""
+    if not force and not _stale(out):
+        return out
     rocm = os.environ.get("ROCM_PATH", "/opt/rocm")
     hipcc = shutil.which("hipcc") or os.path.join(rocm, "bin", "hipcc")
     tlib = torch_lib_dir()
-    objdir = os.path.join(HERE, "build")
+    objdir = os.path.join(HERE, "build") if out == LIB else out + ".objs"
     os.makedirs(objdir, exist_ok=True)
-    os.makedirs(LIBDIR, exist_ok=True)
+    os.makedirs(os.path.dirname(out), exist_ok=True)
+    dflags = [f"-D{d}" for d in defines]
     objs, cmds = [], []
     for src in SOURCES_HIP:
         obj = os.path.join(objdir, src + ".o")
-        cmds.append([hipcc, f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17", "-I", INCLUDE,
+        cmds.append([hipcc, f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17", *dflags, "-I", INCLUDE,
                      "-c", os.path.join(CSRC, src), "-o", obj])
         objs.append(obj)
     for src in SOURCES_CPP:
@@ -79,11 +82,11 @@ def build(force: bool = False, verbose: bool = False) -> str:
     # the translation units compile independently: in parallel
     with ThreadPoolExecutor(max_workers=len(cmds)) as ex:
         list(ex.map(lambda c: _run(c, verbose), cmds))
-    tmp = LIB + ".tmp"
+    tmp = out + ".tmp"
     _run(["g++", "-shared", "-o", tmp, *objs, f"-L{tlib}", "-lamdhip64", f"-Wl,-rpath,{tlib}",
           "-Wl,--no-undefined", "-lpthread"], verbose)
-    os.replace(tmp, LIB)
-    return LIB
+    os.replace(tmp, out)
+    return out
 
 
 if __name__ == "__main__":

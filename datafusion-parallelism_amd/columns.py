@@ -142,6 +142,66 @@ class DeviceColumn:
                                 dst.data_ptr(), dvalid.data_ptr(), s))
         return DeviceColumn(self.type, n, data=dst, valid=dvalid, voff=0)
 
+    def key_tensor(self) -> torch.Tensor:
+        """An Int32 / Int64 column's values as a device tensor (no copy)."""
+        if pa.types.is_int64(self.type):
+            return self.data.view(torch.int64)[: self.length]
+        if pa.types.is_int32(self.type):
+            return self.data.view(torch.int32)[: self.length]
+        raise TypeError(f"{self.type} is not an Int32/Int64 key column")
+
+    def valid_bools(self) -> torch.Tensor | None:
+        """The validity bitmap as one bool per row (device), or None without nulls."""
+        if self.valid is None:
+            return None
+        i = torch.arange(self.length, dtype=torch.int64, device=self.device) + self.voff
+        return ((self.valid[i >> 3] >> (i & 7).to(torch.uint8)) & 1).bool()
+
+    @classmethod
+    def concat(cls, cols: list["DeviceColumn"]) -> "DeviceColumn":
+        """Arrow concat of columns of one type, on the device (the build side's
+        cooperative concatenation in canonical order,
+        src/operator/version10/parallel_join_execution_state.rs:256-298,317-347): fixed
+        width values and Utf8/Binary values are copied device to device, offsets re-based,
+        validity bitmaps re-packed from bit 0. One host read: the value ranges of the
+        variable-width pieces."""
+        if not cols:
+            raise ValueError("concat of no columns")
+        t = cols[0].type
+        if any(c.type != t for c in cols):
+            raise TypeError("concat of columns of different types")
+        if len(cols) == 1 and cols[0].voff == 0:
+            return cols[0]
+        n = sum(c.length for c in cols)
+        dev = cols[0].device
+        valid = None
+        if any(c.valid is not None for c in cols):
+            bits = torch.cat([c.valid_bools() if c.valid is not None
+                              else torch.ones(c.length, dtype=torch.bool, device=dev) for c in cols])
+            pad = torch.zeros(_bitmap_bytes(n) * 8, dtype=torch.uint8, device=dev)
+            pad[:n] = bits.to(torch.uint8)
+            w = torch.tensor([1, 2, 4, 8, 16, 32, 64, 128], dtype=torch.uint8, device=dev)
+            valid = (pad.view(-1, 8) * w).sum(1, dtype=torch.int32).to(torch.uint8)
+            if valid.numel() < 8:
+                valid = torch.cat([valid, torch.zeros(8 - valid.numel(), dtype=torch.uint8, device=dev)])
+        if _is_var(t):
+            bounds = torch.stack([torch.stack([c.offsets[0], c.offsets[c.length]]) for c in cols]).to(torch.int64)
+            b = bounds.tolist()  # the one host read
+            offs, vals, base = [], [], 0
+            for c, (a, e) in zip(cols, b):
+                offs.append(c.offsets[: c.length].to(torch.int64) - a + base)
+                vals.append(c.values[a:e])
+                base += e - a
+            odt = cols[0].offsets.dtype
+            offs.append(torch.tensor([base], dtype=torch.int64, device=dev))
+            values = torch.cat(vals) if base else torch.zeros(1, dtype=torch.uint8, device=dev)
+            return cls(t, n, offsets=torch.cat(offs).to(odt), values=values, valid=valid, voff=0)
+        w = _fixed_width(t)
+        data = torch.cat([c.data[: c.length * w] for c in cols])
+        if data.numel() == 0:
+            data = torch.zeros(w, dtype=torch.uint8, device=dev)
+        return cls(t, n, data=data, valid=valid, voff=0)
+
     def to_arrow(self) -> pa.Array:
         n, t = self.length, self.type
         vbuf = None
@@ -236,3 +296,38 @@ def select_rows(flags: torch.Tensor, want: int, n: int | None = None) -> torch.T
     check(L.hj_select_rows(flags.data_ptr() if n else None, n, want, out.data_ptr(), cnt.data_ptr(), ws.data_ptr(),
                            _stream(dev)))
     return out[: int(cnt.item())]
+
+
+class DeviceRecordBatch:
+    """The concatenated build RecordBatch, resident in HBM (row i <-> build index i): what
+    the reference hands every partition's consumer with the lookup
+    (src/operator/lookup_consumers.rs:4-9). `num_rows`, `schema` and the device columns
+    need no host copy; `column(i)` / `to_batch()` bring columns to the host on demand."""
+
+    def __init__(self, schema: pa.Schema, columns: list[DeviceColumn], num_rows: int):
+        self.schema = schema
+        self.device_columns = columns
+        self.num_rows = num_rows
+        self._host: pa.RecordBatch | None = None
+
+    @property
+    def num_columns(self) -> int:
+        return len(self.device_columns)
+
+    def to_batch(self) -> pa.RecordBatch:
+        if self._host is None:
+            if not self.device_columns:
+                self._host = pa.RecordBatch.from_pylist([], schema=self.schema)
+            else:
+                self._host = pa.RecordBatch.from_arrays([c.to_arrow() for c in self.device_columns],
+                                                        schema=self.schema)
+        return self._host
+
+    def column(self, i: int | str) -> pa.Array:
+        if isinstance(i, str):
+            i = self.schema.get_field_index(i)
+        return self.device_columns[i].to_arrow()
+
+    @property
+    def columns(self) -> list[pa.Array]:
+        return self.to_batch().columns

@@ -647,13 +647,21 @@ hj_status note_probe(const hj_table* t, hipStream_t s) {
     return HJ_OK;
 }
 
-hj_status probe_impl(const hj_table* t, const void* keys, const uint8_t* valid, int64_t voff,
-                     const uint32_t* probe_ids, uint32_t pbase, int64_t n, uint64_t* out_b, uint32_t* out_p,
-                     int64_t cap, int64_t* d_total, void* ws, hipStream_t s) {
+// argument checks shared by the single- and multi-GPU probes (probe rows are numbered
+// in u32: base + row, or the row inside a radix piece)
+hj_status check_probe_args(int64_t n, uint32_t pbase, int64_t cap, const void* ws) {
     if (n < 0 || n > 0xFFFFFFFFll) return fail(HJ_ERR_INVALID, "probe batch must have < 2^32 rows");
     if ((int64_t)pbase + n > 0x100000000ll) return fail(HJ_ERR_INVALID, "probe_base + rows exceeds 2^32");
     if (cap < 0) return fail(HJ_ERR_INVALID, "negative capacity");
     if (reinterpret_cast<uintptr_t>(ws) & 7) return fail(HJ_ERR_INVALID, "workspace must be 8-byte aligned");
+    return HJ_OK;
+}
+
+hj_status probe_impl(const hj_table* t, const void* keys, const uint8_t* valid, int64_t voff,
+                     const uint32_t* probe_ids, uint32_t pbase, int64_t n, uint64_t* out_b, uint32_t* out_p,
+                     int64_t cap, int64_t* d_total, void* ws, hipStream_t s) {
+    hj_status st = check_probe_args(n, pbase, cap, ws);
+    if (st != HJ_OK) return st;
     // the probe orders itself after the build (on another stream) at its first table read
     HIP_TRY(launch_probe(t->key_bytes, view_of(t), keys, valid, voff, probe_ids, pbase, n, out_b, out_p, cap, d_total, ws,
                          s != t->bstream ? t->res.ev1 : nullptr, s));
@@ -709,11 +717,21 @@ int ptr_device(const void* p, int dflt) {
     return (a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged) ? a.device : dflt;
 }
 
-// device buffers of one multi operation, returned to the cache at scope exit (after the
-// caller has synchronised the streams that use them)
+// device buffers of one multi operation, returned to the cache at scope exit. Before
+// that, every stream that may still use them is drained — on the success path they are
+// idle already; on an error return, earlier shards' copies, partitions, builds or probes
+// may still be queued, and a block handed back to the cache could be reused under them.
+void drain_multi(const MultiTable* m);
 struct TmpBufs {
     std::vector<std::tuple<int, void*, size_t>> v;
+    const MultiTable* m = nullptr;                      // its shard streams and builds
+    std::vector<std::pair<int, hipStream_t>> streams;  // other streams that used the blocks
     ~TmpBufs() {
+        if (m != nullptr) drain_multi(m);
+        for (auto& ds : streams) {
+            (void)hipSetDevice(ds.first);
+            (void)hipStreamSynchronize(ds.second);
+        }
         for (auto& b : v) cache_free(std::get<0>(b), std::get<1>(b), std::get<2>(b));
     }
     void* get(int dev, size_t bytes) {
@@ -735,6 +753,28 @@ hj_status sync_streams(const MultiTable* m) {
         HIP_TRY(hipStreamSynchronize(m->streams[g]));
     }
     return HJ_OK;
+}
+
+// error-path drain (TmpBufs): the shard streams, and every shard build that was enqueued
+// (an empty shard builds on its own resource stream)
+void drain_multi(const MultiTable* m) {
+    for (size_t g = 0; g < m->streams.size(); ++g) {
+        (void)hipSetDevice(m->devices[g]);
+        (void)hipStreamSynchronize(m->streams[g]);
+    }
+    for (const hj_table* sh : m->shards)
+        if (sh != nullptr && sh->built && sh->build_st == HJ_OK) {
+            (void)hipSetDevice(sh->device);
+            (void)hipEventSynchronize(sh->res.ev1);
+        }
+}
+
+// DFP_HJ_MULTI_STAGE=1: treat every shard's device as foreign, so that the staging
+// copies (keys, validity re-based at voff & 7, ids) run even when all shards share one
+// GPU (tests of the cross-device branches on a one-GPU box)
+bool force_stage() {
+    const char* e = getenv("DFP_HJ_MULTI_STAGE");
+    return e != nullptr && e[0] == '1';
 }
 
 // owner shard of a key under the radix plan (hj_partition_rows' hash map, G a power of two)
@@ -759,7 +799,12 @@ hj_status run_multi_build(hj_table* t, const std::vector<Segment>& segs, const s
     for (int g = 0; g < G; ++g)
         if ((st = hj_build_begin(m->devices[g], 1, t->kt, 0, &m->shards[g])) != HJ_OK) return st;
     TmpBufs tmp;
+    tmp.m = m;
     const uint32_t keep = HJ_INPUT_DEVICE | HJ_BORROW | HJ_BORROW_KEEP;
+    // fault injection for the error-path tests: fail before shard `inject` builds, after
+    // the earlier shards' builds were enqueued
+    const char* inj = getenv("DFP_HJ_INJECT_SHARD_FAIL");
+    const int inject = inj ? atoi(inj) : -1;
     if (m->plan == HJ_MULTI_BROADCAST) {
         // every shard appends every segment in canonical order (its rows keep their
         // canonical numbers, or the caller's ids)
@@ -773,7 +818,7 @@ hj_status run_multi_build(hj_table* t, const std::vector<Segment>& segs, const s
                 const void* k = sg.keys;
                 const uint8_t* v = sg.valid;
                 const uint64_t* ids = sg.ids;
-                if (ptr_device(sg.keys, t->device) != dev) {  // over xGMI into this GPU's HBM
+                if (force_stage() || ptr_device(sg.keys, t->device) != dev) {  // over xGMI into this GPU's HBM
                     MT_ALLOC(kd, void*, dev, (size_t)sg.n * kb);
                     HIP_TRY(copy_to(kd, sg.keys, (size_t)sg.n * kb, s));
                     k = kd;
@@ -794,6 +839,7 @@ hj_status run_multi_build(hj_table* t, const std::vector<Segment>& segs, const s
                                           keep | (ids && t->ids_u31 ? HJ_IDS_U31 : 0), s)) != HJ_OK)
                     return st;
             }
+            if (g == inject) return fail(HJ_ERR_HIP, "injected shard failure (DFP_HJ_INJECT_SHARD_FAIL)");
             if ((st = hj_build_finish(m->shards[g], 0)) != HJ_OK) return st;
         }
         // the shards hold borrowed copies: keep them with the table
@@ -808,6 +854,7 @@ hj_status run_multi_build(hj_table* t, const std::vector<Segment>& segs, const s
         int dev;
         void* keys;
         uint64_t* ids;
+        std::vector<void*> scratch;  // counts and partition workspace
         std::vector<int64_t> cnt;
     };
     std::vector<Piece> pcs(segs.size());
@@ -817,6 +864,7 @@ hj_status run_multi_build(hj_table* t, const std::vector<Segment>& segs, const s
         pc.dev = ptr_device(sg.keys, t->device);
         HIP_TRY(hipSetDevice(pc.dev));
         hipStream_t s = thread_stream(pc.dev);
+        tmp.streams.emplace_back(pc.dev, s);
         if (hsegs[i]->ready) HIP_TRY(hipStreamWaitEvent(s, hsegs[i]->ready, 0));
         MT_ALLOC(ok, void*, pc.dev, (size_t)sg.n * kb);
         MT_ALLOC(oi, uint64_t*, pc.dev, (size_t)sg.n * 8);
@@ -827,6 +875,7 @@ hj_status run_multi_build(hj_table* t, const std::vector<Segment>& segs, const s
             return st;
         pc.keys = ok;
         pc.ids = oi;
+        pc.scratch = {cn, ws};
         pc.cnt.assign(G, 0);
         HIP_TRY(hipMemcpyAsync(pc.cnt.data(), cn, 8 * (size_t)G, hipMemcpyDeviceToHost, s));
         HIP_TRY(hipStreamSynchronize(s));
@@ -857,17 +906,22 @@ hj_status run_multi_build(hj_table* t, const std::vector<Segment>& segs, const s
         if (tot > 0 && (st = hj_build_append(m->shards[g], 0, rk, nullptr, 0, ri, tot, keep | (u31 ? HJ_IDS_U31 : 0),
                                              s)) != HJ_OK)
             return st;
+        if (g == inject) return fail(HJ_ERR_HIP, "injected shard failure (DFP_HJ_INJECT_SHARD_FAIL)");
         if ((st = hj_build_finish(m->shards[g], 0)) != HJ_OK) return st;
     }
     if ((st = sync_streams(m)) != HJ_OK) return st;
-    // keep the shards' borrowed receive buffers; the partition scratch goes back now
+    // keep the shards' borrowed receive buffers; the partition outputs, counts and
+    // workspaces go back to the cache at scope exit
     std::vector<std::tuple<int, void*, size_t>> keep_bufs, drop;
     for (auto& b : tmp.v) {
         bool is_piece = false;
-        for (auto& pc : pcs) is_piece |= std::get<1>(b) == pc.keys || std::get<1>(b) == (void*)pc.ids;
+        for (auto& pc : pcs) {
+            is_piece |= std::get<1>(b) == pc.keys || std::get<1>(b) == (void*)pc.ids;
+            for (void* q : pc.scratch) is_piece |= std::get<1>(b) == q;
+        }
         (is_piece ? drop : keep_bufs).push_back(b);
     }
-    tmp.v = drop;  // partition outputs, counts and workspaces: freed at scope exit
+    tmp.v = drop;
     for (auto& b : keep_bufs) t->multi_bufs.push_back(b);
     return HJ_OK;
 }
@@ -876,12 +930,18 @@ hj_status run_multi_build(hj_table* t, const std::vector<Segment>& segs, const s
 hj_status multi_probe(const hj_table* t, const void* keys, const uint8_t* valid, int64_t voff,
                       const uint32_t* probe_ids, uint32_t pbase, int64_t n, uint64_t* out_b, uint32_t* out_p,
                       int64_t cap, int64_t* d_total, void* workspace, hipStream_t s) {
+    {
+        const hj_status cs = check_probe_args(n, pbase, cap, workspace);
+        if (cs != HJ_OK) return cs;
+    }
     MultiTable* m = t->multi;
     std::lock_guard<std::mutex> lk(m->probe_mu);
     const int G = (int)m->devices.size();
     const int kb = t->key_bytes;
     const int d = ptr_device(keys ? (const void*)keys : (const void*)out_b, t->device);
     TmpBufs tmp;
+    tmp.m = m;
+    tmp.streams.emplace_back(d, s);
     hj_status st;
     HIP_TRY(hipSetDevice(d));
     hipEvent_t ready;  // the caller's inputs are produced in stream s's order
@@ -916,7 +976,7 @@ hj_status multi_probe(const hj_table* t, const void* keys, const uint8_t* valid,
             P.n = b - a;
             HIP_TRY(hipSetDevice(dev));
             HIP_TRY(hipStreamWaitEvent(sg, ready, 0));
-            if (dev == d) {
+            if (dev == d && !force_stage()) {
                 P.k = (const char*)keys + a * kb;
                 P.v = valid;
                 P.voff = voff + a;

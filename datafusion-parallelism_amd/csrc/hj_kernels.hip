@@ -1687,11 +1687,21 @@ __device__ __forceinline__ uint32_t lds_bucket_ref(const uint4* __restrict__ img
 
 constexpr uint32_t kBigCorr = 1u << 16;  // counts - 1 from here on correct the tile count directly
 
+// Timing ablations (wrong pairs by design) exist only in a diagnostic build of the
+// library (tools/build_ablation.py defines DFP_HJ_ABLATIONS); the product library folds
+// kAbl to 0 and reads no environment for them.
+#ifdef DFP_HJ_ABLATIONS
+__constant__ int kAblDev;
+#define DFP_ABL(bit) (kAblDev & (bit))
+#else
+#define DFP_ABL(bit) 0
+#endif
+
 template <bool HASHED, int W>
 __global__ void __launch_bounds__(kSlThreads)
 sl_lookup_kernel(TableView tv, uint32_t wlog, uint32_t nslices, int64_t ntiles, uint32_t parts,
                  const void* __restrict__ ko, uint32_t* __restrict__ res, const uint16_t* __restrict__ toff,
-                 unsigned long long* __restrict__ tcnt, int dbg) {
+                 unsigned long long* __restrict__ tcnt) {
     extern __shared__ __attribute__((aligned(16))) uint32_t s_tab[];  // dense: 2^wlog refs; hashed: 2048 buckets
     __shared__ uint32_t s_base[kSlThreads];
     __shared__ uint32_t s_lane[kSlThreads];  // per wave: tile lane of each non-empty segment, by rank
@@ -1700,7 +1710,7 @@ sl_lookup_kernel(TableView tv, uint32_t wlog, uint32_t nslices, int64_t ntiles, 
     __shared__ uint32_t s_cst[kSlThreads];
     __shared__ uint32_t s_end[HASHED ? kSlThreads : 1];  // hashed, per wave: end position of each fragment, by rank
     __shared__ unsigned long long s_mask[kSlThreads / 64][W / 64];
-    const uint32_t item = (dbg & 128) ? blockIdx.x : xcd_item(blockIdx.x, gridDim.x);
+    const uint32_t item = DFP_ABL(128) ? blockIdx.x : xcd_item(blockIdx.x, gridDim.x);
     const uint32_t s = item % nslices, part = item / nslices;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     uint32_t sbase = 0;  // hashed: first bucket of the slice
@@ -1839,7 +1849,7 @@ sl_lookup_kernel(TableView tv, uint32_t wlog, uint32_t nslices, int64_t ntiles, 
                     if (o == kOob) {
                         v = kMiss;  // no store, no correction
                         c = 1;
-                    } else if (dbg & 4) {  // timing ablation: no bucket lookup (wrong pairs)
+                    } else if (DFP_ABL(4)) {  // timing ablation: no bucket lookup (wrong pairs)
                         v = (uint32_t)sk & 0xFFFFFFu;
                         c = 1;
                     } else if (sk == 0) {  // key 0: the side bucket (rare; loaded at the start)
@@ -2029,7 +2039,7 @@ __global__ void __launch_bounds__(kSlEmitThreads, 4)  // two workgroups per CU: 
 sl_emit_kernel(TableView tv, uint32_t nslices, const uint16_t* __restrict__ rl, const uint32_t* __restrict__ res,
                const uint16_t* __restrict__ toff, const uint32_t* __restrict__ probe_ids, uint32_t pbase,
                const unsigned long long* __restrict__ tcnt, int64_t ntiles, uint64_t* __restrict__ out_b,
-               uint32_t* __restrict__ out_p, int64_t cap, int64_t* __restrict__ d_total, int dbg) {
+               uint32_t* __restrict__ out_p, int64_t cap, int64_t* __restrict__ d_total) {
     __shared__ __attribute__((aligned(16))) uint32_t s_ref[kSlTile];  // the tile's refs, kMiss = none
     __shared__ unsigned long long s_w[kSlEmitThreads / 64];
     __shared__ unsigned long long s_pre[kSlEmitThreads / 64];
@@ -2051,7 +2061,7 @@ sl_emit_kernel(TableView tv, uint32_t nslices, const uint16_t* __restrict__ rl, 
         return v;
     };
     auto fetch = [&](int64_t t) {
-        cnt = (dbg & 2) ? 0u : toff[t * (int64_t)(nslices + 1) + nslices];
+        cnt = DFP_ABL(2) ? 0u : toff[t * (int64_t)(nslices + 1) + nslices];
         const uint16_t* te = rl + t * kSlTile;
         const uint32_t* tr = res + t * kSlTile;
 #pragma unroll
@@ -2105,7 +2115,7 @@ sl_emit_kernel(TableView tv, uint32_t nslices, const uint16_t* __restrict__ rl, 
             tile_total += s_w[w];
         }
         if (tile == ntiles - 1 && threadIdx.x == 0) *d_total = (int64_t)(base + tile_total);
-        if (!(dbg & 1)) {
+        if (!DFP_ABL(1)) {
             // pass 2: write the wave's pairs, 64 rows per step. Steps whose rows all have
             // at most one pair store them directly; a step with a duplicated key expands
             // its pairs over the lanes, 64 output positions at a time (owner row by a
@@ -2151,7 +2161,7 @@ sl_emit_kernel(TableView tv, uint32_t nslices, const uint16_t* __restrict__ rl, 
                         const unsigned long long o = pos + p;
                         if (p < total && o < (unsigned long long)cap) {
                             const uint32_t br = !(rj & kDupFlag) ? rj
-                                                : (dbg & 8) ? (rj & tv.off_mask) + (p - xj)  // ablation: no segment reads
+                                                : DFP_ABL(8) ? (rj & tv.off_mask) + (p - xj)  // ablation: no segment reads
                                                             : tv.dup_rows[(rj & tv.off_mask) + 1 + (p - xj)];
                             const int64_t rowj = tile0 + row_w + k + j;
                             out_b[o] = HAS_ROW_IDS ? tv.row_ids[br] : (uint64_t)br;
@@ -2886,12 +2896,16 @@ hipError_t launch_probe_sliced(int key_bytes, const TableView& tv, const void* k
     }();
     uint32_t parts = std::max<uint32_t>(1, (target + nsl - 1) / nsl);
     parts = (uint32_t)std::min<int64_t>(parts, (nt + 63) / 64);
-    // timing ablations only (wrong pairs): emit 1 no stores, 2 no entries, 8 no duplicate
+#ifdef DFP_HJ_ABLATIONS
+    // diagnostic build only (wrong pairs): emit 1 no stores, 2 no entries, 8 no duplicate
     // segment reads; lookup 4 no bucket lookup (hashed), 128 plain item order
-    static const int sl_dbg = [] {
-        const char* ev = getenv("DFP_HJ_SL_DBG");
-        return ev ? atoi(ev) : 0;
+    static const bool abl_set = [] {
+        const char* ev = getenv("DFP_HJ_ABLATE");
+        const int v = ev ? atoi(ev) : 0;
+        return hipMemcpyToSymbol(HIP_SYMBOL(kAblDev), &v, sizeof(v)) == hipSuccess;
     }();
+    (void)abl_set;
+#endif
     const size_t tab_lds = hashed ? (sizeof(Bucket) << kHsSliceLog) : (sizeof(uint32_t) << wlog);
     const void* lk = hashed ? (const void*)sl_lookup_kernel<true, kSlOwnWinHashed>
                             : (const void*)sl_lookup_kernel<false, kSlOwnWin>;
@@ -2903,15 +2917,15 @@ hipError_t launch_probe_sliced(int key_bytes, const TableView& tv, const void* k
     }
     if (hashed)
         sl_lookup_kernel<true, kSlOwnWinHashed><<<nsl * parts, kSlThreads, tab_lds, s>>>(tv, wlog, nsl, nt, parts, w.ko,
-                                                                                       w.res, w.toff, w.tcnt, sl_dbg);
+                                                                                       w.res, w.toff, w.tcnt);
     else
         sl_lookup_kernel<false, kSlOwnWin><<<nsl * parts, kSlThreads, tab_lds, s>>>(tv, wlog, nsl, nt, parts, w.ko,
-                                                                                  w.res, w.toff, w.tcnt, sl_dbg);
+                                                                                  w.res, w.toff, w.tcnt);
     const bool ri = tv.row_ids != nullptr, pi = probe_ids != nullptr;
     const unsigned egrid = (unsigned)std::min<int64_t>(nt, (int64_t)sl_emit_wgs_per_cu() * sl_num_cus());
 #define DFP_SLE(RI, PI)                                                                                           \
     sl_emit_kernel<RI, PI><<<egrid, kSlEmitThreads, 0, s>>>(tv, nsl, w.rl, w.res, w.toff, probe_ids, pbase, w.tcnt, nt, \
-                                                           out_b, out_p, cap, d_total, sl_dbg)
+                                                           out_b, out_p, cap, d_total)
     if (ri && pi) DFP_SLE(true, true);
     else if (ri) DFP_SLE(true, false);
     else if (pi) DFP_SLE(false, true);

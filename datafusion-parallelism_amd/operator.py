@@ -51,7 +51,7 @@ import pyarrow.compute as pc
 import torch
 
 from ._lib import HjError, HJ_ERR_INVALID
-from .columns import DeviceColumn, composite_keys, filter_equal_pairs, mark_rows, select_rows
+from .columns import DeviceColumn, DeviceRecordBatch, composite_keys, filter_equal_pairs, mark_rows, select_rows
 from .table import HashTable
 
 
@@ -162,34 +162,30 @@ class GpuIndexLookup:
         equality filter as device tensors (build int64, probe int32). One Int32/Int64
         key: the table compares exact keys (fused). Composite keys: candidates of equal
         composite key, then hj_filter_equal_pairs on the key columns."""
-        arrays = [probe_keys] if isinstance(probe_keys, (pa.Array, pa.ChunkedArray)) else list(probe_keys)
+        arrays = ([probe_keys] if isinstance(probe_keys, (pa.Array, pa.ChunkedArray, DeviceColumn))
+                  else list(probe_keys))
         if self._shared is not None and (self._shared.composite or not _is_simple_key(arrays)):
             return self._composite_matches(arrays, build_side_records)
         if not _is_simple_key(arrays):
             raise HjError(HJ_ERR_INVALID, "probe keys do not match the build keys (one Int32/Int64 column)")
         probe_keys = arrays[0]
-        keys = DeviceColumn.from_arrow(probe_keys, self.device)
-        n = len(probe_keys)
+        n = probe_keys.length if isinstance(probe_keys, DeviceColumn) else len(probe_keys)
         if n == 0:
             return (torch.empty(0, dtype=torch.int64, device=self.device),
                     torch.empty(0, dtype=torch.int32, device=self.device))
-        dt = torch.int64 if pa.types.is_int64(probe_keys.type) else torch.int32
-        kt = keys.data.view(dt)[:n]
-        valid = None
-        if keys.valid is not None:
-            bits = np.unpackbits(keys.valid.cpu().numpy(), bitorder="little")[keys.voff:keys.voff + n]
-            valid = bits.astype(bool)
-        return self.table.probe(kt, valid, device_output=True)
+        keys = probe_keys if isinstance(probe_keys, DeviceColumn) else DeviceColumn.from_arrow(probe_keys, self.device)
+        # the device validity bitmap goes to the probe as is, from bit voff (no host read)
+        return self.table.probe(keys.key_tensor(), keys.valid, device_output=True, valid_offset=keys.voff)
 
     def _composite_matches(self, arrays: list[pa.Array], build_side_records: pa.RecordBatch | None):
         sh = self._shared
         if len(arrays) != len(sh.key_exprs):
             raise HjError(HJ_ERR_INVALID, f"{len(arrays)} probe key columns for {len(sh.key_exprs)} build key columns")
-        n = len(arrays[0])
+        pcols = [a if isinstance(a, DeviceColumn) else DeviceColumn.from_arrow(a, self.device) for a in arrays]
+        n = pcols[0].length
         if n == 0:
             return (torch.empty(0, dtype=torch.int64, device=self.device),
                     torch.empty(0, dtype=torch.int32, device=self.device))
-        pcols = [DeviceColumn.from_arrow(a, self.device) for a in arrays]
         keys, valid = composite_keys(pcols)
         b, p = self.table.probe(keys, valid, device_output=True)
         rb = build_side_records if build_side_records is not None else sh.concatenated()
@@ -202,7 +198,9 @@ class GpuIndexLookup:
         b, p = self.table.probe(probe_keys)
         return pa.array(b, type=pa.uint64()), pa.array(p, type=pa.uint32())
 
-    def build_columns(self, build_side_records: pa.RecordBatch) -> list[DeviceColumn]:
+    def build_columns(self, build_side_records) -> list[DeviceColumn]:
+        if isinstance(build_side_records, DeviceRecordBatch):  # resident since the build
+            return build_side_records.device_columns
         if self._shared is not None:
             return self._shared.device_columns(build_side_records, self.device)
         return [DeviceColumn.from_arrow(c, self.device) for c in build_side_records.columns]
@@ -217,10 +215,12 @@ class _SharedBuild:
         self.lock = threading.Lock()
         self.table: HashTable | None = None
         self.key_type: str | None = None
-        self.batches: list[list[pa.RecordBatch]] = [[] for _ in range(parallelism)]
+        # per partition, its batches' columns uploaded once on arrival (DeviceColumn) and
+        # their row counts
+        self.batches: list[list[tuple[list[DeviceColumn], int]]] = [[] for _ in range(parallelism)]
         self.taken = [False] * parallelism
         self.ready = threading.Barrier(parallelism)
-        self.record_batch: pa.RecordBatch | None = None
+        self.record_batch: DeviceRecordBatch | None = None
         self.schema: pa.Schema | None = None
         self._dev_cols: list[DeviceColumn] | None = None
         self.composite = False          # keys through hj_composite_keys (several / non-integer columns)
@@ -235,23 +235,29 @@ class _SharedBuild:
                 raise HjError(HJ_ERR_INVALID, "all build batches must have the same key type")
             return self.table
 
-    def concatenated(self) -> pa.RecordBatch:
-        """Build RecordBatch in canonical order (partition 0 batches, then 1, ...):
-        row i <-> build index i (cooperatively_concatenate_arrow_arrays,
-        src/operator/version10/parallel_join_execution_state.rs:256-298)."""
+    def concatenated(self) -> DeviceRecordBatch:
+        """Build RecordBatch in canonical order (partition 0 batches, then 1, ...): row i
+        <-> build index i, concatenated on the device from the batches' resident columns
+        (cooperatively_concatenate_arrow_arrays,
+        src/operator/version10/parallel_join_execution_state.rs:256-298): no host
+        combine_chunks and no second upload."""
         with self.lock:
             if self.record_batch is None:
-                all_batches = [b for part in self.batches for b in part]
-                if all_batches:
-                    tbl = pa.Table.from_batches(all_batches).combine_chunks()
-                    self.record_batch = tbl.to_batches()[0] if tbl.num_rows else pa.RecordBatch.from_pylist(
-                        [], schema=tbl.schema)
+                parts = [b for part in self.batches for b in part]
+                schema = self.schema or pa.schema([])
+                if parts:
+                    ncol = len(parts[0][0])
+                    cols = [DeviceColumn.concat([p[0][j] for p in parts]) for j in range(ncol)]
+                    self.record_batch = DeviceRecordBatch(schema, cols, sum(p[1] for p in parts))
                 else:
-                    self.record_batch = pa.RecordBatch.from_pylist([], schema=self.schema or pa.schema([]))
+                    dev = torch.device("cuda", self.device)
+                    empty = [DeviceColumn.from_arrow(pa.array([], type=f.type), dev) for f in schema]
+                    self.record_batch = DeviceRecordBatch(schema, empty, 0)
             return self.record_batch
 
     def device_columns(self, rb: pa.RecordBatch, device) -> list[DeviceColumn]:
-        """The concatenated build batch in HBM, uploaded once for all partitions."""
+        """A host build batch's columns in HBM, uploaded once for all partitions (callers
+        that pass their own RecordBatch instead of the resident one)."""
         with self.lock:
             if self._dev_cols is None:
                 self._dev_cols = [DeviceColumn.from_arrow(c, device) for c in rb.columns]
@@ -287,18 +293,25 @@ class BuildImplementation:
             raise HjError(HJ_ERR_INVALID, "an equi-join needs at least one key column")
         with sh.lock:
             sh.key_exprs = list(build_expressions)
+        dev = torch.device("cuda", sh.device)
         for batch in stream:
-            sh.batches[partition].append(batch)
-            if sh.schema is None:
-                sh.schema = batch.schema
+            with sh.lock:
+                if sh.schema is None:
+                    sh.schema = batch.schema
             if batch.num_rows == 0:
                 continue
+            # the batch's columns go to HBM once: the table reads its key column there, and
+            # the concatenated build batch is assembled from them on the device
+            dcols = [DeviceColumn.from_arrow(c, dev) for c in batch.columns]
+            sh.batches[partition].append((dcols, batch.num_rows))
             arrays = evaluate_expressions(build_expressions, batch)
+            kcols = [dcols[e if isinstance(e, int) else batch.schema.get_field_index(e)] for e in build_expressions]
             if _is_simple_key(arrays):
-                sh.table_for(_key_type(arrays[0])).append(partition, arrays[0])
+                k = kcols[0]
+                sh.table_for(_key_type(arrays[0])).append(partition, k.key_tensor(), valid=k.valid,
+                                                          valid_offset=k.voff)
             else:  # calculate_hash over every key column -> one int64 key per row
-                dev = torch.device("cuda", sh.device)
-                keys, valid = composite_keys([DeviceColumn.from_arrow(a, dev) for a in arrays])
+                keys, valid = composite_keys(kcols)
                 with sh.lock:
                     sh.composite = True
                 sh.table_for("int64").append(partition, keys, valid=valid)
@@ -337,12 +350,14 @@ def probe_batch(join_type: JoinType, probe_expressions: Sequence[str | int], bui
     jt = JoinType.parse(join_type)
     lookup = read_only_join_map
     dev = lookup.device
-    probe_keys = evaluate_expressions(probe_expressions, probe_batch)
     n = probe_batch.num_rows
-    b, p = lookup.matching_indices_device(probe_keys, build_side_records)
+    # the probe batch goes to HBM once: its key columns feed the lookup, all columns the take
+    probe_cols = [DeviceColumn.from_arrow(c, dev) for c in probe_batch.columns]
+    key_cols = [probe_cols[e if isinstance(e, int) else probe_batch.schema.get_field_index(e)]
+                for e in probe_expressions]
+    b, p = lookup.matching_indices_device(key_cols, build_side_records)
     build_cols = lookup.build_columns(build_side_records)
     bnames, pnames = list(build_side_records.schema.names), list(probe_batch.schema.names)
-    probe_cols = [DeviceColumn.from_arrow(c, dev) for c in probe_batch.columns]
     if filter is not None:
         b, p = _apply_filter(filter, build_cols, bnames, probe_cols, pnames, b, p)
     if jt.marks_build and build_visited is not None:

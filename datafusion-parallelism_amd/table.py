@@ -41,8 +41,10 @@ def _key_type_of_dtype(dt) -> int:
     raise TypeError(f"join keys must be int32 or int64, got {dt}")
 
 
-def as_key_input(keys, valid=None) -> KeyInput:
-    """Normalise a key column into raw pointers for the C ABI."""
+def as_key_input(keys, valid=None, valid_offset: int = 0) -> KeyInput:
+    """Normalise a key column into raw pointers for the C ABI. `valid`: a bool mask (one
+    per row), or an LSB validity bitmap (uint8 tensor / array) whose bit `valid_offset` is
+    row 0 — a device bitmap goes to the ABI as is (no host round trip)."""
     if pa is not None and isinstance(keys, pa.ChunkedArray):
         keys = keys.combine_chunks()
     if pa is not None and isinstance(keys, pa.Array):
@@ -63,25 +65,35 @@ def as_key_input(keys, valid=None) -> KeyInput:
         kt = _key_type_of_dtype(keys.dtype)
         t = keys.contiguous()
         flags = HJ_INPUT_DEVICE if t.is_cuda else 0
-        vptr, keep_v = None, None
+        vptr, keep_v, voff = None, None, 0
         if valid is not None:
             vb = torch.as_tensor(valid)
             if vb.dtype == torch.bool:  # mask -> LSB bitmap
+                if valid_offset:
+                    raise ValueError("valid_offset applies to a bitmap, not to a bool mask")
                 bits = np.packbits(vb.cpu().numpy(), bitorder="little")
                 vb = torch.from_numpy(bits)
-                if t.is_cuda:
-                    vb = vb.to(t.device)
+            elif vb.dtype == torch.uint8:
+                voff = int(valid_offset)
+            else:
+                raise TypeError("validity must be a bool mask or a uint8 bitmap")
+            if t.is_cuda and not vb.is_cuda:
+                vb = vb.to(t.device)
             keep_v = vb.contiguous()
             vptr = keep_v.data_ptr()
-        return KeyInput(t.data_ptr(), vptr, 0, t.numel(), flags, kt, (t, keep_v))
+        return KeyInput(t.data_ptr(), vptr, voff, t.numel(), flags, kt, (t, keep_v))
     a = np.ascontiguousarray(np.asarray(keys))
     kt = _key_type_of_dtype(a.dtype)
-    vptr, keep_v = None, None
+    vptr, keep_v, voff = None, None, 0
     if valid is not None:
-        bits = np.packbits(np.asarray(valid, dtype=bool), bitorder="little")
+        va = np.asarray(valid)
+        if va.dtype == np.uint8:  # already a bitmap
+            bits, voff = np.ascontiguousarray(va), int(valid_offset)
+        else:
+            bits = np.packbits(va.astype(bool), bitorder="little")
         keep_v = bits
         vptr = bits.ctypes.data
-    return KeyInput(a.ctypes.data if a.size else 0, vptr, 0, a.size, 0, kt, (a, keep_v))
+    return KeyInput(a.ctypes.data if a.size else 0, vptr, voff, a.size, 0, kt, (a, keep_v))
 
 
 def _producer_stream(keys, device: int) -> int | None:
@@ -118,10 +130,12 @@ class HashTable:
         self._keep = []  # borrowed device inputs stay alive until the table is freed
 
     # -- build --------------------------------------------------------------
-    def append(self, partition: int, keys, valid=None, ids=None, borrow: bool = True, ids_u31: bool = False) -> None:
+    def append(self, partition: int, keys, valid=None, ids=None, borrow: bool = True, ids_u31: bool = False,
+               valid_offset: int = 0) -> None:
         """ids_u31: the explicit ids are < 2^31 and ascend in canonical row order (the
-        table then stores them in place of row numbers, HJ_IDS_U31)."""
-        ki = as_key_input(keys, valid)
+        table then stores them in place of row numbers, HJ_IDS_U31). valid: bool mask or
+        LSB bitmap starting at bit valid_offset (as_key_input)."""
+        ki = as_key_input(keys, valid, valid_offset)
         if ki.n and ki.key_type != self.key_type:
             raise TypeError("key type of the batch differs from the table's")
         # borrowed device inputs are kept alive (self._keep) until close(), which frees the
@@ -206,13 +220,14 @@ class HashTable:
         return out[:nrows]
 
     # -- probe --------------------------------------------------------------
-    def probe(self, keys, valid=None, device_output: bool = False):
+    def probe(self, keys, valid=None, device_output: bool = False, valid_offset: int = 0):
         """Synchronous probe; returns (build_idx uint64, probe_idx uint32) in canonical
         order as numpy arrays, or as torch device tensors (int64, int32) with
-        device_output=True (then keys must be a device tensor)."""
+        device_output=True (then keys must be a device tensor; a device bitmap `valid`
+        with `valid_offset` is read in place)."""
         if device_output:
-            return self._probe_device(keys, valid)
-        ki = as_key_input(keys, valid)
+            return self._probe_device(keys, valid, valid_offset)
+        ki = as_key_input(keys, valid, valid_offset)
         if ki.n and ki.key_type != self.key_type:
             raise TypeError("probe key type differs from the build key type")
         pr = _lib.HjPairs()
@@ -227,10 +242,10 @@ class HashTable:
         finally:
             self._L.hj_pairs_free(ctypes.byref(pr))
 
-    def _probe_device(self, keys: torch.Tensor, valid=None):
+    def _probe_device(self, keys: torch.Tensor, valid=None, valid_offset: int = 0):
         if not (isinstance(keys, torch.Tensor) and keys.is_cuda):
             raise TypeError("device_output=True takes a device tensor of keys")
-        ki = as_key_input(keys, valid)
+        ki = as_key_input(keys, valid, valid_offset)
         if ki.n and ki.key_type != self.key_type:
             raise TypeError("probe key type differs from the build key type")
         dev = keys.device
@@ -255,7 +270,10 @@ class HashTable:
                     d_total_ptr: int, workspace_ptr: int, stream: int = 0, valid_ptr: int | None = None,
                     voff: int = 0, probe_ids_ptr: int | None = None, probe_base: int = 0) -> None:
         """hj_probe_async(_ids, _base) on raw device pointers (no sync, no allocation):
-        probe_idx = row, probe_ids[row], or probe_base + row."""
+        probe_idx = row, probe_ids[row], or probe_base + row (ids and a base together are
+        refused: the ids are the probe indices)."""
+        if probe_ids_ptr is not None and probe_base:
+            raise ValueError("probe_ids_ptr and probe_base are exclusive: add the base to the ids")
         if probe_ids_ptr is None and probe_base:
             check(self._L.hj_probe_async_base(self._h, keys_ptr, valid_ptr, voff, n, probe_base, out_build_ptr,
                                               out_probe_ptr, capacity, d_total_ptr, workspace_ptr, stream or None))
