@@ -459,8 +459,9 @@ def main():
                     help="single GPU: HIP stream priorities of the probe / build streams")
     ap.add_argument("--force-dist", action="store_true",
                     help="use the radix-exchange path even with one rank (testing)")
-    ap.add_argument("--chunks", type=int, default=4,
-                    help="multi-GPU: probe-side chunks whose exchange overlaps the previous chunk's probe")
+    ap.add_argument("--chunks", type=int, default=1,
+                    help="multi-GPU radix plan: probe-side chunks whose exchange overlaps the previous chunk's probe "
+                         "(each chunk's probe reloads the table's slices; 1 = one probe)")
     ap.add_argument("--same-stream", action="store_true",
                     help="run each build on the probe's stream (no build/probe overlap)")
     ap.add_argument("--sync-steps", action="store_true",
@@ -646,10 +647,13 @@ def main():
 
 
 class DistJob:
-    """One step = radix-partition + RCCL all-to-all of the build side, local build, then
-    the probe side in chunks whose all-to-all overlaps the previous chunk's probe.
-    exchange_ms = the build-side exchange; probe_ms (HIP events) = local build +
-    pipelined probe-side exchange and probes."""
+    """One step = the radix plan (DistributedHashJoin.join): global key range (one host
+    read), both sides partitioned in one pass each into per-destination regions (runtime
+    filter, int32 key offsets, u32 ids), one count exchange for both sides (one host read),
+    the build side's regions exchanged (RCCL point to point; a rank's own region stays in
+    place) and built with global ids, the probe side's exchanged and probed once with
+    global probe ids. exchange_ms = from the end of the partitions to the end of the
+    exchanges (events); probe_ms = the whole step on the device."""
 
     def __init__(self, dj, bk, pk, bbase, pbase, dev):
         self.dj, self.bk, self.pk, self.dev = dj, bk, pk, dev
@@ -658,41 +662,34 @@ class DistJob:
         self.probe_ms, self.build_ms, self.exchange_ms = [], [], []
         self.matches = 0
         self.cap = pk.numel()
-        self.kernel_desc = "radix partition + RCCL all-to-all + local build + probe"
-        self._ev = None
+        self.kernel_desc = ("one-pass region partition (both sides) + RCCL point-to-point exchange + local build + "
+                            "sliced probe with global ids")
+        self._pending = None
 
     def step(self):
-        t0 = time.perf_counter()
-        plan = self.dj.prepare(self.bk, self.pk, self.bbase)
-        bk, bi = self.dj.shard_build(self.bk, self.bbase, plan)
-        torch.cuda.synchronize(self.dev)
-        t1 = time.perf_counter()
-        self.exchange_ms.append((t1 - t0) * 1e3)
-        ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
-        ev[0].record()
-        if self.dj.chunks > 1:
-            outs = self.dj.run_pipelined(bk, bi, self.pk, self.pbase, plan)
-        else:
-            from datafusion_parallelism_amd.distributed import gpu_local_join
-
-            pk, pi, _ = self.dj.shard(self.pk, self.pbase, torch.int32, key_offset=plan.key_offset, spec=plan.spec)
-            outs = [gpu_local_join(bk, bi, pk, pi, self.cap)]
-        ev[1].record()
-        self._ev = ev
-        self._t1 = t1
-        self.matches = sum(b.numel() for b, _ in outs)
+        ev = {k: torch.cuda.Event(enable_timing=True) for k in ("start", "partitioned", "exchanged", "end")}
+        self.dj.events = ev
+        ev["start"].record()
+        table, result = self.dj.join(self.bk, self.bbase, self.pk, self.pbase, self.cap, check=False)
+        ev["end"].record()
+        self.dj.events = None
+        self._pending = (table, result, ev)
 
     def collect(self):
-        if self._ev is None:
+        if self._pending is None:
             return
-        torch.cuda.synchronize(self.dev)
-        # local build + probe as one device interval (build is synchronous inside)
-        self.probe_ms.append(self._ev[0].elapsed_time(self._ev[1]))
+        table, result, ev = self._pending
+        b, _ = result()
+        self.matches = int(b.numel())
+        ev["end"].synchronize()
+        self.probe_ms.append(ev["start"].elapsed_time(ev["end"]))
+        self.exchange_ms.append(ev["partitioned"].elapsed_time(ev["exchanged"]))
         self.build_ms.append(0.0)
-        self._ev = None
+        table.close()
+        self._pending = None
 
     def finish(self):
-        pass
+        self.collect()
 
 
 class BroadcastJob:

@@ -449,12 +449,17 @@ hj_status build_attempt(hj_table* t, const std::vector<Segment>& segs, double lf
         fbig = (BigSeg*)p;
         if (t->has_ids) {  // explicit ids in row order: the table's row_ids, or scratch when held in place of rows
             uint64_t* dst = t->row_ids;
-            if (ids_as_rows) {
+            if (ids_as_rows && segs.size() == 1) {
+                ids32 = const_cast<uint64_t*>(segs[0].ids);  // one device segment: read in place (borrowed)
+                dst = nullptr;
+            } else if (ids_as_rows) {
                 if ((st = dev_alloc(t, t->scratch, &p, sizeof(uint64_t) * (size_t)total)) != HJ_OK) return st;
                 dst = ids32 = (uint64_t*)p;
             }
-            for (const Segment& sg : segs)
-                HIP_TRY(hipMemcpyAsync(dst + sg.row_base, sg.ids, sizeof(uint64_t) * (size_t)sg.n, hipMemcpyDefault, s));
+            if (dst != nullptr)
+                for (const Segment& sg : segs)
+                    HIP_TRY(hipMemcpyAsync(dst + sg.row_base, sg.ids, sizeof(uint64_t) * (size_t)sg.n,
+                                           hipMemcpyDefault, s));
         }
         hipDeviceProp_t* prop = device_props(t->device);
         const int cus = prop ? prop->multiProcessorCount : 256;
@@ -1598,6 +1603,67 @@ hj_status hj_radix_partition(hj_key_type key_type, const void* keys, const uint8
                              void* workspace, void* stream) {
     return hj_partition_rows(key_type, keys, validity, validity_offset, ids, id_base, n, nparts, nullptr, out_keys,
                              out_key_bytes, key_offset, out_ids, id_bytes, counts, workspace, stream);
+}
+
+namespace {
+// shared argument checks of hj_partition_rows / hj_partition_regions -> the kernel's map
+hj_status part_args(hj_key_type key_type, const void* keys, const uint8_t* validity, const uint64_t* ids,
+                    uint64_t id_base, int64_t n, int nparts, const hj_part_spec* spec, const void* out_keys,
+                    int out_key_bytes, int64_t key_offset, const void* out_ids, int id_bytes, const int64_t* counts,
+                    const void* workspace, PartSpec* ps) {
+    if (device_count() == 0) return fail(HJ_ERR_NO_DEVICE, "no GPU visible");
+    if (nparts < 1 || nparts > 64 || (nparts & (nparts - 1)))
+        return fail(HJ_ERR_INVALID, "nparts must be a power of two <= 64");
+    if (n < 0) return fail(HJ_ERR_INVALID, "negative length");
+    if (id_bytes != 4 && id_bytes != 8) return fail(HJ_ERR_INVALID, "id_bytes must be 4 or 8");
+    if (key_type != HJ_INT32 && key_type != HJ_INT64) return fail(HJ_ERR_INVALID, "unsupported key type");
+    const int kb = key_type == HJ_INT64 ? 8 : 4;
+    if ((out_key_bytes != 4 && out_key_bytes != 8) || out_key_bytes > kb)
+        return fail(HJ_ERR_INVALID, "out_key_bytes must be 4 or the key width");
+    if (kb == 4 && key_offset != 0) return fail(HJ_ERR_INVALID, "key_offset applies to int64 keys");
+    if (id_bytes == 4 && ids == nullptr && (uint64_t)id_base + (uint64_t)n > 0x100000000ull)
+        return fail(HJ_ERR_INVALID, "32-bit ids overflow: id_base + n > 2^32");
+    if (!is_device_ptr(keys) || !is_device_ptr(validity) || !is_device_ptr(ids) || !is_device_ptr(out_keys) ||
+        !is_device_ptr(out_ids) || !is_device_ptr(counts) || !is_device_ptr(workspace))
+        return fail(HJ_ERR_INVALID, "the partition takes device pointers");
+    *ps = PartSpec{INT64_MIN, INT64_MAX, 0, 0};
+    if (spec != nullptr) {
+        if (spec->key_lo > spec->key_hi) return fail(HJ_ERR_INVALID, "hj_part_spec: key_lo > key_hi");
+        ps->lo = spec->key_lo;
+        ps->hi = spec->key_hi;
+        ps->by_range = spec->by_range != 0;
+        if (ps->by_range) {
+            // mul = floor(2^64 * nparts / range), range = hi - lo + 1 in [1, 2^64]
+            const unsigned __int128 range = (unsigned __int128)((uint64_t)ps->hi - (uint64_t)ps->lo) + 1;
+            const unsigned __int128 m = ((unsigned __int128)nparts << 64) / range;
+            ps->mul = m > (unsigned __int128)UINT64_MAX ? UINT64_MAX : (uint64_t)m;
+        }
+    }
+    return HJ_OK;
+}
+}  // namespace
+
+int64_t hj_partition_regions_workspace_bytes(int64_t n, int nparts) {
+    return radix_regions_workspace(n < 0 ? 0 : n, nparts < 1 ? 1 : nparts);
+}
+
+hj_status hj_partition_regions(hj_key_type key_type, const void* keys, const uint8_t* validity,
+                               int64_t validity_offset, const uint64_t* ids, uint64_t id_base, int64_t n, int nparts,
+                               const hj_part_spec* spec, void* out_keys, int out_key_bytes, int64_t key_offset,
+                               void* out_ids, int id_bytes, int64_t region_rows, int64_t* counts, void* workspace,
+                               void* stream) {
+    PartSpec ps;
+    hj_status st = part_args(key_type, keys, validity, ids, id_base, n, nparts, spec, out_keys, out_key_bytes,
+                             key_offset, out_ids, id_bytes, counts, workspace, &ps);
+    if (st != HJ_OK) return st;
+    if (region_rows < 0) return fail(HJ_ERR_INVALID, "negative region_rows");
+    if (n > 0 && (keys == nullptr || out_keys == nullptr || out_ids == nullptr || counts == nullptr ||
+                  workspace == nullptr))
+        return fail(HJ_ERR_INVALID, "null pointer");
+    HIP_TRY(launch_radix_regions(key_type == HJ_INT64 ? 8 : 4, keys, validity, validity_offset, ids, id_base, n,
+                                 nparts, ps, out_keys, out_key_bytes, key_offset, out_ids, id_bytes, region_rows,
+                                 counts, workspace, (hipStream_t)stream));
+    return HJ_OK;
 }
 
 hj_status hj_partition_rows(hj_key_type key_type, const void* keys, const uint8_t* validity, int64_t validity_offset,

@@ -1335,7 +1335,8 @@ sl_partition_kernel(int64_t dmin, uint64_t drange, uint32_t wlog, uint32_t nslic
                     uint16_t* __restrict__ ko, uint16_t* __restrict__ rl, uint16_t* __restrict__ toff, int nt,
                     int64_t tile_off, int64_t row_base, uint32_t* __restrict__ tile_base,
                     unsigned long long* __restrict__ hdr,  // probe: workspace header (error word at [1]); build: null
-                    unsigned long long* __restrict__ tcnt) {    // probe: the tile's entry count; build: null
+                    unsigned long long* __restrict__ tcnt,      // probe: the tile's entry count; build: null
+                    uint32_t* __restrict__ tent) {  // probe: entries of the tile so far (earlier passes: append after them)
     __shared__ __attribute__((aligned(16))) uint32_t s_ent[kSlTile];
     __shared__ uint32_t s_hist[2 * kSlThreads];  // bins 0..nslices (<= kSlMaxSlices + 1)
     __shared__ uint32_t s_w[kSlThreads / 64];
@@ -1343,6 +1344,9 @@ sl_partition_kernel(int64_t dmin, uint64_t drange, uint32_t wlog, uint32_t nslic
     const int64_t gtile = tile + tile_off;    // its output region (the build partitions several arrays)
     const int64_t tile0 = tile * kSlTile;
     const uint32_t nbins = nslices + 1;  // bin nslices stays empty: its prefix is the total
+    // multi-pass probe (tables beyond kSlMaxSlices slices): this pass's entries follow the
+    // tile's entries of the earlier passes (hdr == null marks a later pass)
+    const uint32_t ebase = (tent != nullptr && hdr == nullptr) ? tent[gtile] : 0u;
     for (uint32_t b = threadIdx.x; b < 2 * kSlThreads; b += kSlThreads) s_hist[b] = 0;
     // probe: zero the workspace header incl. the error word (no memset launch)
     if (hdr != nullptr && blockIdx.x == 0 && threadIdx.x == 0) hdr[0] = hdr[1] = 0;
@@ -1375,11 +1379,13 @@ sl_partition_kernel(int64_t dmin, uint64_t drange, uint32_t wlog, uint32_t nslic
     s_hist[b0 + 1] = ex + h0;
     __syncthreads();
     uint16_t* to = toff + gtile * (int64_t)nbins;
-    for (uint32_t b = threadIdx.x; b < nbins; b += kSlThreads) to[b] = (uint16_t)s_hist[b];
+    for (uint32_t b = threadIdx.x; b < nbins; b += kSlThreads) to[b] = (uint16_t)(ebase + s_hist[b]);
     if (tile_base != nullptr && threadIdx.x == 0) tile_base[gtile] = (uint32_t)(row_base + tile0);  // build only
     // probe: the tile's pair count starts as its entries (in-range rows); S2 adds count - 1
-    // for every entry whose key is missing (-1) or duplicated (+count - 1)
-    if (tcnt != nullptr && threadIdx.x == 0) tcnt[gtile] = tot;
+    // for every entry whose key is missing (-1) or duplicated (+count - 1). A later pass
+    // adds its entries to the count the earlier passes (and their lookups) left.
+    if (tcnt != nullptr && threadIdx.x == 0) tcnt[gtile] = (ebase ? tcnt[gtile] : 0ull) + tot;
+    if (tent != nullptr && threadIdx.x == 0) tent[gtile] = ebase + tot;
 #pragma unroll
     for (int g = 0; g < kSlGroups; ++g)
 #pragma unroll
@@ -1391,6 +1397,14 @@ sl_partition_kernel(int64_t dmin, uint64_t drange, uint32_t wlog, uint32_t nslic
     // the tile (u16, read by S3)
     uint16_t* dst = ko + gtile * kSlTile;
     uint16_t* dsr = rl + gtile * kSlTile;
+    if (ebase != 0) {  // a later pass: unaligned base, one entry per thread (2-byte stores)
+        for (uint32_t i = threadIdx.x; i < tot; i += kSlThreads) {
+            const uint32_t v = s_ent[i];
+            dst[ebase + i] = (uint16_t)(v >> kSlTileLog);
+            dsr[ebase + i] = (uint16_t)(v & (kSlTile - 1));
+        }
+        return;
+    }
     const uint32_t n4 = tot & ~3u;
     for (uint32_t i = threadIdx.x * 4; i < n4; i += kSlThreads * 4) {
         const uint4 v = *reinterpret_cast<const uint4*>(s_ent + i);
@@ -1701,7 +1715,7 @@ template <bool HASHED, int W>
 __global__ void __launch_bounds__(kSlThreads)
 sl_lookup_kernel(TableView tv, uint32_t wlog, uint32_t nslices, int64_t ntiles, uint32_t parts,
                  const void* __restrict__ ko, uint32_t* __restrict__ res, const uint16_t* __restrict__ toff,
-                 unsigned long long* __restrict__ tcnt) {
+                 unsigned long long* __restrict__ tcnt, uint32_t soff) {  // soff: first slice of this pass (hashed)
     extern __shared__ __attribute__((aligned(16))) uint32_t s_tab[];  // dense: 2^wlog refs; hashed: 2048 buckets
     __shared__ uint32_t s_base[kSlThreads];
     __shared__ uint32_t s_lane[kSlThreads];  // per wave: tile lane of each non-empty segment, by rank
@@ -1715,7 +1729,7 @@ sl_lookup_kernel(TableView tv, uint32_t wlog, uint32_t nslices, int64_t ntiles, 
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     uint32_t sbase = 0;  // hashed: first bucket of the slice
     if constexpr (HASHED) {
-        sbase = s << kHsSliceLog;
+        sbase = (soff + s) << kHsSliceLog;
         const uint32_t nbk = min<uint32_t>(1u << kHsSliceLog, tv.nb - sbase);
         const uint4* src = reinterpret_cast<const uint4*>(tv.tbl + sbase);
         uint4* dst = reinterpret_cast<uint4*>(s_tab);
@@ -1927,15 +1941,17 @@ sl_lookup_kernel(TableView tv, uint32_t wlog, uint32_t nslices, int64_t ntiles, 
 // once this tile's keys are staged, while they and the rows are written out.
 template <typename K, bool HAS_VALID>
 __global__ void __launch_bounds__(kSlThreads, 4)  // 16 waves per CU: <= 128 VGPRs
-hs_partition_kernel(uint32_t nb, uint32_t nslices, const void* __restrict__ keys,
+hs_partition_kernel(uint32_t nb, uint32_t s0, uint32_t nslices, const void* __restrict__ keys,
                     const uint8_t* __restrict__ valid, int64_t voff, int64_t n, int64_t ntiles, bool vec,
                     unsigned long long* __restrict__ ko, uint16_t* __restrict__ rl, uint16_t* __restrict__ toff,
-                    unsigned long long* __restrict__ hdr, unsigned long long* __restrict__ tcnt) {
+                    unsigned long long* __restrict__ hdr, unsigned long long* __restrict__ tcnt,
+                    uint32_t* __restrict__ tent) {  // pass: slices [s0, s0 + nslices); hdr null = a later pass
     __shared__ __attribute__((aligned(16))) unsigned long long s_key[kSlTile];  // also the rows (u16) pass
     __shared__ uint32_t s_hist[2 * kSlThreads];
     __shared__ uint32_t s_w[kSlThreads / 64];
     const uint32_t nbins = nslices + 1;
-    if (blockIdx.x == 0 && threadIdx.x == 0) hdr[0] = hdr[1] = 0;  // workspace header (error word)
+    const bool later = hdr == nullptr;
+    if (!later && blockIdx.x == 0 && threadIdx.x == 0) hdr[0] = hdr[1] = 0;  // workspace header (error word)
     int64_t k[kSlGroups][4], nk[kSlGroups][4];
     auto load = [&](int64_t t, int64_t (&dst)[kSlGroups][4]) {
 #pragma unroll
@@ -1951,6 +1967,7 @@ hs_partition_kernel(uint32_t nb, uint32_t nslices, const void* __restrict__ keys
 #pragma unroll
             for (int q = 0; q < 4; ++q) k[g][q] = nk[g][q];
         for (uint32_t b = threadIdx.x; b < 2 * kSlThreads; b += kSlThreads) s_hist[b] = 0;
+        const uint32_t ebase = later ? tent[tile] : 0u;
         __syncthreads();
         uint32_t sr[kSlGroups][4];  // slice << 14 | rank in slice, ~0 = no entry
 #pragma unroll
@@ -1959,9 +1976,9 @@ hs_partition_kernel(uint32_t nb, uint32_t nslices, const void* __restrict__ keys
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 const int64_t row = tile0 + loc0 + q;
-                const bool ok = row < n && (!HAS_VALID || bit_valid(valid, voff, row));
                 const unsigned long long sk = stored_key(k[g][q]);
-                const uint32_t sl = stored_bucket(sk, nb) >> kHsSliceLog;
+                const uint32_t sl = (stored_bucket(sk, nb) >> kHsSliceLog) - s0;  // wraps past the pass: no entry
+                const bool ok = row < n && (!HAS_VALID || bit_valid(valid, voff, row)) && sl < nslices;
                 sr[g][q] = ok ? (sl << kSlTileLog) | atomicAdd(&s_hist[sl], 1u) : 0xFFFFFFFFu;
             }
         }
@@ -1974,8 +1991,11 @@ hs_partition_kernel(uint32_t nb, uint32_t nslices, const void* __restrict__ keys
         s_hist[b0 + 1] = ex + h0;
         __syncthreads();
         uint16_t* to = toff + tile * (int64_t)nbins;
-        for (uint32_t b = threadIdx.x; b < nbins; b += kSlThreads) to[b] = (uint16_t)s_hist[b];
-        if (threadIdx.x == 0) tcnt[tile] = tot;  // S2 corrects it to the tile's pair count
+        for (uint32_t b = threadIdx.x; b < nbins; b += kSlThreads) to[b] = (uint16_t)(ebase + s_hist[b]);
+        if (threadIdx.x == 0) {
+            tcnt[tile] = (later ? tcnt[tile] : 0ull) + tot;  // S2 corrects it to the tile's pair count
+            tent[tile] = ebase + tot;
+        }
         // pass 1: stored keys in slice order
 #pragma unroll
         for (int g = 0; g < kSlGroups; ++g)
@@ -1985,10 +2005,14 @@ hs_partition_kernel(uint32_t nb, uint32_t nslices, const void* __restrict__ keys
                     s_key[s_hist[sr[g][q] >> kSlTileLog] + (sr[g][q] & (kSlTile - 1))] = stored_key(k[g][q]);
         __syncthreads();
         if (tile + (int64_t)gridDim.x < ntiles) load(tile + gridDim.x, nk);  // in flight during the write-out
-        unsigned long long* dk = ko + tile0;
-        for (uint32_t i = threadIdx.x * 2; i < tot; i += kSlThreads * 2) {
-            if (i + 2 <= tot) *reinterpret_cast<ulonglong2*>(dk + i) = *reinterpret_cast<const ulonglong2*>(s_key + i);
-            else dk[i] = s_key[i];
+        unsigned long long* dk = ko + tile0 + ebase;
+        if (ebase & 1) {  // a later pass at an odd base: 8-byte stores
+            for (uint32_t i = threadIdx.x; i < tot; i += kSlThreads) dk[i] = s_key[i];
+        } else {
+            for (uint32_t i = threadIdx.x * 2; i < tot; i += kSlThreads * 2) {
+                if (i + 2 <= tot) *reinterpret_cast<ulonglong2*>(dk + i) = *reinterpret_cast<const ulonglong2*>(s_key + i);
+                else dk[i] = s_key[i];
+            }
         }
         __syncthreads();
         // pass 2: rows in the tile (u16), same order
@@ -2001,10 +2025,14 @@ hs_partition_kernel(uint32_t nb, uint32_t nslices, const void* __restrict__ keys
                     s_row[s_hist[sr[g][q] >> kSlTileLog] + (sr[g][q] & (kSlTile - 1))] =
                         (uint16_t)(g * (kSlThreads * 4) + threadIdx.x * 4 + q);
         __syncthreads();
-        uint16_t* dr = rl + tile0;
-        for (uint32_t i = threadIdx.x * 8; i < tot; i += kSlThreads * 8) {
-            if (i + 8 <= tot) *reinterpret_cast<uint4*>(dr + i) = *reinterpret_cast<const uint4*>(s_row + i);
-            else for (uint32_t j = i; j < tot; ++j) dr[j] = s_row[j];
+        uint16_t* dr = rl + tile0 + ebase;
+        if (ebase & 7) {  // a later pass at an unaligned base: 2-byte stores
+            for (uint32_t i = threadIdx.x; i < tot; i += kSlThreads) dr[i] = s_row[i];
+        } else {
+            for (uint32_t i = threadIdx.x * 8; i < tot; i += kSlThreads * 8) {
+                if (i + 8 <= tot) *reinterpret_cast<uint4*>(dr + i) = *reinterpret_cast<const uint4*>(s_row + i);
+                else for (uint32_t j = i; j < tot; ++j) dr[j] = s_row[j];
+            }
         }
         __syncthreads();  // s_key / s_hist are rewritten for the next tile
     }
@@ -2036,8 +2064,8 @@ constexpr int kSlWaveRows = kSlTile / (kSlEmitThreads / 64);  // 2048
 
 template <bool HAS_ROW_IDS, bool HAS_PROBE_IDS>
 __global__ void __launch_bounds__(kSlEmitThreads, 4)  // two workgroups per CU: <= 128 VGPRs
-sl_emit_kernel(TableView tv, uint32_t nslices, const uint16_t* __restrict__ rl, const uint32_t* __restrict__ res,
-               const uint16_t* __restrict__ toff, const uint32_t* __restrict__ probe_ids, uint32_t pbase,
+sl_emit_kernel(TableView tv, const uint32_t* __restrict__ tent, const uint16_t* __restrict__ rl,
+               const uint32_t* __restrict__ res, const uint32_t* __restrict__ probe_ids, uint32_t pbase,
                const unsigned long long* __restrict__ tcnt, int64_t ntiles, uint64_t* __restrict__ out_b,
                uint32_t* __restrict__ out_p, int64_t cap, int64_t* __restrict__ d_total) {
     __shared__ __attribute__((aligned(16))) uint32_t s_ref[kSlTile];  // the tile's refs, kMiss = none
@@ -2061,7 +2089,7 @@ sl_emit_kernel(TableView tv, uint32_t nslices, const uint16_t* __restrict__ rl, 
         return v;
     };
     auto fetch = [&](int64_t t) {
-        cnt = DFP_ABL(2) ? 0u : toff[t * (int64_t)(nslices + 1) + nslices];
+        cnt = DFP_ABL(2) ? 0u : tent[t];  // the tile's entries over every pass
         const uint16_t* te = rl + t * kSlTile;
         const uint32_t* tr = res + t * kSlTile;
 #pragma unroll
@@ -2332,6 +2360,147 @@ part_scatter_kernel(const void* keys, const uint8_t* valid, int64_t voff, const 
 }
 
 // ---------------------------------------------------------------------------
+// radix partition into per-destination regions, one pass (the multi-GPU exchange's send
+// buffers). part_hist + scan + part_scatter read the keys twice and run five launches; here
+// every 16384-row tile reads its rows once: a stable wave multi-split (per-bit ballots)
+// ranks each row among its wave's rows of the same destination, a per-destination scan
+// over the tile's (iteration, wave) counts places it inside the tile, and a decoupled
+// look-back over the tiles' per-destination flags gives the tile's offset in each
+// destination region. Region d of the outputs starts at element d * cap: the regions are
+// the per-peer send buffers (no grouped copy), each in source row order (stable: received
+// build ids ascend, and a rank's received probe rows stay in global row order).
+// ---------------------------------------------------------------------------
+// 256-thread tiles of 4096 rows: several workgroups per CU, so that one tile's look-back
+// wait overlaps the others' loads (1024-thread, 16384-row tiles — one per CU — measured
+// 472 us for 10^8 rows: the CU idles through every look-back)
+constexpr int kRpThreads = 256;
+constexpr int kRpIters = 16;
+constexpr int kRpTile = kRpThreads * kRpIters;  // rows per tile
+constexpr int kRpSlots = kRpIters * (kRpThreads / 64);  // (iteration, wave) counts per destination
+static_assert(kRpSlots % 64 == 0, "the per-destination scan gives each lane whole slots");
+constexpr unsigned kRpSpinLimit = 1u << 22;
+
+template <typename K, typename OK, typename ID, bool HAS_VALID, bool HAS_IDS>
+__global__ void __launch_bounds__(kRpThreads)
+part_regions_kernel(const void* __restrict__ keys, const uint8_t* __restrict__ valid, int64_t voff,
+                    const uint64_t* __restrict__ ids, uint64_t id_base, int64_t n, int nparts, int bits, PartSpec sp,
+                    int64_t key_offset, OK* __restrict__ out_keys, ID* __restrict__ out_ids, int64_t cap,
+                    unsigned long long* flags, int64_t* __restrict__ counts, unsigned long long* err) {
+    extern __shared__ uint32_t s_cnt[];  // [nparts][kRpSlots]: rows per (iteration, wave), then their prefix
+    __shared__ unsigned long long s_off[kMaxParts];  // the tile's offset in each region
+    __shared__ uint32_t s_tot[kMaxParts];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int64_t tile0 = (int64_t)blockIdx.x * kRpTile;
+    for (int i = threadIdx.x; i < nparts * kRpSlots; i += kRpThreads) s_cnt[i] = 0;
+    __syncthreads();
+    int64_t key[kRpIters];
+    uint32_t dr[kRpIters];  // destination << 8 | rank among the wave's rows of it; ~0 = dropped
+    const unsigned long long lt = (1ull << lane) - 1;
+#pragma unroll
+    for (int it = 0; it < kRpIters; ++it) {
+        const int64_t row = tile0 + (int64_t)it * kRpThreads + threadIdx.x;
+        int p = -1;
+        key[it] = 0;
+        if (row < n) {
+            key[it] = (int64_t)reinterpret_cast<const K*>(keys)[row];
+            const bool ok = (!HAS_VALID || bit_valid(valid, voff, row)) && key[it] >= sp.lo && key[it] <= sp.hi;
+            if (ok)
+                p = sp.by_range ? (int)__umul64hi((uint64_t)key[it] - (uint64_t)sp.lo, sp.mul)
+                                : (int)(mix64((uint64_t)key[it]) & (uint64_t)(nparts - 1));
+        }
+        unsigned long long same = __ballot(p >= 0);
+        for (int bt = 0; bt < bits; ++bt) {
+            const unsigned long long m = __ballot(p >= 0 && ((p >> bt) & 1));
+            same &= ((p >> bt) & 1) ? m : ~m;
+        }
+        const uint32_t rank = (uint32_t)__popcll(same & lt);
+        if (p >= 0 && rank == 0) s_cnt[p * kRpSlots + it * (kRpThreads / 64) + wave] = (uint32_t)__popcll(same);
+        dr[it] = p >= 0 ? ((uint32_t)p << 8) | rank : 0xFFFFFFFFu;
+    }
+    __syncthreads();
+    // per destination: exclusive prefix over the (iteration, wave) slots in row order
+    for (int d = wave; d < nparts; d += kRpThreads / 64) {
+        uint32_t* c = s_cnt + d * kRpSlots;
+        constexpr int PER = kRpSlots / 64;
+        uint32_t v[PER], sum = 0;
+#pragma unroll
+        for (int q = 0; q < PER; ++q) {
+            v[q] = c[lane * PER + q];
+            sum += v[q];
+        }
+        const uint32_t incl = wave_incl_scan_dpp(sum);
+        uint32_t ex = incl - sum;
+#pragma unroll
+        for (int q = 0; q < PER; ++q) {
+            c[lane * PER + q] = ex;
+            ex += v[q];
+        }
+        if (lane == 63) s_tot[d] = incl;
+    }
+    __syncthreads();
+    // look-back (wave 0): lane l looks at destination l % nparts of tile t - 1 - l / nparts
+    // (a window of 64 / nparts tiles per round); per destination, the nearest inclusive
+    // flag ends its walk. Flags: status (1 aggregate, 2 inclusive) << 62 | value.
+    if (wave == 0) {
+        const int d = lane & (nparts - 1), k = lane >> bits;  // nparts <= 64: every lane maps
+        const int per = 64 >> bits;                           // tiles per window
+        const int64_t t = blockIdx.x;
+        const unsigned long long tot = s_tot[d];
+        if (k == 0) flag_store(flags + t * nparts + d, (t == 0 ? kFlagIncl : kFlagAgg) | tot);
+        unsigned long long excl = 0;
+        // lanes of one destination: bits d, d + nparts, ... of a mask
+        unsigned long long dmask = 0;
+        for (int q = 0; q < per; ++q) dmask |= 1ull << (q * nparts + d);
+        bool done = t == 0;
+        int64_t j0 = t - 1;  // window: tiles j0 - k
+        unsigned spins = 0;
+        while (__ballot(!done) != 0) {
+            const int64_t j = j0 - k;
+            unsigned long long f = kFlagIncl;  // before tile 0: an inclusive zero
+            if (!done && j >= 0) f = flag_load(flags + j * nparts + d);
+            const unsigned long long st = f >> 62;
+            const unsigned long long incl_m = __ballot(st == 2) & dmask;
+            const unsigned long long zero_m = __ballot(st == 0) & dmask;
+            // this destination's lanes up to its nearest inclusive flag (all if none)
+            const int first = incl_m ? __ffsll((long long)incl_m) - 1 : 63;
+            const unsigned long long need = dmask & ((2ull << first) - 1);
+            const bool wait = !done && (zero_m & need) != 0;
+            if (__ballot(wait) != 0) {
+                if (++spins > kRpSpinLimit) {  // never expected: report, do not hang
+                    if (lane == 0) atomicOr(err, 1ull);
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+                continue;
+            }
+            unsigned long long v = (!done && ((need >> lane) & 1)) ? (f & kFlagVal) : 0ull;
+            for (int o = nparts; o < 64; o <<= 1) v += __shfl_xor(v, o, 64);  // sum over the destination's lanes
+            if (!done) excl += v;
+            if (incl_m) done = true;
+            j0 -= per;
+        }
+        if (k == 0) {
+            if (t > 0) flag_store(flags + t * nparts + d, kFlagIncl | (excl + tot));
+            s_off[d] = excl;
+            if (t == (int64_t)gridDim.x - 1) counts[d] = (int64_t)(excl + tot);
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int it = 0; it < kRpIters; ++it) {
+        if (dr[it] == 0xFFFFFFFFu) continue;
+        const int d = (int)(dr[it] >> 8);
+        const int64_t row = tile0 + (int64_t)it * kRpThreads + threadIdx.x;
+        const unsigned long long pos =
+            s_off[d] + s_cnt[d * kRpSlots + it * (kRpThreads / 64) + wave] + (dr[it] & 0xFF);
+        if (pos >= (unsigned long long)cap) continue;  // region overflow: counts say so
+        const int64_t o = (int64_t)d * cap + (int64_t)pos;
+        out_keys[o] = (OK)(key[it] - key_offset);  // OK narrower: the caller checked the range
+        out_ids[o] = (ID)(HAS_IDS ? ids[row] : id_base + (uint64_t)row);
+    }
+}
+
+// ---------------------------------------------------------------------------
 // generators
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
@@ -2594,7 +2763,7 @@ hipError_t launch_build_frag(int key_bytes, const Segment* h_segs, int nseg, con
 #define DFP_BLP(KT, HV)                                                                                          \
     sl_partition_kernel<KT, HV><<<(unsigned)nt, kSlThreads, 0, s>>>(g.dmin, drange, wlog, nblk, sg.keys, sg.valid, \
                                                                    sg.voff, sg.n, vec, ko, rl, toff, 0, t0,          \
-                                                                   sg.row_base, tile_base, nullptr, nullptr)
+                                                                   sg.row_base, tile_base, nullptr, nullptr, nullptr)
         if (key_bytes == 8) {
             if (sg.valid) DFP_BLP(int64_t, true); else DFP_BLP(int64_t, false);
         } else {
@@ -2746,11 +2915,13 @@ ProbeWs probe_ws_layout(void* base, int64_t n) {
 }
 
 // sliced probe workspace (16384-row tiles), after the 16-byte header (error word at
-// bytes 8..15): tcnt u64[nt + 2] (pair counts) | toff u16[nt][kSlMaxSlices + 1] | toffT |
+// bytes 8..15): tcnt u64[nt + 2] (pair counts) | tent u32[nt + 2] (entries per tile over
+// the passes) | toff u16[nt][kSlMaxSlices + 1] (one pass's bounds) |
 // ko (entries: u16 key offsets in a dense slice, u64 stored keys in a hashed one; 8 B per
 // row reserved) | rl u16[nt * kSlTile] (rows in tile) | res u32[nt * kSlTile] (refs)
 struct SlicedWs {
     unsigned long long* tcnt;
+    uint32_t* tent;
     uint16_t* toff;
     void* ko;
     uint16_t* rl;
@@ -2762,7 +2933,8 @@ SlicedWs sliced_ws_layout(void* base, int64_t n) {
     SlicedWs w;
     uintptr_t p = (uintptr_t)base + 256;
     w.tcnt = (unsigned long long*)p;  p = al256(p + 8 * (nt + 2));
-    w.toff = (uint16_t*)p;            p = al256(p + 2 * nt * (kSlMaxSlices + 1));
+    w.tent = (uint32_t*)p;            p = al256(p + 4 * (nt + 2));
+    w.toff = (uint16_t*)p;            p = al256(p + 2 * nt * (kSlMaxSlices + 1));  // one pass's bounds
     w.ko = (void*)p;                  p = al256(p + 8 * nt * kSlTile);
     w.rl = (uint16_t*)p;              p = al256(p + 2 * nt * kSlTile);
     w.res = (uint32_t*)p;             p = al256(p + 4 * nt * kSlTile);
@@ -2838,12 +3010,20 @@ uint32_t sl_slices(const TableView& tv) {
 // the L2s (direct-addressed: > 1 M key values = 4 MB of refs; hashed: > 2^16 buckets =
 // 4 MB) and the probe side outweighs the slice loads (every slice is read once or a few
 // times per probe)
+// A table of more than kSlMaxSlices slices is probed in passes over consecutive slice
+// ranges (each pass partitions the probe rows of its range, appending to the tiles'
+// entries, and looks them up; one emission at the end). Every pass re-reads the probe
+// keys: auto takes up to kSlAutoPasses passes, a forced sliced probe any number.
+constexpr uint32_t kSlAutoPasses = 4;
+uint32_t sl_passes(uint32_t nsl) { return (nsl + kSlMaxSlices - 1) / kSlMaxSlices; }
+
 bool sl_auto(const TableView& tv, int64_t n) {
     static const int64_t min_range = [] {
         const char* e = getenv("DFP_HJ_SLICED_MIN_RANGE");
         return e ? atoll(e) : (int64_t)1 << 20;
     }();
     if (n < 4 * (int64_t)kSlTile) return false;
+    if (sl_passes(sl_slices(tv)) > kSlAutoPasses) return false;
     if (tv.dense == nullptr) return (int64_t)tv.nb * 16 >= min_range && n >= (int64_t)tv.nb;
     return (int64_t)tv.drange >= min_range && n >= (int64_t)tv.drange;
 }
@@ -2854,7 +3034,8 @@ hipError_t launch_probe_sliced(int key_bytes, const TableView& tv, const void* k
                                hipStream_t s) {
     const bool hashed = tv.dense == nullptr;
     const int64_t nt = (n + kSlTile - 1) / kSlTile;
-    const uint32_t nsl = sl_slices(tv), wlog = sl_wlog();
+    const uint32_t nsl_all = sl_slices(tv), wlog = sl_wlog();
+    const uint32_t npass = sl_passes(nsl_all);
     SlicedWs w = sliced_ws_layout((void*)(((uintptr_t)workspace + 255) & ~(uintptr_t)255), n);
     const bool vec = (reinterpret_cast<uintptr_t>(keys) & 15) == 0;
     hipError_t e = hipSuccess;
@@ -2865,37 +3046,6 @@ hipError_t launch_probe_sliced(int key_bytes, const TableView& tv, const void* k
         const char* ev = getenv("DFP_HJ_SL_NT");
         return ev ? atoi(ev) : 0;
     }();
-    if (hashed) {
-        const unsigned pgrid = (unsigned)std::min<int64_t>(nt, sl_num_cus());
-#define DFP_HSP(KT, HV)                                                                                           \
-    hs_partition_kernel<KT, HV><<<pgrid, kSlThreads, 0, s>>>(tv.nb, nsl, keys, valid, voff, n, nt, vec,            \
-                                                            (unsigned long long*)w.ko, w.rl, w.toff, hdr, w.tcnt)
-        if (key_bytes == 8) {
-            if (valid) DFP_HSP(int64_t, true); else DFP_HSP(int64_t, false);
-        } else {
-            if (valid) DFP_HSP(int32_t, true); else DFP_HSP(int32_t, false);
-        }
-#undef DFP_HSP
-    } else {
-#define DFP_SLP(KT, HV)                                                                                      \
-    sl_partition_kernel<KT, HV><<<(unsigned)nt, kSlThreads, 0, s>>>(tv.dmin, tv.drange, wlog, nsl, keys, valid, voff, n, \
-                                                                   vec, (uint16_t*)w.ko, w.rl, w.toff, sl_nt, 0, 0,   \
-                                                                   nullptr, hdr, w.tcnt)
-        if (key_bytes == 8) {
-            if (valid) DFP_SLP(int64_t, true); else DFP_SLP(int64_t, false);
-        } else {
-            if (valid) DFP_SLP(int32_t, true); else DFP_SLP(int32_t, false);
-        }
-#undef DFP_SLP
-    }
-    // (slice, tile range) work items: about 1024 of them, so that the resident workgroups
-    // (one per CU at 128 KB slices) run several rounds and the tail stays short
-    static const uint32_t target = [] {
-        const char* ev = getenv("DFP_HJ_SLICED_ITEMS");
-        return ev ? (uint32_t)std::max(1, atoi(ev)) : 1024u;
-    }();
-    uint32_t parts = std::max<uint32_t>(1, (target + nsl - 1) / nsl);
-    parts = (uint32_t)std::min<int64_t>(parts, (nt + 63) / 64);
 #ifdef DFP_HJ_ABLATIONS
     // diagnostic build only (wrong pairs): emit 1 no stores, 2 no entries, 8 no duplicate
     // segment reads; lookup 4 no bucket lookup (hashed), 128 plain item order
@@ -2911,20 +3061,66 @@ hipError_t launch_probe_sliced(int key_bytes, const TableView& tv, const void* k
                             : (const void*)sl_lookup_kernel<false, kSlOwnWin>;
     e = hipFuncSetAttribute(lk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)tab_lds);
     if (e != hipSuccess) return e;
-    if (built != nullptr) {  // S1 reads no table memory: the build may still be running
-        e = hipStreamWaitEvent(s, built, 0);
-        if (e != hipSuccess) return e;
+    // (slice, tile range) work items: about 1024 of them, so that the resident workgroups
+    // (one per CU at 128 KB slices) run several rounds and the tail stays short
+    static const uint32_t target = [] {
+        const char* ev = getenv("DFP_HJ_SLICED_ITEMS");
+        return ev ? (uint32_t)std::max(1, atoi(ev)) : 1024u;
+    }();
+    for (uint32_t pass = 0; pass < npass; ++pass) {
+        const uint32_t s0 = pass * (uint32_t)kSlMaxSlices;
+        const uint32_t nsl = std::min<uint32_t>(nsl_all - s0, (uint32_t)kSlMaxSlices);
+        unsigned long long* h = pass == 0 ? hdr : nullptr;  // a later pass appends to the tiles' entries
+        if (hashed) {
+            const unsigned pgrid = (unsigned)std::min<int64_t>(nt, sl_num_cus());
+#define DFP_HSP(KT, HV)                                                                                           \
+    hs_partition_kernel<KT, HV><<<pgrid, kSlThreads, 0, s>>>(tv.nb, s0, nsl, keys, valid, voff, n, nt, vec,        \
+                                                            (unsigned long long*)w.ko, w.rl, w.toff, h, w.tcnt, w.tent)
+            if (key_bytes == 8) {
+                if (valid) DFP_HSP(int64_t, true); else DFP_HSP(int64_t, false);
+            } else {
+                if (valid) DFP_HSP(int32_t, true); else DFP_HSP(int32_t, false);
+            }
+#undef DFP_HSP
+        } else {
+            // this pass's key range: slices [s0, s0 + nsl) of 2^wlog values from dmin
+            const uint64_t lo = (uint64_t)s0 << wlog;
+            const int64_t dmin_p = (int64_t)((uint64_t)tv.dmin + lo);
+            const uint64_t drange_p = std::min<uint64_t>(tv.drange - lo, (uint64_t)nsl << wlog);
+#define DFP_SLP(KT, HV)                                                                                      \
+    sl_partition_kernel<KT, HV><<<(unsigned)nt, kSlThreads, 0, s>>>(dmin_p, drange_p, wlog, nsl, keys, valid, voff, n, \
+                                                                   vec, (uint16_t*)w.ko, w.rl, w.toff, sl_nt, 0, 0,   \
+                                                                   nullptr, h, w.tcnt, w.tent)
+            if (key_bytes == 8) {
+                if (valid) DFP_SLP(int64_t, true); else DFP_SLP(int64_t, false);
+            } else {
+                if (valid) DFP_SLP(int32_t, true); else DFP_SLP(int32_t, false);
+            }
+#undef DFP_SLP
+        }
+        uint32_t parts = std::max<uint32_t>(1, (target + nsl - 1) / nsl);
+        parts = (uint32_t)std::min<int64_t>(parts, (nt + 63) / 64);
+        if (pass == 0 && built != nullptr) {  // S1 reads no table memory: the build may still be running
+            e = hipStreamWaitEvent(s, built, 0);
+            if (e != hipSuccess) return e;
+        }
+        TableView tp = tv;  // this pass's table slices
+        if (!hashed) {
+            const uint64_t lo = (uint64_t)s0 << wlog;
+            tp.dense = tv.dense + lo;
+            tp.drange = std::min<uint64_t>(tv.drange - lo, (uint64_t)nsl << wlog);
+        }
+        if (hashed)
+            sl_lookup_kernel<true, kSlOwnWinHashed><<<nsl * parts, kSlThreads, tab_lds, s>>>(
+                tp, wlog, nsl, nt, parts, w.ko, w.res, w.toff, w.tcnt, s0);
+        else
+            sl_lookup_kernel<false, kSlOwnWin><<<nsl * parts, kSlThreads, tab_lds, s>>>(tp, wlog, nsl, nt, parts, w.ko,
+                                                                                      w.res, w.toff, w.tcnt, 0u);
     }
-    if (hashed)
-        sl_lookup_kernel<true, kSlOwnWinHashed><<<nsl * parts, kSlThreads, tab_lds, s>>>(tv, wlog, nsl, nt, parts, w.ko,
-                                                                                       w.res, w.toff, w.tcnt);
-    else
-        sl_lookup_kernel<false, kSlOwnWin><<<nsl * parts, kSlThreads, tab_lds, s>>>(tv, wlog, nsl, nt, parts, w.ko,
-                                                                                  w.res, w.toff, w.tcnt);
     const bool ri = tv.row_ids != nullptr, pi = probe_ids != nullptr;
     const unsigned egrid = (unsigned)std::min<int64_t>(nt, (int64_t)sl_emit_wgs_per_cu() * sl_num_cus());
 #define DFP_SLE(RI, PI)                                                                                           \
-    sl_emit_kernel<RI, PI><<<egrid, kSlEmitThreads, 0, s>>>(tv, nsl, w.rl, w.res, w.toff, probe_ids, pbase, w.tcnt, nt, \
+    sl_emit_kernel<RI, PI><<<egrid, kSlEmitThreads, 0, s>>>(tv, w.tent, w.rl, w.res, probe_ids, pbase, w.tcnt, nt,   \
                                                            out_b, out_p, cap, d_total)
     if (ri && pi) DFP_SLE(true, true);
     else if (ri) DFP_SLE(true, false);
@@ -2941,7 +3137,7 @@ hipError_t launch_probe(int key_bytes, const TableView& tv, const void* keys, co
     const int64_t nt = probe_tiles(n);
     const int mode = probe_mode();
     const uint32_t nsl = sl_slices(tv);
-    if (nt > 0 && nsl >= 1 && nsl <= (uint32_t)kSlMaxSlices && (mode == 4 || (mode == 0 && sl_auto(tv, n))))
+    if (nt > 0 && nsl >= 1 && (mode == 4 || (mode == 0 && sl_auto(tv, n))))
         return launch_probe_sliced(key_bytes, tv, keys, valid, voff, probe_ids, pbase, n, out_b, out_p, cap, d_total,
                                    workspace, built, s);  // S1 zeroes the error word
     if (built != nullptr) {
@@ -3034,6 +3230,56 @@ hipError_t launch_radix_partition(int key_bytes, const void* keys, const uint8_t
         if (id_bytes == 8) DFP_PS(int32_t, int32_t, uint64_t); else DFP_PS(int32_t, int32_t, uint32_t);
     }
 #undef DFP_PS
+    return hipGetLastError();
+}
+
+int64_t radix_regions_workspace(int64_t n, int nparts) {
+    const int64_t nt = (n + kRpTile - 1) / kRpTile;
+    return 256 + 8 * std::max<int64_t>(nt, 1) * nparts;
+}
+
+hipError_t launch_radix_regions(int key_bytes, const void* keys, const uint8_t* valid, int64_t voff,
+                                const uint64_t* ids, uint64_t id_base, int64_t n, int nparts, const PartSpec& spec,
+                                void* out_keys, int out_key_bytes, int64_t key_offset, void* out_ids, int id_bytes,
+                                int64_t cap, int64_t* counts, void* workspace, hipStream_t s) {
+    if (nparts < 1 || nparts > kMaxParts || (nparts & (nparts - 1))) return hipErrorInvalidValue;
+    const int64_t nt = (n + kRpTile - 1) / kRpTile;
+    unsigned long long* err = reinterpret_cast<unsigned long long*>((char*)workspace + 8);
+    unsigned long long* flags = reinterpret_cast<unsigned long long*>((char*)workspace + 256);
+    hipError_t e = hipMemsetAsync(workspace, 0, (size_t)radix_regions_workspace(n, nparts), s);
+    if (e != hipSuccess) return e;
+    if (nt == 0) return hipMemsetAsync(counts, 0, sizeof(int64_t) * nparts, s);
+    int bits = 0;
+    while ((1 << bits) < nparts) ++bits;
+    const size_t lds = sizeof(uint32_t) * (size_t)nparts * kRpSlots;
+#define DFP_RP(K, OK, ID, HV, HI)                                                                                  \
+    do {                                                                                                           \
+        auto kfn = part_regions_kernel<K, OK, ID, HV, HI>;                                                         \
+        if (lds > 64 * 1024) {                                                                                     \
+            const hipError_t ea = hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, \
+                                                      (int)lds);                                                   \
+            if (ea != hipSuccess) return ea;                                                                       \
+        }                                                                                                          \
+        kfn<<<(unsigned)nt, kRpThreads, lds, s>>>(keys, valid, voff, ids, id_base, n, nparts, bits, spec,           \
+                                                  key_offset, (OK*)out_keys, (ID*)out_ids, cap, flags, counts, err); \
+    } while (0)
+#define DFP_RP_V(K, OK, ID)                                                      \
+    do {                                                                         \
+        if (valid) {                                                             \
+            if (ids) DFP_RP(K, OK, ID, true, true); else DFP_RP(K, OK, ID, true, false);   \
+        } else {                                                                 \
+            if (ids) DFP_RP(K, OK, ID, false, true); else DFP_RP(K, OK, ID, false, false); \
+        }                                                                        \
+    } while (0)
+    if (key_bytes == 8 && out_key_bytes == 8) {
+        if (id_bytes == 8) DFP_RP_V(int64_t, int64_t, uint64_t); else DFP_RP_V(int64_t, int64_t, uint32_t);
+    } else if (key_bytes == 8) {
+        if (id_bytes == 8) DFP_RP_V(int64_t, int32_t, uint64_t); else DFP_RP_V(int64_t, int32_t, uint32_t);
+    } else {
+        if (id_bytes == 8) DFP_RP_V(int32_t, int32_t, uint64_t); else DFP_RP_V(int32_t, int32_t, uint32_t);
+    }
+#undef DFP_RP_V
+#undef DFP_RP
     return hipGetLastError();
 }
 

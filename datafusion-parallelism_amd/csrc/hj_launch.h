@@ -100,6 +100,15 @@ hipError_t launch_radix_partition(int key_bytes, const void* keys, const uint8_t
                                   int out_key_bytes, int64_t key_offset, void* out_ids, int id_bytes,
                                   int64_t* counts, void* workspace, hipStream_t s);
 int64_t radix_partition_workspace(int64_t n, int nparts);
+// One-pass stable partition into per-destination regions: region d holds its rows at
+// out[d * cap + i]; counts[d] = the destination's rows (all of them, even past cap: rows
+// beyond cap are not written). Workspace: radix_regions_workspace (zeroed here); its
+// word at byte 8 is the look-back's error flag.
+int64_t radix_regions_workspace(int64_t n, int nparts);
+hipError_t launch_radix_regions(int key_bytes, const void* keys, const uint8_t* valid, int64_t voff,
+                                const uint64_t* ids, uint64_t id_base, int64_t n, int nparts, const PartSpec& spec,
+                                void* out_keys, int out_key_bytes, int64_t key_offset, void* out_ids, int id_bytes,
+                                int64_t cap, int64_t* counts, void* workspace, hipStream_t s);
 
 // in-place exclusive scan of u64 (scratch: scan_scratch_bytes(len)); *total = sum
 hipError_t launch_scan_u64(unsigned long long* a, int64_t len, void* scratch, unsigned long long* total,

@@ -76,6 +76,49 @@ def gpu_radix_partition(keys: torch.Tensor, ids: torch.Tensor | None, id_base: i
     return out_k, out_i, counts
 
 
+def gpu_partition_regions(keys: torch.Tensor, ids: torch.Tensor | None, id_base: int, nparts: int,
+                          cap: int | None = None, id_dtype: torch.dtype = torch.int64, key_offset: int | None = None,
+                          spec: PartSpec | None = None, stream: int | None = None):
+    """hj_partition_regions on device tensors: one pass over the rows into per-destination
+    regions -> (keys, ids, counts[nparts] int64 device tensor, cap): region d's rows are
+    keys[d * cap : d * cap + counts[d]] (source row order), likewise ids. cap defaults to
+    the row count (any distribution fits)."""
+    L = _lib.load()
+    n = keys.numel()
+    cap = max(n, 1) if cap is None else max(int(cap), 1)
+    kt = HJ_INT64 if keys.dtype == torch.int64 else HJ_INT32
+    narrow = key_offset is not None and keys.dtype == torch.int64
+    out_k = torch.empty(nparts * cap, dtype=torch.int32 if narrow else keys.dtype, device=keys.device)
+    out_i = torch.empty(nparts * cap, dtype=id_dtype, device=keys.device)
+    counts = torch.empty(nparts, dtype=torch.int64, device=keys.device)
+    ws = torch.empty(max(L.hj_partition_regions_workspace_bytes(n, nparts), 8), dtype=torch.uint8,
+                     device=keys.device)
+    s = stream if stream is not None else torch.cuda.current_stream(keys.device).cuda_stream
+    sp = None
+    if spec is not None and spec != PartSpec():
+        sp = ctypes.byref(_lib.HjPartSpec(int(spec.by_range), spec.key_lo, spec.key_hi))
+    check(L.hj_partition_regions(kt, keys.data_ptr(), None, 0, None if ids is None else ids.data_ptr(), id_base, n,
+                                 nparts, sp, out_k.data_ptr(), out_k.element_size(), key_offset if narrow else 0,
+                                 out_i.data_ptr(), 8 if id_dtype == torch.int64 else 4, cap, counts.data_ptr(),
+                                 ws.data_ptr(), s))
+    return out_k, out_i, counts, cap
+
+
+def regions_from_grouped(k: torch.Tensor, i: torch.Tensor, counts: torch.Tensor, nparts: int):
+    """Destination-grouped partition output (hj_partition_rows' layout, or a host stand-in's)
+    as regions of cap = len(k) rows (tests' stand-ins feed the region exchange this way)."""
+    cap = max(k.numel(), 1)
+    rk = torch.zeros(nparts * cap, dtype=k.dtype, device=k.device)
+    ri = torch.zeros(nparts * cap, dtype=i.dtype, device=i.device)
+    c = [int(x) for x in counts.tolist()]
+    at = 0
+    for d in range(nparts):
+        rk[d * cap:d * cap + c[d]] = k[at:at + c[d]]
+        ri[d * cap:d * cap + c[d]] = i[at:at + c[d]]
+        at += c[d]
+    return rk, ri, counts, cap
+
+
 class GpuLocalTable:
     """One rank's shard table (global build ids held in place of row numbers when they
     fit 31 bits and ascend, HJ_IDS_U31) and asynchronous probes of received chunks."""
@@ -171,8 +214,11 @@ A2A_MAX_BYTES = 256 << 20
 def _count_matrix(counts: torch.Tensor, group=None) -> list[list[int]]:
     """m[s][d] = rows rank s sends to rank d (one all_gather of G int64, one host sync):
     every rank learns its receive sizes and everyone's, so all ranks agree on the
-    number of exchange rounds without another collective."""
+    number of exchange rounds without another collective. One rank: its own counts, no
+    collective."""
     world = dist.get_world_size(group)
+    if world == 1:
+        return [counts.tolist()]
     parts = [torch.empty_like(counts) for _ in range(world)]
     dist.all_gather(parts, counts, group=group)
     return torch.stack(parts).cpu().tolist()
@@ -216,6 +262,49 @@ def _exchange_cols(cols: list[torch.Tensor], m: list[list[int]], group=None, asy
                 o[r_off[p] + a:r_off[p] + b].copy_(tout[q:q + b - a])
                 q += b - a
     return outs, []
+
+
+def exchange_regions(cols: list[torch.Tensor], cap: int, m: list[list[int]], group=None, async_op: bool = False):
+    """Exchange per-destination regions (gpu_partition_regions' layout) with point-to-point
+    sends and receives (RCCL ncclSend/ncclRecv in one group; xGMI links are point to point,
+    so the per-peer messages of one rank use its links in parallel): -> (received columns,
+    each the concatenation of the sources' rows in source-rank order, works in flight).
+    The rank's own region is copied on the device (one rank: it is returned as is, no
+    copy). Messages above A2A_MAX_BYTES travel in pieces (both sides derive the same
+    split from the count matrix)."""
+    me = dist.get_rank(group)
+    world = len(m)
+    recv = [m[s][me] for s in range(world)]
+    if world == 1:
+        return [c[:recv[0]] for c in cols], []
+    r_off = [sum(recv[:p]) for p in range(world)]
+    outs = [torch.empty(sum(recv), dtype=c.dtype, device=c.device) for c in cols]
+    ops = []
+
+    def pieces(nrows, esz):
+        rounds = max(1, -(-nrows * esz // A2A_MAX_BYTES))
+        return [(nrows * j // rounds, nrows * (j + 1) // rounds) for j in range(rounds)]
+
+    peer_rank = (lambda p: dist.get_global_rank(group, p)) if group is not None else (lambda p: p)
+    for c, o in zip(cols, outs):
+        esz = c.element_size()
+        if recv[me]:
+            o[r_off[me]:r_off[me] + recv[me]].copy_(c[me * cap:me * cap + recv[me]])
+        for p in range(world):
+            if p == me:
+                continue
+            for a, b in pieces(m[me][p], esz):
+                if b > a:
+                    ops.append(dist.P2POp(dist.isend, c[p * cap + a:p * cap + b], peer_rank(p), group))
+            for a, b in pieces(m[p][me], esz):
+                if b > a:
+                    ops.append(dist.P2POp(dist.irecv, o[r_off[p] + a:r_off[p] + b], peer_rank(p), group))
+    works = dist.batch_isend_irecv(ops) if ops else []
+    if not async_op:
+        for w in works:
+            w.wait()
+        works = []
+    return outs, works
 
 
 def check_ids(ids: torch.Tensor, bound: int, what: str = "ids") -> None:
@@ -266,10 +355,11 @@ class DistributedHashJoin:
         self.chunks = max(1, int(chunks))
         self.compress_keys = compress_keys
         self.runtime_filter = runtime_filter
+        self.events: dict | None = None  # {"partitioned", "exchanged"}: torch.cuda.Event recorded by join()
 
     def prepare(self, build_keys: torch.Tensor, probe_keys: torch.Tensor, build_base: int) -> ExchangePlan:
         """Plan the exchange from the global key ranges (one aminmax pass over each side,
-        two 16-byte all-reduces and one host read):
+        two 16-byte all-reduces and one host read; one rank: no collective):
 
         * runtime filter: probe rows outside the global build key range [bmin, bmax]
           cannot match and are dropped by the partition kernel before they travel;
@@ -295,8 +385,9 @@ class DistributedHashJoin:
                 mn, mx = torch.aminmax(k.to(torch.int64) if k.dtype != torch.int64 else k)
                 lo[j] = mn
                 hi[j] = mx
-        dist.all_reduce(lo, op=dist.ReduceOp.MIN, group=self.group)
-        dist.all_reduce(hi, op=dist.ReduceOp.MAX, group=self.group)
+        if self.world > 1:
+            dist.all_reduce(lo, op=dist.ReduceOp.MIN, group=self.group)
+            dist.all_reduce(hi, op=dist.ReduceOp.MAX, group=self.group)
         bmin, pmin, bmax, pmax, bend = torch.cat([lo, hi]).tolist()
         plan.build_rows = bend
         if bend < 2**31:
@@ -315,26 +406,33 @@ class DistributedHashJoin:
 
     def _partition(self, keys: torch.Tensor, id_base: int, id_dtype: torch.dtype, key_offset: int | None,
                    spec: PartSpec | None = None):
+        """-> per-destination regions (keys, ids, counts, cap) of gpu_partition_regions."""
         if self.partition_fn is gpu_radix_partition:
-            return gpu_radix_partition(keys, None, id_base, self.world, id_dtype=id_dtype, key_offset=key_offset,
-                                       spec=spec)
-        # host stand-ins (tests): partition on the original keys, then narrow
+            return gpu_partition_regions(keys, None, id_base, self.world, id_dtype=id_dtype, key_offset=key_offset,
+                                         spec=spec)
+        # host stand-ins (tests): a grouped partition of the original keys, as regions
         if spec is not None and spec != PartSpec():
             k, i, c = self.partition_fn(keys, None, id_base, self.world, spec=spec)
         else:
             k, i, c = self.partition_fn(keys, None, id_base, self.world)
         if key_offset is not None and k.dtype == torch.int64:
             k = (k - key_offset).to(torch.int32)
-        return k, i, c
+        return regions_from_grouped(k, i.to(id_dtype), c, self.world)
 
     def shard(self, keys: torch.Tensor, id_base: int, id_dtype: torch.dtype = torch.int64, async_op: bool = False,
               key_offset: int | None = None, spec: PartSpec | None = None):
-        """Partition by destination rank and exchange: -> (keys, global ids, stats).
+        """Partition by destination rank and exchange: -> (keys, global ids, stats[, works]).
         Build rows carry u64 ids (int64), probe rows u32 ids (int32, the reference's
         UInt32 probe index): 16 resp. 12 bytes per int64-key row on the wire, 8 with a
         narrowing plan (prepare)."""
-        k, i, c = self._partition(keys, id_base, id_dtype, key_offset, spec)
-        return all_to_all_rows(k, i, c, self.group, async_op=async_op)
+        k, i, c, cap = self._partition(keys, id_base, id_dtype, key_offset, spec)
+        m = _count_matrix(c, self.group)
+        (rk, ri), works = exchange_regions([k, i], cap, m, self.group, async_op)
+        me = self.rank
+        st = ExchangeStats(sum(m[me]), sum(r[me] for r in m))
+        if async_op:
+            return rk, ri, st, works
+        return rk, ri, st
 
     def shard_build(self, build_keys: torch.Tensor, build_base: int, plan: ExchangePlan,
                     global_rows: int | None = None):
@@ -349,14 +447,52 @@ class DistributedHashJoin:
             check_ids(bi, global_rows, "received build ids")
         return bk, bi
 
+    def _local_table(self, bk: torch.Tensor, bi: torch.Tensor, plan: ExchangePlan):
+        if self.local_build_fn is GpuLocalTable:
+            return GpuLocalTable(bk, bi, ids_u31=True if plan.build_id_dtype == torch.int32 else None)
+        return self.local_build_fn(bk, bi)
+
+    def join(self, build_keys: torch.Tensor, build_base: int, probe_keys: torch.Tensor, probe_base: int,
+             capacity_hint: int | None = None, check: bool = True):
+        """The radix plan, one pass per side: plan (one host read), both sides partitioned
+        into per-destination regions, ONE count exchange for both (one host read), the
+        build side's regions exchanged and built (asynchronously: a direct-addressed build
+        overlaps the probe side's exchange), the probe side's exchanged and probed once.
+        -> (table, result): result() waits and yields this rank's pairs (canonical for
+        its keys); close the table afterwards."""
+        ev = self.events  # optional stage events (bench): partitioned, exchanged
+        plan = self.prepare(build_keys, probe_keys, build_base)
+        bk_r, bi_r, bc, bcap = self._partition(build_keys, build_base, plan.build_id_dtype, plan.key_offset, plan.spec)
+        pk_r, pi_r, pc, pcap = self._partition(probe_keys, probe_base, torch.int32, plan.key_offset, plan.spec)
+        if ev is not None:
+            ev["partitioned"].record()
+        w = self.world
+        m = _count_matrix(torch.cat([bc, pc]), self.group)
+        (bk, bi), _ = exchange_regions([bk_r, bi_r], bcap, [row[:w] for row in m], self.group)
+        bi = bi.to(torch.int64) if bi.dtype != torch.int64 else bi
+        if check and plan.build_rows is not None:
+            check_ids(bi, plan.build_rows, "received build ids")
+        table = self._local_table(bk, bi, plan)
+        (pk, pi), works = exchange_regions([pk_r, pi_r], pcap, [row[w:] for row in m], self.group, async_op=True)
+        for wk in works:
+            if wk is not None:
+                wk.wait()
+        if ev is not None:
+            ev["exchanged"].record()
+        result = self._probe_chunk(table, pk, pi, [], capacity_hint)
+        return table, result
+
     def run(self, build_keys: torch.Tensor, build_base: int, probe_keys: torch.Tensor, probe_base: int,
             capacity_hint: int | None = None):
         """-> this rank's share of the global pairs (build_idx, probe_idx)."""
+        if self.chunks <= 1:
+            table, result = self.join(build_keys, build_base, probe_keys, probe_base, capacity_hint)
+            try:
+                return result()
+            finally:
+                table.close()
         plan = self.prepare(build_keys, probe_keys, build_base)
         bk, bi = self.shard_build(build_keys, build_base, plan, global_rows=plan.build_rows)
-        if self.chunks <= 1:
-            pk, pi, _ = self.shard(probe_keys, probe_base, torch.int32, key_offset=plan.key_offset, spec=plan.spec)
-            return self.local_join_fn(bk, bi, pk, pi, capacity_hint)
         outs = self.run_pipelined(bk, bi, probe_keys, probe_base, plan)
         return torch.cat([b for b, _ in outs]), torch.cat([p for _, p in outs])
 
@@ -364,13 +500,10 @@ class DistributedHashJoin:
                       plan: ExchangePlan | None = None):
         """Local build, then the probe side in `chunks` slices. Every slice is partitioned
         up front and their counts travel in one all_gather (one host sync); then the
-        exchange of slice c is in flight (RCCL stream) while slice c-1 is probed
-        (compute stream). -> list of per-chunk (build_idx, probe_idx)."""
+        exchange of slice c is in flight (RCCL P2P) while slice c-1 is probed (compute
+        stream). -> list of per-chunk (build_idx, probe_idx)."""
         plan = plan or ExchangePlan()
-        if self.local_build_fn is GpuLocalTable:
-            table = GpuLocalTable(bk, bi, ids_u31=True if plan.build_id_dtype == torch.int32 else None)
-        else:
-            table = self.local_build_fn(bk, bi)
+        table = self._local_table(bk, bi, plan)
         try:
             n = probe_keys.numel()
             w = self.world
@@ -381,7 +514,8 @@ class DistributedHashJoin:
             results, pending = [], None
             for c in range(self.chunks):
                 m = [[row[c * w + d] for d in range(w)] for row in mats]
-                (rk, ri), works = _exchange_cols([parts[c][0], parts[c][1]], m, self.group, async_op=True)
+                (rk, ri), works = exchange_regions([parts[c][0], parts[c][1]], parts[c][3], m, self.group,
+                                                   async_op=True)
                 if pending is not None:
                     results.append(self._probe_chunk(table, *pending))
                 pending = (rk, ri, works)
@@ -434,11 +568,11 @@ class DistributedHashJoin:
         raise RuntimeError("unreachable")
 
     @staticmethod
-    def _probe_chunk(table, rk, ri, works):
+    def _probe_chunk(table, rk, ri, works, capacity=None):
         for w in works:
             if w is not None:
                 w.wait()  # RCCL: the compute stream waits for the exchange (no host block)
-        return table.probe(rk, ri, rk.numel())
+        return table.probe(rk, ri, capacity or rk.numel())
 
 
 # ---- relational exchanges for multi-GPU query plans (TPC-H C4/C5, tpch.py) -------------

@@ -227,23 +227,23 @@ class Q3Result:
     groups: int  # qualifying (order) groups before the limit
 
 
-def q3(t: Tables, segment: str = "BUILDING", date: str = "1995-03-15", limit: int = 10) -> Q3Result:
+def q3(t: Tables, segment: str = "BUILDING", date: str = "1995-03-15", limit: int = 10,
+       join_fn=None) -> Q3Result:
+    """join_fn(build, probe) -> (build rows, probe rows): the one-GPU hash join by default;
+    multi_join(devices) runs every join on a table sharded over several GPUs."""
+    join = join_fn or _join
     dev = t.device
     seg = SEGMENTS.index(segment)
     d = day(date)
     # customer ⋈ orders: build on the segment's customers, probe the date-filtered orders
     cust = t.c_custkey[t.c_mktsegment == seg]
     o_rows = torch.nonzero(t.o_orderdate < d).squeeze(1)
-    with HashTable(1, "int64", dev.index or 0) as tc:
-        tc.build(cust)
-        _, po = tc.probe(t.o_custkey[o_rows].contiguous(), device_output=True)
-    sel = o_rows[po.to(torch.int64)]  # qualifying orders (custkeys are unique: <= 1 match each)
+    _, po = join(cust, t.o_custkey[o_rows])
+    sel = o_rows[po]  # qualifying orders (custkeys are unique: <= 1 match each)
     # orders ⋈ lineitem: build on the qualifying orders' keys, probe the date-filtered lines
     l_rows = torch.nonzero(t.l_shipdate > d).squeeze(1)
-    with HashTable(1, "int64", dev.index or 0) as to:
-        to.build(t.o_orderkey[sel].contiguous())
-        bo, pl = to.probe(t.l_orderkey[l_rows].contiguous(), device_output=True)
-    lines = l_rows[pl.to(torch.int64)]
+    bo, pl = join(t.o_orderkey[sel], t.l_orderkey[l_rows])
+    lines = l_rows[pl]
     rev = t.l_extendedprice[lines] * (100 - t.l_discount[lines].to(torch.int64))
     sums = torch.zeros(sel.numel(), dtype=torch.int64, device=dev).index_add_(0, bo, rev)
     has = torch.zeros(sel.numel(), dtype=torch.bool, device=dev)
@@ -279,10 +279,28 @@ def _join(build: torch.Tensor, probe: torch.Tensor):
     return b, p.to(torch.int64)
 
 
-def q9(t: Tables, color_flag: str = "green") -> list[tuple[str, int, int]]:
-    """-> [(nation, o_year, sum_profit in 1e-4 units)] ordered by nation, o_year desc."""
+def multi_join(devices: list[int], plan: str = "radix"):
+    """A join_fn whose every join runs on one table sharded over `devices`
+    (hj_build_begin_multi): the radix plan gives each GPU 1/G of the build side by key
+    hash and merges the shards' pairs into canonical order — the in-process form of C4/C5's
+    sharded builds (a build side larger than one GPU's HBM). Devices may repeat (tests on
+    one GPU)."""
+    def join(build: torch.Tensor, probe: torch.Tensor):
+        with HashTable(1, "int64", devices=list(devices), plan=plan) as t:
+            t.append(0, build.contiguous())
+            t.finish(0)
+            b, p = t.probe(probe.contiguous(), device_output=True)
+        return b, p.to(torch.int64)
+
+    return join
+
+
+def q9(t: Tables, color_flag: str = "green", join_fn=None) -> list[tuple[str, int, int]]:
+    """-> [(nation, o_year, sum_profit in 1e-4 units)] ordered by nation, o_year desc.
+    join_fn: as q3's."""
     if t.l_partkey is None:
         raise ValueError("generate(..., q9=True) tables are needed")
+    _join = join_fn or globals()["_join"]
     dev = t.device
     # lineitem ⋈ part (p_name like '%green%')
     _, li = _join(t.p_partkey[t.p_green], t.l_partkey)

@@ -276,6 +276,22 @@ hj_status hj_partition_rows(hj_key_type key_type, const void* keys,
                             int64_t key_offset, void* out_ids, int id_bytes, int64_t* counts,
                             void* workspace, void* stream);
 
+/* One-pass partition into per-destination regions (the exchange's send buffers): the
+ * rows of destination d go to out_keys / out_ids elements [d * region_rows, d *
+ * region_rows + counts[d]) in source row order (stable), with hj_partition_rows' map,
+ * filter, key narrowing and ids. Every row is read once (a decoupled look-back over the
+ * tiles gives each tile's offset in each region), and a region is a contiguous send
+ * buffer for one peer, so no grouped copy precedes the exchange. counts[d] is exact even
+ * when it exceeds region_rows (rows past the region are not written): region_rows >= n
+ * always suffices. workspace: hj_partition_regions_workspace_bytes(n, nparts). */
+int64_t hj_partition_regions_workspace_bytes(int64_t n, int nparts);
+hj_status hj_partition_regions(hj_key_type key_type, const void* keys,
+                               const uint8_t* validity, int64_t validity_offset,
+                               const uint64_t* ids, uint64_t id_base, int64_t n, int nparts,
+                               const hj_part_spec* spec, void* out_keys, int out_key_bytes,
+                               int64_t key_offset, void* out_ids, int id_bytes, int64_t region_rows,
+                               int64_t* counts, void* workspace, void* stream);
+
 /* ---- join types and output materialisation. Device pointers,
  *      asynchronous on `stream`. Index arrays are uint32 (idx_bytes 4) or uint64 (8);
  *      an all-ones index is a null index (the outer joins' missing side). ---------- */

@@ -100,8 +100,8 @@ def _worker(rank, world, port, bks, pks, q, chunks=1, max_bytes=None, rfilter=Tr
     else:  # pipelined probe side: canonical per chunk
         plan = dj.prepare(torch.from_numpy(bks[rank]), torch.from_numpy(pks[rank]), bbase)
         allb = np.concatenate(bks)
-        span = allb.max() - allb.min() if rfilter else max(allb.max(), max(p.max() for p in pks)) - min(
-            allb.min(), min(p.min() for p in pks))
+        allp = np.concatenate(pks)
+        span = allb.max() - allb.min() if rfilter else max(allb.max(), allp.max()) - min(allb.min(), allp.min())
         assert (plan.key_offset is None) == (span >= 2**32)
         assert plan.spec.by_range == (rfilter and allb.max() - allb.min() + 1 <= 8 * len(allb))
         bk, bi = dj.shard_build(torch.from_numpy(bks[rank]), bbase, plan)
@@ -129,7 +129,8 @@ def _free_port():
 
 @pytest.mark.parametrize("world,chunks,wide,max_bytes,rfilter", [
     (2, 1, False, None, True), (2, 3, False, None, True), (2, 3, True, None, True), (2, 1, False, 5000, True),
-    (2, 3, True, 7000, True), (2, 3, False, None, False), (2, 1, True, None, False)])
+    (2, 3, True, 7000, True), (2, 3, False, None, False), (2, 1, True, None, False), (4, 1, False, 3000, True),
+    (4, 2, True, None, False)])
 def test_distributed_exchange_matches_single_join(oracle_mod, world, chunks, wide, max_bytes, rfilter):
     """rfilter: runtime min/max filter + range map for dense build domains (the default);
     off: every probe row travels, hash map."""
@@ -140,8 +141,10 @@ def test_distributed_exchange_matches_single_join(oracle_mod, world, chunks, wid
     pk = rng.integers(0, 5000, 14000).astype(np.int64)
     if wide:
         bk, pk = bk * (2**33) - 2**40, pk * (2**33) - 2**40
-    bks = [bk[:4000], bk[4000:]]
-    pks = [pk[:9000], pk[9000:]]
+    bb = [0, 4000, 9000] if world == 2 else [0, 1000, 4000, 4001, 9000]
+    pb = [0, 9000, 14000] if world == 2 else [0, 5000, 5000, 11000, 14000]
+    bks = [bk[bb[r]:bb[r + 1]] for r in range(world)]
+    pks = [pk[pb[r]:pb[r + 1]] for r in range(world)]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()

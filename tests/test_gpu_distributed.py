@@ -119,3 +119,61 @@ def test_large_exchange_one_rank(dfp):
         assert torch.equal(ri, torch.arange(n, device=dev))
     finally:
         dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("nparts", [1, 2, 8, 64])
+@pytest.mark.parametrize("n", [0, 1, 16383, 16384, 1_000_003])
+@pytest.mark.parametrize("mode", ["hash", "range_narrow", "ids_u64_nulls"])
+def test_partition_regions_kernel(dfp, nparts, n, mode):
+    """hj_partition_regions (one pass, look-back over 16384-row tiles): region d holds the
+    rows of destination d in source row order, with hj_partition_rows' map, filter,
+    narrowing and ids; counts exact."""
+    import ctypes
+
+    from datafusion_parallelism_amd import _lib
+    from datafusion_parallelism_amd.distributed import PartSpec
+
+    L = _lib.load()
+    rng = np.random.default_rng(n + nparts)
+    k = rng.integers(-(2**40), 2**40, n) if mode != "range_narrow" else rng.integers(-500, 3 * 10**6, n)
+    dev = torch.device("cuda", 0)
+    keys = torch.from_numpy(k.astype(np.int64)).to(dev)
+    spec, off, ids, valid_np = None, 0, None, np.ones(n, bool)
+    if mode == "range_narrow":
+        spec = PartSpec(True, 0, 2 * 10**6)
+        off = 0 + 2**31
+    id_base = 77
+    if mode == "ids_u64_nulls":
+        ids_np = rng.integers(0, 2**62, n).astype(np.uint64)
+        ids = torch.from_numpy(ids_np.view(np.int64)).to(dev)
+        valid_np = rng.random(n) > 0.1
+    bitmap = torch.from_numpy(np.packbits(np.concatenate([np.zeros(3, bool), valid_np]), bitorder="little")).to(dev)
+    cap = max(n, 1)
+    ob = 4 if mode == "range_narrow" else 8
+    out_k = torch.empty(nparts * cap, dtype=torch.int32 if ob == 4 else torch.int64, device=dev)
+    idb = 8 if mode == "ids_u64_nulls" else 4
+    out_i = torch.empty(nparts * cap, dtype=torch.int64 if idb == 8 else torch.int32, device=dev)
+    counts = torch.full((nparts,), -1, dtype=torch.int64, device=dev)
+    ws = torch.empty(L.hj_partition_regions_workspace_bytes(n, nparts), dtype=torch.uint8, device=dev)
+    sp = ctypes.byref(_lib.HjPartSpec(1, spec.key_lo, spec.key_hi)) if spec else None
+    _lib.check(L.hj_partition_regions(1, keys.data_ptr() if n else None, bitmap.data_ptr(), 3,
+                                      ids.data_ptr() if ids is not None else None, id_base, n, nparts, sp,
+                                      out_k.data_ptr(), ob, off, out_i.data_ptr(), idb, cap, counts.data_ptr(),
+                                      ws.data_ptr(), None))
+    torch.cuda.synchronize()
+    assert int(ws[8:16].view(torch.int64).item()) == 0  # look-back never gave up
+    keep = valid_np.copy()
+    if spec is not None:
+        dest, inr = spec.part_of(k, nparts)
+        keep &= inr
+    else:
+        dest = (_mix64(k) & np.uint64(nparts - 1)).astype(np.int64)
+    c = counts.cpu().numpy()
+    assert np.array_equal(c, np.bincount(dest[keep], minlength=nparts))
+    ok_, oi_ = out_k.cpu().numpy(), out_i.cpu().numpy()
+    for d in range(nparts):
+        rows = np.nonzero(keep & (dest == d))[0]  # ascending: stable
+        want_k = k[rows] if ob == 8 else (k[rows] - off).astype(np.int32)
+        assert np.array_equal(ok_[d * cap:d * cap + c[d]], want_k)
+        want_i = ids_np[rows].view(np.int64) if ids is not None else (rows + id_base).astype(np.int32)
+        assert np.array_equal(oi_[d * cap:d * cap + c[d]], want_i)

@@ -409,11 +409,22 @@ def test_explicit_build_ids(dfp, oracle_mod, probe_mode, ids_u31, dups):
     assert_same(b, p, ids[ob.astype(np.int64)].astype(np.uint64), op)
 
 
-def test_large_build_120m_rows(dfp):
+@pytest.mark.parametrize("pmode", [0, 4])
+def test_large_build_120m_rows(dfp, pmode):
     """A 1.2e8-row build (past the 5.9e7-row limit of round-1's first table geometry):
     size-independent properties on the GPU - every pair has equal keys, every probe key
     below N matches exactly its one build row (a permutation build side), canonical
-    order, no pair for keys >= N."""
+    order, no pair for keys >= N. pmode 4: the sliced probe over its 3663 slices (two
+    passes over slice ranges); 0: the auto choice."""
+    L = dfp.load()
+    old_p = L.hj_set_probe_mode(pmode)
+    try:
+        _large_build_120m(dfp)
+    finally:
+        L.hj_set_probe_mode(old_p)
+
+
+def _large_build_120m(dfp):
     L = dfp.load()
     N, P = 120_000_000, 10_000_000
     s = torch.cuda.current_stream().cuda_stream
@@ -474,7 +485,8 @@ def sliced_mode(dfp):
 
 @pytest.mark.parametrize("nb,krange,np_,null_frac,key_type", [
     (9_000_000, 2047 * 32768, 2_000_000, 0.0, "int64"),     # 2047 slices: the largest sliced table
-    (9_000_000, 2048 * 32768, 1_000_000, 0.0, "int64"),     # 2048 slices: falls back to fused
+    (9_000_000, 2048 * 32768, 1_000_000, 0.0, "int64"),     # 2048 slices: two passes over slice ranges
+    (17_000_000, 4100 * 32768, 2_000_000, 0.01, "int64"),   # 4100 slices: three passes, nulls
     (5_000_000, 2047 * 16384, 2_000_000, 0.0, "int64"),     # ~1024 slices
     (300_000, 1_000_000, 3_000_001, 0.02, "int32"),         # nulls, ragged last tile
     (2_000_000, 600_000, 1_500_000, 0.0, "int64"),          # duplicated keys (counts <= 15 and more)
@@ -494,6 +506,65 @@ def test_sliced_probe_parity(dfp, oracle_mod, sliced_mode, nb, krange, np_, null
     assert st["buckets"] == 0  # direct-addressed
     ob, op = oracle_mod.inner_join(bk, pk, bv, pv)
     assert_same(b, p, ob, op)
+
+
+@pytest.mark.parametrize("nb,np_,dup_frac", [(12_000_000, 2_000_000, 0.0), (11_000_000, 1_500_001, 0.2)])
+def test_sliced_hashed_multipass_parity(dfp, oracle_mod, sliced_mode, nb, np_, dup_frac):
+    """Hashed tables past 2047 slices of 2048 buckets (12 M keys at load 0.5 = 2344
+    slices): the probe runs two passes over slice ranges, appending to the tiles' entries,
+    one emission; duplicated keys and key 0 (the side bucket, slice 0) included."""
+    rng = np.random.default_rng(nb)
+    distinct = rng.integers(-(2**63), 2**63 - 1, nb, dtype=np.int64)
+    bk = distinct.copy()
+    nd = int(nb * dup_frac)
+    if nd:
+        bk[:nd] = distinct[rng.integers(nd, nb, nd)]
+    bk[-1] = 0
+    pk = np.concatenate([bk[rng.integers(0, nb, np_ // 2)], rng.integers(-(2**63), 2**63 - 1, np_ - np_ // 2)])
+    pk[:2] = [0, bk[5]]
+    b, p, st = gpu_join(dfp, bk, pk)
+    assert st["buckets"] > 2047 * 2048  # beyond one pass
+    ob, op = oracle_mod.inner_join(bk, pk)
+    assert_same(b, p, ob, op)
+
+
+def test_c2h_40m_multipass_closed_form(dfp):
+    """A 4*10^7-key hashed build (16 M buckets = 7813 slices: four sliced passes, the auto
+    choice) probed with 10^8 rows: C2's closed form under the bijection k -> k * M —
+    probe keys below B match exactly the row k * inv(7368787) mod B; count, order, values."""
+    B, P = 40_000_000, 10**8
+    dev = torch.device("cuda", 0)
+    lib = dfp.load()
+    bk = torch.empty(B, dtype=torch.int64, device=dev)
+    pk = torch.empty(P, dtype=torch.int64, device=dev)
+    s = torch.cuda.current_stream().cuda_stream
+    assert lib.hj_gen_perm_keys(bk.data_ptr(), B, 7368787, B, s) == 0
+    assert lib.hj_gen_uniform_keys(pk.data_ptr(), P, 0xC0FFEE, 2 * B, s) == 0
+    expected = int((pk < B).sum().item())
+    sample = torch.randint(0, P, (20000,), device=dev)
+    raw = pk[sample].cpu().numpy()
+    bk.mul_(MIX_MUL_I64)
+    pk.mul_(MIX_MUL_I64)
+    with dfp.HashTable(1, "int64", 0) as t:
+        t.build(bk)
+        st = t.stats()
+        assert st["buckets"] > 3 * 2047 * 2048  # four passes
+        b, p = t.probe(pk, device_output=True)
+    assert b.numel() == expected
+    pl = p.long()
+    assert bool((pl[1:] > pl[:-1]).all().item())  # one pair per matched row, ascending
+    assert bool((bk[b] == pk[pl]).all().item())
+    # closed form on a sample of probe rows: row r matches iff raw key < B, at k * inv mod B
+    inv = pow(7368787, -1, B)
+    hit = torch.zeros(P, dtype=torch.int64, device=dev).index_fill_(0, pl, 1)
+    where = torch.full((P,), -1, dtype=torch.int64, device=dev).index_copy_(0, pl, b)
+    h, w = hit[sample].cpu().numpy(), where[sample].cpu().numpy()
+    for k, hh, ww in zip(raw.tolist(), h.tolist(), w.tolist()):
+        assert hh == (k < B)
+        if k < B:
+            assert ww == (k * inv) % B
+    del bk, pk, b, p, hit, where
+    torch.cuda.empty_cache()
 
 
 @pytest.mark.parametrize("mode", [4, 3])

@@ -75,5 +75,50 @@ def test_distributed_plans_one_rank(dfp):
         assert got9 == tpch.q9(t)
         _, orders, lineitem, part, supplier, partsupp = t.to_pandas()
         assert got9 == q9_pandas(orders, lineitem, part, supplier, partsupp)
+        # the same plans with every local join on an 8-shard radix table
+        j = tpch.multi_join([0] * 8, "radix")
+        assert tpch.q3_dist(t, "BUILDING", "1995-03-15", join_fn=j) == one3
+        assert tpch.q9_dist(t, join_fn=j) == got9
     finally:
         dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("plan", ["radix", "broadcast"])
+def test_q3_q9_eight_shards_match_pandas(dfp, plan):
+    """C4/C5's sharded joins in process: every join of Q3 and Q9 runs on a table sharded
+    over 8 GPUs (hj_build_begin_multi with devices [0] * 8 on this one-GPU box: the radix
+    plan gives each shard 1/8 of the build side by key hash and merges the shards' pairs;
+    the broadcast plan splits the probe rows), at SF 1, against pandas."""
+    from tpch_ref import q3_pandas
+
+    from datafusion_parallelism_amd import tpch
+
+    t = tpch.generate(1, "cuda:0", seed=13, q9=True)
+    j = tpch.multi_join([0] * 8, plan)
+    got3 = tpch.q3(t, "BUILDING", "1995-03-15", join_fn=j)
+    customer, orders, lineitem, part, supplier, partsupp = t.to_pandas()
+    want, ngroups = q3_pandas(customer, orders, lineitem, tpch.SEGMENTS.index("BUILDING"), tpch.day("1995-03-15"))
+    assert got3.groups == ngroups
+    assert got3.l_orderkey == want.l_orderkey.tolist() and got3.revenue == want.revenue.tolist()
+    assert got3.o_orderdate == want.o_orderdate.tolist() and got3.o_shippriority == want.o_shippriority.tolist()
+    got9 = tpch.q9(t, join_fn=j)
+    assert len(got9) > 0 and got9 == q9_pandas(orders, lineitem, part, supplier, partsupp)
+
+
+def test_q3_q9_eight_shards_sf100_equal_one_gpu(dfp):
+    """Full size (C4 = Q3 SF100, C5's query Q9 at SF100): the 8-shard radix plans equal the
+    one-GPU plans (size-independent property; pandas cannot hold SF100 here)."""
+    import torch
+
+    from datafusion_parallelism_amd import tpch
+
+    j = tpch.multi_join([0] * 8, "radix")
+    t = tpch.generate(100, "cuda:0", seed=1, q9=True)
+    one3 = tpch.q3(t, "BUILDING", "1995-03-15")
+    assert one3.groups > 0
+    assert tpch.q3(t, "BUILDING", "1995-03-15", join_fn=j) == one3
+    one9 = tpch.q9(t)
+    assert len(one9) == 25 * 7
+    assert tpch.q9(t, join_fn=j) == one9
+    del t
+    torch.cuda.empty_cache()

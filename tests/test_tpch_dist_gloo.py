@@ -1,4 +1,4 @@
-"""CPU, world_size 2 (gloo): the multi-GPU TPC-H plans (tpch.q3_dist / q9_dist: broadcast
+"""CPU, world_size 2 and 8 (gloo; 8 = C4/C5's GPU count): the multi-GPU TPC-H plans (tpch.q3_dist / q9_dist: broadcast
 of filtered dimension sides, hash-repartition shuffles with payload, all-reduce / top-k
 merges) on rank-sharded generated tables, with the oracle as the per-rank local join and a
 numpy restatement of the partition (test-local stand-ins for the HIP kernels). Results
@@ -81,7 +81,7 @@ def test_generator_shape_cpu():
     assert all((a, b) in ps for a, b in zip(t.l_partkey[:2000].tolist(), t.l_suppkey[:2000].tolist()))
 
 
-@pytest.mark.parametrize("world,max_bytes", [(2, None), (2, 20000)])
+@pytest.mark.parametrize("world,max_bytes", [(2, None), (2, 20000), (8, None)])
 def test_q3_q9_distributed_match_pandas(oracle_mod, world, max_bytes):
     from tpch_ref import frames, q3_pandas, q9_pandas
 
