@@ -409,6 +409,8 @@ hj_status build_attempt(hj_table* t, const std::vector<Segment>& segs, double lf
     for (size_t i = 0; i < segs.size(); ++i) seg_n[i] = segs[i].n;
     const int64_t ftiles = frag_build_tiles(seg_n.data(), (int)segs.size());
     const bool frag = dense && total > 0 && frag_build_mode() && frag_build_ok(g, ftiles);
+    // hashed tables: the frag build unless mode 2 keeps the histogram path (DFP_HJ_FRAG_BUILD=0)
+    const bool hfrag = !dense && total > 0 && build_mode_raw() != 2 && hashed_frag_ok(g, ftiles);
     hipDeviceProp_t* prop0 = device_props(t->device);
     const int64_t ntiles = build_tiles(total, prop0 ? prop0->multiProcessorCount : 256);
     const int64_t tile_rows = build_tile_rows(total, ntiles);
@@ -436,12 +438,14 @@ hj_status build_attempt(hj_table* t, const std::vector<Segment>& segs, double lf
             return st;
         t->row_ids = (uint64_t*)p;
     }
-    if (frag) {
+    if (frag || hfrag) {
         void* fscr;
         uint32_t* d_tb;
         uint64_t* ids32 = nullptr;
         BigSeg* fbig;
-        if ((st = dev_alloc(t, t->scratch, &fscr, (size_t)frag_build_scratch_bytes(g, ftiles, total))) != HJ_OK) return st;
+        const int64_t fbytes =
+            frag ? frag_build_scratch_bytes(g, ftiles, total) : hashed_frag_scratch_bytes(g, ftiles, total);
+        if ((st = dev_alloc(t, t->scratch, &fscr, (size_t)fbytes)) != HJ_OK) return st;
         if ((st = dev_alloc(t, t->scratch, &p, sizeof(uint32_t) * (size_t)ftiles)) != HJ_OK) return st;
         d_tb = (uint32_t*)p;
         if ((st = dev_alloc(t, t->scratch, &p, sizeof(BigSeg) * (size_t)(total / (kSmallSeg + 1) + 2))) != HJ_OK)
@@ -463,10 +467,25 @@ hj_status build_attempt(hj_table* t, const std::vector<Segment>& segs, double lf
         }
         hipDeviceProp_t* prop = device_props(t->device);
         const int cus = prop ? prop->multiProcessorCount : 256;
-        HIP_TRY(launch_build_frag(t->key_bytes, segs.data(), (int)segs.size(), g, ftiles, fscr, d_tb, ids32, t->dense,
-                                  t->dup_rows, fbig, ctr, d_segs, total, ids_as_rows, cus, s));
-        // a direct-addressed build cannot overflow (no retry): nothing to read back, the
-        // build stays asynchronous; consumers wait on its completion event
+        if (frag) {
+            HIP_TRY(launch_build_frag(t->key_bytes, segs.data(), (int)segs.size(), g, ftiles, fscr, d_tb, ids32,
+                                      t->dense, t->dup_rows, fbig, ctr, d_segs, total, ids_as_rows, cus, s));
+            // a direct-addressed build cannot overflow (no retry): nothing to read back, the
+            // build stays asynchronous; consumers wait on its completion event
+            return HJ_OK;
+        }
+        HIP_TRY(launch_build_hashed_frag(t->key_bytes, segs.data(), (int)segs.size(), g, ftiles, fscr, d_tb, ids32,
+                                         t->tbl, t->dup_rows, fbig, ctr, d_segs, total, ids_as_rows, cus, s));
+        // a chunk can overflow (adversarial keys): read the error word back, rebuild at half load
+        BuildCounters hc;
+        HIP_TRY(hipMemcpyAsync(&hc, ctr, sizeof(hc), hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        free_list(t, t->scratch);
+        if (hc.err) {
+            *retry = true;
+            free_list(t, t->allocs);
+            t->row_ids = nullptr;
+        }
         return HJ_OK;
     }
     uint32_t *hist, *hist1, *srows, *trows;

@@ -1322,11 +1322,23 @@ constexpr int kSlTileLog = 14;
 constexpr int kSlTile = 1 << kSlTileLog;                // probe rows per tile
 constexpr int kSlGroups = kSlTile / (kSlThreads * 4);  // 4 groups of 4096 rows
 constexpr int kSlWidthLogMax = 15;                      // key values per slice: 2^wlog <= 32768 (128 KB of refs)
-constexpr int kSlMaxSlices = 2047;                      // key ranges up to ~2^25 values
+constexpr int kSlHistBins = 4096;                       // per-tile slice histogram in LDS (16 KB)
+constexpr int kSlMaxSlices = kSlHistBins - 1;           // slices per pass: key ranges up to ~2^27 values
 constexpr int kSlOwnWin = 2048;        // flattened segment positions per owner window (32 per lane)
 constexpr int kSlOwnWinHashed = 1024;  // hashed slices: 16 per lane (u64 entries)
 static_assert(kSlWidthLogMax + kSlTileLog <= 32, "entry = offset << tile bits | row");
 static_assert(kSlWidthLogMax <= 16 && kSlTileLog <= 16, "key offsets and rows leave as u16");
+
+// in-place exclusive scan of a tile's kSlHistBins slice counts (kSlThreads threads, four
+// bins each); *tot = the tile's rows. Ends with a barrier.
+static_assert(kSlHistBins == 4 * kSlThreads, "four bins per thread");
+__device__ __forceinline__ void hist_excl_scan(uint32_t* s_hist, uint32_t* s_w, uint32_t* tot) {
+    const uint32_t b0 = threadIdx.x * 4;
+    const uint4 h = *reinterpret_cast<const uint4*>(s_hist + b0);
+    const uint32_t ex = block_excl_scan<uint32_t>(h.x + h.y + h.z + h.w, s_w, tot);
+    *reinterpret_cast<uint4*>(s_hist + b0) = make_uint4(ex, ex + h.x, ex + h.x + h.y, ex + h.x + h.y + h.z);
+    __syncthreads();
+}
 
 template <typename K, bool HAS_VALID>
 __global__ void __launch_bounds__(kSlThreads, 8)  // 8 waves per SIMD = two workgroups per CU: <= 64 VGPRs
@@ -1338,7 +1350,7 @@ sl_partition_kernel(int64_t dmin, uint64_t drange, uint32_t wlog, uint32_t nslic
                     unsigned long long* __restrict__ tcnt,      // probe: the tile's entry count; build: null
                     uint32_t* __restrict__ tent) {  // probe: entries of the tile so far (earlier passes: append after them)
     __shared__ __attribute__((aligned(16))) uint32_t s_ent[kSlTile];
-    __shared__ uint32_t s_hist[2 * kSlThreads];  // bins 0..nslices (<= kSlMaxSlices + 1)
+    __shared__ __attribute__((aligned(16))) uint32_t s_hist[kSlHistBins];  // bins 0..nslices (<= kSlMaxSlices + 1)
     __shared__ uint32_t s_w[kSlThreads / 64];
     const int64_t tile = blockIdx.x;          // tile of this key array
     const int64_t gtile = tile + tile_off;    // its output region (the build partitions several arrays)
@@ -1347,7 +1359,7 @@ sl_partition_kernel(int64_t dmin, uint64_t drange, uint32_t wlog, uint32_t nslic
     // multi-pass probe (tables beyond kSlMaxSlices slices): this pass's entries follow the
     // tile's entries of the earlier passes (hdr == null marks a later pass)
     const uint32_t ebase = (tent != nullptr && hdr == nullptr) ? tent[gtile] : 0u;
-    for (uint32_t b = threadIdx.x; b < 2 * kSlThreads; b += kSlThreads) s_hist[b] = 0;
+    for (uint32_t b = threadIdx.x; b < kSlHistBins; b += kSlThreads) s_hist[b] = 0;
     // probe: zero the workspace header incl. the error word (no memset launch)
     if (hdr != nullptr && blockIdx.x == 0 && threadIdx.x == 0) hdr[0] = hdr[1] = 0;
     __syncthreads();
@@ -1370,14 +1382,9 @@ sl_partition_kernel(int64_t dmin, uint64_t drange, uint32_t wlog, uint32_t nslic
         }
     }
     __syncthreads();
-    // exclusive scan of the bins, two per thread
-    const uint32_t b0 = threadIdx.x * 2;
-    const uint32_t h0 = s_hist[b0], h1 = s_hist[b0 + 1];
+    // exclusive scan of the bins, four per thread
     uint32_t tot;
-    const uint32_t ex = block_excl_scan<uint32_t>(h0 + h1, s_w, &tot);
-    s_hist[b0] = ex;
-    s_hist[b0 + 1] = ex + h0;
-    __syncthreads();
+    hist_excl_scan(s_hist, s_w, &tot);
     uint16_t* to = toff + gtile * (int64_t)nbins;
     for (uint32_t b = threadIdx.x; b < nbins; b += kSlThreads) to[b] = (uint16_t)(ebase + s_hist[b]);
     if (tile_base != nullptr && threadIdx.x == 0) tile_base[gtile] = (uint32_t)(row_base + tile0);  // build only
@@ -1665,6 +1672,286 @@ dense_frag_build_kernel(ChunkGeom g, uint32_t nblk, int64_t ntiles, const uint16
     for (uint32_t i = threadIdx.x; i < GV / 4; i += T) dst[i] = src[i];
 }
 
+// ---------------------------------------------------------------------------
+// build (hashed, <= kFragMaxTiles tiles): the probe's hashed partition (hs_partition_kernel
+// on the build keys, slices of kHbSliceLog buckets) replaces the two-level histogram /
+// scan / staged-scatter chain; each workgroup then gathers one slice's rows (stored key +
+// row) from every tile's fragment, as the dense frag build does, and builds the slice's
+// chunks in LDS exactly as chunk_build_kernel does (CAS inserts inside each key's chunk,
+// duplicate counts, directory, canonical descending segments, inline meta counts). Key 0
+// (stored 0, home bucket 0: slice 0) goes to the side bucket, written by slice 0's
+// workgroup. Tables past 2047 build slices are built in passes over slice ranges.
+// ---------------------------------------------------------------------------
+constexpr int kHbSliceLog = 10;  // buckets per build slice: 1024 x 64 B = 64 KB of LDS
+constexpr uint32_t kHbSideSlot = (1u << kHbSliceLog) * kSlots;  // the side bucket's slot in the image
+
+template <int T, int RR>
+__global__ void __launch_bounds__(T)
+hashed_frag_build_kernel(uint32_t nb, uint32_t clog2, uint32_t s0, uint32_t nsl, int64_t ntiles,
+                         const uint16_t* __restrict__ toffT, const unsigned long long* __restrict__ ko,
+                         const uint16_t* __restrict__ rl, const uint32_t* __restrict__ tile_base,
+                         const uint64_t* __restrict__ ids32, Bucket* __restrict__ tbl, uint32_t* __restrict__ dup_rows,
+                         BigSeg* __restrict__ big, BuildCounters* ctr, unsigned long long* __restrict__ spill,
+                         uint32_t dupcap) {
+    constexpr uint32_t SB = 1u << kHbSliceLog;
+    // dynamic LDS: the image (SB buckets + the side bucket at img[SB]) | s_to u32[ntiles + 1]
+    // (exclusive position of each tile's fragment) | s_pb u32[ntiles] | the duplicate
+    // directory (3 x dupcap u32; a slice with more duplicated keys keeps its directory in
+    // the spill pool instead)
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    Bucket* img = reinterpret_cast<Bucket*>(smem);
+    uint32_t* s_to = reinterpret_cast<uint32_t*>(smem + (size_t)(SB + 1) * sizeof(Bucket));
+    uint32_t* s_pb = s_to + ntiles + 1;
+    uint32_t* s_dir = s_pb + ntiles;
+    __shared__ unsigned s_ndup, s_dup;
+    __shared__ uint32_t* s_dirp;
+    __shared__ unsigned long long s_w[T / 64];
+    __shared__ unsigned long long s_base, s_sp;
+    __shared__ uint32_t s_carry;
+    const uint32_t c = blockIdx.x;  // slice of this pass
+    const uint32_t b0 = (s0 + c) << kHbSliceLog;
+    const uint32_t nimg = min(SB, nb - b0);
+    const uint32_t cmask = (1u << clog2) - 1;
+    const uint32_t nbins = nsl + 1;
+    const bool has_side = (s0 + c) == 0;
+    {
+        uint4* p = reinterpret_cast<uint4*>(img);
+        for (uint32_t k = threadIdx.x; k < (SB + 1) * 4; k += T) p[k] = make_uint4(0, 0, 0, 0);
+        if (threadIdx.x == 0) {
+            s_ndup = 0;
+            s_dup = 0;
+            s_carry = 0;
+        }
+    }
+    __syncthreads();
+    // fragment bounds of this slice in every tile -> exclusive positions (block scan)
+    for (int64_t t0 = 0; t0 < ntiles; t0 += T) {
+        const int64_t t = t0 + threadIdx.x;
+        uint32_t st = 0, len = 0;
+        if (t < ntiles) {
+            const uint16_t* to = toffT + ((t >> 6) * nbins + c) * 64 + (t & 63);
+            st = to[0];
+            len = (uint32_t)to[64] - st;
+        }
+        uint32_t tot;
+        const uint32_t ex = block_excl_scan<uint32_t>(len, reinterpret_cast<uint32_t*>(s_w), &tot) + s_carry;
+        if (t < ntiles) {
+            s_to[t] = ex;
+            s_pb[t] = (uint32_t)t * kSlTile + st - ex;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) s_carry += tot;
+        __syncthreads();
+    }
+    const uint32_t R = s_carry;
+    if (threadIdx.x == 0) {
+        s_to[ntiles] = R;
+        if (R) atomicAdd(&ctr->n_valid, (unsigned long long)R);
+    }
+    __syncthreads();
+    auto fetch = [&](uint32_t r, unsigned long long* sk, uint32_t* row) {
+        int lo = 0, hi = (int)ntiles - 1;  // largest tile with s_to[tile] <= r
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (s_to[mid] <= r) lo = mid; else hi = mid - 1;
+        }
+        const uint32_t pos = s_pb[lo] + r;
+        *sk = ko[pos];
+        const uint32_t rw = tile_base[lo] + rl[pos];
+        *row = ids32 ? (uint32_t)ids32[rw] : rw;
+    };
+    // slot of a stored key in the image (claiming insert: | kSlotNew); key 0: the side slot,
+    // claimed by the first row that flips its LDS marker
+    auto slot_of = [&](unsigned long long sk, bool insert) -> int {
+        if (sk == 0) {
+            if (!insert) return (int)kHbSideSlot;
+            const unsigned long long was = atomicCAS(&img[SB].key[0], 0ull, 1ull);
+            return (int)kHbSideSlot | (was == 0 ? kSlotNew : 0);
+        }
+        const uint32_t b = stored_bucket(sk, nb) - b0;  // < nimg: the partition put the row in this slice
+        Bucket* ch = img + (b & ~cmask);
+        const int v = insert ? chunk_slot<true>(ch, cmask, b & cmask, sk) : chunk_slot<false>(ch, cmask, b & cmask, sk);
+        if (v < 0) return -1;
+        return (int)(((b & ~cmask) * kSlots + (uint32_t)(v & ~kSlotNew)) | (uint32_t)(v & kSlotNew));
+    };
+    auto ref_at = [&](uint32_t sl) -> unsigned& { return img[sl / kSlots].ref[sl % kSlots]; };
+    const bool in_regs = R <= (uint32_t)(T * RR);
+    if (threadIdx.x == 0 && !in_regs) s_sp = atomicAdd(&ctr->spill_used, 2ull * R);
+    __syncthreads();
+    // more rows than the registers hold: gathered once into the spill pool (key, row)
+    unsigned long long* sp = spill + (in_regs ? 0ull : s_sp);
+    if (!in_regs) {
+        for (uint32_t r = threadIdx.x; r < R; r += T) {
+            unsigned long long k;
+            uint32_t rw;
+            fetch(r, &k, &rw);
+            sp[2 * r] = k;
+            sp[2 * r + 1] = rw;
+        }
+        __syncthreads();
+    }
+    uint32_t rrow[RR];
+    int rslot[RR];
+    // pass A: claim slots; the claiming insert stores its row (final for a single-row key)
+    if (in_regs) {
+        unsigned long long rk[RR];
+#pragma unroll
+        for (int u = 0; u < RR; ++u) {
+            const uint32_t r = u * T + threadIdx.x;
+            rk[u] = 0;
+            rrow[u] = 0;
+            if (r < R) fetch(r, &rk[u], &rrow[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < RR; ++u) {
+            rslot[u] = -1;
+            if (u * T + threadIdx.x >= R) continue;
+            const int v = slot_of(rk[u], true);
+            if (v < 0) { atomicOr(&ctr->err, 1ull); continue; }  // chunk full: the host rebuilds at half load
+            rslot[u] = v & ~kSlotNew;
+            if (v & kSlotNew) ref_at(rslot[u]) = rrow[u];
+            else s_dup = 1u;
+        }
+    } else {
+        if (threadIdx.x == 0) s_dup = 1u;
+        for (uint32_t r = threadIdx.x; r < R; r += T) {
+            if (slot_of(sp[2 * r], true) < 0) atomicOr(&ctr->err, 1ull);
+        }
+    }
+    __syncthreads();
+    const uint32_t nslot = SB * kSlots + kSlots;  // the image's slots and the side bucket's
+    if (s_dup) {  // uniform
+        // row counts per slot
+        for (uint32_t sl = threadIdx.x; sl < nslot; sl += T) ref_at(sl) = 0;
+        __syncthreads();
+        if (in_regs) {
+#pragma unroll
+            for (int u = 0; u < RR; ++u)
+                if (rslot[u] >= 0) atomicAdd(&ref_at(rslot[u]), 1u);
+        } else {
+            for (uint32_t r = threadIdx.x; r < R; r += T) {
+                const int v = slot_of(sp[2 * r], false);
+                if (v >= 0) atomicAdd(&ref_at(v), 1u);
+            }
+        }
+        __syncthreads();
+        // the directory of duplicated keys (count > 1): in LDS when it fits, else in the
+        // spill pool (generic pointers: the same code serves both)
+        for (uint32_t sl = threadIdx.x; sl < nslot; sl += T)
+            if (ref_at(sl) > 1) atomicAdd(&s_ndup, 1u);
+        __syncthreads();
+        const unsigned ndup = s_ndup;
+        if (threadIdx.x == 0) {
+            if (ndup <= dupcap) {
+                s_dirp = s_dir;
+            } else {
+                const unsigned long long at = atomicAdd(&ctr->spill_used, (3ull * ndup + 1) / 2);
+                s_dirp = reinterpret_cast<uint32_t*>(spill + at);
+            }
+            s_ndup = 0;
+        }
+        __syncthreads();
+        uint32_t* d_off = s_dirp;
+        uint32_t* d_cur = d_off + ndup;
+        uint32_t* d_cnt = d_cur + ndup;
+        for (uint32_t sl = threadIdx.x; sl < nslot; sl += T) {
+            unsigned& ref = ref_at(sl);
+            const unsigned cnt = ref;
+            if (cnt > 1) {
+                const unsigned li = atomicAdd(&s_ndup, 1u);
+                d_cnt[li] = cnt;
+                d_cur[li] = 0;
+                ref = kDupFlag | li;
+            }
+        }
+        __syncthreads();
+        unsigned long long carry = 0;
+        for (unsigned bb = 0; bb < ndup; bb += T) {
+            const unsigned li = bb + threadIdx.x;
+            const unsigned long long v = li < ndup ? (unsigned long long)d_cnt[li] + 1 : 0;
+            unsigned long long tot;
+            const unsigned long long ex = block_excl_scan<unsigned long long>(v, s_w, &tot);
+            if (li < ndup) d_off[li] = (uint32_t)(carry + ex);
+            carry += tot;
+        }
+        if (threadIdx.x == 0) s_base = carry ? atomicAdd(&ctr->dup_used, carry) : 0;
+        __syncthreads();
+        for (unsigned li = threadIdx.x; li < ndup; li += T) {
+            d_off[li] += (uint32_t)s_base;
+            dup_rows[d_off[li]] = d_cnt[li];
+        }
+        __syncthreads();
+        auto place = [&](int sl, uint32_t row) {
+            unsigned& ref = ref_at(sl);
+            const unsigned rv = ref;
+            if (rv & kDupFlag) {
+                const unsigned li = rv & ~kDupFlag;
+                dup_rows[d_off[li] + 1 + atomicAdd(&d_cur[li], 1u)] = row;
+            } else if (rv == 1) {
+                ref = row;  // the key's only row
+            }
+        };
+        if (in_regs) {
+#pragma unroll
+            for (int u = 0; u < RR; ++u)
+                if (rslot[u] >= 0) place(rslot[u], rrow[u]);
+        } else {
+            for (uint32_t r = threadIdx.x; r < R; r += T) {
+                const int v = slot_of(sp[2 * r], false);
+                if (v >= 0) place(v, (uint32_t)sp[2 * r + 1]);
+            }
+        }
+        __syncthreads();
+        // canonical order inside segments (descending rows), final refs and inline counts
+        for (unsigned li = threadIdx.x; li < ndup; li += T) {
+            const unsigned n = d_cnt[li], off = d_off[li];
+            if (n <= (unsigned)kSmallSeg) {
+                uint32_t v[16];
+#pragma unroll
+                for (int i = 0; i < 16; ++i) v[i] = (i < (int)n) ? dup_rows[off + 1 + i] : 0u;
+                sort16_desc(v);
+#pragma unroll
+                for (int i = 0; i < 16; ++i)
+                    if (i < (int)n) dup_rows[off + 1 + i] = v[i];
+            }
+        }
+        for (uint32_t sl = threadIdx.x; sl < nslot; sl += T) {
+            Bucket& B = img[sl / kSlots];
+            unsigned& ref = B.ref[sl % kSlots];
+            if (ref & kDupFlag) {
+                const unsigned li = ref & ~kDupFlag;
+                const bool side = sl == kHbSideSlot;
+                if (d_cnt[li] > (unsigned)kSmallSeg) {
+                    const unsigned bi = (unsigned)atomicAdd(&ctr->n_big, 1ull);
+                    big[bi] = BigSeg{side ? 0ull : unmix64(B.key[sl % kSlots]), d_off[li], 0u};
+                }
+                ref = kDupFlag | d_off[li];
+                if (!side && d_cnt[li] <= kInlineCount) atomicOr(&B.meta, d_cnt[li] << (1 + 6 * (sl % kSlots)));
+            }
+        }
+        __syncthreads();
+    }
+    // write the finished buckets (coalesced 16-byte stores); slice 0 also writes the side
+    // bucket (keys 0, ref[0], meta = the key-0 rows)
+    {
+        const uint4* src = reinterpret_cast<const uint4*>(img);
+        uint4* dst = reinterpret_cast<uint4*>(tbl + b0);
+        for (uint32_t k = threadIdx.x; k < nimg * 4; k += T) dst[k] = src[k];
+    }
+    if (has_side && threadIdx.x == 0) {
+        Bucket& S = tbl[nb];
+        const bool used = img[SB].key[0] != 0;
+        uint32_t rows0 = 0;
+        if (used) rows0 = (img[SB].ref[0] & kDupFlag) ? dup_rows[img[SB].ref[0] & ~kDupFlag] : 1u;
+        for (int j = 0; j < kSlots; ++j) {
+            S.key[j] = 0;
+            S.ref[j] = 0;
+        }
+        S.ref[0] = used ? img[SB].ref[0] : 0u;
+        S.meta = rows0;
+    }
+}
+
 // grid = nslices x parts; item i: slice i % nslices, tiles [part range) with
 // part = i / nslices. Each wave walks runs of 64 tiles: lane l reads tile l's segment
 // bounds (prefetched one run ahead), a wave scan flattens the segments over the lanes,
@@ -1941,17 +2228,19 @@ sl_lookup_kernel(TableView tv, uint32_t wlog, uint32_t nslices, int64_t ntiles, 
 // once this tile's keys are staged, while they and the rows are written out.
 template <typename K, bool HAS_VALID>
 __global__ void __launch_bounds__(kSlThreads, 4)  // 16 waves per CU: <= 128 VGPRs
-hs_partition_kernel(uint32_t nb, uint32_t s0, uint32_t nslices, const void* __restrict__ keys,
+hs_partition_kernel(uint32_t nb, uint32_t slog, uint32_t s0, uint32_t nslices, const void* __restrict__ keys,
                     const uint8_t* __restrict__ valid, int64_t voff, int64_t n, int64_t ntiles, bool vec,
                     unsigned long long* __restrict__ ko, uint16_t* __restrict__ rl, uint16_t* __restrict__ toff,
                     unsigned long long* __restrict__ hdr, unsigned long long* __restrict__ tcnt,
-                    uint32_t* __restrict__ tent) {  // pass: slices [s0, s0 + nslices); hdr null = a later pass
+                    uint32_t* __restrict__ tent,  // probe pass: slices [s0, s0 + nslices); hdr null = a later pass
+                    int64_t tile_off, int64_t row_base, uint32_t* __restrict__ tile_base) {  // build: tcnt null
     __shared__ __attribute__((aligned(16))) unsigned long long s_key[kSlTile];  // also the rows (u16) pass
-    __shared__ uint32_t s_hist[2 * kSlThreads];
+    __shared__ __attribute__((aligned(16))) uint32_t s_hist[kSlHistBins];
     __shared__ uint32_t s_w[kSlThreads / 64];
     const uint32_t nbins = nslices + 1;
-    const bool later = hdr == nullptr;
-    if (!later && blockIdx.x == 0 && threadIdx.x == 0) hdr[0] = hdr[1] = 0;  // workspace header (error word)
+    const bool probe = tcnt != nullptr;  // else the hashed frag build's partition of one build segment
+    const bool later = probe && hdr == nullptr;
+    if (probe && !later && blockIdx.x == 0 && threadIdx.x == 0) hdr[0] = hdr[1] = 0;  // workspace header (error word)
     int64_t k[kSlGroups][4], nk[kSlGroups][4];
     auto load = [&](int64_t t, int64_t (&dst)[kSlGroups][4]) {
 #pragma unroll
@@ -1962,11 +2251,12 @@ hs_partition_kernel(uint32_t nb, uint32_t s0, uint32_t nslices, const void* __re
     if (tile < ntiles) load(tile, nk);
     for (; tile < ntiles; tile += gridDim.x) {
         const int64_t tile0 = tile * kSlTile;
+        const int64_t gtile = tile + tile_off;  // its output region (the build partitions several segments)
 #pragma unroll
         for (int g = 0; g < kSlGroups; ++g)
 #pragma unroll
             for (int q = 0; q < 4; ++q) k[g][q] = nk[g][q];
-        for (uint32_t b = threadIdx.x; b < 2 * kSlThreads; b += kSlThreads) s_hist[b] = 0;
+        for (uint32_t b = threadIdx.x; b < kSlHistBins; b += kSlThreads) s_hist[b] = 0;
         const uint32_t ebase = later ? tent[tile] : 0u;
         __syncthreads();
         uint32_t sr[kSlGroups][4];  // slice << 14 | rank in slice, ~0 = no entry
@@ -1977,25 +2267,21 @@ hs_partition_kernel(uint32_t nb, uint32_t s0, uint32_t nslices, const void* __re
             for (int q = 0; q < 4; ++q) {
                 const int64_t row = tile0 + loc0 + q;
                 const unsigned long long sk = stored_key(k[g][q]);
-                const uint32_t sl = (stored_bucket(sk, nb) >> kHsSliceLog) - s0;  // wraps past the pass: no entry
+                const uint32_t sl = (stored_bucket(sk, nb) >> slog) - s0;  // wraps past the pass: no entry
                 const bool ok = row < n && (!HAS_VALID || bit_valid(valid, voff, row)) && sl < nslices;
                 sr[g][q] = ok ? (sl << kSlTileLog) | atomicAdd(&s_hist[sl], 1u) : 0xFFFFFFFFu;
             }
         }
         __syncthreads();
-        const uint32_t b0 = threadIdx.x * 2;
-        const uint32_t h0 = s_hist[b0], h1 = s_hist[b0 + 1];
         uint32_t tot;
-        const uint32_t ex = block_excl_scan<uint32_t>(h0 + h1, s_w, &tot);
-        s_hist[b0] = ex;
-        s_hist[b0 + 1] = ex + h0;
-        __syncthreads();
-        uint16_t* to = toff + tile * (int64_t)nbins;
+        hist_excl_scan(s_hist, s_w, &tot);
+        uint16_t* to = toff + gtile * (int64_t)nbins;
         for (uint32_t b = threadIdx.x; b < nbins; b += kSlThreads) to[b] = (uint16_t)(ebase + s_hist[b]);
-        if (threadIdx.x == 0) {
+        if (threadIdx.x == 0 && probe) {
             tcnt[tile] = (later ? tcnt[tile] : 0ull) + tot;  // S2 corrects it to the tile's pair count
             tent[tile] = ebase + tot;
         }
+        if (threadIdx.x == 0 && tile_base != nullptr) tile_base[gtile] = (uint32_t)(row_base + tile0);
         // pass 1: stored keys in slice order
 #pragma unroll
         for (int g = 0; g < kSlGroups; ++g)
@@ -2005,7 +2291,7 @@ hs_partition_kernel(uint32_t nb, uint32_t s0, uint32_t nslices, const void* __re
                     s_key[s_hist[sr[g][q] >> kSlTileLog] + (sr[g][q] & (kSlTile - 1))] = stored_key(k[g][q]);
         __syncthreads();
         if (tile + (int64_t)gridDim.x < ntiles) load(tile + gridDim.x, nk);  // in flight during the write-out
-        unsigned long long* dk = ko + tile0 + ebase;
+        unsigned long long* dk = ko + gtile * kSlTile + ebase;
         if (ebase & 1) {  // a later pass at an odd base: 8-byte stores
             for (uint32_t i = threadIdx.x; i < tot; i += kSlThreads) dk[i] = s_key[i];
         } else {
@@ -2025,7 +2311,7 @@ hs_partition_kernel(uint32_t nb, uint32_t s0, uint32_t nslices, const void* __re
                     s_row[s_hist[sr[g][q] >> kSlTileLog] + (sr[g][q] & (kSlTile - 1))] =
                         (uint16_t)(g * (kSlThreads * 4) + threadIdx.x * 4 + q);
         __syncthreads();
-        uint16_t* dr = rl + tile0 + ebase;
+        uint16_t* dr = rl + gtile * kSlTile + ebase;
         if (ebase & 7) {  // a later pass at an unaligned base: 2-byte stores
             for (uint32_t i = threadIdx.x; i < tot; i += kSlThreads) dr[i] = s_row[i];
         } else {
@@ -2396,18 +2682,22 @@ part_regions_kernel(const void* __restrict__ keys, const uint8_t* __restrict__ v
     int64_t key[kRpIters];
     uint32_t dr[kRpIters];  // destination << 8 | rank among the wave's rows of it; ~0 = dropped
     const unsigned long long lt = (1ull << lane) - 1;
+    // every load of the tile issued before any use: the ballots below are convergence
+    // points, and loads interleaved with them wait one round trip per iteration (16 per
+    // tile: 520 us for 10^8 rows, against one round trip)
+    bool vb[kRpIters];
 #pragma unroll
     for (int it = 0; it < kRpIters; ++it) {
         const int64_t row = tile0 + (int64_t)it * kRpThreads + threadIdx.x;
+        key[it] = row < n ? (int64_t)reinterpret_cast<const K*>(keys)[row] : 0;
+        vb[it] = row < n && (!HAS_VALID || bit_valid(valid, voff, row));
+    }
+#pragma unroll
+    for (int it = 0; it < kRpIters; ++it) {
         int p = -1;
-        key[it] = 0;
-        if (row < n) {
-            key[it] = (int64_t)reinterpret_cast<const K*>(keys)[row];
-            const bool ok = (!HAS_VALID || bit_valid(valid, voff, row)) && key[it] >= sp.lo && key[it] <= sp.hi;
-            if (ok)
-                p = sp.by_range ? (int)__umul64hi((uint64_t)key[it] - (uint64_t)sp.lo, sp.mul)
-                                : (int)(mix64((uint64_t)key[it]) & (uint64_t)(nparts - 1));
-        }
+        if (vb[it] && key[it] >= sp.lo && key[it] <= sp.hi)
+            p = sp.by_range ? (int)__umul64hi((uint64_t)key[it] - (uint64_t)sp.lo, sp.mul)
+                            : (int)(mix64((uint64_t)key[it]) & (uint64_t)(nparts - 1));
         unsigned long long same = __ballot(p >= 0);
         for (int bt = 0; bt < bits; ++bt) {
             const unsigned long long m = __ballot(p >= 0 && ((p >> bt) & 1));
@@ -2787,6 +3077,71 @@ hipError_t launch_build_frag(int key_bytes, const Segment* h_segs, int nseg, con
     return hipGetLastError();
 }
 
+// hashed frag build: chunks of <= 2^kHbSliceLog buckets, <= kFragMaxTiles tiles
+bool hashed_frag_ok(const ChunkGeom& g, int64_t ftiles) {
+    return !g.dense && g.clog2 <= (uint32_t)kHbSliceLog && ftiles <= kFragMaxTiles && ftiles > 0;
+}
+uint32_t hashed_frag_slices(const ChunkGeom& g) { return (g.nb + (1u << kHbSliceLog) - 1) >> kHbSliceLog; }
+int64_t hashed_frag_scratch_bytes(const ChunkGeom& g, int64_t ftiles, int64_t total) {
+    const int64_t nbins = std::min<uint32_t>(hashed_frag_slices(g), (uint32_t)kSlMaxSlices) + 1;
+    return 8 * ftiles * kSlTile + 2 * ftiles * kSlTile + 2 * ftiles * nbins + 2 * ((ftiles + 63) & ~(int64_t)63) * nbins +
+           32 * total + 6 * 256;  // spill pool: 16 B per row (rows) + up to 16 B per row (directories)
+}
+hipError_t launch_build_hashed_frag(int key_bytes, const Segment* h_segs, int nseg, const ChunkGeom& g, int64_t ftiles,
+                                    void* scratch, uint32_t* tile_base, const uint64_t* ids32, Bucket* tbl,
+                                    uint32_t* dup_rows, BigSeg* big, BuildCounters* ctr, const Segment* d_segs,
+                                    int64_t total, bool ids_as_rows, int cus, hipStream_t s) {
+    constexpr int T = 512, RR = 8;
+    const uint32_t nsl_all = hashed_frag_slices(g);
+    const int64_t nbins_max = std::min<uint32_t>(nsl_all, (uint32_t)kSlMaxSlices) + 1;
+    auto a256 = [](uintptr_t x) { return (x + 255) & ~(uintptr_t)255; };
+    uintptr_t p = a256((uintptr_t)scratch);
+    unsigned long long* ko = (unsigned long long*)p; p = a256(p + 8 * ftiles * kSlTile);
+    uint16_t* rl = (uint16_t*)p;   p = a256(p + 2 * ftiles * kSlTile);
+    uint16_t* toff = (uint16_t*)p; p = a256(p + 2 * ftiles * nbins_max);
+    uint16_t* toffT = (uint16_t*)p; p = a256(p + 2 * ((ftiles + 63) & ~(int64_t)63) * nbins_max);
+    unsigned long long* spill = (unsigned long long*)p;  // rows past the registers + directories past the LDS
+    // LDS: the slice image + side bucket, the tiles' fragment positions, then a duplicate
+    // directory of what is left of 80 KB (two workgroups per CU); slices with more
+    // duplicated keys keep their directory in the spill pool
+    const size_t img = (size_t)((1u << kHbSliceLog) + 1) * sizeof(Bucket) + 8 * (size_t)ftiles + 4;
+    const size_t budget = 80 * 1024 - 256;
+    const uint32_t dupcap = img < budget ? (uint32_t)((budget - img) / 12) : 0u;
+    const size_t lds = img + (size_t)dupcap * 12;
+    const void* kfn = (const void*)hashed_frag_build_kernel<T, RR>;
+    hipError_t e = hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+    for (uint32_t s0 = 0; s0 < nsl_all; s0 += (uint32_t)kSlMaxSlices) {
+        const uint32_t nsl = std::min<uint32_t>(nsl_all - s0, (uint32_t)kSlMaxSlices), nbins = nsl + 1;
+        int64_t t0 = 0;
+        for (int i = 0; i < nseg; ++i) {
+            const Segment& sg = h_segs[i];
+            const int64_t nt = (sg.n + kSlTile - 1) / kSlTile;
+            if (nt == 0) continue;
+            const bool vec = (reinterpret_cast<uintptr_t>(sg.keys) & 15) == 0;
+            const unsigned pgrid = (unsigned)std::min<int64_t>(nt, cus);
+#define DFP_HBP(KT, HV)                                                                                           \
+    hs_partition_kernel<KT, HV><<<pgrid, kSlThreads, 0, s>>>(g.nb, kHbSliceLog, s0, nsl, sg.keys, sg.valid, sg.voff,  \
+                                                            sg.n, nt, vec, ko, rl, toff, nullptr, nullptr, nullptr,  \
+                                                            t0, sg.row_base, tile_base)
+            if (key_bytes == 8) {
+                if (sg.valid) DFP_HBP(int64_t, true); else DFP_HBP(int64_t, false);
+            } else {
+                if (sg.valid) DFP_HBP(int32_t, true); else DFP_HBP(int32_t, false);
+            }
+#undef DFP_HBP
+            t0 += nt;
+        }
+        sl_toff_transpose_kernel<<<(unsigned)((ftiles + 63) / 64 * ((nbins + kSlTrChunk - 1) / kSlTrChunk)), 256, 0,
+                                   s>>>(toff, nbins, ftiles, toffT);
+        hashed_frag_build_kernel<T, RR><<<nsl, T, lds, s>>>(g.nb, g.clog2, s0, nsl, ftiles, toffT, ko, rl, tile_base,
+                                                           ids_as_rows ? ids32 : nullptr, tbl, dup_rows, big, ctr,
+                                                           spill, dupcap);
+    }
+    dup_sort_big_kernel<<<cus, kBigThreads, 0, s>>>(dup_rows, big, ctr, d_segs, nseg, total, key_bytes, ids_as_rows);
+    return hipGetLastError();
+}
+
 hipError_t launch_build(int key_bytes, const Segment* d_segs, int nseg, int64_t total, const ChunkGeom& g,
                         uint32_t* hist, uint32_t* hist1, uint32_t* chunk_starts, int64_t ntiles,
                         int64_t tile_rows, void* scan_scratch,
@@ -3074,8 +3429,9 @@ hipError_t launch_probe_sliced(int key_bytes, const TableView& tv, const void* k
         if (hashed) {
             const unsigned pgrid = (unsigned)std::min<int64_t>(nt, sl_num_cus());
 #define DFP_HSP(KT, HV)                                                                                           \
-    hs_partition_kernel<KT, HV><<<pgrid, kSlThreads, 0, s>>>(tv.nb, s0, nsl, keys, valid, voff, n, nt, vec,        \
-                                                            (unsigned long long*)w.ko, w.rl, w.toff, h, w.tcnt, w.tent)
+    hs_partition_kernel<KT, HV><<<pgrid, kSlThreads, 0, s>>>(tv.nb, kHsSliceLog, s0, nsl, keys, valid, voff, n, nt, \
+                                                            vec, (unsigned long long*)w.ko, w.rl, w.toff, h, w.tcnt,   \
+                                                            w.tent, 0, 0, nullptr)
             if (key_bytes == 8) {
                 if (valid) DFP_HSP(int64_t, true); else DFP_HSP(int64_t, false);
             } else {

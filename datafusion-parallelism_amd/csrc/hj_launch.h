@@ -49,6 +49,17 @@ hipError_t launch_build_frag(int key_bytes, const Segment* h_segs, int nseg, con
                              void* scratch, uint32_t* tile_base, const uint64_t* ids32, uint32_t* dense,
                              uint32_t* dup_rows, BigSeg* big, BuildCounters* ctr, const Segment* d_segs, int64_t total,
                              bool ids_as_rows, int big_grid, hipStream_t s);
+// Hashed builds of chunks <= 1024 buckets and <= kFragMaxTiles tiles: the probe's hashed
+// partition on the build keys (1024-bucket slices, passes of <= 2047 slices), then one
+// workgroup per slice gathers its rows from the tiles' fragments and builds the slice's
+// chunks in LDS. scratch: hashed_frag_scratch_bytes; tile_base u32[ftiles]. Sets ctr->err
+// like launch_build when a chunk overflows (the caller rebuilds at half load).
+bool hashed_frag_ok(const ChunkGeom& g, int64_t ftiles);
+int64_t hashed_frag_scratch_bytes(const ChunkGeom& g, int64_t ftiles, int64_t total);
+hipError_t launch_build_hashed_frag(int key_bytes, const Segment* h_segs, int nseg, const ChunkGeom& g, int64_t ftiles,
+                                    void* scratch, uint32_t* tile_base, const uint64_t* ids32, Bucket* tbl,
+                                    uint32_t* dup_rows, BigSeg* big, BuildCounters* ctr, const Segment* d_segs,
+                                    int64_t total, bool ids_as_rows, int cus, hipStream_t s);
 // min and max of the valid keys of the build segments -> out[0], out[1] (int64);
 // out holds 2 + 2 * kMinmaxMaxBlocks int64 (per-block partials behind the result);
 // mbox (optional, fine-grained host memory): min, max, then seq stored with system-scope

@@ -212,12 +212,14 @@ hj_status hj_probe_async_base(const hj_table* t, const void* keys, const uint8_t
                               int64_t* d_total, void* workspace, void* stream);
 
 /* Probe strategy for later probes of this process: 0 auto (sliced for tables past the L2s
- * - more than 2^20 key values or 2^16 buckets, at most 2047 slices - with a probe side at
- * least as large as the key range / bucket count, else fused),
+ * - more than 2^20 key values or 2^16 buckets, at most 4 passes of 2047 slices - with a
+ * probe side at least as large as the key range / bucket count, else fused),
  * 3 fused (lookup + emission in one launch, tile offsets by decoupled look-back),
  * 4 sliced (probe rows partitioned by slice - 32768 key values of a direct-addressed table
- * or 2048 buckets of a hashed one - lookups out of LDS, then ordered emission; tables of
- * more than 2047 slices fused). Results are identical;
+ * or 2048 buckets of a hashed one - lookups out of LDS, then ordered emission; a table of
+ * more than 2047 slices is probed in passes over slice ranges, each pass partitioning the
+ * probe rows of its range and looking them up, one emission at the end). Results are
+ * identical;
  * returns the previous mode, -1 for a bad value (1 and 2 named strategies measured slower
  * and removed). Also settable with DFP_HJ_PROBE_MODE=fused|sliced. */
 int hj_set_probe_mode(int mode);
@@ -225,10 +227,10 @@ int hj_set_probe_mode(int mode);
 /* Table layout for later builds of this process: 0 auto (a direct-addressed table - one
  * u32 ref per key value - when the build keys' range is at most 8x the build rows, the
  * "perfect hash" of dense integer keys; else 5-slot hashed buckets), 1 hashed buckets
- * always, 2 as 0 but the direct-addressed build partitions its rows by histogram + scan
- * + scatter instead of the tile-local partition. Results are identical; returns the
- * previous mode, -1 for a bad value. Also settable with DFP_HJ_DENSE=0 (hashed) and
- * DFP_HJ_FRAG_BUILD=0 (mode 2). */
+ * always, 2 as 0 but the build partitions its rows by histogram + scan + scatter (both
+ * layouts) instead of the tile-local partition and per-slice LDS build from its
+ * fragments. Results are identical; returns the previous mode, -1 for a bad value. Also
+ * settable with DFP_HJ_DENSE=0 (hashed) and DFP_HJ_FRAG_BUILD=0 (mode 2). */
 int hj_set_build_mode(int mode);
 
 /* Makes `stream` wait for the build of `t` (for probes on other streams). */

@@ -359,6 +359,28 @@ def test_hashed_sliced_auto(dfp, oracle_mod, nb, np_, dup_frac, null_frac, key_t
         L.hj_set_build_mode(old_b)
 
 
+@pytest.mark.parametrize("layout", [0, 2])
+def test_hashed_build_every_key_twice(dfp, oracle_mod, layout):
+    """Hashed table whose every key has two rows (plus a few with 3..40): each 1024-bucket
+    build slice then has more duplicated keys than its LDS directory holds, so the frag
+    build keeps those directories in the spill pool (layout 0); layout 2 is the histogram
+    path. Same pairs as the oracle."""
+    L = dfp.load()
+    old = L.hj_set_build_mode(layout)
+    try:
+        rng = np.random.default_rng(41)
+        d = rng.integers(-(2**63), 2**63 - 1, 700_000, dtype=np.int64)
+        bk = np.concatenate([d, d, d[:1000], np.full(40, d[7])])
+        rng.shuffle(bk)
+        pk = np.concatenate([d[rng.integers(0, len(d), 900_000)], rng.integers(-(2**63), 2**63 - 1, 300_000)])
+        b, p, st = gpu_join(dfp, bk, pk)
+        assert st["buckets"] > 0 and st["dup_keys"] == 700_000
+        ob, op = oracle_mod.inner_join(bk, pk)
+        assert_same(b, p, ob, op)
+    finally:
+        L.hj_set_build_mode(old)
+
+
 def test_c3_full_size_digest(dfp, oracle_mod):
     """C3 (10^7 exponential build keys x 10^8 uniform probe keys): the pair count and
     per-probe-row match counts against the closed form multiplicity of each key."""
@@ -485,8 +507,8 @@ def sliced_mode(dfp):
 
 @pytest.mark.parametrize("nb,krange,np_,null_frac,key_type", [
     (9_000_000, 2047 * 32768, 2_000_000, 0.0, "int64"),     # 2047 slices: the largest sliced table
-    (9_000_000, 2048 * 32768, 1_000_000, 0.0, "int64"),     # 2048 slices: two passes over slice ranges
-    (17_000_000, 4100 * 32768, 2_000_000, 0.01, "int64"),   # 4100 slices: three passes, nulls
+    (9_000_000, 2048 * 32768, 1_000_000, 0.0, "int64"),     # 2048 slices: past round 2's 2047-slice limit
+    (17_000_000, 4100 * 32768, 2_000_000, 0.01, "int64"),   # 4100 slices: two passes over slice ranges, nulls
     (5_000_000, 2047 * 16384, 2_000_000, 0.0, "int64"),     # ~1024 slices
     (300_000, 1_000_000, 3_000_001, 0.02, "int32"),         # nulls, ragged last tile
     (2_000_000, 600_000, 1_500_000, 0.0, "int64"),          # duplicated keys (counts <= 15 and more)
@@ -508,11 +530,13 @@ def test_sliced_probe_parity(dfp, oracle_mod, sliced_mode, nb, krange, np_, null
     assert_same(b, p, ob, op)
 
 
-@pytest.mark.parametrize("nb,np_,dup_frac", [(12_000_000, 2_000_000, 0.0), (11_000_000, 1_500_001, 0.2)])
+@pytest.mark.parametrize("nb,np_,dup_frac", [(12_000_000, 2_000_000, 0.0), (11_000_000, 1_500_001, 0.2),
+                                               (22_000_000, 2_000_000, 0.05)])
 def test_sliced_hashed_multipass_parity(dfp, oracle_mod, sliced_mode, nb, np_, dup_frac):
-    """Hashed tables past 2047 slices of 2048 buckets (12 M keys at load 0.5 = 2344
-    slices): the probe runs two passes over slice ranges, appending to the tiles' entries,
-    one emission; duplicated keys and key 0 (the side bucket, slice 0) included."""
+    """Hashed tables past round 2's 2047 slices of 2048 buckets (12 M keys at load 0.5 =
+    2344 slices: one pass of up to 4095), and past one pass (22 M keys = 4297 slices: two
+    passes over slice ranges, appending to the tiles' entries, one emission); duplicated
+    keys and key 0 (the side bucket, slice 0) included."""
     rng = np.random.default_rng(nb)
     distinct = rng.integers(-(2**63), 2**63 - 1, nb, dtype=np.int64)
     bk = distinct.copy()
@@ -523,13 +547,13 @@ def test_sliced_hashed_multipass_parity(dfp, oracle_mod, sliced_mode, nb, np_, d
     pk = np.concatenate([bk[rng.integers(0, nb, np_ // 2)], rng.integers(-(2**63), 2**63 - 1, np_ - np_ // 2)])
     pk[:2] = [0, bk[5]]
     b, p, st = gpu_join(dfp, bk, pk)
-    assert st["buckets"] > 2047 * 2048  # beyond one pass
+    assert st["buckets"] > 2047 * 2048  # beyond round 2's sliced limit
     ob, op = oracle_mod.inner_join(bk, pk)
     assert_same(b, p, ob, op)
 
 
 def test_c2h_40m_multipass_closed_form(dfp):
-    """A 4*10^7-key hashed build (16 M buckets = 7813 slices: four sliced passes, the auto
+    """A 4*10^7-key hashed build (16 M buckets = 7813 slices: two sliced passes, the auto
     choice) probed with 10^8 rows: C2's closed form under the bijection k -> k * M —
     probe keys below B match exactly the row k * inv(7368787) mod B; count, order, values."""
     B, P = 40_000_000, 10**8
@@ -548,7 +572,7 @@ def test_c2h_40m_multipass_closed_form(dfp):
     with dfp.HashTable(1, "int64", 0) as t:
         t.build(bk)
         st = t.stats()
-        assert st["buckets"] > 3 * 2047 * 2048  # four passes
+        assert st["buckets"] > 4095 * 2048  # two passes of up to 4095 slices
         b, p = t.probe(pk, device_output=True)
     assert b.numel() == expected
     pl = p.long()
