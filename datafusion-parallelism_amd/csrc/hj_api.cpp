@@ -481,6 +481,8 @@ hj_status build_attempt(hj_table* t, const std::vector<Segment>& segs, double lf
         HIP_TRY(hipMemcpyAsync(&hc, ctr, sizeof(hc), hipMemcpyDeviceToHost, s));
         HIP_TRY(hipStreamSynchronize(s));
         free_list(t, t->scratch);
+        if (hc.err & ~3ull)
+            return fail(HJ_ERR_HIP, "hashed build: internal check failed (error bits " + std::to_string(hc.err) + ")");
         if (hc.err) {
             *retry = true;
             free_list(t, t->allocs);

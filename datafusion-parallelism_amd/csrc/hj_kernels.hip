@@ -1351,7 +1351,9 @@ sl_partition_kernel(int64_t dmin, uint64_t drange, uint32_t wlog, uint32_t nslic
                     uint32_t* __restrict__ tent) {  // probe: entries of the tile so far (earlier passes: append after them)
     __shared__ __attribute__((aligned(16))) uint32_t s_ent[kSlTile];
     __shared__ __attribute__((aligned(16))) uint32_t s_hist[kSlHistBins];  // bins 0..nslices (<= kSlMaxSlices + 1)
-    __shared__ uint32_t s_w[kSlThreads / 64];
+    // the scan's wave totals alias the entry staging area (free until the scatter), so the
+    // workgroup stays within 80 KB: two per CU
+    uint32_t* s_w = s_ent;
     const int64_t tile = blockIdx.x;          // tile of this key array
     const int64_t gtile = tile + tile_off;    // its output region (the build partitions several arrays)
     const int64_t tile0 = tile * kSlTile;
@@ -1692,7 +1694,7 @@ hashed_frag_build_kernel(uint32_t nb, uint32_t clog2, uint32_t s0, uint32_t nsl,
                          const uint16_t* __restrict__ rl, const uint32_t* __restrict__ tile_base,
                          const uint64_t* __restrict__ ids32, Bucket* __restrict__ tbl, uint32_t* __restrict__ dup_rows,
                          BigSeg* __restrict__ big, BuildCounters* ctr, unsigned long long* __restrict__ spill,
-                         uint32_t dupcap) {
+                         uint32_t dupcap, uint64_t dup_cap, uint64_t spill_cap) {
     constexpr uint32_t SB = 1u << kHbSliceLog;
     // dynamic LDS: the image (SB buckets + the side bucket at img[SB]) | s_to u32[ntiles + 1]
     // (exclusive position of each tile's fragment) | s_pb u32[ntiles] | the duplicate
@@ -1756,6 +1758,12 @@ hashed_frag_build_kernel(uint32_t nb, uint32_t clog2, uint32_t s0, uint32_t nsl,
             if (s_to[mid] <= r) lo = mid; else hi = mid - 1;
         }
         const uint32_t pos = s_pb[lo] + r;
+        if (pos >= (uint64_t)ntiles * kSlTile) {  // internal check (never expected)
+            atomicOr(&ctr->err, 8ull);
+            *sk = 0;
+            *row = 0;
+            return;
+        }
         *sk = ko[pos];
         const uint32_t rw = tile_base[lo] + rl[pos];
         *row = ids32 ? (uint32_t)ids32[rw] : rw;
@@ -1769,6 +1777,10 @@ hashed_frag_build_kernel(uint32_t nb, uint32_t clog2, uint32_t s0, uint32_t nsl,
             return (int)kHbSideSlot | (was == 0 ? kSlotNew : 0);
         }
         const uint32_t b = stored_bucket(sk, nb) - b0;  // < nimg: the partition put the row in this slice
+        if (b >= nimg) {  // internal check (never expected)
+            atomicOr(&ctr->err, 16ull);
+            return -1;
+        }
         Bucket* ch = img + (b & ~cmask);
         const int v = insert ? chunk_slot<true>(ch, cmask, b & cmask, sk) : chunk_slot<false>(ch, cmask, b & cmask, sk);
         if (v < 0) return -1;
@@ -1776,8 +1788,12 @@ hashed_frag_build_kernel(uint32_t nb, uint32_t clog2, uint32_t s0, uint32_t nsl,
     };
     auto ref_at = [&](uint32_t sl) -> unsigned& { return img[sl / kSlots].ref[sl % kSlots]; };
     const bool in_regs = R <= (uint32_t)(T * RR);
-    if (threadIdx.x == 0 && !in_regs) s_sp = atomicAdd(&ctr->spill_used, 2ull * R);
+    if (threadIdx.x == 0 && !in_regs) {
+        s_sp = atomicAdd(&ctr->spill_used, 2ull * R);
+        if (s_sp + 2ull * R > spill_cap) atomicOr(&ctr->err, 64ull);  // internal check
+    }
     __syncthreads();
+    if (!in_regs && s_sp + 2ull * R > spill_cap) return;
     // more rows than the registers hold: gathered once into the spill pool (key, row)
     unsigned long long* sp = spill + (in_regs ? 0ull : s_sp);
     if (!in_regs) {
@@ -1841,16 +1857,19 @@ hashed_frag_build_kernel(uint32_t nb, uint32_t clog2, uint32_t s0, uint32_t nsl,
             if (ref_at(sl) > 1) atomicAdd(&s_ndup, 1u);
         __syncthreads();
         const unsigned ndup = s_ndup;
+        __syncthreads();  // every wave holds ndup before thread 0 resets the counter for the assignment
         if (threadIdx.x == 0) {
             if (ndup <= dupcap) {
                 s_dirp = s_dir;
             } else {
                 const unsigned long long at = atomicAdd(&ctr->spill_used, (3ull * ndup + 1) / 2);
-                s_dirp = reinterpret_cast<uint32_t*>(spill + at);
+                s_dirp = at + (3ull * ndup + 1) / 2 <= spill_cap ? reinterpret_cast<uint32_t*>(spill + at) : nullptr;
+                if (s_dirp == nullptr) atomicOr(&ctr->err, 64ull);  // internal check
             }
             s_ndup = 0;
         }
         __syncthreads();
+        if (s_dirp == nullptr) return;
         uint32_t* d_off = s_dirp;
         uint32_t* d_cur = d_off + ndup;
         uint32_t* d_cnt = d_cur + ndup;
@@ -1874,8 +1893,12 @@ hashed_frag_build_kernel(uint32_t nb, uint32_t clog2, uint32_t s0, uint32_t nsl,
             if (li < ndup) d_off[li] = (uint32_t)(carry + ex);
             carry += tot;
         }
-        if (threadIdx.x == 0) s_base = carry ? atomicAdd(&ctr->dup_used, carry) : 0;
+        if (threadIdx.x == 0) {
+            s_base = carry ? atomicAdd(&ctr->dup_used, carry) : 0;
+            if (s_base + carry > dup_cap) atomicOr(&ctr->err, 32ull);  // internal check
+        }
         __syncthreads();
+        if (s_base + carry > dup_cap) return;
         for (unsigned li = threadIdx.x; li < ndup; li += T) {
             d_off[li] += (uint32_t)s_base;
             dup_rows[d_off[li]] = d_cnt[li];
@@ -1886,7 +1909,9 @@ hashed_frag_build_kernel(uint32_t nb, uint32_t clog2, uint32_t s0, uint32_t nsl,
             const unsigned rv = ref;
             if (rv & kDupFlag) {
                 const unsigned li = rv & ~kDupFlag;
-                dup_rows[d_off[li] + 1 + atomicAdd(&d_cur[li], 1u)] = row;
+                const uint64_t at = (uint64_t)d_off[li] + 1 + atomicAdd(&d_cur[li], 1u);
+                if (at < dup_cap) dup_rows[at] = row;
+                else atomicOr(&ctr->err, 32ull);  // internal check
             } else if (rv == 1) {
                 ref = row;  // the key's only row
             }
@@ -2656,11 +2681,18 @@ part_scatter_kernel(const void* keys, const uint8_t* valid, int64_t voff, const 
 // the per-peer send buffers (no grouped copy), each in source row order (stable: received
 // build ids ascend, and a rank's received probe rows stay in global row order).
 // ---------------------------------------------------------------------------
-// 256-thread tiles of 4096 rows: several workgroups per CU, so that one tile's look-back
-// wait overlaps the others' loads (1024-thread, 16384-row tiles — one per CU — measured
-// 472 us for 10^8 rows: the CU idles through every look-back)
-constexpr int kRpThreads = 256;
-constexpr int kRpIters = 16;
+// 512-thread tiles of 8192 rows, several workgroups per CU (so that one tile's look-back
+// wait overlaps the others' loads). 10^8 rows into one region with the runtime filter
+// (tools/part_bench.py, tools/rp_variants.py): 512 x 16 355 us, 256 x 16 380, 256 x 32 397,
+// 1024 x 8 428; the first 1024 x 16 form (loads interleaved with the ballots) 472-520
+#ifndef DFP_RP_THREADS
+#define DFP_RP_THREADS 512
+#endif
+#ifndef DFP_RP_ITERS
+#define DFP_RP_ITERS 16
+#endif
+constexpr int kRpThreads = DFP_RP_THREADS;
+constexpr int kRpIters = DFP_RP_ITERS;
 constexpr int kRpTile = kRpThreads * kRpIters;  // rows per tile
 constexpr int kRpSlots = kRpIters * (kRpThreads / 64);  // (iteration, wave) counts per destination
 static_assert(kRpSlots % 64 == 0, "the per-destination scan gives each lane whole slots");
@@ -3111,6 +3143,14 @@ hipError_t launch_build_hashed_frag(int key_bytes, const Segment* h_segs, int ns
     const void* kfn = (const void*)hashed_frag_build_kernel<T, RR>;
     hipError_t e = hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
+    // DFP_HJ_DEBUG_SYNC=1: synchronise after every launch and report the failing one (stderr)
+    static const bool dbg_sync = getenv("DFP_HJ_DEBUG_SYNC") != nullptr;
+    auto chk = [&](const char* what) -> hipError_t {
+        if (!dbg_sync) return hipSuccess;
+        const hipError_t q = hipStreamSynchronize(s);
+        if (q != hipSuccess) fprintf(stderr, "dfp-hj: %s failed: %s\n", what, hipGetErrorString(q));
+        return q;
+    };
     for (uint32_t s0 = 0; s0 < nsl_all; s0 += (uint32_t)kSlMaxSlices) {
         const uint32_t nsl = std::min<uint32_t>(nsl_all - s0, (uint32_t)kSlMaxSlices), nbins = nsl + 1;
         int64_t t0 = 0;
@@ -3130,13 +3170,17 @@ hipError_t launch_build_hashed_frag(int key_bytes, const Segment* h_segs, int ns
                 if (sg.valid) DFP_HBP(int32_t, true); else DFP_HBP(int32_t, false);
             }
 #undef DFP_HBP
+            if ((e = chk("hs_partition (build)")) != hipSuccess) return e;
             t0 += nt;
         }
         sl_toff_transpose_kernel<<<(unsigned)((ftiles + 63) / 64 * ((nbins + kSlTrChunk - 1) / kSlTrChunk)), 256, 0,
                                    s>>>(toff, nbins, ftiles, toffT);
+        if ((e = chk("toff transpose")) != hipSuccess) return e;
         hashed_frag_build_kernel<T, RR><<<nsl, T, lds, s>>>(g.nb, g.clog2, s0, nsl, ftiles, toffT, ko, rl, tile_base,
                                                            ids_as_rows ? ids32 : nullptr, tbl, dup_rows, big, ctr,
-                                                           spill, dupcap);
+                                                           spill, dupcap, (uint64_t)(2 * total + 2),
+                                                           (uint64_t)(4 * total));
+        if ((e = chk("hashed_frag_build")) != hipSuccess) return e;
     }
     dup_sort_big_kernel<<<cus, kBigThreads, 0, s>>>(dup_rows, big, ctr, d_segs, nseg, total, key_bytes, ids_as_rows);
     return hipGetLastError();
