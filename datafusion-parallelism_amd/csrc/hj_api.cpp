@@ -271,6 +271,8 @@ struct hj_table {
     bool packed = false;        // dense refs with inline counts (dup_rows offsets < 2^27)
     int64_t dmin = 0;
     uint64_t drange = 0;
+    bool has_range = false;     // hj_build_key_range: the caller's key range replaces the reduction
+    int64_t range_lo = 0, range_hi = 0;
     BuildResources res;
     // the stream the build runs on: the producers' stream when every append came on the
     // same one (a probe there needs no cross-stream wait), else res.stream
@@ -348,8 +350,9 @@ hj_status build_attempt(hj_table* t, const std::vector<Segment>& segs, double lf
     ctr = (BuildCounters*)p;
     if ((st = dev_alloc(t, t->scratch, &p, (2 + 2 * kMinmaxMaxBlocks) * sizeof(int64_t))) != HJ_OK) return st;
     d_minmax = (int64_t*)p;
-    // few segments: the key-range kernel publishes them and zeroes the counters
-    const bool minmax = total > 0 && build_mode() == 0;
+    // few segments: the key-range kernel publishes them and zeroes the counters (no
+    // reduction when the caller gave the range)
+    const bool minmax = total > 0 && build_mode() == 0 && !t->has_range;
     const bool by_arg = minmax && segs.size() <= (size_t)kArgSegs;
     if (!by_arg) {
         if (!segs.empty())
@@ -360,12 +363,17 @@ hj_status build_attempt(hj_table* t, const std::vector<Segment>& segs, double lf
     // layout: a dense key range gets the direct-addressed table (one u32 ref per key value)
     ChunkGeom g{};
     bool dense = false;
-    if (minmax) {
-        int64_t* mm = t->res.h_minmax;
-        const int64_t seq = ++t->res.mb_seq;
-        HIP_TRY(launch_key_minmax(t->key_bytes, segs.data(), d_segs, (int)segs.size(), by_arg ? ctr : nullptr, total,
-                                  d_minmax, t->res.d_mbox, seq, s));
-        HIP_TRY(wait_mailbox(mm, seq, d_minmax, s));
+    if (minmax || (t->has_range && total > 0 && build_mode() == 0)) {
+        int64_t mm[2] = {t->range_lo, t->range_hi};
+        if (minmax) {
+            int64_t* mb = t->res.h_minmax;
+            const int64_t seq = ++t->res.mb_seq;
+            HIP_TRY(launch_key_minmax(t->key_bytes, segs.data(), d_segs, (int)segs.size(), by_arg ? ctr : nullptr,
+                                      total, d_minmax, t->res.d_mbox, seq, s));
+            HIP_TRY(wait_mailbox(mb, seq, d_minmax, s));
+            mm[0] = mb[0];
+            mm[1] = mb[1];
+        }
         if (mm[0] <= mm[1]) {
             const uint64_t range = (uint64_t)mm[1] - (uint64_t)mm[0] + 1;
             const uint64_t nch = (range + (1u << kDenseShift) - 1) >> kDenseShift;
@@ -822,8 +830,10 @@ hj_status run_multi_build(hj_table* t, const std::vector<Segment>& segs, const s
     if (t->has_ids && t->has_no_ids) return fail(HJ_ERR_INVALID, "explicit build ids must be given for every batch or none");
     hj_status st;
     m->shards.assign(G, nullptr);
-    for (int g = 0; g < G; ++g)
+    for (int g = 0; g < G; ++g) {
         if ((st = hj_build_begin(m->devices[g], 1, t->kt, 0, &m->shards[g])) != HJ_OK) return st;
+        if (t->has_range && (st = hj_build_key_range(m->shards[g], t->range_lo, t->range_hi)) != HJ_OK) return st;
+    }
     TmpBufs tmp;
     tmp.m = m;
     const uint32_t keep = HJ_INPUT_DEVICE | HJ_BORROW | HJ_BORROW_KEEP;
@@ -1319,6 +1329,19 @@ hj_status hj_build_finish(hj_table* t, int partition) {
                                             "hj_build_finish concurrently");
     }
     if (t->build_st != HJ_OK) return fail(t->build_st, t->build_err);
+    return HJ_OK;
+}
+
+hj_status hj_build_key_range(hj_table* t, int64_t key_lo, int64_t key_hi) {
+    if (t == nullptr) return fail(HJ_ERR_INVALID, "null table");
+    if (key_lo > key_hi) return fail(HJ_ERR_INVALID, "hj_build_key_range: key_lo > key_hi");
+    if (t->key_bytes == 4 && (key_lo < INT32_MIN || key_hi > INT32_MAX))
+        return fail(HJ_ERR_INVALID, "hj_build_key_range: outside the int32 key domain");
+    std::lock_guard<std::mutex> g(t->mu);
+    if (t->built || t->arrived > 0) return fail(HJ_ERR_INVALID, "hj_build_key_range: after the barrier started");
+    t->has_range = true;
+    t->range_lo = key_lo;
+    t->range_hi = key_hi;
     return HJ_OK;
 }
 

@@ -123,9 +123,11 @@ class GpuLocalTable:
     """One rank's shard table (global build ids held in place of row numbers when they
     fit 31 bits and ascend, HJ_IDS_U31) and asynchronous probes of received chunks."""
 
-    def __init__(self, build_keys: torch.Tensor, build_ids: torch.Tensor, ids_u31: bool | None = None):
+    def __init__(self, build_keys: torch.Tensor, build_ids: torch.Tensor, ids_u31: bool | None = None,
+                 key_range: tuple[int, int] | None = None):
         """ids_u31: the caller knows the ids ascend and are < 2^31 (DistributedHashJoin:
-        stable partition, ranks in order, global build side < 2^31 rows); None checks."""
+        stable partition, ranks in order, global build side < 2^31 rows); None checks.
+        key_range: every build key lies in it (hj_build_key_range: no key-range reduction)."""
         dev = build_keys.device
         kt = "int64" if build_keys.dtype == torch.int64 else "int32"
         # received build ids ascend (stable partition, ranks in order): when they also
@@ -137,6 +139,8 @@ class GpuLocalTable:
                                     (nbi < 2 or bool((build_ids[1:] > build_ids[:-1]).all()))).item())
         self.table = HashTable(1, kt, dev.index or 0)
         self.table.append(0, build_keys, ids=build_ids, ids_u31=u31)
+        if key_range is not None and nbi:
+            self.table.key_range(*key_range)
         self.table.finish(0)
         self.device = dev
 
@@ -147,7 +151,7 @@ class GpuLocalTable:
         n = probe_keys.numel()
         pid32 = probe_ids if probe_ids.dtype == torch.int32 else probe_ids.to(torch.int32)
         ws = torch.empty(HashTable.workspace_bytes(n), dtype=torch.uint8, device=dev)
-        d_total = torch.zeros(1, dtype=torch.int64, device=dev)
+        d_total = torch.empty(1, dtype=torch.int64, device=dev)  # written by the probe
         cap = max(capacity or n, 1)
         s = torch.cuda.current_stream(dev).cuda_stream
 
@@ -197,6 +201,28 @@ class ExchangePlan:
     build_id_dtype: torch.dtype = torch.int64
     spec: PartSpec = field(default_factory=PartSpec)
     build_rows: int | None = None  # global build rows (received ids are checked against it)
+    build_lo: int | None = None    # global build key range (None: unknown / empty)
+    build_hi: int | None = None
+
+    def local_key_range(self, rank: int, world: int) -> tuple[int, int] | None:
+        """The key range of `rank`'s received build rows, in the travelling key domain
+        (after narrowing): the rank's contiguous share of [build_lo, build_hi] under a range
+        map (the partition kernel's multiply-high map, restated exactly), the whole range
+        under the hash map; None when unknown."""
+        if self.build_lo is None:
+            return None
+        lo, hi = self.build_lo, self.build_hi
+        if self.spec.by_range and world > 1:
+            rng = hi - lo + 1
+            mul = min((world << 64) // rng, 2**64 - 1)
+            first = lambda r: -(-(r << 64) // mul)  # smallest offset x with (x * mul) >> 64 >= r
+            a, b = first(rank), first(rank + 1) - 1
+            lo, hi = lo + a, min(hi, lo + b)
+            if lo > hi:
+                return None
+        if self.key_offset is not None:
+            lo, hi = lo - self.key_offset, hi - self.key_offset
+        return lo, hi
 
 
 @dataclass
@@ -394,6 +420,7 @@ class DistributedHashJoin:
             plan.build_id_dtype = torch.int32
         if bmin > bmax:  # empty build side: nothing can match, nothing to plan
             return plan
+        plan.build_lo, plan.build_hi = bmin, bmax
         if self.runtime_filter:
             dense = (bmax - bmin + 1) <= 8 * bend
             plan.spec = PartSpec(bool(dense and self.world > 1), bmin, bmax)
@@ -449,7 +476,10 @@ class DistributedHashJoin:
 
     def _local_table(self, bk: torch.Tensor, bi: torch.Tensor, plan: ExchangePlan):
         if self.local_build_fn is GpuLocalTable:
-            return GpuLocalTable(bk, bi, ids_u31=True if plan.build_id_dtype == torch.int32 else None)
+            # ids < 2^31 ascend (stable partition, ranks in order): held in place of rows;
+            # the rank's key range is known from the plan: no key-range reduction
+            return GpuLocalTable(bk, bi, ids_u31=True if plan.build_id_dtype == torch.int32 else None,
+                                 key_range=plan.local_key_range(self.rank, self.world))
         return self.local_build_fn(bk, bi)
 
     def join(self, build_keys: torch.Tensor, build_base: int, probe_keys: torch.Tensor, probe_base: int,
@@ -462,7 +492,9 @@ class DistributedHashJoin:
         its keys); close the table afterwards."""
         ev = self.events  # optional stage events (bench): partitioned, exchanged
         plan = self.prepare(build_keys, probe_keys, build_base)
-        bk_r, bi_r, bc, bcap = self._partition(build_keys, build_base, plan.build_id_dtype, plan.key_offset, plan.spec)
+        # build ids leave the partition as int64 (the table's id type: no widening pass; the
+        # build side is the small one, 4 more bytes per row on the wire)
+        bk_r, bi_r, bc, bcap = self._partition(build_keys, build_base, torch.int64, plan.key_offset, plan.spec)
         pk_r, pi_r, pc, pcap = self._partition(probe_keys, probe_base, torch.int32, plan.key_offset, plan.spec)
         if ev is not None:
             ev["partitioned"].record()

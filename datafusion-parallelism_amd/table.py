@@ -156,6 +156,11 @@ class HashTable:
         if flags & HJ_BORROW:
             self._keep.append((ki.keepalive, keep_ids))
 
+    def key_range(self, lo: int, hi: int) -> None:
+        """hj_build_key_range: every valid build key lies in [lo, hi] (before the barrier);
+        the build skips its key-range reduction."""
+        check(self._L.hj_build_key_range(self._h, int(lo), int(hi)))
+
     def finish(self, partition: int) -> None:
         check(self._L.hj_build_finish(self._h, partition))
 

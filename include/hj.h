@@ -141,6 +141,15 @@ hj_status hj_build_append(hj_table* t, int partition, const void* keys,
  * hj_table_stream_wait orders any other stream after it. */
 hj_status hj_build_finish(hj_table* t, int partition);
 
+/* Optional, before the barrier: every valid build key lies in [key_lo, key_hi] (the caller
+ * knows the range, e.g. from an exchange plan's global min/max). The build then skips its
+ * key-range reduction and the host's wait for it, and takes its layout from this range
+ * (direct-addressed when it spans at most 8x the build rows). A key outside the range may
+ * be lost (a direct-addressed table has no slot for it): the caller's guarantee is the
+ * contract. New (the
+ * reference sizes its table from the row count, new_map_3.rs:162). */
+hj_status hj_build_key_range(hj_table* t, int64_t key_lo, int64_t key_hi);
+
 /* Canonical id of partition `partition`'s first row (valid after the barrier). */
 hj_status hj_build_partition_offset(const hj_table* t, int partition, int64_t* out);
 

@@ -381,6 +381,25 @@ def test_hashed_build_every_key_twice(dfp, oracle_mod, layout):
         L.hj_set_build_mode(old)
 
 
+@pytest.mark.parametrize("lo_pad,hi_pad", [(0, 0), (1000, 7), (10**12, 10**12)])
+def test_build_key_range_hint(dfp, oracle_mod, lo_pad, hi_pad):
+    """hj_build_key_range: the caller's range (exact, a little wider, far wider -> the
+    hashed layout) replaces the key-range reduction; pairs equal the oracle's."""
+    rng = np.random.default_rng(lo_pad % 97)
+    bk = rng.integers(-5000, 400_000, 300_000).astype(np.int64)
+    pk = rng.integers(-6000, 410_000, 1_000_000).astype(np.int64)
+    with dfp.HashTable(1, "int64", 0) as t:
+        t.append(0, torch.from_numpy(bk).cuda())
+        t.key_range(int(bk.min()) - lo_pad, int(bk.max()) + hi_pad)
+        t.finish(0)
+        st = t.stats()
+        b, p = t.probe(torch.from_numpy(pk).cuda(), device_output=True)
+    assert (st["buckets"] == 0) == (lo_pad < 10**6)  # far wider than 8x the rows: hashed
+    ob, op = oracle_mod.inner_join(bk, pk)
+    assert np.array_equal(b.cpu().numpy().astype(np.uint64), ob)
+    assert np.array_equal(p.cpu().numpy().view(np.uint32), op)
+
+
 def test_c3_full_size_digest(dfp, oracle_mod):
     """C3 (10^7 exponential build keys x 10^8 uniform probe keys): the pair count and
     per-probe-row match counts against the closed form multiplicity of each key."""
