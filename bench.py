@@ -649,8 +649,8 @@ def main():
 class DistJob:
     """One step = the radix plan (DistributedHashJoin.join): global key range (one host
     read), both sides partitioned in one pass each into per-destination regions (runtime
-    filter, int32 key offsets, u32 ids), one count exchange for both sides (one host read),
-    the build side's regions exchanged (RCCL point to point; a rank's own region stays in
+    filter, int32 key offsets, u32 ids), each side's counts exchanged and read while the
+    device runs the next stage, the build side's regions exchanged (RCCL point to point; a rank's own region stays in
     place) and built with global ids, the probe side's exchanged and probed once with
     global probe ids. exchange_ms = from the end of the partitions to the end of the
     exchanges (events); probe_ms = the whole step on the device."""
@@ -666,6 +666,8 @@ class DistJob:
                             "sliced probe with global ids")
         self._pending = None
 
+    pipelined = True  # step k is collected (its pair count read) after step k + 1 is enqueued
+
     def step(self):
         ev = {k: torch.cuda.Event(enable_timing=True) for k in ("start", "partitioned", "exchanged", "end")}
         self.dj.events = ev
@@ -673,12 +675,17 @@ class DistJob:
         table, result = self.dj.join(self.bk, self.bbase, self.pk, self.pbase, self.cap, check=False)
         ev["end"].record()
         self.dj.events = None
-        self._pending = (table, result, ev)
+        prev, self._pending = self._pending, (table, result, ev)
+        if prev is not None:
+            self._collect(*prev)
 
     def collect(self):
         if self._pending is None:
             return
-        table, result, ev = self._pending
+        pending, self._pending = self._pending, None
+        self._collect(*pending)
+
+    def _collect(self, table, result, ev):
         b, _ = result()
         self.matches = int(b.numel())
         ev["end"].synchronize()
@@ -686,7 +693,6 @@ class DistJob:
         self.exchange_ms.append(ev["partitioned"].elapsed_time(ev["exchanged"]))
         self.build_ms.append(0.0)
         table.close()
-        self._pending = None
 
     def finish(self):
         self.collect()

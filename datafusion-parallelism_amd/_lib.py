@@ -87,6 +87,8 @@ SIGNATURES = [
     ("hj_partition_workspace_bytes", I64, [I64, I32]),
     ("hj_radix_partition", I32, [I32, P, P, I64, P, U64, I64, I32, P, I32, I64, P, I32, P, P, P]),
     ("hj_partition_rows", I32, [I32, P, P, I64, P, U64, I64, I32, P, P, I32, I64, P, I32, P, P, P]),
+    ("hj_key_minmax_workspace_bytes", I64, []),
+    ("hj_key_minmax", I32, [I32, P, P, I64, I64, P, P, P]),
     ("hj_partition_regions_workspace_bytes", I64, [I64, I32]),
     ("hj_partition_regions", I32, [I32, P, P, I64, P, U64, I64, I32, P, P, I32, I64, P, I32, I64, P, P, P]),
     ("hj_mark_rows", I32, [P, I32, I64, P, I64, P]),

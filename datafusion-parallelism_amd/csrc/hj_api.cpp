@@ -87,6 +87,7 @@ struct BuildResources {
     int64_t* h_minmax = nullptr;
     int64_t* d_mbox = nullptr;  // its device address
     int64_t mb_seq = 0;
+    unsigned long long* d_mm_done = nullptr;  // the one-launch minmax's ticket counter (left 0)
 };
 std::mutex g_pool_mu;
 std::unordered_map<int, std::vector<BuildResources>> g_pool;
@@ -106,7 +107,9 @@ bool acquire_resources(int dev, BuildResources* r) {
            hipEventCreateWithFlags(&r->evp, hipEventDisableTiming) == hipSuccess &&
            hipHostMalloc((void**)&r->h_minmax, 4 * sizeof(int64_t), hipHostMallocCoherent | hipHostMallocMapped) ==
                hipSuccess &&
-           hipHostGetDevicePointer((void**)&r->d_mbox, r->h_minmax, 0) == hipSuccess;
+           hipHostGetDevicePointer((void**)&r->d_mbox, r->h_minmax, 0) == hipSuccess &&
+           hipMalloc((void**)&r->d_mm_done, sizeof(unsigned long long)) == hipSuccess &&
+           hipMemset(r->d_mm_done, 0, sizeof(unsigned long long)) == hipSuccess;
 }
 
 void release_resources(int dev, const BuildResources& r) {
@@ -369,7 +372,7 @@ hj_status build_attempt(hj_table* t, const std::vector<Segment>& segs, double lf
             int64_t* mb = t->res.h_minmax;
             const int64_t seq = ++t->res.mb_seq;
             HIP_TRY(launch_key_minmax(t->key_bytes, segs.data(), d_segs, (int)segs.size(), by_arg ? ctr : nullptr,
-                                      total, d_minmax, t->res.d_mbox, seq, s));
+                                      total, d_minmax, t->res.d_mm_done, t->res.d_mbox, seq, s));
             HIP_TRY(wait_mailbox(mb, seq, d_minmax, s));
             mm[0] = mb[0];
             mm[1] = mb[1];
@@ -1686,6 +1689,35 @@ hj_status part_args(hj_key_type key_type, const void* keys, const uint8_t* valid
     return HJ_OK;
 }
 }  // namespace
+
+// workspace: [0, 8) the ticket counter, [64, 64 + sizeof(Segment)) the segment, then the
+// build counters the kernel zeroes (unused here), the partials from byte 256
+int64_t hj_key_minmax_workspace_bytes(void) { return 256 + (2 + 2 * (int64_t)kMinmaxMaxBlocks) * 8; }
+
+hj_status hj_key_minmax(hj_key_type key_type, const void* keys, const uint8_t* validity, int64_t validity_offset,
+                        int64_t n, int64_t* out_minmax, void* workspace, void* stream) {
+    static_assert(64 + sizeof(Segment) <= 128 && sizeof(BuildCounters) <= 128, "hj_key_minmax workspace layout");
+    if (device_count() == 0) return fail(HJ_ERR_NO_DEVICE, "no GPU visible");
+    if (key_type != HJ_INT32 && key_type != HJ_INT64) return fail(HJ_ERR_INVALID, "unknown key type");
+    if (n < 0) return fail(HJ_ERR_INVALID, "negative n");
+    if (out_minmax == nullptr || workspace == nullptr || (n > 0 && keys == nullptr))
+        return fail(HJ_ERR_INVALID, "null pointer");
+    if ((reinterpret_cast<uintptr_t>(workspace) & 7) != 0) return fail(HJ_ERR_INVALID, "workspace not 8-byte aligned");
+    char* ws = static_cast<char*>(workspace);
+    Segment sg{};
+    sg.keys = keys;
+    sg.valid = validity;
+    sg.voff = validity_offset;
+    sg.n = n;
+    sg.row_base = 0;
+    hipStream_t s = (hipStream_t)stream;
+    HIP_TRY(hipMemsetAsync(ws, 0, 8, s));
+    HIP_TRY(launch_key_minmax(key_type == HJ_INT64 ? 8 : 4, &sg, reinterpret_cast<Segment*>(ws + 64), 1,
+                              reinterpret_cast<BuildCounters*>(ws + 128), n,
+                              reinterpret_cast<int64_t*>(ws + 256), reinterpret_cast<unsigned long long*>(ws),
+                              nullptr, 0, s, out_minmax));
+    return HJ_OK;
+}
 
 int64_t hj_partition_regions_workspace_bytes(int64_t n, int nparts) {
     return radix_regions_workspace(n < 0 ? 0 : n, nparts < 1 ? 1 : nparts);

@@ -2697,6 +2697,16 @@ constexpr int kRpTile = kRpThreads * kRpIters;  // rows per tile
 constexpr int kRpSlots = kRpIters * (kRpThreads / 64);  // (iteration, wave) counts per destination
 static_assert(kRpSlots % 64 == 0, "the per-destination scan gives each lane whole slots");
 constexpr unsigned kRpSpinLimit = 1u << 22;
+// diagnostic builds only (tools/rp_variants.py, wrong output): 1 no look-back wait, 2 no
+// stores, 4 no ids. The wait costs about half the kernel (355 -> 180 us for 10^8 rows
+// with the filter); batching 2-16 look-back windows per flag round trip, longer spin
+// sleeps and a persistent ticketed form that loads the next tile during the wait were all
+// slower (tools/rp_variants.py history in DESIGN.md §5).
+#if defined(DFP_HJ_ABLATIONS) && defined(DFP_RP_ABL)
+constexpr int kRpAbl = DFP_RP_ABL;
+#else
+constexpr int kRpAbl = 0;
+#endif
 
 template <typename K, typename OK, typename ID, bool HAS_VALID, bool HAS_IDS>
 __global__ void __launch_bounds__(kRpThreads)
@@ -2763,7 +2773,8 @@ part_regions_kernel(const void* __restrict__ keys, const uint8_t* __restrict__ v
     // look-back (wave 0): lane l looks at destination l % nparts of tile t - 1 - l / nparts
     // (a window of 64 / nparts tiles per round); per destination, the nearest inclusive
     // flag ends its walk. Flags: status (1 aggregate, 2 inclusive) << 62 | value.
-    if (wave == 0) {
+    if ((kRpAbl & 1) && threadIdx.x < nparts) s_off[threadIdx.x] = 0;
+    if (wave == 0 && !(kRpAbl & 1)) {
         const int d = lane & (nparts - 1), k = lane >> bits;  // nparts <= 64: every lane maps
         const int per = 64 >> bits;                           // tiles per window
         const int64_t t = blockIdx.x;
@@ -2810,7 +2821,7 @@ part_regions_kernel(const void* __restrict__ keys, const uint8_t* __restrict__ v
     __syncthreads();
 #pragma unroll
     for (int it = 0; it < kRpIters; ++it) {
-        if (dr[it] == 0xFFFFFFFFu) continue;
+        if (dr[it] == 0xFFFFFFFFu || (kRpAbl & 2)) continue;
         const int d = (int)(dr[it] >> 8);
         const int64_t row = tile0 + (int64_t)it * kRpThreads + threadIdx.x;
         const unsigned long long pos =
@@ -2818,7 +2829,7 @@ part_regions_kernel(const void* __restrict__ keys, const uint8_t* __restrict__ v
         if (pos >= (unsigned long long)cap) continue;  // region overflow: counts say so
         const int64_t o = (int64_t)d * cap + (int64_t)pos;
         out_keys[o] = (OK)(key[it] - key_offset);  // OK narrower: the caller checked the range
-        out_ids[o] = (ID)(HAS_IDS ? ids[row] : id_base + (uint64_t)row);
+        if (!(kRpAbl & 4)) out_ids[o] = (ID)(HAS_IDS ? ids[row] : id_base + (uint64_t)row);
     }
 }
 
@@ -2896,11 +2907,19 @@ hipError_t launch_scan_u64(unsigned long long* a, int64_t len, void* scratch, un
     return launch_scan<unsigned long long>(a, len, (unsigned long long*)scratch, total, s);
 }
 
+// One launch: every block reduces its share to a partial (out[2 + 2b], out[3 + 2b]; a
+// single word sustains ~88 atomics/us, so per-block atomics on the result would cost
+// ~12 us at 1024 blocks) and takes a ticket; the last block reduces the partials, writes
+// out[0], out[1] (and the host mailbox) and re-arms the ticket counter (*done = 0 on
+// entry and on exit). No second launch, no launch gap before the result.
+constexpr int kMinmaxThreads = 256;
 template <typename K>
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(kMinmaxThreads)
 key_minmax_kernel(const Segment* __restrict__ segs, SegArgs sa, int nseg, int64_t total, long long* out,
-                  BuildCounters* __restrict__ ctr) {
-    __shared__ long long s_mn[4], s_mx[4];
+                  BuildCounters* __restrict__ ctr, unsigned long long* done, long long* mbox, long long seq,
+                  long long* res) {
+    __shared__ long long s_mn[kMinmaxThreads / 64], s_mx[kMinmaxThreads / 64];
+    __shared__ bool s_last;
     long long mn = LLONG_MAX, mx = LLONG_MIN;
     const bool by_arg = ctr != nullptr;  // segments in the argument; block 0 publishes them
     if (by_arg && blockIdx.x == 0) {
@@ -2955,54 +2974,49 @@ key_minmax_kernel(const Segment* __restrict__ segs, SegArgs sa, int nseg, int64_
             }
         }
     }
+    auto block_reduce = [&]() {
 #pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) {
-        const long long a = __shfl_xor(mn, d, 64), b = __shfl_xor(mx, d, 64);
-        mn = a < mn ? a : mn;
-        mx = b > mx ? b : mx;
-    }
-    if ((threadIdx.x & 63) == 0) {
-        s_mn[threadIdx.x >> 6] = mn;
-        s_mx[threadIdx.x >> 6] = mx;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        for (int w = 1; w < 4; ++w) {
+        for (int d = 32; d >= 1; d >>= 1) {
+            const long long a = __shfl_xor(mn, d, 64), b = __shfl_xor(mx, d, 64);
+            mn = a < mn ? a : mn;
+            mx = b > mx ? b : mx;
+        }
+        if ((threadIdx.x & 63) == 0) {
+            s_mn[threadIdx.x >> 6] = mn;
+            s_mx[threadIdx.x >> 6] = mx;
+        }
+        __syncthreads();
+        for (int w = 0; w < kMinmaxThreads / 64; ++w) {
             mn = s_mn[w] < mn ? s_mn[w] : mn;
             mx = s_mx[w] > mx ? s_mx[w] : mx;
         }
-        // per-block partials (out[2 + 2b], out[3 + 2b]), reduced by minmax_final_kernel: a
-        // single word sustains ~88 atomics/us, so 1024 blocks' atomics would cost ~12 us
+    };
+    block_reduce();
+    if (threadIdx.x == 0) {
         out[2 + 2 * blockIdx.x] = mn;
         out[3 + 2 * blockIdx.x] = mx;
-    }
-}
-
-__global__ void __launch_bounds__(1024) minmax_final_kernel(long long* out, unsigned nblk, long long* mbox,
-                                                            long long seq) {
-    __shared__ long long s_mn[16], s_mx[16];
-    long long mn = LLONG_MAX, mx = LLONG_MIN;
-    for (unsigned b = threadIdx.x; b < nblk; b += blockDim.x) {
-        mn = min(mn, out[2 + 2 * b]);
-        mx = max(mx, out[3 + 2 * b]);
-    }
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) {
-        mn = min(mn, (long long)__shfl_xor(mn, d, 64));
-        mx = max(mx, (long long)__shfl_xor(mx, d, 64));
-    }
-    if ((threadIdx.x & 63) == 0) {
-        s_mn[threadIdx.x >> 6] = mn;
-        s_mx[threadIdx.x >> 6] = mx;
+        __threadfence();  // the partial is visible on every XCD before the ticket
+        s_last = atomicAdd(done, 1ull) == (unsigned long long)gridDim.x - 1;
     }
     __syncthreads();
+    if (!s_last) return;  // uniform
+    __threadfence();
+    mn = LLONG_MAX;
+    mx = LLONG_MIN;
+    for (unsigned b = threadIdx.x; b < gridDim.x; b += kMinmaxThreads) {
+        mn = min(mn, __hip_atomic_load(&out[2 + 2 * b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        mx = max(mx, __hip_atomic_load(&out[3 + 2 * b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    }
+    __syncthreads();  // s_mn / s_mx reused
+    block_reduce();
     if (threadIdx.x == 0) {
-        for (int w = 1; w < (int)(blockDim.x >> 6); ++w) {
-            mn = min(mn, s_mn[w]);
-            mx = max(mx, s_mx[w]);
-        }
         out[0] = mn;
         out[1] = mx;
+        if (res != nullptr) {
+            res[0] = mn;
+            res[1] = mx;
+        }
+        *done = 0;  // re-armed for the next launch
         if (mbox != nullptr) {  // host mailbox (fine-grained): result, then the sequence number
             mbox[0] = mn;
             mbox[1] = mx;
@@ -3012,7 +3026,8 @@ __global__ void __launch_bounds__(1024) minmax_final_kernel(long long* out, unsi
 }
 
 hipError_t launch_key_minmax(int key_bytes, const Segment* h_segs, Segment* d_segs, int nseg, BuildCounters* ctr,
-                             int64_t total, int64_t* out, int64_t* mbox, int64_t seq, hipStream_t s) {
+                             int64_t total, int64_t* out, unsigned long long* done, int64_t* mbox, int64_t seq,
+                             hipStream_t s, int64_t* res) {
     const unsigned grid =
         (unsigned)std::max<int64_t>(1, std::min<int64_t>((total + 4095) / 4096, kMinmaxMaxBlocks));
     SegArgs sa{};
@@ -3021,10 +3036,11 @@ hipError_t launch_key_minmax(int key_bytes, const Segment* h_segs, Segment* d_se
         for (int i = 0; i < nseg; ++i) sa.s[i] = h_segs[i];
     }
     if (key_bytes == 8)
-        key_minmax_kernel<int64_t><<<grid, 256, 0, s>>>(d_segs, sa, nseg, total, (long long*)out, ctr);
+        key_minmax_kernel<int64_t><<<grid, kMinmaxThreads, 0, s>>>(d_segs, sa, nseg, total, (long long*)out, ctr, done,
+                                                                   (long long*)mbox, (long long)seq, (long long*)res);
     else
-        key_minmax_kernel<int32_t><<<grid, 256, 0, s>>>(d_segs, sa, nseg, total, (long long*)out, ctr);
-    minmax_final_kernel<<<1, 1024, 0, s>>>((long long*)out, grid, (long long*)mbox, (long long)seq);
+        key_minmax_kernel<int32_t><<<grid, kMinmaxThreads, 0, s>>>(d_segs, sa, nseg, total, (long long*)out, ctr, done,
+                                                                   (long long*)mbox, (long long)seq, (long long*)res);
     return hipGetLastError();
 }
 

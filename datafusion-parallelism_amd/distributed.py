@@ -237,17 +237,58 @@ class ExchangeStats:
 A2A_MAX_BYTES = 256 << 20
 
 
-def _count_matrix(counts: torch.Tensor, group=None) -> list[list[int]]:
-    """m[s][d] = rows rank s sends to rank d (one all_gather of G int64, one host sync):
-    every rank learns its receive sizes and everyone's, so all ranks agree on the
-    number of exchange rounds without another collective. One rank: its own counts, no
-    collective."""
+def host_read_async(t: torch.Tensor) -> Callable[[], list]:
+    """Start reading a small device tensor to the host without blocking the stream: a
+    non-blocking copy into pinned memory and an event, enqueued now (work the caller
+    enqueues afterwards does not delay it). -> a callable that waits for the event only and
+    returns t.tolist(). Host tensors are read at once."""
+    if not t.is_cuda:
+        vals = t.tolist()
+        return lambda: vals
+    h = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
+    h.copy_(t, non_blocking=True)
+    ev = torch.cuda.Event()
+    ev.record()
+
+    def get():
+        ev.synchronize()
+        return h.tolist()
+    return get
+
+
+def _count_matrix_async(counts: torch.Tensor, group=None) -> Callable[[], list[list[int]]]:
+    """m[s][d] = rows rank s sends to rank d: one all_gather of G int64 (enqueued now; one
+    rank: no collective) and an asynchronous host read. -> a callable that waits for the
+    read only: every rank learns its receive sizes and everyone's, so all ranks agree on
+    the number of exchange rounds without another collective."""
     world = dist.get_world_size(group)
     if world == 1:
-        return [counts.tolist()]
+        get = host_read_async(counts)
+        return lambda: [get()]
     parts = [torch.empty_like(counts) for _ in range(world)]
     dist.all_gather(parts, counts, group=group)
-    return torch.stack(parts).cpu().tolist()
+    return host_read_async(torch.stack(parts))
+
+
+def _count_matrix(counts: torch.Tensor, group=None) -> list[list[int]]:
+    return _count_matrix_async(counts, group)()
+
+
+def key_minmax(k: torch.Tensor, out: torch.Tensor) -> None:
+    """out[0], out[1] = min, max of k (INT64_MAX, INT64_MIN when empty) into a device int64
+    tensor: hj_key_minmax, one launch on the current stream (host tensors: torch)."""
+    if not k.is_cuda:
+        if k.numel():
+            mn, mx = torch.aminmax(k.to(torch.int64))
+            out[0], out[1] = mn, mx
+        else:
+            out[0], out[1] = 2**63 - 1, -(2**63)
+        return
+    L = _lib.load()
+    ws = torch.empty(L.hj_key_minmax_workspace_bytes(), dtype=torch.uint8, device=k.device)
+    kt = HJ_INT64 if k.dtype == torch.int64 else HJ_INT32
+    check(L.hj_key_minmax(kt, k.data_ptr(), None, 0, k.numel(), out.data_ptr(), ws.data_ptr(),
+                          torch.cuda.current_stream(k.device).cuda_stream))
 
 
 def _exchange_cols(cols: list[torch.Tensor], m: list[list[int]], group=None, async_op: bool = False):
@@ -384,7 +425,7 @@ class DistributedHashJoin:
         self.events: dict | None = None  # {"partitioned", "exchanged"}: torch.cuda.Event recorded by join()
 
     def prepare(self, build_keys: torch.Tensor, probe_keys: torch.Tensor, build_base: int) -> ExchangePlan:
-        """Plan the exchange from the global key ranges (one aminmax pass over each side,
+        """Plan the exchange from the global key ranges (one hj_key_minmax launch per side,
         two 16-byte all-reduces and one host read; one rank: no collective):
 
         * runtime filter: probe rows outside the global build key range [bmin, bmax]
@@ -401,20 +442,24 @@ class DistributedHashJoin:
         if not (self.compress_keys or self.runtime_filter):
             return plan
         dev = build_keys.device
-        big, small = 2**63 - 1, -(2**63)
-        lo = torch.full((2,), big, dtype=torch.int64, device=dev)  # [build min, probe min]
-        hi = torch.tensor([small, small, build_base + build_keys.numel()], dtype=torch.int64, device=dev)
         # with the runtime filter only build-range keys travel: the probe range is not needed
         sides = (build_keys,) if self.runtime_filter else (build_keys, probe_keys)
+        mm = torch.empty(2 * len(sides), dtype=torch.int64, device=dev)  # build min, max[, probe min, max]
         for j, k in enumerate(sides):
-            if k.numel():
-                mn, mx = torch.aminmax(k.to(torch.int64) if k.dtype != torch.int64 else k)
-                lo[j] = mn
-                hi[j] = mx
+            key_minmax(k, mm[2 * j:2 * j + 2])
+        bend = build_base + build_keys.numel()
         if self.world > 1:
+            lo = mm[0::2].contiguous()  # [build min[, probe min]]
+            hi = torch.cat([mm[1::2], torch.tensor([bend], dtype=torch.int64, device=dev)])
             dist.all_reduce(lo, op=dist.ReduceOp.MIN, group=self.group)
             dist.all_reduce(hi, op=dist.ReduceOp.MAX, group=self.group)
-        bmin, pmin, bmax, pmax, bend = torch.cat([lo, hi]).tolist()
+            vlo, vhi = lo.tolist(), hi.tolist()
+            bmin, bmax, bend = vlo[0], vhi[0], vhi[-1]
+            pmin, pmax = (vlo[1], vhi[1]) if len(sides) == 2 else (2**63 - 1, -(2**63))
+        else:
+            v = host_read_async(mm)()
+            bmin, bmax = v[0], v[1]
+            pmin, pmax = (v[2], v[3]) if len(sides) == 2 else (2**63 - 1, -(2**63))
         plan.build_rows = bend
         if bend < 2**31:
             plan.build_id_dtype = torch.int32
@@ -495,17 +540,20 @@ class DistributedHashJoin:
         # build ids leave the partition as int64 (the table's id type: no widening pass; the
         # build side is the small one, 4 more bytes per row on the wire)
         bk_r, bi_r, bc, bcap = self._partition(build_keys, build_base, torch.int64, plan.key_offset, plan.spec)
+        # each side's counts travel and are read as soon as its partition ends: the host
+        # waits for the build side's counts while the probe side's partition runs, and for the
+        # probe side's while the build runs, so the device does not idle on either read
+        mb = _count_matrix_async(bc, self.group)
         pk_r, pi_r, pc, pcap = self._partition(probe_keys, probe_base, torch.int32, plan.key_offset, plan.spec)
+        mp = _count_matrix_async(pc, self.group)
         if ev is not None:
             ev["partitioned"].record()
-        w = self.world
-        m = _count_matrix(torch.cat([bc, pc]), self.group)
-        (bk, bi), _ = exchange_regions([bk_r, bi_r], bcap, [row[:w] for row in m], self.group)
+        (bk, bi), _ = exchange_regions([bk_r, bi_r], bcap, mb(), self.group)
         bi = bi.to(torch.int64) if bi.dtype != torch.int64 else bi
         if check and plan.build_rows is not None:
             check_ids(bi, plan.build_rows, "received build ids")
         table = self._local_table(bk, bi, plan)
-        (pk, pi), works = exchange_regions([pk_r, pi_r], pcap, [row[w:] for row in m], self.group, async_op=True)
+        (pk, pi), works = exchange_regions([pk_r, pi_r], pcap, mp(), self.group, async_op=True)
         for wk in works:
             if wk is not None:
                 wk.wait()

@@ -303,6 +303,19 @@ hj_status hj_partition_regions(hj_key_type key_type, const void* keys,
                                int64_t key_offset, void* out_ids, int id_bytes, int64_t region_rows,
                                int64_t* counts, void* workspace, void* stream);
 
+/* Key range of one column, one kernel launch, asynchronous on `stream`: out_minmax[0] =
+ * min, out_minmax[1] = max of the valid keys (INT64_MAX, INT64_MIN when there are none;
+ * out_minmax is device memory). The radix plan's prepare step (DistributedHashJoin.prepare:
+ * runtime filter bounds, range map and key narrowing from the global build key range,
+ * the range the reference's partitioned map spreads keys over,
+ * src/utils/partitioned_concurrent_self_hash_join_map.rs:13-16) and the build's key-range
+ * reduction share this kernel. workspace: hj_key_minmax_workspace_bytes() bytes, 8-byte
+ * aligned (the call re-arms it: no caller initialisation). */
+int64_t hj_key_minmax_workspace_bytes(void);
+hj_status hj_key_minmax(hj_key_type key_type, const void* keys, const uint8_t* validity,
+                        int64_t validity_offset, int64_t n, int64_t* out_minmax, void* workspace,
+                        void* stream);
+
 /* ---- join types and output materialisation. Device pointers,
  *      asynchronous on `stream`. Index arrays are uint32 (idx_bytes 4) or uint64 (8);
  *      an all-ones index is a null index (the outer joins' missing side). ---------- */

@@ -177,3 +177,34 @@ def test_partition_regions_kernel(dfp, nparts, n, mode):
         assert np.array_equal(ok_[d * cap:d * cap + c[d]], want_k)
         want_i = ids_np[rows].view(np.int64) if ids is not None else (rows + id_base).astype(np.int32)
         assert np.array_equal(oi_[d * cap:d * cap + c[d]], want_i)
+
+
+@pytest.mark.parametrize("n", [0, 1, 2, 4095, 4097, 3_000_001, 40_000_000])
+@pytest.mark.parametrize("kind", ["i64", "i32", "i64_nulls"])
+def test_key_minmax(dfp, n, kind):
+    """hj_key_minmax (one launch, the last block reduces the partials): min and max of the
+    valid keys, INT64_MAX / INT64_MIN for none; back-to-back calls reuse one workspace
+    (the ticket counter is re-armed), against numpy."""
+    from datafusion_parallelism_amd import _lib
+
+    L = _lib.load()
+    rng = np.random.default_rng(n)
+    dev = torch.device("cuda", 0)
+    dt = np.int32 if kind == "i32" else np.int64
+    lo, hi = (-(2**31), 2**31 - 1) if kind == "i32" else (-(2**62), 2**62)
+    k = rng.integers(lo, hi, n, dtype=dt)
+    valid = rng.random(n) > 0.3 if kind == "i64_nulls" else np.ones(n, bool)
+    keys = torch.from_numpy(k).to(dev)
+    bitmap = torch.from_numpy(np.packbits(np.concatenate([np.zeros(5, bool), valid]), bitorder="little")).to(dev)
+    ws = torch.empty(L.hj_key_minmax_workspace_bytes(), dtype=torch.uint8, device=dev)
+    out = torch.empty(2, dtype=torch.int64, device=dev)
+    kt = 0 if kind == "i32" else 1
+    for _ in range(3):
+        out.fill_(7)
+        _lib.check(L.hj_key_minmax(kt, keys.data_ptr() if n else None,
+                                   bitmap.data_ptr() if kind == "i64_nulls" else None, 5 if kind == "i64_nulls" else 0,
+                                   n, out.data_ptr(), ws.data_ptr(), None))
+        got = out.tolist()
+        v = k[valid]
+        want = [int(v.min()), int(v.max())] if v.size else [2**63 - 1, -(2**63)]
+        assert got == want
