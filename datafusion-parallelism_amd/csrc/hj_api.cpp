@@ -87,7 +87,7 @@ struct BuildResources {
     int64_t* h_minmax = nullptr;
     int64_t* d_mbox = nullptr;  // its device address
     int64_t mb_seq = 0;
-    unsigned long long* d_mm_done = nullptr;  // the one-launch minmax's ticket counter (left 0)
+    unsigned long long* d_mm_done = nullptr;  // the one-launch minmax's accumulators + ticket (left 0)
 };
 std::mutex g_pool_mu;
 std::unordered_map<int, std::vector<BuildResources>> g_pool;
@@ -108,8 +108,8 @@ bool acquire_resources(int dev, BuildResources* r) {
            hipHostMalloc((void**)&r->h_minmax, 4 * sizeof(int64_t), hipHostMallocCoherent | hipHostMallocMapped) ==
                hipSuccess &&
            hipHostGetDevicePointer((void**)&r->d_mbox, r->h_minmax, 0) == hipSuccess &&
-           hipMalloc((void**)&r->d_mm_done, sizeof(unsigned long long)) == hipSuccess &&
-           hipMemset(r->d_mm_done, 0, sizeof(unsigned long long)) == hipSuccess;
+           hipMalloc((void**)&r->d_mm_done, 3 * sizeof(unsigned long long)) == hipSuccess &&
+           hipMemset(r->d_mm_done, 0, 3 * sizeof(unsigned long long)) == hipSuccess;
 }
 
 void release_resources(int dev, const BuildResources& r) {
@@ -1690,7 +1690,7 @@ hj_status part_args(hj_key_type key_type, const void* keys, const uint8_t* valid
 }
 }  // namespace
 
-// workspace: [0, 8) the ticket counter, [64, 64 + sizeof(Segment)) the segment, then the
+// workspace: [0, 24) the accumulators and ticket, [64, 64 + sizeof(Segment)) the segment, then the
 // build counters the kernel zeroes (unused here), the partials from byte 256
 int64_t hj_key_minmax_workspace_bytes(void) { return 256 + (2 + 2 * (int64_t)kMinmaxMaxBlocks) * 8; }
 
@@ -1711,7 +1711,7 @@ hj_status hj_key_minmax(hj_key_type key_type, const void* keys, const uint8_t* v
     sg.n = n;
     sg.row_base = 0;
     hipStream_t s = (hipStream_t)stream;
-    HIP_TRY(hipMemsetAsync(ws, 0, 8, s));
+    HIP_TRY(hipMemsetAsync(ws, 0, 24, s));
     HIP_TRY(launch_key_minmax(key_type == HJ_INT64 ? 8 : 4, &sg, reinterpret_cast<Segment*>(ws + 64), 1,
                               reinterpret_cast<BuildCounters*>(ws + 128), n,
                               reinterpret_cast<int64_t*>(ws + 256), reinterpret_cast<unsigned long long*>(ws),

@@ -2683,7 +2683,7 @@ part_scatter_kernel(const void* keys, const uint8_t* valid, int64_t voff, const 
 // ---------------------------------------------------------------------------
 // 512-thread tiles of 8192 rows, several workgroups per CU (so that one tile's look-back
 // wait overlaps the others' loads). 10^8 rows into one region with the runtime filter
-// (tools/part_bench.py, tools/rp_variants.py): 512 x 16 355 us, 256 x 16 380, 256 x 32 397,
+// (tools/part_bench.py, tools/lib_variants.py): 512 x 16 355 us, 256 x 16 380, 256 x 32 397,
 // 1024 x 8 428; the first 1024 x 16 form (loads interleaved with the ballots) 472-520
 #ifndef DFP_RP_THREADS
 #define DFP_RP_THREADS 512
@@ -2697,11 +2697,11 @@ constexpr int kRpTile = kRpThreads * kRpIters;  // rows per tile
 constexpr int kRpSlots = kRpIters * (kRpThreads / 64);  // (iteration, wave) counts per destination
 static_assert(kRpSlots % 64 == 0, "the per-destination scan gives each lane whole slots");
 constexpr unsigned kRpSpinLimit = 1u << 22;
-// diagnostic builds only (tools/rp_variants.py, wrong output): 1 no look-back wait, 2 no
+// diagnostic builds only (tools/lib_variants.py with DFP_HJ_ABLATIONS, DFP_RP_ABL; wrong output): 1 no look-back wait, 2 no
 // stores, 4 no ids. The wait costs about half the kernel (355 -> 180 us for 10^8 rows
 // with the filter); batching 2-16 look-back windows per flag round trip, longer spin
 // sleeps and a persistent ticketed form that loads the next tile during the wait were all
-// slower (tools/rp_variants.py history in DESIGN.md §5).
+// slower (tools/lib_variants.py).
 #if defined(DFP_HJ_ABLATIONS) && defined(DFP_RP_ABL)
 constexpr int kRpAbl = DFP_RP_ABL;
 #else
@@ -2907,19 +2907,30 @@ hipError_t launch_scan_u64(unsigned long long* a, int64_t len, void* scratch, un
     return launch_scan<unsigned long long>(a, len, (unsigned long long*)scratch, total, s);
 }
 
-// One launch: every block reduces its share to a partial (out[2 + 2b], out[3 + 2b]; a
-// single word sustains ~88 atomics/us, so per-block atomics on the result would cost
-// ~12 us at 1024 blocks) and takes a ticket; the last block reduces the partials, writes
-// out[0], out[1] (and the host mailbox) and re-arms the ticket counter (*done = 0 on
-// entry and on exit). No second launch, no launch gap before the result.
-constexpr int kMinmaxThreads = 256;
+// One launch: every block reduces its share and folds it into two accumulator words with
+// 64-bit atomic max (the min as the max of the complemented order-preserving unsigned
+// form, so all-zero words are the identity), then takes a ticket; the block with the last
+// ticket reads and clears the accumulators and the ticket and writes out[0], out[1] (and
+// the host mailbox). acc[0..2] must be zero before the first launch and are left zero. A
+// block's accumulator atomics return before its ticket is taken (their results are
+// consumed first), so the last ticket sees every block's fold; no fences and no partials
+// (a per-block __threadfence + partials took 137 us for 10^7 keys at 2442 blocks).
+#ifndef DFP_MM_THREADS
+#define DFP_MM_THREADS 1024
+#endif
+#ifndef DFP_MM_BLOCKS
+#define DFP_MM_BLOCKS 256
+#endif
+constexpr int kMinmaxThreads = DFP_MM_THREADS;
+constexpr unsigned kMinmaxBlocks = DFP_MM_BLOCKS;  // one per CU: 256 folds per accumulator word
+__device__ __forceinline__ unsigned long long mm_ord(long long v) { return (unsigned long long)v ^ (1ull << 63); }
+__device__ __forceinline__ long long mm_val(unsigned long long u) { return (long long)(u ^ (1ull << 63)); }
 template <typename K>
 __global__ void __launch_bounds__(kMinmaxThreads)
 key_minmax_kernel(const Segment* __restrict__ segs, SegArgs sa, int nseg, int64_t total, long long* out,
-                  BuildCounters* __restrict__ ctr, unsigned long long* done, long long* mbox, long long seq,
+                  BuildCounters* __restrict__ ctr, unsigned long long* acc, long long* mbox, long long seq,
                   long long* res) {
     __shared__ long long s_mn[kMinmaxThreads / 64], s_mx[kMinmaxThreads / 64];
-    __shared__ bool s_last;
     long long mn = LLONG_MAX, mx = LLONG_MIN;
     const bool by_arg = ctr != nullptr;  // segments in the argument; block 0 publishes them
     if (by_arg && blockIdx.x == 0) {
@@ -2930,20 +2941,20 @@ key_minmax_kernel(const Segment* __restrict__ segs, SegArgs sa, int nseg, int64_
         const Segment sg = by_arg ? sa.s[si] : segs[si];
         const int64_t stride = (int64_t)gridDim.x * blockDim.x;
         if (sizeof(K) == 8 && sg.valid == nullptr && (reinterpret_cast<uintptr_t>(sg.keys) & 15) == 0) {
-            // no nulls, 16-byte aligned int64 keys: 16-byte loads, eight in flight per lane
+            // no nulls, 16-byte aligned int64 keys: 16-byte loads, sixteen in flight per lane
             const v2i64* kp = reinterpret_cast<const v2i64*>(sg.keys);
             const int64_t n2 = sg.n >> 1;
-            for (int64_t j0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j0 < n2; j0 += 8 * stride) {
-                v2i64 v[8];
-                bool in[8];
+            for (int64_t j0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j0 < n2; j0 += 16 * stride) {
+                v2i64 v[16];
+                bool in[16];
 #pragma unroll
-                for (int u = 0; u < 8; ++u) {
+                for (int u = 0; u < 16; ++u) {
                     const int64_t j = j0 + u * stride;
                     in[u] = j < n2;
                     v[u] = in[u] ? kp[j] : v2i64{0, 0};
                 }
 #pragma unroll
-                for (int u = 0; u < 8; ++u) {
+                for (int u = 0; u < 16; ++u) {
                     if (!in[u]) continue;
                     const long long a = v[u].x, b = v[u].y;
                     mn = min(mn, min(a, b));
@@ -2977,9 +2988,9 @@ key_minmax_kernel(const Segment* __restrict__ segs, SegArgs sa, int nseg, int64_
     auto block_reduce = [&]() {
 #pragma unroll
         for (int d = 32; d >= 1; d >>= 1) {
-            const long long a = __shfl_xor(mn, d, 64), b = __shfl_xor(mx, d, 64);
-            mn = a < mn ? a : mn;
-            mx = b > mx ? b : mx;
+            const long long x = __shfl_xor(mn, d, 64), y = __shfl_xor(mx, d, 64);
+            mn = x < mn ? x : mn;
+            mx = y > mx ? y : mx;
         }
         if ((threadIdx.x & 63) == 0) {
             s_mn[threadIdx.x >> 6] = mn;
@@ -2992,44 +3003,34 @@ key_minmax_kernel(const Segment* __restrict__ segs, SegArgs sa, int nseg, int64_
         }
     };
     block_reduce();
-    if (threadIdx.x == 0) {
-        out[2 + 2 * blockIdx.x] = mn;
-        out[3 + 2 * blockIdx.x] = mx;
-        __threadfence();  // the partial is visible on every XCD before the ticket
-        s_last = atomicAdd(done, 1ull) == (unsigned long long)gridDim.x - 1;
+    if (threadIdx.x != 0) return;
+    const unsigned long long r0 = atomicMax(&acc[0], ~mm_ord(mn));
+    const unsigned long long r1 = atomicMax(&acc[1], mm_ord(mx));
+    asm volatile("" ::"v"(r0), "v"(r1));  // both folds have returned before the ticket
+    if (atomicAdd(&acc[2], 1ull) != (unsigned long long)gridDim.x - 1) return;
+    const long long rmn = mm_val(~atomicExch(&acc[0], 0ull));
+    const long long rmx = mm_val(atomicExch(&acc[1], 0ull));
+    atomicExch(&acc[2], 0ull);  // re-armed for the next launch
+    out[0] = rmn;
+    out[1] = rmx;
+    if (res != nullptr) {
+        res[0] = rmn;
+        res[1] = rmx;
     }
-    __syncthreads();
-    if (!s_last) return;  // uniform
-    __threadfence();
-    mn = LLONG_MAX;
-    mx = LLONG_MIN;
-    for (unsigned b = threadIdx.x; b < gridDim.x; b += kMinmaxThreads) {
-        mn = min(mn, __hip_atomic_load(&out[2 + 2 * b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-        mx = max(mx, __hip_atomic_load(&out[3 + 2 * b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-    }
-    __syncthreads();  // s_mn / s_mx reused
-    block_reduce();
-    if (threadIdx.x == 0) {
-        out[0] = mn;
-        out[1] = mx;
-        if (res != nullptr) {
-            res[0] = mn;
-            res[1] = mx;
-        }
-        *done = 0;  // re-armed for the next launch
-        if (mbox != nullptr) {  // host mailbox (fine-grained): result, then the sequence number
-            mbox[0] = mn;
-            mbox[1] = mx;
-            __hip_atomic_store(&mbox[2], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-        }
+    if (mbox != nullptr) {  // host mailbox (fine-grained): result, then the sequence number
+        mbox[0] = rmn;
+        mbox[1] = rmx;
+        __hip_atomic_store(&mbox[2], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
 
 hipError_t launch_key_minmax(int key_bytes, const Segment* h_segs, Segment* d_segs, int nseg, BuildCounters* ctr,
                              int64_t total, int64_t* out, unsigned long long* done, int64_t* mbox, int64_t seq,
                              hipStream_t s, int64_t* res) {
-    const unsigned grid =
-        (unsigned)std::max<int64_t>(1, std::min<int64_t>((total + 4095) / 4096, kMinmaxMaxBlocks));
+    // blocks fold into the accumulators one at a time (~27 ns per atomic on one word:
+    // 2048 blocks took 87 us for 10^7 keys, 128 blocks 27 us; tools/minmax_bench.py)
+    const int64_t cap = total <= (int64_t)1 << 24 ? kMinmaxBlocks / 2 : kMinmaxBlocks;
+    const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>((total + 4095) / 4096, cap));
     SegArgs sa{};
     if (ctr != nullptr) {
         if (nseg > kArgSegs) return hipErrorInvalidValue;
@@ -3553,7 +3554,9 @@ hipError_t launch_probe(int key_bytes, const TableView& tv, const void* keys, co
     const int64_t nt = probe_tiles(n);
     const int mode = probe_mode();
     const uint32_t nsl = sl_slices(tv);
-    if (nt > 0 && nsl >= 1 && (mode == 4 || (mode == 0 && sl_auto(tv, n))))
+    // a hashed key's probe sequence stays inside its chunk: chunks must not span slices
+    const bool sl_ok = tv.dense != nullptr || tv.clog2 <= (uint32_t)kHsSliceLog;
+    if (nt > 0 && nsl >= 1 && sl_ok && (mode == 4 || (mode == 0 && sl_auto(tv, n))))
         return launch_probe_sliced(key_bytes, tv, keys, valid, voff, probe_ids, pbase, n, out_b, out_p, cap, d_total,
                                    workspace, built, s);  // S1 zeroes the error word
     if (built != nullptr) {

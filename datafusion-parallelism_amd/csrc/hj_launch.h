@@ -62,7 +62,7 @@ hipError_t launch_build_hashed_frag(int key_bytes, const Segment* h_segs, int ns
                                     int64_t total, bool ids_as_rows, int cus, hipStream_t s);
 // min and max of the valid keys of the build segments -> out[0], out[1] (int64), one
 // launch; out holds 2 + 2 * kMinmaxMaxBlocks int64 (per-block partials behind the result);
-// done: a ticket counter that is 0 before the launch and is left 0 after it;
+// done: three accumulator / ticket words, zero before the launch and left zero after it;
 // mbox (optional, fine-grained host memory): min, max, then seq stored with system-scope
 // release once both are visible
 // Up to kArgSegs segments travel as a kernel argument: the kernel's first block then

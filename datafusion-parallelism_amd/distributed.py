@@ -163,11 +163,12 @@ class GpuLocalTable:
             return ob, op
 
         ob, op = launch(cap)
+        read_total = host_read_async(d_total)  # waits for this probe only, not later work
 
         def result(total: int | None = None):
             """total: d_total already read by the caller (one host sync for many probes)."""
             nonlocal ob, op
-            total = int(d_total.item()) if total is None else total
+            total = int(read_total()[0]) if total is None else total
             if total > cap:  # rare (duplicate-heavy keys): once more with the exact size
                 ob, op = launch(total)
                 total = int(d_total.item())

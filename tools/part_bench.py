@@ -10,7 +10,7 @@ import torch  # noqa: E402
 
 from datafusion_parallelism_amd import _lib  # noqa: E402
 
-if os.environ.get("DFP_HJ_LIB_VARIANT"):  # a diagnostic build (tools/rp_variants.py)
+if os.environ.get("DFP_HJ_LIB_VARIANT"):  # a diagnostic build (tools/lib_variants.py)
     _lib.LIB_PATH = os.environ["DFP_HJ_LIB_VARIANT"]
 L = _lib.load()
 dev = torch.device("cuda", 0)

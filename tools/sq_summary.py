@@ -11,7 +11,7 @@ path = glob.glob(sys.argv[1] + "/**/*counter_collection.csv", recursive=True)[0]
 acc = collections.defaultdict(lambda: collections.defaultdict(list))
 for r in csv.DictReader(open(path)):
     name = r["Kernel_Name"].split("(")[0].replace("void ", "").replace("dfp::", "")
-    if not any(k in name for k in ("sl_", "hs_", "dense_frag", "key_minmax")):
+    if not any(k in name for k in ("sl_", "hs_", "dense_frag", "hashed_frag", "key_minmax")):
         continue
     acc[name][r["Counter_Name"]].append(float(r["Counter_Value"]))
 for name, cs in acc.items():
