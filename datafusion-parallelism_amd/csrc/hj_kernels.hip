@@ -3439,9 +3439,16 @@ bool sl_auto(const TableView& tv, int64_t n) {
         return e ? atoll(e) : (int64_t)1 << 20;
     }();
     if (n < 4 * (int64_t)kSlTile) return false;
-    if (sl_passes(sl_slices(tv)) > kSlAutoPasses) return false;
-    if (tv.dense == nullptr) return (int64_t)tv.nb * 16 >= min_range && n >= (int64_t)tv.nb;
-    return (int64_t)tv.drange >= min_range && n >= (int64_t)tv.drange;
+    const uint32_t passes = sl_passes(sl_slices(tv));
+    if (passes > kSlAutoPasses) return false;
+    // hashed: one pass only. A second pass re-reads the probe keys and halves the
+    // fragments (slice x tile) the lookups walk: a 4*10^7-key table probed by 10^8 rows
+    // took 2.77 ms sliced (two passes) and 2.53 ms fused (tools/large_tables.py, r03)
+    if (tv.dense == nullptr) return passes == 1 && (int64_t)tv.nb * 16 >= min_range && n >= (int64_t)tv.nb;
+    // direct-addressed: the slice loads (4 bytes per key value) pay off well before the
+    // probe side outnumbers the key range: 1.2*10^8 values probed by 10^8 rows took 1.00 ms
+    // sliced and 1.21 ms fused
+    return (int64_t)tv.drange >= min_range && 4 * n >= (int64_t)tv.drange;
 }
 
 hipError_t launch_probe_sliced(int key_bytes, const TableView& tv, const void* keys, const uint8_t* valid,

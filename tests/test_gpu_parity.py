@@ -571,10 +571,21 @@ def test_sliced_hashed_multipass_parity(dfp, oracle_mod, sliced_mode, nb, np_, d
     assert_same(b, p, ob, op)
 
 
-def test_c2h_40m_multipass_closed_form(dfp):
-    """A 4*10^7-key hashed build (16 M buckets = 7813 slices: two sliced passes, the auto
-    choice) probed with 10^8 rows: C2's closed form under the bijection k -> k * M —
-    probe keys below B match exactly the row k * inv(7368787) mod B; count, order, values."""
+@pytest.mark.parametrize("pmode", [4, 0])
+def test_c2h_40m_multipass_closed_form(dfp, pmode):
+    """A 4*10^7-key hashed build (16 M buckets = 7813 slices) probed with 10^8 rows: C2's
+    closed form under the bijection k -> k * M — probe keys below B match exactly the row
+    k * inv(7368787) mod B; count, order, values. pmode 4: the sliced probe in two passes
+    over slice ranges; 0: the auto choice (the fused probe for a two-pass hashed table)."""
+    lib = dfp.load()
+    old_p = lib.hj_set_probe_mode(pmode)
+    try:
+        _c2h_40m(dfp)
+    finally:
+        lib.hj_set_probe_mode(old_p)
+
+
+def _c2h_40m(dfp):
     B, P = 40_000_000, 10**8
     dev = torch.device("cuda", 0)
     lib = dfp.load()

@@ -7,6 +7,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 
 import datafusion_parallelism_amd as dfp  # noqa: E402
+from datafusion_parallelism_amd import _lib  # noqa: E402
 from datafusion_parallelism_amd.table import HashTable  # noqa: E402
 
 args = [a for a in sys.argv[1:] if not a.startswith("--")]
@@ -14,6 +15,8 @@ B = int(float(args[0])) if len(args) > 0 else 10**7
 P = int(float(args[1])) if len(args) > 1 else 10**8
 MIX = "--mix" in sys.argv  # C2h: keys mapped by k -> k * 0x9E3779B97F4A7C15 (hashed table)
 CFG = next((a.split("=", 1)[1] for a in sys.argv if a.startswith("--config=")), None)  # a bench.py config
+if os.environ.get("DFP_HJ_LIB_VARIANT"):  # a diagnostic build (tools/lib_variants.py)
+    _lib.LIB_PATH = os.environ["DFP_HJ_LIB_VARIANT"]
 L = dfp.load()
 dev = torch.device("cuda", 0)
 if CFG:
