@@ -26,12 +26,12 @@ PROBE_KERNELS = ("probe_fused_kernel", "probe_lookup_kernel", "probe_emit_kernel
 BUILD_KERNELS = ("key_minmax_kernel", "minmax_final_kernel", "coarse_hist_kernel", "coarse_scatter", "fine_hist_kernel",
                  "fine_scatter", "chunk_starts_kernel", "scan_reduce_kernel<unsigned int>",
                  "scan_down_kernel<unsigned int>", "chunk_build_kernel", "dup_sort_big_kernel", "sl_partition_kernel",
-                 "sl_toff_transpose_kernel", "dense_frag_build_kernel")
+                 "sl_toff_transpose_kernel", "dense_frag_build_kernel", "hs_partition_kernel", "hashed_frag_build_kernel")
 
 
 # kernels that run in both phases (the dense build reuses the sliced probe's partition):
 # in dispatch order, the launch after a key_minmax_kernel belongs to the build
-SHARED = ("sl_partition_kernel", "sl_toff_transpose_kernel")
+SHARED = ("sl_partition_kernel", "sl_toff_transpose_kernel", "hs_partition_kernel")
 
 
 def per_kernel(path):
@@ -42,7 +42,8 @@ def per_kernel(path):
         name = r["Kernel_Name"]
         if "key_minmax_kernel" in name:
             in_build = True
-        elif "dense_frag_build_kernel" in name or "dup_sort_big_kernel" in name:
+        elif any(k in name for k in ("dense_frag_build_kernel", "hashed_frag_build_kernel", "dup_sort_big_kernel",
+                                     "chunk_build_kernel")):
             in_build = False
         if any(k in name for k in SHARED):
             name = ("build:" if in_build else "probe:") + name
