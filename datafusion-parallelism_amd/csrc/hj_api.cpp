@@ -87,7 +87,6 @@ struct BuildResources {
     int64_t* h_minmax = nullptr;
     int64_t* d_mbox = nullptr;  // its device address
     int64_t mb_seq = 0;
-    unsigned long long* d_mm_done = nullptr;  // the one-launch minmax's accumulators + ticket (left 0)
 };
 std::mutex g_pool_mu;
 std::unordered_map<int, std::vector<BuildResources>> g_pool;
@@ -107,9 +106,7 @@ bool acquire_resources(int dev, BuildResources* r) {
            hipEventCreateWithFlags(&r->evp, hipEventDisableTiming) == hipSuccess &&
            hipHostMalloc((void**)&r->h_minmax, 4 * sizeof(int64_t), hipHostMallocCoherent | hipHostMallocMapped) ==
                hipSuccess &&
-           hipHostGetDevicePointer((void**)&r->d_mbox, r->h_minmax, 0) == hipSuccess &&
-           hipMalloc((void**)&r->d_mm_done, 3 * sizeof(unsigned long long)) == hipSuccess &&
-           hipMemset(r->d_mm_done, 0, 3 * sizeof(unsigned long long)) == hipSuccess;
+           hipHostGetDevicePointer((void**)&r->d_mbox, r->h_minmax, 0) == hipSuccess;
 }
 
 void release_resources(int dev, const BuildResources& r) {
@@ -372,7 +369,7 @@ hj_status build_attempt(hj_table* t, const std::vector<Segment>& segs, double lf
             int64_t* mb = t->res.h_minmax;
             const int64_t seq = ++t->res.mb_seq;
             HIP_TRY(launch_key_minmax(t->key_bytes, segs.data(), d_segs, (int)segs.size(), by_arg ? ctr : nullptr,
-                                      total, d_minmax, t->res.d_mm_done, t->res.d_mbox, seq, s));
+                                      total, d_minmax, t->res.d_mbox, seq, s));
             HIP_TRY(wait_mailbox(mb, seq, d_minmax, s));
             mm[0] = mb[0];
             mm[1] = mb[1];
@@ -1712,7 +1709,7 @@ hj_status hj_key_minmax(hj_key_type key_type, const void* keys, const uint8_t* v
     sg.row_base = 0;
     hipStream_t s = (hipStream_t)stream;
     HIP_TRY(hipMemsetAsync(ws, 0, 24, s));
-    HIP_TRY(launch_key_minmax(key_type == HJ_INT64 ? 8 : 4, &sg, reinterpret_cast<Segment*>(ws + 64), 1,
+    HIP_TRY(launch_key_minmax_one(key_type == HJ_INT64 ? 8 : 4, &sg, reinterpret_cast<Segment*>(ws + 64), 1,
                               reinterpret_cast<BuildCounters*>(ws + 128), n,
                               reinterpret_cast<int64_t*>(ws + 256), reinterpret_cast<unsigned long long*>(ws),
                               nullptr, 0, s, out_minmax));

@@ -3024,9 +3024,9 @@ key_minmax_kernel(const Segment* __restrict__ segs, SegArgs sa, int nseg, int64_
     }
 }
 
-hipError_t launch_key_minmax(int key_bytes, const Segment* h_segs, Segment* d_segs, int nseg, BuildCounters* ctr,
-                             int64_t total, int64_t* out, unsigned long long* done, int64_t* mbox, int64_t seq,
-                             hipStream_t s, int64_t* res) {
+hipError_t launch_key_minmax_one(int key_bytes, const Segment* h_segs, Segment* d_segs, int nseg, BuildCounters* ctr,
+                                 int64_t total, int64_t* out, unsigned long long* done, int64_t* mbox, int64_t seq,
+                                 hipStream_t s, int64_t* res) {
     // blocks fold into the accumulators one at a time (~27 ns per atomic on one word:
     // 2048 blocks took 87 us for 10^7 keys, 128 blocks 27 us; tools/minmax_bench.py)
     const int64_t cap = total <= (int64_t)1 << 24 ? kMinmaxBlocks / 2 : kMinmaxBlocks;
@@ -3042,6 +3042,142 @@ hipError_t launch_key_minmax(int key_bytes, const Segment* h_segs, Segment* d_se
     else
         key_minmax_kernel<int32_t><<<grid, kMinmaxThreads, 0, s>>>(d_segs, sa, nseg, total, (long long*)out, ctr, done,
                                                                    (long long*)mbox, (long long)seq, (long long*)res);
+    return hipGetLastError();
+}
+
+template <typename K>
+__global__ void __launch_bounds__(256)
+key_minmax_part_kernel(const Segment* __restrict__ segs, SegArgs sa, int nseg, int64_t total, long long* out,
+                  BuildCounters* __restrict__ ctr) {
+    __shared__ long long s_mn[4], s_mx[4];
+    long long mn = LLONG_MAX, mx = LLONG_MIN;
+    const bool by_arg = ctr != nullptr;  // segments in the argument; block 0 publishes them
+    if (by_arg && blockIdx.x == 0) {
+        if (threadIdx.x < (unsigned)nseg) const_cast<Segment*>(segs)[threadIdx.x] = sa.s[threadIdx.x];
+        if (threadIdx.x == 0) *ctr = BuildCounters{};
+    }
+    for (int si = 0; si < nseg; ++si) {
+        const Segment sg = by_arg ? sa.s[si] : segs[si];
+        const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+        if (sizeof(K) == 8 && sg.valid == nullptr && (reinterpret_cast<uintptr_t>(sg.keys) & 15) == 0) {
+            // no nulls, 16-byte aligned int64 keys: 16-byte loads, eight in flight per lane
+            const v2i64* kp = reinterpret_cast<const v2i64*>(sg.keys);
+            const int64_t n2 = sg.n >> 1;
+            for (int64_t j0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j0 < n2; j0 += 8 * stride) {
+                v2i64 v[8];
+                bool in[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const int64_t j = j0 + u * stride;
+                    in[u] = j < n2;
+                    v[u] = in[u] ? kp[j] : v2i64{0, 0};
+                }
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    if (!in[u]) continue;
+                    const long long a = v[u].x, b = v[u].y;
+                    mn = min(mn, min(a, b));
+                    mx = max(mx, max(a, b));
+                }
+            }
+            if ((sg.n & 1) && blockIdx.x == 0 && threadIdx.x == 0) {
+                const long long k = (long long)ld_key<K>(sg.keys, sg.n - 1);
+                mn = min(mn, k);
+                mx = max(mx, k);
+            }
+            continue;
+        }
+        for (int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i0 < sg.n; i0 += 4 * stride) {
+            long long k[4];
+            bool ok[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {  // four independent loads in flight
+                const int64_t i = i0 + u * stride;
+                ok[u] = i < sg.n && bit_valid(sg.valid, sg.voff, i);
+                k[u] = i < sg.n ? (long long)ld_key<K>(sg.keys, i) : 0;
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                if (!ok[u]) continue;
+                mn = k[u] < mn ? k[u] : mn;
+                mx = k[u] > mx ? k[u] : mx;
+            }
+        }
+    }
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+        const long long a = __shfl_xor(mn, d, 64), b = __shfl_xor(mx, d, 64);
+        mn = a < mn ? a : mn;
+        mx = b > mx ? b : mx;
+    }
+    if ((threadIdx.x & 63) == 0) {
+        s_mn[threadIdx.x >> 6] = mn;
+        s_mx[threadIdx.x >> 6] = mx;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < 4; ++w) {
+            mn = s_mn[w] < mn ? s_mn[w] : mn;
+            mx = s_mx[w] > mx ? s_mx[w] : mx;
+        }
+        // per-block partials (out[2 + 2b], out[3 + 2b]), reduced by minmax_final_kernel: a
+        // single word sustains ~88 atomics/us, so 1024 blocks' atomics would cost ~12 us
+        out[2 + 2 * blockIdx.x] = mn;
+        out[3 + 2 * blockIdx.x] = mx;
+    }
+}
+
+__global__ void __launch_bounds__(1024) minmax_final_kernel(long long* out, unsigned nblk, long long* mbox,
+                                                            long long seq) {
+    __shared__ long long s_mn[16], s_mx[16];
+    long long mn = LLONG_MAX, mx = LLONG_MIN;
+    for (unsigned b = threadIdx.x; b < nblk; b += blockDim.x) {
+        mn = min(mn, out[2 + 2 * b]);
+        mx = max(mx, out[3 + 2 * b]);
+    }
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+        mn = min(mn, (long long)__shfl_xor(mn, d, 64));
+        mx = max(mx, (long long)__shfl_xor(mx, d, 64));
+    }
+    if ((threadIdx.x & 63) == 0) {
+        s_mn[threadIdx.x >> 6] = mn;
+        s_mx[threadIdx.x >> 6] = mx;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < (int)(blockDim.x >> 6); ++w) {
+            mn = min(mn, s_mn[w]);
+            mx = max(mx, s_mx[w]);
+        }
+        out[0] = mn;
+        out[1] = mx;
+        if (mbox != nullptr) {  // host mailbox (fine-grained): result, then the sequence number
+            mbox[0] = mn;
+            mbox[1] = mx;
+            __hip_atomic_store(&mbox[2], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
+}
+
+// The build's key-range reduction: per-block partials, then minmax_final_kernel (result
+// and host mailbox). Two launches, but 256-thread blocks that fit beside the previous
+// step's probe kernels in the pipelined bench: the one-launch form (1024-thread blocks)
+// waited for free CUs there and stretched the pipelined C2 build span 0.26 -> 0.60 ms.
+hipError_t launch_key_minmax(int key_bytes, const Segment* h_segs, Segment* d_segs, int nseg, BuildCounters* ctr,
+                             int64_t total, int64_t* out, int64_t* mbox, int64_t seq, hipStream_t s) {
+    const unsigned grid =
+        (unsigned)std::max<int64_t>(1, std::min<int64_t>((total + 4095) / 4096, kMinmaxMaxBlocks));
+    SegArgs sa{};
+    if (ctr != nullptr) {
+        if (nseg > kArgSegs) return hipErrorInvalidValue;
+        for (int i = 0; i < nseg; ++i) sa.s[i] = h_segs[i];
+    }
+    if (key_bytes == 8)
+        key_minmax_part_kernel<int64_t><<<grid, 256, 0, s>>>(d_segs, sa, nseg, total, (long long*)out, ctr);
+    else
+        key_minmax_part_kernel<int32_t><<<grid, 256, 0, s>>>(d_segs, sa, nseg, total, (long long*)out, ctr);
+    minmax_final_kernel<<<1, 1024, 0, s>>>((long long*)out, grid, (long long*)mbox, (long long)seq);
     return hipGetLastError();
 }
 

@@ -60,9 +60,8 @@ hipError_t launch_build_hashed_frag(int key_bytes, const Segment* h_segs, int ns
                                     void* scratch, uint32_t* tile_base, const uint64_t* ids32, Bucket* tbl,
                                     uint32_t* dup_rows, BigSeg* big, BuildCounters* ctr, const Segment* d_segs,
                                     int64_t total, bool ids_as_rows, int cus, hipStream_t s);
-// min and max of the valid keys of the build segments -> out[0], out[1] (int64), one
-// launch; out holds 2 + 2 * kMinmaxMaxBlocks int64 (per-block partials behind the result);
-// done: three accumulator / ticket words, zero before the launch and left zero after it;
+// min and max of the valid keys of the build segments -> out[0], out[1] (int64);
+// out holds 2 + 2 * kMinmaxMaxBlocks int64 (per-block partials behind the result);
 // mbox (optional, fine-grained host memory): min, max, then seq stored with system-scope
 // release once both are visible
 // Up to kArgSegs segments travel as a kernel argument: the kernel's first block then
@@ -74,8 +73,13 @@ struct SegArgs {
     Segment s[kArgSegs];
 };
 hipError_t launch_key_minmax(int key_bytes, const Segment* h_segs, Segment* d_segs, int nseg, BuildCounters* ctr,
-                             int64_t total, int64_t* out, unsigned long long* done, int64_t* mbox, int64_t seq,
-                             hipStream_t s, int64_t* res = nullptr);  // res: the result also here
+                             int64_t total, int64_t* out, int64_t* mbox, int64_t seq, hipStream_t s);
+// the same reduction in one launch (hj_key_minmax): blocks fold into accumulator words
+// with atomics and the last ticket writes the result to out[0..1] and res[0..1]; done:
+// three words, zero before the launch and left zero after it
+hipError_t launch_key_minmax_one(int key_bytes, const Segment* h_segs, Segment* d_segs, int nseg, BuildCounters* ctr,
+                                 int64_t total, int64_t* out, unsigned long long* done, int64_t* mbox, int64_t seq,
+                                 hipStream_t s, int64_t* res = nullptr);
 
 // ---- probe ---------------------------------------------------------------
 // 0 auto, 3 fused, 4 sliced
