@@ -31,6 +31,9 @@ def main():
     ap.add_argument("runs", nargs="*", default=["q3:10"])
     ap.add_argument("--dist", action="store_true", help="multi-GPU plans (torch.distributed, RCCL)")
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--shards", type=int, default=0,
+                    help="one-GPU plans with every join on a table of this many radix shards on GPU 0 "
+                         "(hj_build_begin_multi on [0] * K: C4/C5's sharded builds in one process)")
     a = ap.parse_args()
     rank, world = 0, 1
     if a.dist:
@@ -54,6 +57,10 @@ def main():
             fn = tpch.q3_dist if q == "q3" else tpch.q9_dist
         else:
             fn = tpch.q3 if q == "q3" else tpch.q9
+            if a.shards:
+                jf = tpch.multi_join([0] * a.shards)
+                base = fn
+                fn = lambda tt, base=base, jf=jf: base(tt, join_fn=jf)  # noqa: E731
         r = fn(t)  # warm-up
         times = []
         for _ in range(a.reps):
@@ -77,7 +84,9 @@ def main():
         line = {
             "what": f"TPC-H-shaped {q.upper()} on {world} GPU(s), tables resident in HBM"
                     + (" (multi-GPU plan: broadcast + RCCL shuffles)" if a.dist else ""),
-            "query": q, "sf": sf, "n_gpus": world, "plan": "dist" if a.dist else "single", "lineitem_rows": nl,
+            "query": q, "sf": sf, "n_gpus": world,
+            "plan": "dist" if a.dist else (f"{a.shards} radix shards on one GPU" if a.shards else "single"),
+            "lineitem_rows": nl,
             "query_ms_min": round(best * 1e3, 3), "query_ms_median": round(sorted(times)[len(times) // 2] * 1e3, 3),
             "lineitem_mrows_s": round(nl / best / 1e6, 1),
         }
