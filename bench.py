@@ -721,39 +721,51 @@ class BroadcastJob:
         self.cap = n
         self.ob = torch.empty(n, dtype=torch.int64, device=dev)
         self.op = torch.empty(n, dtype=torch.int32, device=dev)
-        self.kernel_desc = "RCCL all_gather of the build shards + local build + sliced probe of the local rows"
+        self.kernel_desc = ("RCCL all_gather of the build shards (int32 key offsets for a direct-addressed build "
+                            "domain) + local build + sliced probe of the local rows")
         W = dj.world  # shard sizes of the strong split (rows [rB/W, (r+1)B/W)), exchanged once
         nb = torch.tensor([int(bk.numel())], dtype=torch.int64, device=dev)
         allb = [torch.empty_like(nb) for _ in range(W)]
         dist.all_gather(allb, nb, group=dj.group)
         self.sizes = [int(x) for x in torch.cat(allb).tolist()]  # known before the timed steps
-        # two gather buffers: step k + 2 reuses step k's once step k is collected
-        self.gbuf = [torch.empty(sum(self.sizes), dtype=bk.dtype, device=dev) for _ in range(2)]
+        # two gather buffers per key width: step k + 2 reuses step k's once step k is collected
+        self.gbuf = {dt: [torch.empty(sum(self.sizes), dtype=dt, device=dev) for _ in range(2)]
+                     for dt in {bk.dtype, torch.int32}}
         self.cstream = torch.cuda.Stream(dev)  # the gathers
         self.bstream = torch.cuda.Stream(dev)  # the builds
         self.evs = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(2)]
         self.k = 0
         self.prev = None
 
-    def _gather(self, out):
+    def _gather(self, out, src):
         if len(set(self.sizes)) == 1:
-            return dist.all_gather_into_tensor(out, self.bk, group=self.dj.group, async_op=True)
+            return dist.all_gather_into_tensor(out, src, group=self.dj.group, async_op=True)
         parts = list(torch.split(out, self.sizes))
-        return dist.all_gather(parts, self.bk, group=self.dj.group, async_op=True)
+        return dist.all_gather(parts, src, group=self.dj.group, async_op=True)
 
     def step(self):
+        from datafusion_parallelism_amd.distributed import broadcast_key_plan
+
         ev = self.evs[self.k & 1]
-        g = self.gbuf[self.k & 1]
+        slot = self.k & 1
         self.k += 1
         with torch.cuda.stream(self.cstream):
             ev[0].record(self.cstream)
-            work = self._gather(g)
+            # the global key range (hj_key_minmax + one all-reduce; the host waits for this
+            # stream only): a direct-addressed build domain travels as int32 offsets
+            plan = broadcast_key_plan(self.bk, sum(self.sizes), self.dj.group) if self.dj.compress_keys else None
+            src = self.bk if plan is None else (self.bk - plan[0]).to(torch.int32)
+            g = self.gbuf[src.dtype][slot]
+            work = self._gather(g, src)
             work.wait()  # the gather stream waits for the collective
             ev[1].record(self.cstream)
         self.bstream.wait_stream(self.cstream)
-        t = HashTable(1, "int64", self.dev.index or 0)
+        t = HashTable(1, "int64" if plan is None else "int32", self.dev.index or 0)
         with torch.cuda.stream(self.bstream):
             t.append(0, g)
+            if plan is not None:  # keyed back to the int64 probe keys, no key-range reduction
+                t.key_range(0, plan[1] - 1)
+                t.key_base(plan[0])
             t.finish(0)
         cur = torch.cuda.current_stream(self.dev)
         ev[2].record(cur)

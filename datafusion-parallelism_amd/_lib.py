@@ -69,6 +69,7 @@ SIGNATURES = [
     ("hj_build_append", I32, [P, I32, P, P, I64, P, I64, U32, P]),
     ("hj_build_finish", I32, [P, I32]),
     ("hj_build_key_range", I32, [P, I64, I64]),
+    ("hj_build_key_base", I32, [P, I64]),
     ("hj_build_partition_offset", I32, [P, I32, ctypes.POINTER(ctypes.c_int64)]),
     ("hj_table_stats_get", I32, [P, ctypes.POINTER(HjTableStats)]),
     ("hj_table_build_ns", I64, [P]),

@@ -273,6 +273,8 @@ struct hj_table {
     uint64_t drange = 0;
     bool has_range = false;     // hj_build_key_range: the caller's key range replaces the reduction
     int64_t range_lo = 0, range_hi = 0;
+    bool has_base = false;      // hj_build_key_base: int32 build keys are offsets from key_base;
+    int64_t key_base = 0;       // the built (direct-addressed) table is keyed in the int64 domain
     BuildResources res;
     // the stream the build runs on: the producers' stream when every append came on the
     // same one (a probe there needs no cross-stream wait), else res.stream
@@ -386,6 +388,9 @@ hj_status build_attempt(hj_table* t, const std::vector<Segment>& segs, double lf
             }
         }
     }
+    if (!dense && t->has_base && total > 0)
+        return fail(HJ_ERR_INVALID, "hj_build_key_base: the build keys do not make a direct-addressed table "
+                                    "(key range > 8 x rows); build from int64 keys instead");
     if (!dense) {
         // geometry: 5-slot buckets, chunks of 2^clog2 buckets (one workgroup builds one)
         const double want = (double)total / (kSlots * lf);
@@ -592,6 +597,11 @@ hj_status run_build(hj_table* t) {
     // (hipStreamWaitEvent, no host synchronisation); build_ns is read when first asked
     HIP_TRY(hipEventRecord(t->res.ev1, s));
     t->build_ns = -1;
+    if (t->has_base) {  // offsets from key_base -> the int64 keys they stand for
+        if (t->dense != nullptr) t->dmin += t->key_base;
+        t->kt = HJ_INT64;
+        t->key_bytes = 8;
+    }
     return HJ_OK;
 }
 
@@ -1342,6 +1352,17 @@ hj_status hj_build_key_range(hj_table* t, int64_t key_lo, int64_t key_hi) {
     t->has_range = true;
     t->range_lo = key_lo;
     t->range_hi = key_hi;
+    return HJ_OK;
+}
+
+hj_status hj_build_key_base(hj_table* t, int64_t key_base) {
+    if (t == nullptr) return fail(HJ_ERR_INVALID, "null table");
+    if (t->multi != nullptr) return fail(HJ_ERR_INVALID, "hj_build_key_base: not for a multi-GPU table");
+    if (t->kt != HJ_INT32) return fail(HJ_ERR_INVALID, "hj_build_key_base: the build keys must be int32 offsets");
+    std::lock_guard<std::mutex> g(t->mu);
+    if (t->built || t->arrived > 0) return fail(HJ_ERR_INVALID, "hj_build_key_base: after the barrier started");
+    t->has_base = true;
+    t->key_base = key_base;
     return HJ_OK;
 }
 

@@ -401,6 +401,46 @@ def all_to_all_rows(keys_by_dest: torch.Tensor, ids_by_dest: torch.Tensor, count
     return rk, ri, st
 
 
+DENSE_FACTOR = 8                 # hj_api.cpp kDenseFactor: direct-addressed when range <= 8 x rows
+DENSE_MAX_RANGE = 131071 << 11   # kMaxChunks << kDenseShift: the widest direct-addressed range
+
+
+def gather_sizes(n: int, dev, group=None) -> list[int]:
+    """Every rank's row count (one all_gather of one int64 and a host read)."""
+    world = dist.get_world_size(group)
+    if world == 1:
+        return [int(n)]
+    t = torch.tensor([n], dtype=torch.int64, device=dev)
+    ns = [torch.empty_like(t) for _ in range(world)]
+    dist.all_gather(ns, t, group=group)
+    return [int(x) for x in torch.cat(ns).tolist()]
+
+
+def broadcast_key_plan(build_keys: torch.Tensor, global_rows: int, group=None) -> tuple[int, int] | None:
+    """(base, range) when the global int64 build keys make a direct-addressed table
+    (range <= 8 x global rows, within the widest dense range): the broadcast plan then
+    gathers int32 offsets key - base (half the exchange bytes and half the build's key
+    reads) and builds with hj_build_key_range(0, range - 1) + hj_build_key_base(base), a
+    table keyed by the int64 keys again. One hj_key_minmax launch on the shard, one 16-byte
+    all-reduce (MIN over [min, ~max]) and a host read that waits for this stream only.
+    None: keep int64 keys."""
+    if build_keys.dtype != torch.int64 or global_rows <= 0:
+        return None
+    mm = torch.empty(2, dtype=torch.int64, device=build_keys.device)
+    key_minmax(build_keys, mm)
+    mm[1:].bitwise_not_()  # ~max is order-reversing: one MIN all-reduce gives both ends
+    if dist.is_initialized() and dist.get_world_size(group) > 1:
+        dist.all_reduce(mm, op=dist.ReduceOp.MIN, group=group)
+    lo, nhi = host_read_async(mm)()
+    hi = ~nhi
+    if lo > hi:
+        return None
+    rng = hi - lo + 1
+    if rng > DENSE_FACTOR * global_rows or rng > DENSE_MAX_RANGE:
+        return None
+    return lo, rng
+
+
 class DistributedHashJoin:
     """Inner equi-join of a build and a probe column that are each spread over the ranks
     (rank r holds rows [base_r, base_r + n_r) of the global column).
@@ -621,17 +661,26 @@ class DistributedHashJoin:
         global canonical row order, so the local table's row numbers are the global build
         ids) and probes only its own probe rows: no probe-side exchange. -> this rank's
         pairs (global build idx int64, global probe idx int32); the ranks' outputs in rank
-        order are the global canonical output. Needs equal-typed shards on every rank."""
-        (gathered,) = all_gather_rows([build_keys], self.group)
+        order are the global canonical output. Needs equal-typed shards on every rank. When
+        the global int64 build keys make a direct-addressed table (broadcast_key_plan), the
+        shards travel as int32 offsets and the table is keyed back (hj_build_key_base)."""
         dev = build_keys.device
         n = probe_keys.numel()
         if self.local_join_fn is not gpu_local_join:  # host stand-in (gloo tests): explicit ids
+            (gathered,) = all_gather_rows([build_keys], self.group)
             bi = torch.arange(gathered.numel(), dtype=torch.int64, device=dev)
             pi = torch.arange(probe_base, probe_base + n, dtype=torch.int64, device=dev).to(torch.int32)
             return self.local_join_fn(gathered, bi, probe_keys, pi, capacity_hint)
+        sizes = gather_sizes(build_keys.numel(), dev, self.group)
+        plan = broadcast_key_plan(build_keys, sum(sizes), self.group) if self.compress_keys else None
+        src = build_keys if plan is None else (build_keys - plan[0]).to(torch.int32)
+        (gathered,) = all_gather_rows([src], self.group, sizes=sizes)
         kt = "int64" if gathered.dtype == torch.int64 else "int32"
         with HashTable(1, kt, dev.index or 0) as t:  # canonical numbering = the global build ids
             t.append(0, gathered)
+            if plan is not None:  # int32 offsets, keyed back to the int64 keys
+                t.key_range(0, plan[1] - 1)
+                t.key_base(plan[0])
             t.finish(0)
             ws = torch.empty(HashTable.workspace_bytes(n), dtype=torch.uint8, device=dev)
             d_total = torch.zeros(1, dtype=torch.int64, device=dev)
@@ -669,10 +718,7 @@ def all_gather_rows(cols: list[torch.Tensor], group=None, sizes: list[int] | Non
     me = dist.get_rank(group)
     dev = cols[0].device
     if sizes is None:
-        n = torch.tensor([cols[0].numel()], dtype=torch.int64, device=dev)
-        ns = [torch.empty_like(n) for _ in range(world)]
-        dist.all_gather(ns, n, group=group)
-        sizes = [int(x) for x in torch.cat(ns).tolist()]
+        sizes = gather_sizes(cols[0].numel(), dev, group)
     ns = list(sizes)
     for c in cols:
         assert c.numel() == ns[me], "all_gather_rows: columns of unequal length"

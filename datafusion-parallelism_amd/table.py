@@ -161,8 +161,17 @@ class HashTable:
         the build skips its key-range reduction."""
         check(self._L.hj_build_key_range(self._h, int(lo), int(hi)))
 
+    def key_base(self, base: int) -> None:
+        """hj_build_key_base: this int32 table's build keys are offsets from `base`; once
+        built, the table is keyed by base + offset and takes int64 probe keys (a
+        direct-addressed table only; before the barrier)."""
+        check(self._L.hj_build_key_base(self._h, int(base)))
+        self._rekey = True
+
     def finish(self, partition: int) -> None:
         check(self._L.hj_build_finish(self._h, partition))
+        if getattr(self, "_rekey", False):
+            self.key_type = HJ_INT64
 
     def finish_all(self) -> None:
         """Call the barrier for every partition concurrently (one thread each), as

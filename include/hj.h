@@ -150,6 +150,15 @@ hj_status hj_build_finish(hj_table* t, int partition);
  * reference sizes its table from the row count, new_map_3.rs:162). */
 hj_status hj_build_key_range(hj_table* t, int64_t key_lo, int64_t key_hi);
 
+/* The build keys (an HJ_INT32 table) are int32 offsets v from key_base: the table is keyed
+ * by key_base + v in the int64 domain, and once built it takes int64 keys in every probe
+ * and lookup. Only a direct-addressed table can be re-keyed this way (it stores no keys,
+ * only refs indexed by key - min): a build whose key range exceeds 8 x its rows fails with
+ * HJ_ERR_INVALID. The broadcast-build plan gathers 4-byte offsets instead of 8-byte keys
+ * with it (half the exchange bytes, half the build's key reads) and probes the original
+ * int64 keys. Before the barrier; not for multi-GPU tables. */
+hj_status hj_build_key_base(hj_table* t, int64_t key_base);
+
 /* Canonical id of partition `partition`'s first row (valid after the barrier). */
 hj_status hj_build_partition_offset(const hj_table* t, int partition, int64_t* out);
 

@@ -95,6 +95,41 @@ def test_distributed_join_one_rank(dfp, oracle_mod, chunks):
         dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("keys", ["dense", "sparse", "dense_far"])
+def test_broadcast_join_one_rank(dfp, oracle_mod, keys):
+    """The broadcast plan on one RCCL rank: a dense build domain travels as int32 offsets
+    (broadcast_key_plan + hj_build_key_base), a sparse one as int64 keys; far from zero
+    (offsets from 2^62) too. Pairs equal the oracle's, probe ids = probe_base + row."""
+    from datafusion_parallelism_amd.distributed import DistributedHashJoin, broadcast_key_plan
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1")
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        rng = np.random.default_rng(7)
+        off = 2**62 if keys == "dense_far" else 0
+        if keys == "sparse":
+            bk = rng.integers(-(2**50), 2**50, 200_000)
+            pk = np.concatenate([rng.choice(bk, 300_000), rng.integers(-(2**50), 2**50, 300_000)])
+        else:
+            bk = rng.integers(0, 150_000, 200_000) + off
+            pk = rng.integers(-1000, 200_000, 600_000) + off
+        tb, tp = torch.from_numpy(bk).cuda(), torch.from_numpy(pk).cuda()
+        plan = broadcast_key_plan(tb, bk.size)
+        assert (plan is None) == (keys == "sparse")
+        if plan is not None:
+            assert plan == (int(bk.min()), int(bk.max() - bk.min() + 1))
+        b, p = DistributedHashJoin().run_broadcast(tb, tp, 5)
+        ob, op = oracle_mod.inner_join(bk, pk)
+        assert np.array_equal(b.cpu().numpy().astype(np.uint64), ob)
+        assert np.array_equal(p.cpu().numpy().astype(np.uint32), op + 5)
+    finally:
+        dist.destroy_process_group()
+
+
 def test_large_exchange_one_rank(dfp):
     """A 1.3 GB exchange (above the size where single RCCL self-copies come back wrong,
     tools/debug_shuffle.py) runs in rounds and arrives exact."""

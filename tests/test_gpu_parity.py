@@ -400,6 +400,47 @@ def test_build_key_range_hint(dfp, oracle_mod, lo_pad, hi_pad):
     assert np.array_equal(p.cpu().numpy().view(np.uint32), op)
 
 
+@pytest.mark.parametrize("base", [0, -(2**62), 2**62 - 10**6, 123_456_789_012])
+def test_build_key_base(dfp, oracle_mod, base):
+    """hj_build_key_base: an int32 table built from offsets key - base (with duplicates and
+    nulls) takes int64 probe keys afterwards; pairs equal the oracle's over the int64 keys,
+    and get_iter answers int64 keys."""
+    rng = np.random.default_rng(abs(base) % 1000)
+    off = rng.integers(0, 400_000, 300_000)
+    bk = off + base
+    pk = rng.integers(-50_000, 450_000, 1_000_000) + base
+    valid = rng.random(off.size) > 0.05
+    with dfp.HashTable(1, "int32", 0) as t:
+        t.append(0, torch.from_numpy(off.astype(np.int32)).cuda(), valid=torch.from_numpy(valid).cuda())
+        t.key_range(0, int(off.max()))
+        t.key_base(base)
+        t.finish(0)
+        assert t.stats()["buckets"] == 0  # direct-addressed
+        b, p = t.probe(torch.from_numpy(pk).cuda(), device_output=True)
+        k0 = int(bk[valid][0])
+        rows = t.lookup(k0)
+    ob, op = oracle_mod.inner_join(bk, pk, valid)
+    assert np.array_equal(b.cpu().numpy().astype(np.uint64), ob)
+    assert np.array_equal(p.cpu().numpy().view(np.uint32), op)
+    want = np.nonzero((bk == k0) & valid)[0][::-1]
+    assert rows == [int(x) for x in want]
+
+
+def test_build_key_base_needs_dense(dfp):
+    """A key range wider than 8 x the rows cannot be re-keyed: the build fails loudly."""
+    from datafusion_parallelism_amd import HjError
+
+    off = np.arange(0, 10_000 * 100, 100, dtype=np.int32)
+    t = dfp.HashTable(1, "int32", 0)
+    try:
+        t.append(0, torch.from_numpy(off).cuda())
+        t.key_base(5)
+        with pytest.raises(HjError, match="direct-addressed"):
+            t.finish(0)
+    finally:
+        t.close()
+
+
 def test_c3_full_size_digest(dfp, oracle_mod):
     """C3 (10^7 exponential build keys x 10^8 uniform probe keys): the pair count and
     per-probe-row match counts against the closed form multiplicity of each key."""
