@@ -468,7 +468,7 @@ def main():
                     help="synchronize the device after every step (no host/device overlap between steps)")
     ap.add_argument("--no-compress-keys", action="store_true",
                     help="multi-GPU: exchange full int64 keys / u64 build ids even when 32 bits suffice")
-    ap.add_argument("--plan", default="auto", choices=["auto", "broadcast", "radix"],
+    ap.add_argument("--plan", default="auto", choices=["auto", "broadcast", "radix", "sharded"],
                     help="multi-GPU plan for the strong-scaling line (auto: broadcast when B*G < B+P)")
     ap.add_argument("--no-weak", action="store_true",
                     help="multi-GPU: skip the weak-scaling extra (a config-sized join per rank, radix exchange)")
@@ -517,8 +517,14 @@ def main():
 
         dj = DistributedHashJoin(chunks=args.chunks, compress_keys=not args.no_compress_keys)
         plan = args.plan if args.plan != "auto" else DistributedHashJoin.choose_plan(gB, gP, world)
+        if args.plan == "auto" and plan == "broadcast":
+            # the broadcast side's sharded form: each rank builds 1/G of the table and the
+            # pieces are gathered (join_sharded falls back to a whole build per rank for a
+            # sparse build domain)
+            plan = "sharded"
         job = (BroadcastJob(dj, bk, pk, pbase, dev) if plan == "broadcast" else
-               DistJob(dj, bk, pk, bbase, pbase, dev))
+               ShardedJob(dj, bk, pk, bbase, pbase, dev) if plan == "sharded" else
+               DistJob(dj, bk, pk, bbase, pbase, dev, same_stream=args.same_stream))
 
     def barrier():
         if use_dist:
@@ -655,7 +661,7 @@ class DistJob:
     global probe ids. exchange_ms = from the end of the partitions to the end of the
     exchanges (events); probe_ms = the whole step on the device."""
 
-    def __init__(self, dj, bk, pk, bbase, pbase, dev):
+    def __init__(self, dj, bk, pk, bbase, pbase, dev, same_stream=False):
         self.dj, self.bk, self.pk, self.dev = dj, bk, pk, dev
         self.bbase = bbase
         self.pbase = pbase
@@ -665,6 +671,13 @@ class DistJob:
         self.kernel_desc = ("one-pass region partition (both sides) + RCCL point-to-point exchange + local build + "
                             "sliced probe with global ids")
         self._pending = None
+        # the next join's plan (key range + host read) on its own stream, as SingleGpuJoin's
+        # builds: the inputs are resident before the timed steps, so step k + 1's plan is read
+        # while step k's probe runs instead of idling the device behind it
+        if not same_stream:
+            from datafusion_parallelism_amd.distributed import concurrent_stream
+
+            dj.prepare_stream = concurrent_stream(dev)
 
     pipelined = True  # step k is collected (its pair count read) after step k + 1 is enqueued
 
@@ -691,6 +704,59 @@ class DistJob:
         ev["end"].synchronize()
         self.probe_ms.append(ev["start"].elapsed_time(ev["end"]))
         self.exchange_ms.append(ev["partitioned"].elapsed_time(ev["exchanged"]))
+        self.build_ms.append(0.0)
+        table.close()
+
+    def finish(self):
+        self.collect()
+
+
+class ShardedJob:
+    """One step = the sharded-build broadcast plan (DistributedHashJoin.join_sharded): the
+    build side range-partitioned and exchanged (RCCL), a local build of the rank's own key
+    range, an all_gather of the table pieces, and the probe of the rank's own probe rows
+    (no probe-side exchange, no replicated build). The build side runs on its own stream,
+    so step k's overlaps step k - 1's probe; step k - 1 is collected after step k is
+    enqueued. exchange_ms = the whole build side (plan, exchange, local build, gather) on
+    its stream; probe_ms = the probe, from its launch to its end."""
+
+    pipelined = True
+
+    def __init__(self, dj, bk, pk, bbase, pbase, dev):
+        self.dj, self.bk, self.pk, self.bbase, self.pbase, self.dev = dj, bk, pk, bbase, pbase, dev
+        self.probe_ms, self.build_ms, self.exchange_ms = [], [], []
+        self.matches = 0
+        self.cap = pk.numel()
+        from datafusion_parallelism_amd.distributed import concurrent_stream
+
+        self.bstream = concurrent_stream(dev)  # on another hardware queue than the probes'
+        self.kernel_desc = ("sharded build: range exchange of the build side (RCCL), local build of the rank's key "
+                            "range, all_gather of the table pieces, sliced probe of the local rows")
+        self._pending = None
+
+    def step(self):
+        ev = {k: torch.cuda.Event(enable_timing=True) for k in ("partitioned", "exchanged", "start", "end")}
+        self.dj.events = ev
+        cur = torch.cuda.current_stream(self.dev)
+        table, result = self.dj.join_sharded(self.bk, self.bbase, self.pk, self.pbase, self.cap,
+                                             build_stream=self.bstream)
+        self.dj.events = None
+        ev["end"].record(cur)
+        prev, self._pending = self._pending, (table, result, ev)
+        if prev is not None:
+            self._collect(*prev)
+
+    def collect(self):
+        if self._pending is not None:
+            pending, self._pending = self._pending, None
+            self._collect(*pending)
+
+    def _collect(self, table, result, ev):
+        b, _ = result()
+        self.matches = int(b.numel())
+        ev["end"].synchronize()
+        self.exchange_ms.append(ev["partitioned"].elapsed_time(ev["exchanged"]))
+        self.probe_ms.append(ev["exchanged"].elapsed_time(ev["end"]))
         self.build_ms.append(0.0)
         table.close()
 
@@ -731,8 +797,11 @@ class BroadcastJob:
         # two gather buffers per key width: step k + 2 reuses step k's once step k is collected
         self.gbuf = {dt: [torch.empty(sum(self.sizes), dtype=dt, device=dev) for _ in range(2)]
                      for dt in {bk.dtype, torch.int32}}
-        self.cstream = torch.cuda.Stream(dev)  # the gathers
-        self.bstream = torch.cuda.Stream(dev)  # the builds
+        from datafusion_parallelism_amd.distributed import concurrent_stream
+
+        # on other hardware queues than the probes' (concurrent_stream)
+        self.cstream = concurrent_stream(dev)  # the gathers
+        self.bstream = concurrent_stream(dev)  # the builds
         self.evs = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(2)]
         self.k = 0
         self.prev = None

@@ -70,6 +70,11 @@ SIGNATURES = [
     ("hj_build_finish", I32, [P, I32]),
     ("hj_build_key_range", I32, [P, I64, I64]),
     ("hj_build_key_base", I32, [P, I64]),
+    ("hj_table_dense_piece", I32, [P, PP, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_int64), PP, PP,
+                                   ctypes.POINTER(ctypes.c_int)]),
+    ("hj_table_dense_export", I32, [P, P, U64, U64, P, U64, P, P]),
+    ("hj_table_wrap_dense", I32, [I32, I32, I64, U64, P, P, I32, P, PP]),
+    ("hj_dense_rebase_dups", I32, [P, U64, U32, I32, P]),
     ("hj_build_partition_offset", I32, [P, I32, ctypes.POINTER(ctypes.c_int64)]),
     ("hj_table_stats_get", I32, [P, ctypes.POINTER(HjTableStats)]),
     ("hj_table_build_ns", I64, [P]),

@@ -266,6 +266,8 @@ struct hj_table {
     Bucket* tbl = nullptr;
     uint32_t nb = 0, clog2 = 10, nchunks = 0;
     uint32_t* dup_rows = nullptr;
+    BuildCounters* ctr = nullptr;  // the build's counters (dup_rows words in use), table-owned
+    bool wrapped = false;          // hj_table_wrap_dense: arrays borrowed from the caller
     uint64_t* row_ids = nullptr;
     uint32_t* dense = nullptr;  // direct-addressed layout (dense key range), else buckets
     bool packed = false;        // dense refs with inline counts (dup_rows offsets < 2^27)
@@ -348,8 +350,10 @@ hj_status build_attempt(hj_table* t, const std::vector<Segment>& segs, double lf
     int64_t* d_minmax;
     if ((st = dev_alloc(t, t->scratch, &p, sizeof(Segment) * std::max<size_t>(segs.size(), 1))) != HJ_OK) return st;
     d_segs = (Segment*)p;
-    if ((st = dev_alloc(t, t->scratch, &p, sizeof(BuildCounters))) != HJ_OK) return st;
+    // the counters live with the table: hj_table_dense_piece hands out dup_used
+    if ((st = dev_alloc(t, t->allocs, &p, sizeof(BuildCounters))) != HJ_OK) return st;
     ctr = (BuildCounters*)p;
+    t->ctr = ctr;
     if ((st = dev_alloc(t, t->scratch, &p, (2 + 2 * kMinmaxMaxBlocks) * sizeof(int64_t))) != HJ_OK) return st;
     d_minmax = (int64_t*)p;
     // few segments: the key-range kernel publishes them and zeroes the counters (no
@@ -1363,6 +1367,96 @@ hj_status hj_build_key_base(hj_table* t, int64_t key_base) {
     if (t->built || t->arrived > 0) return fail(HJ_ERR_INVALID, "hj_build_key_base: after the barrier started");
     t->has_base = true;
     t->key_base = key_base;
+    return HJ_OK;
+}
+
+hj_status hj_table_dense_piece(const hj_table* t, uint32_t** refs, uint64_t* nvalues, int64_t* key_min,
+                               uint32_t** dup_rows, const uint64_t** dup_used, int* packed) {
+    hj_status st = check_table(t);
+    if (st != HJ_OK) return st;
+    if (!refs || !nvalues || !key_min || !dup_rows || !dup_used || !packed) return fail(HJ_ERR_INVALID, "null out");
+    if (t->multi != nullptr || t->dense == nullptr || t->ctr == nullptr || t->wrapped)
+        return fail(HJ_ERR_INVALID, "hj_table_dense_piece: not a built direct-addressed single-device table");
+    *refs = t->dense;
+    *nvalues = t->drange;
+    *key_min = t->dmin;
+    *dup_rows = t->dup_rows;
+    *dup_used = reinterpret_cast<const uint64_t*>(&t->ctr->dup_used);
+    *packed = t->packed ? 1 : 0;
+    return HJ_OK;
+}
+
+hj_status hj_table_dense_export(const hj_table* t, uint32_t* refs_dst, uint64_t v0, uint64_t n, uint32_t* dup_dst,
+                                uint64_t dup_n, uint64_t* dup_used_dst, void* stream) {
+    hj_status st = check_table(t);
+    if (st != HJ_OK) return st;
+    if (t->multi != nullptr || t->dense == nullptr || t->ctr == nullptr || t->wrapped)
+        return fail(HJ_ERR_INVALID, "hj_table_dense_export: not a built direct-addressed single-device table");
+    if (refs_dst != nullptr && (v0 > t->drange || n > t->drange - v0))
+        return fail(HJ_ERR_INVALID, "hj_table_dense_export: refs range past the table's key range");
+    if (dup_dst != nullptr && dup_n > (uint64_t)(2 * t->total_rows + 2))
+        return fail(HJ_ERR_INVALID, "hj_table_dense_export: more segment words than the table holds");
+    HIP_TRY(hipSetDevice(t->device));
+    hipStream_t s = (hipStream_t)stream;
+    if (s != t->bstream) HIP_TRY(hipStreamWaitEvent(s, t->res.ev1, 0));  // after the build
+    if (refs_dst != nullptr && n > 0)
+        HIP_TRY(hipMemcpyAsync(refs_dst, t->dense + v0, n * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
+    if (dup_dst != nullptr && dup_n > 0)
+        HIP_TRY(hipMemcpyAsync(dup_dst, t->dup_rows, dup_n * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
+    if (dup_used_dst != nullptr)
+        HIP_TRY(hipMemcpyAsync(dup_used_dst, &t->ctr->dup_used, sizeof(uint64_t), hipMemcpyDeviceToDevice, s));
+    return note_probe(t, s);  // hj_table_free waits for these reads too
+}
+
+hj_status hj_table_wrap_dense(int device, hj_key_type probe_key_type, int64_t key_min, uint64_t nvalues,
+                              const uint32_t* refs, const uint32_t* dup_rows, int packed, void* stream,
+                              hj_table** out) {
+    if (out == nullptr) return fail(HJ_ERR_INVALID, "null out");
+    *out = nullptr;
+    if (probe_key_type != HJ_INT32 && probe_key_type != HJ_INT64) return fail(HJ_ERR_INVALID, "unsupported key type");
+    if (refs == nullptr || dup_rows == nullptr || nvalues == 0)
+        return fail(HJ_ERR_INVALID, "hj_table_wrap_dense: null arrays or an empty key range");
+    if (nvalues > ((uint64_t)kMaxChunks << kDenseShift))
+        return fail(HJ_ERR_INVALID, "hj_table_wrap_dense: key range beyond the direct-addressed layout");
+    const int nd = device_count();
+    if (nd == 0) return fail(HJ_ERR_NO_DEVICE, "no GPU visible: the HIP path cannot run (no CPU fallback)");
+    if (device < 0 || device >= nd) return fail(HJ_ERR_INVALID, "bad device ordinal");
+    HIP_TRY(hipSetDevice(device));
+    hj_table* t = new hj_table();
+    t->device = device;
+    t->kt = probe_key_type;
+    t->key_bytes = probe_key_type == HJ_INT64 ? 8 : 4;
+    t->parts.resize(1);
+    t->finished.assign(1, 1);
+    t->arrived = 1;
+    if (!acquire_resources(device, &t->res)) {
+        delete t;
+        return fail(HJ_ERR_HIP, "stream/event creation failed");
+    }
+    t->wrapped = true;
+    t->dense = const_cast<uint32_t*>(refs);
+    t->dup_rows = const_cast<uint32_t*>(dup_rows);
+    t->dmin = key_min;
+    t->drange = nvalues;
+    t->packed = packed != 0;
+    t->bstream = (hipStream_t)stream;
+    // the arrays are ready at this point of `stream`: probes elsewhere wait for it
+    if (hipEventRecord(t->res.ev0, t->bstream) != hipSuccess || hipEventRecord(t->res.ev1, t->bstream) != hipSuccess) {
+        release_resources(device, t->res);
+        delete t;
+        return fail(HJ_ERR_HIP, "hipEventRecord failed");
+    }
+    t->built = true;
+    *out = t;
+    return HJ_OK;
+}
+
+hj_status hj_dense_rebase_dups(uint32_t* refs, uint64_t n, uint32_t base, int packed, void* stream) {
+    if (n > 0 && refs == nullptr) return fail(HJ_ERR_INVALID, "null refs");
+    if (device_count() == 0) return fail(HJ_ERR_NO_DEVICE, "no GPU visible");
+    const uint32_t mask = packed ? kPackedMask : kFullMask;
+    if (base > mask) return fail(HJ_ERR_INVALID, "hj_dense_rebase_dups: base beyond the offset field");
+    HIP_TRY(launch_dense_rebase(refs, n, base, mask, (hipStream_t)stream));
     return HJ_OK;
 }
 

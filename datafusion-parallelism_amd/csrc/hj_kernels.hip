@@ -3742,6 +3742,25 @@ hipError_t launch_probe(int key_bytes, const TableView& tv, const void* keys, co
     return hipGetLastError();
 }
 
+// A gathered direct-addressed table (the sharded-build broadcast plan): each piece's
+// duplicated-key refs point into its own segment array; once the pieces' segment arrays
+// sit one after another, the refs of one piece move by that piece's base. Streams the
+// piece's refs once (a piece starts at any element: 4-byte accesses, coalesced).
+__global__ void __launch_bounds__(256) dense_rebase_kernel(uint32_t* __restrict__ refs, uint64_t n, uint32_t base,
+                                                           uint32_t mask) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t r = refs[i];
+        if (r != kMiss && (r & kDupFlag)) refs[i] = (r & ~mask) | ((r & mask) + base);
+    }
+}
+
+hipError_t launch_dense_rebase(uint32_t* refs, uint64_t n, uint32_t base, uint32_t mask, hipStream_t s) {
+    if (n == 0 || base == 0) return hipSuccess;
+    const uint64_t blocks = std::min<uint64_t>((n + 255) / 256, 8192);
+    dense_rebase_kernel<<<(unsigned)blocks, 256, 0, s>>>(refs, n, base, mask);
+    return hipGetLastError();
+}
+
 hipError_t launch_table_stats(const TableView& tv, unsigned long long* out, hipStream_t s) {
     table_stats_kernel<<<1024, 256, 0, s>>>(tv, out);
     return hipGetLastError();

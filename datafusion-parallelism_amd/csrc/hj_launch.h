@@ -97,6 +97,8 @@ hipError_t launch_probe(int key_bytes, const TableView& tv, const void* keys, co
                         hipEvent_t built, hipStream_t s);
 
 // ---- table queries -------------------------------------------------------
+// refs[v] of a duplicated key (bit 31, not kMiss): offset field (mask) + base, v < n
+hipError_t launch_dense_rebase(uint32_t* refs, uint64_t n, uint32_t base, uint32_t mask, hipStream_t s);
 hipError_t launch_table_stats(const TableView& tv,
                               unsigned long long* out /* [4]: distinct, dupkeys, duprows, maxrows */,
                               hipStream_t s);

@@ -15,6 +15,7 @@ only product) implementations are the HIP kernels.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 from dataclasses import dataclass, field
 from typing import Callable
@@ -236,6 +237,37 @@ class ExchangeStats:
 # ~800 MB come back wrong on this stack (tools/debug_shuffle.py: 1.6 GB -> the second
 # half differs), so larger exchanges run in rounds of at most this size.
 A2A_MAX_BYTES = 256 << 20
+
+
+def concurrent_stream(device, avoid: torch.cuda.Stream | None = None, tries: int = 8) -> torch.cuda.Stream:
+    """A torch pool stream whose work runs concurrently with `avoid` (default: the current
+    stream). HIP multiplexes streams onto a few hardware queues (GPU_MAX_HW_QUEUES, 4 here)
+    in creation order, and two streams on one queue run one after the other: a side stream
+    that lands on the current stream's queue serializes every overlap a pipeline counts on
+    (seen in kernel traces: the plan's key-range read queued behind the previous probe).
+    Tested, not assumed: a spin kernel on `avoid`, a tiny one on the candidate, and the
+    candidate must finish while the spin still runs. -> the first candidate that does (else
+    the last one tried)."""
+    avoid = avoid or torch.cuda.current_stream(device)
+    cand = None
+    for _ in range(tries):
+        cand = torch.cuda.Stream(device)
+        if cand.cuda_stream == avoid.cuda_stream:
+            continue
+        spin_done = torch.cuda.Event()
+        with torch.cuda.stream(avoid):
+            torch.cuda._sleep(20_000_000)
+            spin_done.record(avoid)
+        mark = torch.cuda.Event()
+        with torch.cuda.stream(cand):
+            torch.cuda._sleep(1000)
+            mark.record(cand)
+        mark.synchronize()
+        overlapped = not spin_done.query()
+        spin_done.synchronize()
+        if overlapped:
+            return cand
+    return cand
 
 
 def host_read_async(t: torch.Tensor) -> Callable[[], list]:
@@ -464,6 +496,12 @@ class DistributedHashJoin:
         self.compress_keys = compress_keys
         self.runtime_filter = runtime_filter
         self.events: dict | None = None  # {"partitioned", "exchanged"}: torch.cuda.Event recorded by join()
+        # prepare()'s key-range reads and its host read run on this stream when set. Only for
+        # callers whose build keys are complete with respect to it (inputs resident before a
+        # pipeline of joins starts): the next join's plan is then read while the previous
+        # join's probe still runs, instead of queueing behind it on the current stream with
+        # the device idle during the host read and the plan.
+        self.prepare_stream: torch.cuda.Stream | None = None
 
     def prepare(self, build_keys: torch.Tensor, probe_keys: torch.Tensor, build_base: int) -> ExchangePlan:
         """Plan the exchange from the global key ranges (one hj_key_minmax launch per side,
@@ -485,22 +523,22 @@ class DistributedHashJoin:
         dev = build_keys.device
         # with the runtime filter only build-range keys travel: the probe range is not needed
         sides = (build_keys,) if self.runtime_filter else (build_keys, probe_keys)
-        mm = torch.empty(2 * len(sides), dtype=torch.int64, device=dev)  # build min, max[, probe min, max]
-        for j, k in enumerate(sides):
-            key_minmax(k, mm[2 * j:2 * j + 2])
-        bend = build_base + build_keys.numel()
-        if self.world > 1:
-            lo = mm[0::2].contiguous()  # [build min[, probe min]]
-            hi = torch.cat([mm[1::2], torch.tensor([bend], dtype=torch.int64, device=dev)])
-            dist.all_reduce(lo, op=dist.ReduceOp.MIN, group=self.group)
-            dist.all_reduce(hi, op=dist.ReduceOp.MAX, group=self.group)
-            vlo, vhi = lo.tolist(), hi.tolist()
-            bmin, bmax, bend = vlo[0], vhi[0], vhi[-1]
-            pmin, pmax = (vlo[1], vhi[1]) if len(sides) == 2 else (2**63 - 1, -(2**63))
-        else:
-            v = host_read_async(mm)()
-            bmin, bmax = v[0], v[1]
-            pmin, pmax = (v[2], v[3]) if len(sides) == 2 else (2**63 - 1, -(2**63))
+        ps = self.prepare_stream if build_keys.is_cuda else None
+        with torch.cuda.stream(ps) if ps is not None else contextlib.nullcontext():
+            mm = torch.empty(2 * len(sides), dtype=torch.int64, device=dev)  # build min, max[, probe min, max]
+            for j, k in enumerate(sides):
+                key_minmax(k, mm[2 * j:2 * j + 2])
+            bend = build_base + build_keys.numel()
+            if self.world > 1:
+                lo = mm[0::2].contiguous()  # [build min[, probe min]]
+                hi = torch.cat([mm[1::2], torch.tensor([bend], dtype=torch.int64, device=dev)])
+                vlo, vhi = self._allreduce_range(lo, hi)
+                bmin, bmax, bend = vlo[0], vhi[0], vhi[-1]
+                pmin, pmax = (vlo[1], vhi[1]) if len(sides) == 2 else (2**63 - 1, -(2**63))
+            else:
+                v = host_read_async(mm)()
+                bmin, bmax = v[0], v[1]
+                pmin, pmax = (v[2], v[3]) if len(sides) == 2 else (2**63 - 1, -(2**63))
         plan.build_rows = bend
         if bend < 2**31:
             plan.build_id_dtype = torch.int32
@@ -647,6 +685,172 @@ class DistributedHashJoin:
             return [r() for r in results]
         finally:
             table.close()
+
+    # -- sharded-build broadcast plan --------------------------------------------------
+    @staticmethod
+    def sharded_ok(plan: ExchangePlan, world: int) -> bool:
+        """The sharded-build plan needs a direct-addressed build domain split by key range
+        (prepare's range map; one rank: the whole range), build ids held in place of rows
+        (< 2^31 rows) and every piece's segment offsets, rebased, inside the packed refs'
+        27 bits (2·B + 2·G + 2 < 2^27)."""
+        if plan.build_lo is None or plan.build_rows is None or plan.build_id_dtype != torch.int32:
+            return False
+        dense = (plan.build_hi - plan.build_lo + 1) <= 8 * plan.build_rows
+        return dense and (world == 1 or plan.spec.by_range) and 2 * plan.build_rows + 2 * world + 2 < 2**27
+
+    def join_sharded(self, build_keys: torch.Tensor, build_base: int, probe_keys: torch.Tensor, probe_base: int,
+                     capacity_hint: int | None = None, build_stream: torch.cuda.Stream | None = None):
+        """The sharded-build broadcast plan: the build side goes through the radix plan's
+        range partition and exchange, each rank builds the direct-addressed table of its
+        own contiguous key range (global build ids in place of rows), the ranks all-gather
+        those pieces (and their duplicate segments, re-pointed at their place in the
+        concatenated segment array) into one table, and each rank probes its own probe rows
+        against it with the global probe ids base + row. No probe-side exchange and no
+        replicated build: per rank 1/G of the build and B·4 bytes of table received, against
+        the broadcast plan's whole build and B·4 bytes of keys. The ranks' outputs in rank
+        order are the canonical output. build_stream: the build side (plan, partition,
+        exchange, local build, gather) runs there and the probe on the current stream
+        waits for the gathered table only. Falls back to run_broadcast's shape (whole
+        build per rank) when sharded_ok is false.
+        -> (table, result): result() waits and yields this rank's pairs; close the table
+        afterwards."""
+        cur = torch.cuda.current_stream(probe_keys.device)
+        bs = build_stream or cur
+        ev = self.events  # optional (bench): "partitioned" / "exchanged" = start / end of the build side
+        with torch.cuda.stream(bs):
+            if ev is not None:
+                ev["partitioned"].record(bs)
+            plan = self.prepare(build_keys, probe_keys, build_base)
+            if not self.sharded_ok(plan, self.world):
+                return self._broadcast_table(build_keys, probe_keys, probe_base, capacity_hint, bs, cur)
+            table = self._gather_pieces(build_keys, build_base, plan, probe_keys.dtype, bs)
+            if ev is not None:
+                ev["exchanged"].record(bs)
+        result = self._probe_own(table, probe_keys, probe_base, capacity_hint, cur)
+        return table, result
+
+    def _gather_pieces(self, build_keys, build_base, plan: ExchangePlan, probe_dtype, bs):
+        dev = build_keys.device
+        W, me = self.world, self.rank
+        bk_r, bi_r, bc, bcap = self._partition(build_keys, build_base, torch.int64, plan.key_offset, plan.spec)
+        bk, bi = self._exchange_build(bk_r, bi_r, bc, bcap)
+        # every rank's key range, as the partition's range map cut it (they tile the domain)
+        rngs = [plan.local_key_range(d, W) for d in range(W)]
+        lens = [0 if r is None else r[1] - r[0] + 1 for r in rngs]
+        offs = [sum(lens[:d]) for d in range(W)]
+        full = torch.empty(sum(lens), dtype=torch.int32, device=dev)  # u32 refs of the whole domain
+        mine = full.narrow(0, offs[me], lens[me])
+        used = torch.zeros(1, dtype=torch.int64, device=dev)
+        local = None
+        if bk.numel() and lens[me]:
+            local = GpuLocalTable(bk, bi, ids_u31=True, key_range=rngs[me])
+            local.table.dense_export(refs=mine, dup_used=used, stream=bs.cuda_stream)
+        elif lens[me]:
+            mine.fill_(-1)  # no build rows in this range: every ref kMiss
+        packed = 2 * plan.build_rows + 2 < 2**27
+        try:
+            if W > 1:
+                self._allgather_var(full, offs, lens, mine)
+            du = self._allgather_counts(used)  # segment words per piece (one host read)
+            if sum(du):
+                bases = [sum(du[:d]) for d in range(W)]
+                dup = torch.empty(sum(du), dtype=torch.int32, device=dev)
+                if local is not None and du[me]:
+                    local.table.dense_export(dup=dup.narrow(0, bases[me], du[me]), stream=bs.cuda_stream)
+                if W > 1:
+                    self._allgather_var(dup, bases, du, dup.narrow(0, bases[me], du[me]))
+                for d in range(W):
+                    if du[d] and bases[d]:
+                        HashTable.rebase_dups(full.narrow(0, offs[d], lens[d]), bases[d], packed, bs.cuda_stream)
+            else:
+                dup = torch.zeros(4, dtype=torch.int32, device=dev)
+        finally:
+            if local is not None:
+                local.close()
+        kt = "int64" if probe_dtype == torch.int64 else "int32"
+        # the gathered table is keyed in the probe keys' domain: narrowing shifted only the
+        # travelling build keys
+        return HashTable.wrap_dense(dev.index or 0, kt, plan.build_lo, full, dup, packed, bs.cuda_stream)
+
+    def _allreduce_range(self, lo: torch.Tensor, hi: torch.Tensor) -> tuple[list[int], list[int]]:
+        """Element-wise MIN of lo and MAX of hi over the ranks -> host lists."""
+        dist.all_reduce(lo, op=dist.ReduceOp.MIN, group=self.group)
+        dist.all_reduce(hi, op=dist.ReduceOp.MAX, group=self.group)
+        return lo.tolist(), hi.tolist()
+
+    # the sharded-build plan's three communication steps (RCCL by default; tests replace
+    # them to run several ranks as threads on one device)
+    def _exchange_build(self, bk_r, bi_r, bc, bcap):
+        """The build side's regions to their owners -> (keys, ids) this rank received."""
+        if self.world == 1:
+            n = int(host_read_async(bc)()[0])
+            return bk_r[:n], bi_r[:n]
+        (bk, bi), _ = exchange_regions([bk_r, bi_r], bcap, _count_matrix(bc, self.group), self.group)
+        return bk, bi
+
+    def _allgather_var(self, out: torch.Tensor, offs: list[int], lens: list[int], src: torch.Tensor) -> None:
+        """out[offs[d] : offs[d] + lens[d]] = rank d's src, on every rank (src may be a view
+        of out)."""
+        src = src.clone()
+        if len(set(lens)) == 1 and offs == [lens[0] * d for d in range(len(lens))] and out.numel() == sum(lens):
+            dist.all_gather_into_tensor(out, src, group=self.group)
+        else:
+            dist.all_gather([out.narrow(0, o, n) for o, n in zip(offs, lens)], src, group=self.group)
+
+    def _allgather_counts(self, t: torch.Tensor) -> list[int]:
+        """Every rank's one-element int64 device tensor -> host list (rank order)."""
+        if self.world == 1:
+            return [int(host_read_async(t)()[0])]
+        allt = torch.empty(self.world, dtype=torch.int64, device=t.device)
+        dist.all_gather_into_tensor(allt, t, group=self.group)
+        return [int(x) for x in host_read_async(allt)()]
+
+    def _probe_own(self, table: HashTable, probe_keys: torch.Tensor, probe_base: int, capacity_hint, cur):
+        """This rank's probe rows against a finished table, probe idx = probe_base + row, on
+        the current stream. -> result() as GpuLocalTable.probe's."""
+        dev = probe_keys.device
+        n = probe_keys.numel()
+        ws = torch.empty(HashTable.workspace_bytes(n), dtype=torch.uint8, device=dev)
+        d_total = torch.empty(1, dtype=torch.int64, device=dev)
+        cap = max(capacity_hint or n, 1)
+
+        def launch(c):
+            ob = torch.empty(c, dtype=torch.int64, device=dev)
+            op = torch.empty(c, dtype=torch.int32, device=dev)
+            table.probe_async(probe_keys.data_ptr(), n, ob.data_ptr(), op.data_ptr(), c, d_total.data_ptr(),
+                              ws.data_ptr(), cur.cuda_stream, probe_base=probe_base)
+            return ob, op
+
+        ob, op = launch(cap)
+        read_total = host_read_async(d_total)
+
+        def result(total: int | None = None):
+            nonlocal ob, op
+            total = int(read_total()[0]) if total is None else total
+            if total > cap:
+                ob, op = launch(total)
+                total = int(d_total.item())
+            return ob[:total], op[:total]
+
+        result.d_total = d_total
+        return result
+
+    def _broadcast_table(self, build_keys, probe_keys, probe_base, capacity_hint, bs, cur):
+        """Fallback of join_sharded: every rank builds the whole gathered build side."""
+        dev = build_keys.device
+        sizes = gather_sizes(build_keys.numel(), dev, self.group)
+        if self.world > 1:
+            g = torch.empty(sum(sizes), dtype=build_keys.dtype, device=dev)
+            dist.all_gather(list(torch.split(g, sizes)), build_keys, group=self.group)
+        else:
+            g = build_keys
+        table = HashTable(1, "int64" if g.dtype == torch.int64 else "int32", dev.index or 0)
+        table.append(0, g)
+        table.finish(0)
+        table._keep.append(g)
+        with torch.cuda.stream(cur):
+            result = self._probe_own(table, probe_keys, probe_base, capacity_hint, cur)
+        return table, result
 
     # -- broadcast-build plan (SURVEY.md §8e) ------------------------------------------
     @staticmethod

@@ -298,6 +298,48 @@ class HashTable:
             check(self._L.hj_probe_async_ids(self._h, keys_ptr, valid_ptr, voff, probe_ids_ptr, n, out_build_ptr,
                                              out_probe_ptr, capacity, d_total_ptr, workspace_ptr, stream or None))
 
+    # -- sharded-build broadcast plan (hj_table_dense_piece / hj_table_wrap_dense) -------
+    def dense_piece(self) -> dict:
+        """A built direct-addressed table's arrays (device pointers): refs, nvalues,
+        key_min, dup_rows, dup_used (device pointer to a u64), packed."""
+        refs, dup, used = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p()
+        nv, kmin, packed = ctypes.c_uint64(), ctypes.c_int64(), ctypes.c_int()
+        check(self._L.hj_table_dense_piece(self._h, ctypes.byref(refs), ctypes.byref(nv), ctypes.byref(kmin),
+                                           ctypes.byref(dup), ctypes.byref(used), ctypes.byref(packed)))
+        return {"refs": refs.value or 0, "nvalues": nv.value, "key_min": kmin.value, "dup_rows": dup.value or 0,
+                "dup_used": used.value or 0, "packed": bool(packed.value)}
+
+    def dense_export(self, refs: torch.Tensor | None = None, v0: int = 0, dup: torch.Tensor | None = None,
+                     dup_used: torch.Tensor | None = None, stream: int = 0) -> None:
+        """Device copies of the refs [v0, v0 + refs.numel()), the first dup.numel() segment
+        words and the segment words in use (one int64) into the given tensors, on `stream`."""
+        check(self._L.hj_table_dense_export(self._h, None if refs is None else refs.data_ptr(), v0,
+                                            0 if refs is None else refs.numel(),
+                                            None if dup is None else dup.data_ptr(), 0 if dup is None else dup.numel(),
+                                            None if dup_used is None else dup_used.data_ptr(), stream or None))
+
+    @classmethod
+    def wrap_dense(cls, device: int, key_type: str | int, key_min: int, refs: torch.Tensor,
+                   dup_rows: torch.Tensor, packed: bool, stream: int = 0) -> "HashTable":
+        """A probe-only table over device tensors (int32/uint32 views of the u32 refs and
+        segments), kept alive by the table: refs[v] for key key_min + v."""
+        self = cls.__new__(cls)
+        self._L = _lib.load()
+        kt = key_type if isinstance(key_type, int) else (HJ_INT64 if key_type == "int64" else HJ_INT32)
+        self.key_type, self.parallelism, self.device, self.devices = kt, 1, device, None
+        h = ctypes.c_void_p()
+        check(self._L.hj_table_wrap_dense(device, kt, int(key_min), refs.numel(), refs.data_ptr(),
+                                          dup_rows.data_ptr(), int(bool(packed)), stream or None, ctypes.byref(h)))
+        self._h = h
+        self._keep = [refs, dup_rows]
+        return self
+
+    @staticmethod
+    def rebase_dups(refs: torch.Tensor, base: int, packed: bool, stream: int = 0) -> None:
+        """hj_dense_rebase_dups on a (view of a) u32 refs tensor."""
+        check(_lib.load().hj_dense_rebase_dups(refs.data_ptr(), refs.numel(), int(base), int(bool(packed)),
+                                               stream or None))
+
     @staticmethod
     def workspace_bytes(n: int) -> int:
         return _lib.load().hj_probe_workspace_bytes(n)

@@ -159,6 +159,44 @@ hj_status hj_build_key_range(hj_table* t, int64_t key_lo, int64_t key_hi);
  * int64 keys. Before the barrier; not for multi-GPU tables. */
 hj_status hj_build_key_base(hj_table* t, int64_t key_base);
 
+/* Sharded-build broadcast plan (multi-GPU, a direct-addressed build domain): every rank
+ * builds the table of its own contiguous key range from the build rows the radix exchange
+ * brought it, the ranks all-gather those pieces into one table, and each probes its own
+ * probe rows against it (no probe-side exchange, no replicated build). Replaces, for the
+ * multi-GPU case, the one shared table every partition probes
+ * (version10/parallel_join_execution_state.rs:405-407, lookup_implementation_3.rs:6-21).
+ *
+ * hj_table_dense_piece: a finished direct-addressed table's arrays, for the gather: refs
+ * (one u32 per key value from *key_min, *nvalues of them: a build row id, kMiss =
+ * 0xFFFFFFFF, or bit 31 + the offset of a duplicated key's segment [count, rows
+ * descending] in *dup_rows), a device pointer to the number of u32 words of *dup_rows in
+ * use (u64, final when the build is), and *packed (refs carry counts <= 15 in bits 27-30,
+ * offsets in bits 0-26; else offsets in bits 0-30). HJ_ERR_INVALID for a hashed table. */
+hj_status hj_table_dense_piece(const hj_table* t, uint32_t** refs, uint64_t* nvalues, int64_t* key_min,
+                               uint32_t** dup_rows, const uint64_t** dup_used, int* packed);
+
+/* Copies of a direct-addressed table's arrays on `stream` (any null destination is
+ * skipped): refs [v0, v0 + n) to refs_dst, the first dup_n words of its segment array to
+ * dup_dst, and the number of segment words in use (u64) to dup_used_dst — device
+ * pointers, the gather's send buffers. */
+hj_status hj_table_dense_export(const hj_table* t, uint32_t* refs_dst, uint64_t v0, uint64_t n, uint32_t* dup_dst,
+                                uint64_t dup_n, uint64_t* dup_used_dst, void* stream);
+
+/* A finished, probe-only direct-addressed table over caller-owned device arrays (borrowed
+ * until hj_table_free; the library frees nothing of them): refs[v] for key key_min + v,
+ * v < nvalues, in the layout hj_table_dense_piece describes, and the segments they point
+ * into. The arrays are ready in `stream` order; probes on other streams wait for that
+ * point. Probes take keys of probe_key_type. */
+hj_status hj_table_wrap_dense(int device, hj_key_type probe_key_type, int64_t key_min, uint64_t nvalues,
+                              const uint32_t* refs, const uint32_t* dup_rows, int packed, void* stream,
+                              hj_table** out);
+
+/* refs[v] += base in the offset field of every duplicated-key ref (bit 31 set, not kMiss),
+ * v < n, on `stream`: a gathered piece's refs re-pointed at its segments' place in the
+ * concatenated segment array. The caller keeps every offset + base below 2^27 (packed) or
+ * 2^31. */
+hj_status hj_dense_rebase_dups(uint32_t* refs, uint64_t n, uint32_t base, int packed, void* stream);
+
 /* Canonical id of partition `partition`'s first row (valid after the barrier). */
 hj_status hj_build_partition_offset(const hj_table* t, int partition, int64_t* out);
 

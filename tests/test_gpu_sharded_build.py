@@ -1,0 +1,161 @@
+"""GPU: the sharded-build broadcast plan (DistributedHashJoin.join_sharded): each rank builds
+the direct-addressed table of its own key range from the build rows the range exchange
+brought it, the pieces (and their duplicate segments, re-pointed) are all-gathered into
+one table, and each rank probes its own probe rows against it.
+
+* one RCCL rank on the box's GPU, against the oracle (dense, far-from-zero, duplicate-heavy
+  and sparse = the whole-build fallback);
+* 2, 4 and 8 ranks as threads on the one GPU: the plan's own code with its three
+  communication steps (range all-reduce, build exchange, variable all-gather) done by a
+  thread barrier instead of RCCL, so the piece boundaries, the duplicate-segment rebase and
+  empty pieces run at world > 1. The ranks' outputs in rank order must equal the oracle's
+  canonical pairs of the whole join.
+"""
+import os
+import socket
+import threading
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+
+pytestmark = pytest.mark.gpu
+
+
+def _keys(kind, rng, nb, np_):
+    off = 2**62 if kind == "dense_far" else 0
+    if kind == "sparse":
+        bk = rng.integers(-(2**50), 2**50, nb)
+        pk = np.concatenate([rng.choice(bk, np_ // 2), rng.integers(-(2**50), 2**50, np_ - np_ // 2)])
+    elif kind == "dups":  # heavy duplicates: segments in every piece, some keys > 15 rows
+        bk = np.concatenate([rng.integers(0, nb // 8, nb - 400), np.full(400, nb // 16)])
+        rng.shuffle(bk)
+        pk = rng.integers(-50, nb // 8 + 50, np_)
+    elif kind == "clustered":  # build keys at both ends of the range: middle pieces empty
+        bk = np.concatenate([rng.integers(0, 1000, nb // 2), rng.integers(7 * nb, 7 * nb + 1000, nb - nb // 2)])
+        pk = rng.integers(-10, 7 * nb + 1010, np_)
+    else:
+        bk = rng.integers(0, nb + nb // 2, nb) + off
+        pk = rng.integers(-1000, nb * 2, np_) + off
+    return bk.astype(np.int64), pk.astype(np.int64)
+
+
+def _init_one_rank():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1")
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+
+
+@pytest.mark.parametrize("kind", ["dense", "dense_far", "dups", "sparse"])
+def test_sharded_build_one_rank(dfp, oracle_mod, kind):
+    from datafusion_parallelism_amd.distributed import DistributedHashJoin
+
+    _init_one_rank()
+    try:
+        rng = np.random.default_rng(11)
+        bk, pk = _keys(kind, rng, 150_000, 500_000)
+        dj = DistributedHashJoin()
+        side = torch.cuda.Stream()
+        table, result = dj.join_sharded(torch.from_numpy(bk).cuda(), 0, torch.from_numpy(pk).cuda(), 7,
+                                        build_stream=side)
+        try:
+            b, p = result()
+        finally:
+            table.close()
+        ob, op = oracle_mod.inner_join(bk, pk)
+        assert np.array_equal(b.cpu().numpy().astype(np.uint64), ob)
+        assert np.array_equal(p.cpu().numpy().astype(np.uint32), op + 7)
+    finally:
+        dist.destroy_process_group()
+
+
+class _ThreadComm:
+    """The collectives of W ranks that are threads of one process on one GPU."""
+
+    def __init__(self, world):
+        self.world = world
+        self.bar = threading.Barrier(world)
+        self.slot = [None] * world
+
+    def share(self, rank, value):
+        """-> every rank's value (rank order); every rank's device work is finished first."""
+        torch.cuda.synchronize()
+        self.slot[rank] = value
+        self.bar.wait()
+        out = list(self.slot)
+        self.bar.wait()
+        return out
+
+
+def _threaded_join(world, comm, rank, bk, pk, out, errs):
+    from datafusion_parallelism_amd.distributed import DistributedHashJoin
+
+    class Rank(DistributedHashJoin):
+        def __init__(self):  # no process group: rank and world of the thread
+            self.group, self.world, self.rank = None, world, rank
+            self.partition_fn = None
+            self.chunks, self.compress_keys, self.runtime_filter = 1, True, True
+            self.events, self.prepare_stream = None, None
+
+        def _partition(self, keys, id_base, id_dtype, key_offset, spec=None):
+            from datafusion_parallelism_amd.distributed import gpu_partition_regions
+
+            return gpu_partition_regions(keys, None, id_base, self.world, id_dtype=id_dtype, key_offset=key_offset,
+                                         spec=spec)
+
+        def _allreduce_range(self, lo, hi):
+            all_ = comm.share(rank, (lo.tolist(), hi.tolist()))
+            return ([min(v[0][j] for v in all_) for j in range(lo.numel())],
+                    [max(v[1][j] for v in all_) for j in range(hi.numel())])
+
+        def _exchange_build(self, bk_r, bi_r, bc, bcap):
+            all_ = comm.share(rank, (bk_r, bi_r, bc.tolist(), bcap))
+            ks = [k[rank * cap:rank * cap + c[rank]] for k, _, c, cap in all_]
+            ids = [i[rank * cap:rank * cap + c[rank]] for _, i, c, cap in all_]
+            return torch.cat(ks).contiguous(), torch.cat(ids).contiguous()
+
+        def _allgather_var(self, out, offs, lens, src):
+            all_ = comm.share(rank, src.clone())
+            for d in range(world):
+                out.narrow(0, offs[d], lens[d]).copy_(all_[d])
+
+        def _allgather_counts(self, t):
+            return [int(v) for v in comm.share(rank, int(t.item()))]
+
+    try:
+        B, P = bk.size, pk.size
+        b0, b1 = B * rank // world, B * (rank + 1) // world
+        p0, p1 = P * rank // world, P * (rank + 1) // world
+        dj = Rank()
+        table, result = dj.join_sharded(torch.from_numpy(bk[b0:b1]).cuda(), b0, torch.from_numpy(pk[p0:p1]).cuda(), p0)
+        try:
+            b, p = result()
+            out[rank] = (b.cpu().numpy().astype(np.uint64), p.cpu().numpy().astype(np.uint32))
+        finally:
+            table.close()
+    except BaseException as e:  # noqa: BLE001 - reported by the test
+        errs.append((rank, repr(e)))
+        comm.bar.abort()
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+@pytest.mark.parametrize("kind", ["dense", "dups", "clustered"])
+def test_sharded_build_threads(dfp, oracle_mod, world, kind):
+    rng = np.random.default_rng(world * 10 + len(kind))
+    bk, pk = _keys(kind, rng, 120_000, 400_000)
+    comm = _ThreadComm(world)
+    out, errs = [None] * world, []
+    ths = [threading.Thread(target=_threaded_join, args=(world, comm, r, bk, pk, out, errs)) for r in range(world)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join(timeout=120)
+    assert not errs, errs
+    assert all(o is not None for o in out)
+    ob, op = oracle_mod.inner_join(bk, pk)
+    assert np.array_equal(np.concatenate([o[0] for o in out]), ob)
+    assert np.array_equal(np.concatenate([o[1] for o in out]), op)
