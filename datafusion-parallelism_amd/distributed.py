@@ -791,11 +791,20 @@ class DistributedHashJoin:
     def _allgather_var(self, out: torch.Tensor, offs: list[int], lens: list[int], src: torch.Tensor) -> None:
         """out[offs[d] : offs[d] + lens[d]] = rank d's src, on every rank (src may be a view
         of out)."""
-        src = src.clone()
-        if len(set(lens)) == 1 and offs == [lens[0] * d for d in range(len(lens))] and out.numel() == sum(lens):
-            dist.all_gather_into_tensor(out, src, group=self.group)
-        else:
-            dist.all_gather([out.narrow(0, o, n) for o, n in zip(offs, lens)], src, group=self.group)
+        W = len(lens)
+        if len(set(lens)) == 1 and offs == [lens[0] * d for d in range(W)] and out.numel() == sum(lens):
+            dist.all_gather_into_tensor(out, src.clone(), group=self.group)
+            return
+        # uneven pieces (the range map's shares differ by a value or so): the plain all-gather
+        # of pieces padded to the longest, then each piece to its place
+        m = max(lens)
+        pad = torch.empty(m, dtype=src.dtype, device=src.device)
+        pad[:src.numel()].copy_(src)
+        tmp = torch.empty(W * m, dtype=src.dtype, device=src.device)
+        dist.all_gather_into_tensor(tmp, pad, group=self.group)
+        for d in range(W):
+            if lens[d]:
+                out.narrow(0, offs[d], lens[d]).copy_(tmp.narrow(0, d * m, lens[d]))
 
     def _allgather_counts(self, t: torch.Tensor) -> list[int]:
         """Every rank's one-element int64 device tensor -> host list (rank order)."""

@@ -248,3 +248,45 @@ def test_broadcast_key_plan_world(case):
         assert pr.exitcode == 0
     assert all(got[r] == want for r in range(world)), (got, want)
     assert (want is None) == (case in ("sparse", "all_empty"))
+
+
+def _gather_worker(rank, world, port, lens, q):
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from datafusion_parallelism_amd.distributed import DistributedHashJoin
+
+        dj = DistributedHashJoin()
+        offs = [sum(lens[:d]) for d in range(world)]
+        out = torch.full((sum(lens),), -7, dtype=torch.int32)
+        mine = out.narrow(0, offs[rank], lens[rank])
+        mine.copy_(torch.arange(lens[rank], dtype=torch.int32) + 1000 * rank)
+        dj._allgather_var(out, offs, lens, mine)
+        counts = dj._allgather_counts(torch.tensor([rank * 11 + 3], dtype=torch.int64))
+        q.put((rank, out.numpy().copy(), counts))
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("lens", [[5, 5, 5], [6, 5, 4], [3, 0, 7], [4, 4]])
+def test_sharded_plan_gathers(lens):
+    """The sharded-build plan's collectives over gloo ranks: every rank's slice lands at its
+    offset on every rank (even slices: one all-gather; uneven ones, as the range map cuts
+    them: a padded all-gather and a copy to place), and the per-rank segment counts
+    arrive in rank order."""
+    world = len(lens)
+    want = np.concatenate([np.arange(n, dtype=np.int32) + 1000 * r for r, n in enumerate(lens)])
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gather_worker, args=(r, world, port, lens, q)) for r in range(world)]
+    for pr in procs:
+        pr.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for pr in procs:
+        pr.join(timeout=60)
+    for rank, out, counts in res:
+        assert np.array_equal(out, want), rank
+        assert counts == [r * 11 + 3 for r in range(world)]
