@@ -766,3 +766,52 @@ def test_probe_base(dfp, oracle_mod, probe_mode, base):
         assert np.array_equal(p, (op.astype(np.uint64) + base).astype(np.uint32))
         with pytest.raises(dfp.HjError):
             _probe_async_base(dfp, t, pk, 2**32 - 10)
+
+
+# ---- the range-free dense build (the partition learns the key range) -------------
+
+@pytest.mark.parametrize("case", ["aligned", "straddle", "negative", "near_min", "max_blocks", "past_blocks",
+                                  "dups_parts", "nulls"])
+def test_range_free_dense_build(dfp, oracle_mod, case):
+    """The dense build's partition bins rows by absolute 8192-value key block modulo 2048 and
+    reduces the key range itself; the table starts at the minimum rounded down to a block.
+    Key sets at the edges of that map — a minimum on / off a block boundary, negative keys,
+    keys at INT64_MIN, exactly 2048 blocks, more blocks than 2048 (the build falls back to
+    the key-range pass), several partitions with duplicates, null rows — give the oracle's
+    pairs."""
+    rng = np.random.default_rng(hash(case) & 0xFFFF)
+    n = 200_000
+    bvalid = None
+    parts = None
+    if case == "aligned":
+        bk = rng.integers(0, 8192 * 40, n) + 8192 * 7
+    elif case == "straddle":
+        bk = rng.integers(0, 8192 * 40, n) + 8192 * 7 + 5000
+    elif case == "negative":
+        bk = rng.integers(-8192 * 30 - 17, 8192 * 10, n)
+    elif case == "near_min":
+        bk = rng.integers(0, 600_000, n) + I64_MIN
+        bk[:3] = [I64_MIN, I64_MIN, I64_MIN + 1]
+    elif case == "max_blocks":  # [al, al + 2048 blocks): the last block ends the range
+        lo = 8192 * 3 + 100
+        bk = rng.integers(lo, 8192 * 3 + 2048 * 8192, 2_100_000)
+        bk[:2] = [lo, 8192 * 3 + 2048 * 8192 - 1]
+    elif case == "past_blocks":  # 2049 blocks: the key-range pass path
+        lo = 8192 * 3 + 100
+        bk = rng.integers(lo, 8192 * 3 + 2049 * 8192, 2_100_000)
+        bk[:2] = [lo, 8192 * 3 + 2049 * 8192 - 1]
+    elif case == "dups_parts":
+        bk = rng.integers(1000, 1000 + 50_000, n)
+        parts = [0, 50_000, 50_000, 120_000, n]
+    else:
+        bk = rng.integers(-5000, 300_000, n)
+        bvalid = rng.random(n) > 0.1
+    bk = bk.astype(np.int64)
+    span = int(bk.max()) - int(bk.min()) + 1
+    plo = max(int(bk.min()) - 50, int(I64_MIN))
+    pk = np.concatenate([rng.choice(bk, 300_000), rng.integers(plo, int(bk.min()) + span + 50, 300_000)])
+    pk = pk.astype(np.int64)
+    b, p, st = gpu_join(dfp, bk, pk, bvalid=bvalid, parts=parts)
+    assert st["buckets"] == 0, "a direct-addressed table"
+    ob, op = oracle_mod.inner_join(bk, pk, None if bvalid is None else np.asarray(bvalid, bool))
+    assert_same(b, p, ob, op)
