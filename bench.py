@@ -671,13 +671,16 @@ class DistJob:
         self.kernel_desc = ("one-pass region partition (both sides) + RCCL point-to-point exchange + local build + "
                             "sliced probe with global ids")
         self._pending = None
-        # the next join's plan (key range + host read) on its own stream, as SingleGpuJoin's
-        # builds: the inputs are resident before the timed steps, so step k + 1's plan is read
-        # while step k's probe runs instead of idling the device behind it
+        # the plan (key range + host read) and the build side (partition, exchange, local
+        # build) on their own stream, as SingleGpuJoin's builds: the inputs are resident
+        # before the timed steps, so step k + 1's plan is read while step k's probe runs, and
+        # the build side runs beside the probe side's partition
+        self.bstream = None
         if not same_stream:
             from datafusion_parallelism_amd.distributed import concurrent_stream
 
-            dj.prepare_stream = concurrent_stream(dev)
+            # the plan and the build side on their own stream, beside the probe side's partition
+            self.bstream = concurrent_stream(dev)
 
     pipelined = True  # step k is collected (its pair count read) after step k + 1 is enqueued
 
@@ -685,7 +688,8 @@ class DistJob:
         ev = {k: torch.cuda.Event(enable_timing=True) for k in ("start", "partitioned", "exchanged", "end")}
         self.dj.events = ev
         ev["start"].record()
-        table, result = self.dj.join(self.bk, self.bbase, self.pk, self.pbase, self.cap, check=False)
+        table, result = self.dj.join(self.bk, self.bbase, self.pk, self.pbase, self.cap, check=False,
+                                     build_stream=self.bstream)
         ev["end"].record()
         self.dj.events = None
         prev, self._pending = self._pending, (table, result, ev)

@@ -607,31 +607,38 @@ class DistributedHashJoin:
         return self.local_build_fn(bk, bi)
 
     def join(self, build_keys: torch.Tensor, build_base: int, probe_keys: torch.Tensor, probe_base: int,
-             capacity_hint: int | None = None, check: bool = True):
+             capacity_hint: int | None = None, check: bool = True, build_stream: torch.cuda.Stream | None = None):
         """The radix plan, one pass per side: plan (one host read), both sides partitioned
         into per-destination regions, ONE count exchange for both (one host read), the
         build side's regions exchanged and built (asynchronously: a direct-addressed build
         overlaps the probe side's exchange), the probe side's exchanged and probed once.
+        build_stream: the plan and the build side (partition, exchange, local build) run
+        there, beside the probe side's partition on the current stream; the probe waits for
+        the table only (its build event).
         -> (table, result): result() waits and yields this rank's pairs (canonical for
         its keys); close the table afterwards."""
         ev = self.events  # optional stage events (bench): partitioned, exchanged
-        plan = self.prepare(build_keys, probe_keys, build_base)
-        # build ids leave the partition as int64 (the table's id type: no widening pass; the
-        # build side is the small one, 4 more bytes per row on the wire)
-        bk_r, bi_r, bc, bcap = self._partition(build_keys, build_base, torch.int64, plan.key_offset, plan.spec)
-        # each side's counts travel and are read as soon as its partition ends: the host
-        # waits for the build side's counts while the probe side's partition runs, and for the
-        # probe side's while the build runs, so the device does not idle on either read
-        mb = _count_matrix_async(bc, self.group)
+        cur = torch.cuda.current_stream(probe_keys.device) if probe_keys.is_cuda else None
+        bside = torch.cuda.stream(build_stream) if build_stream is not None else contextlib.nullcontext()
+        with bside:
+            plan = self.prepare(build_keys, probe_keys, build_base)
+            # build ids leave the partition as int64 (the table's id type: no widening pass; the
+            # build side is the small one, 4 more bytes per row on the wire)
+            bk_r, bi_r, bc, bcap = self._partition(build_keys, build_base, torch.int64, plan.key_offset, plan.spec)
+            # each side's counts travel and are read as soon as its partition ends: the host
+            # waits for the build side's counts while the probe side's partition runs, and for the
+            # probe side's while the build runs, so the device does not idle on either read
+            mb = _count_matrix_async(bc, self.group)
         pk_r, pi_r, pc, pcap = self._partition(probe_keys, probe_base, torch.int32, plan.key_offset, plan.spec)
         mp = _count_matrix_async(pc, self.group)
         if ev is not None:
             ev["partitioned"].record()
-        (bk, bi), _ = exchange_regions([bk_r, bi_r], bcap, mb(), self.group)
-        bi = bi.to(torch.int64) if bi.dtype != torch.int64 else bi
-        if check and plan.build_rows is not None:
-            check_ids(bi, plan.build_rows, "received build ids")
-        table = self._local_table(bk, bi, plan)
+        with bside:
+            (bk, bi), _ = exchange_regions([bk_r, bi_r], bcap, mb(), self.group)
+            bi = bi.to(torch.int64) if bi.dtype != torch.int64 else bi
+            if check and plan.build_rows is not None:
+                check_ids(bi, plan.build_rows, "received build ids")
+            table = self._local_table(bk, bi, plan)
         (pk, pi), works = exchange_regions([pk_r, pi_r], pcap, mp(), self.group, async_op=True)
         for wk in works:
             if wk is not None:
