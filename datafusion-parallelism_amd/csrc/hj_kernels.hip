@@ -2038,23 +2038,32 @@ sl_lookup_kernel(TableView tv, uint32_t wlog, uint32_t nslices, int64_t ntiles, 
     __shared__ unsigned long long s_mask[kSlThreads / 64][W / 64];
     const uint32_t item = DFP_ABL(128) ? blockIdx.x : xcd_item(blockIdx.x, gridDim.x);
     const uint32_t s = item % nslices, part = item / nslices;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     uint32_t sbase = 0;  // hashed: first bucket of the slice
+    // the slice's image: whole 1 KB pieces by LDS DMA (global_load_lds_dwordx4, one wave
+    // instruction per piece, every piece of a wave in flight at once, no VGPR round trip),
+    // the rest (a table's last partial piece) by ordinary loads
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    auto dma = [&](const uint4* src, uint32_t nq) {  // nq uint4 of src -> s_tab
+        const uint32_t npieces = nq >> 6;
+        for (uint32_t c = (uint32_t)wave; c < npieces; c += kSlThreads / 64)
+            __builtin_amdgcn_global_load_lds(
+                (const __attribute__((address_space(1))) void*)(src + c * 64 + lane),
+                (__attribute__((address_space(3))) void*)(reinterpret_cast<uint4*>(s_tab) + c * 64), 16, 0, 0);
+        return npieces << 6;
+    };
     if constexpr (HASHED) {
         sbase = (soff + s) << kHsSliceLog;
         const uint32_t nbk = min<uint32_t>(1u << kHsSliceLog, tv.nb - sbase);
         const uint4* src = reinterpret_cast<const uint4*>(tv.tbl + sbase);
         uint4* dst = reinterpret_cast<uint4*>(s_tab);
-        for (uint32_t i = threadIdx.x; i < nbk * 4; i += kSlThreads) dst[i] = src[i];
+        for (uint32_t i = dma(src, nbk * 4) + threadIdx.x; i < nbk * 4; i += kSlThreads) dst[i] = src[i];
     } else {
         const uint64_t base = (uint64_t)s << wlog;
         const uint32_t len = (uint32_t)min<uint64_t>(1u << wlog, tv.drange - base);
-        const uint32_t len4 = len & ~3u;
         const uint32_t* __restrict__ dense = tv.dense;
         // dense is 256-byte aligned and slices start at multiples of 64 KB
-        for (uint32_t i = threadIdx.x * 4; i < len4; i += kSlThreads * 4)
-            *reinterpret_cast<uint4*>(s_tab + i) = *reinterpret_cast<const uint4*>(dense + base + i);
-        if (threadIdx.x < (len & 3u)) s_tab[len4 + threadIdx.x] = dense[base + len4 + threadIdx.x];
+        const uint32_t done = dma(reinterpret_cast<const uint4*>(dense + base), len >> 2) * 4;
+        for (uint32_t i = done + threadIdx.x; i < len; i += kSlThreads) s_tab[i] = dense[base + i];
     }
     __syncthreads();
     // part boundaries on 64-tile blocks (the transposed bounds' granule)
