@@ -23,14 +23,14 @@ PROBE_KERNELS = ("probe_fused_kernel", "probe_lookup_kernel", "probe_emit_kernel
                  "scan_down_kernel<unsigned long long>", "pp_partition_kernel", "pp_lookup_kernel",
                  "pp_count_kernel", "sl_partition_kernel", "hs_partition_kernel", "sl_toff_transpose_kernel", "sl_lookup_kernel",
                  "sl_count_kernel", "sl_emit_kernel")
-BUILD_KERNELS = ("key_minmax_kernel", "minmax_final_kernel", "coarse_hist_kernel", "coarse_scatter", "fine_hist_kernel",
+BUILD_KERNELS = ("key_minmax_kernel", "key_minmax_part_kernel", "minmax_final_kernel", "coarse_hist_kernel", "coarse_scatter", "fine_hist_kernel",
                  "fine_scatter", "chunk_starts_kernel", "scan_reduce_kernel<unsigned int>",
                  "scan_down_kernel<unsigned int>", "chunk_build_kernel", "dup_sort_big_kernel", "sl_partition_kernel",
                  "sl_toff_transpose_kernel", "dense_frag_build_kernel", "hs_partition_kernel", "hashed_frag_build_kernel")
 
 
 # kernels that run in both phases (the dense build reuses the sliced probe's partition):
-# in dispatch order, the launch after a key_minmax_kernel belongs to the build
+# in dispatch order, the launches between a key-range kernel and the build's last kernel belong to the build
 SHARED = ("sl_partition_kernel", "sl_toff_transpose_kernel", "hs_partition_kernel")
 
 
@@ -40,7 +40,7 @@ def per_kernel(path):
     in_build = False
     for r in rows:
         name = r["Kernel_Name"]
-        if "key_minmax_kernel" in name:
+        if "key_minmax" in name:  # key_minmax_part_kernel (the build's) or key_minmax_kernel
             in_build = True
         elif any(k in name for k in ("dense_frag_build_kernel", "hashed_frag_build_kernel", "dup_sort_big_kernel",
                                      "chunk_build_kernel")):
