@@ -70,6 +70,7 @@ SIGNATURES = [
     ("hj_build_finish", I32, [P, I32]),
     ("hj_build_key_range", I32, [P, I64, I64]),
     ("hj_build_key_base", I32, [P, I64]),
+    ("hj_build_dense", I32, [P]),
     ("hj_table_dense_piece", I32, [P, PP, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_int64), PP, PP,
                                    ctypes.POINTER(ctypes.c_int)]),
     ("hj_table_dense_export", I32, [P, P, U64, U64, P, U64, P, P]),

@@ -274,6 +274,7 @@ struct hj_table {
     int64_t dmin = 0;
     uint64_t drange = 0;
     bool has_range = false;     // hj_build_key_range: the caller's key range replaces the reduction
+    bool force_dense = false;   // hj_build_dense: direct-addressed over that range whatever the density
     int64_t range_lo = 0, range_hi = 0;
     bool has_base = false;      // hj_build_key_base: int32 build keys are offsets from key_base;
     int64_t key_base = 0;       // the built (direct-addressed) table is keyed in the int64 domain
@@ -369,7 +370,7 @@ hj_status build_attempt(hj_table* t, const std::vector<Segment>& segs, double lf
     // layout: a dense key range gets the direct-addressed table (one u32 ref per key value)
     ChunkGeom g{};
     bool dense = false;
-    if (minmax || (t->has_range && total > 0 && build_mode() == 0)) {
+    if (minmax || (t->has_range && total > 0 && (build_mode() == 0 || t->force_dense))) {
         int64_t mm[2] = {t->range_lo, t->range_hi};
         if (minmax) {
             int64_t* mb = t->res.h_minmax;
@@ -383,7 +384,8 @@ hj_status build_attempt(hj_table* t, const std::vector<Segment>& segs, double lf
         if (mm[0] <= mm[1]) {
             const uint64_t range = (uint64_t)mm[1] - (uint64_t)mm[0] + 1;
             const uint64_t nch = (range + (1u << kDenseShift) - 1) >> kDenseShift;
-            if (range != 0 && range <= kDenseFactor * (uint64_t)total && nch <= (uint64_t)kMaxChunks) {
+            if (range != 0 && (range <= kDenseFactor * (uint64_t)total || t->force_dense) &&
+                nch <= (uint64_t)kMaxChunks) {
                 dense = true;
                 const bool packed = (uint64_t)(2 * total + 2) < (1ull << 27);  // every dup_rows offset fits
                 g = ChunkGeom{0, 0, (uint32_t)nch, kDenseShift, mm[0], 1, packed ? 1 : 0};
@@ -1356,6 +1358,18 @@ hj_status hj_build_key_range(hj_table* t, int64_t key_lo, int64_t key_hi) {
     t->has_range = true;
     t->range_lo = key_lo;
     t->range_hi = key_hi;
+    return HJ_OK;
+}
+
+hj_status hj_build_dense(hj_table* t) {
+    if (t == nullptr) return fail(HJ_ERR_INVALID, "null table");
+    if (t->multi != nullptr) return fail(HJ_ERR_INVALID, "hj_build_dense: not for a multi-GPU table");
+    std::lock_guard<std::mutex> g(t->mu);
+    if (t->built || t->arrived > 0) return fail(HJ_ERR_INVALID, "hj_build_dense: after the barrier started");
+    if (!t->has_range) return fail(HJ_ERR_INVALID, "hj_build_dense: needs hj_build_key_range first");
+    if ((uint64_t)t->range_hi - (uint64_t)t->range_lo >= ((uint64_t)kMaxChunks << kDenseShift))
+        return fail(HJ_ERR_INVALID, "hj_build_dense: key range beyond the direct-addressed layout");
+    t->force_dense = true;
     return HJ_OK;
 }
 

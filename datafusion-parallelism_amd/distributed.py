@@ -125,10 +125,11 @@ class GpuLocalTable:
     fit 31 bits and ascend, HJ_IDS_U31) and asynchronous probes of received chunks."""
 
     def __init__(self, build_keys: torch.Tensor, build_ids: torch.Tensor, ids_u31: bool | None = None,
-                 key_range: tuple[int, int] | None = None):
+                 key_range: tuple[int, int] | None = None, dense: bool = False):
         """ids_u31: the caller knows the ids ascend and are < 2^31 (DistributedHashJoin:
         stable partition, ranks in order, global build side < 2^31 rows); None checks.
-        key_range: every build key lies in it (hj_build_key_range: no key-range reduction)."""
+        key_range: every build key lies in it (hj_build_key_range: no key-range reduction);
+        dense: direct-addressed over key_range whatever the density (hj_build_dense)."""
         dev = build_keys.device
         kt = "int64" if build_keys.dtype == torch.int64 else "int32"
         # received build ids ascend (stable partition, ranks in order): when they also
@@ -142,6 +143,8 @@ class GpuLocalTable:
         self.table.append(0, build_keys, ids=build_ids, ids_u31=u31)
         if key_range is not None and nbi:
             self.table.key_range(*key_range)
+            if dense:
+                self.table.dense()
         self.table.finish(0)
         self.device = dev
 
@@ -750,7 +753,8 @@ class DistributedHashJoin:
         used = torch.zeros(1, dtype=torch.int64, device=dev)
         local = None
         if bk.numel() and lens[me]:
-            local = GpuLocalTable(bk, bi, ids_u31=True, key_range=rngs[me])
+            # direct-addressed whatever the piece's density: a sparse piece exports refs too
+            local = GpuLocalTable(bk, bi, ids_u31=True, key_range=rngs[me], dense=True)
             local.table.dense_export(refs=mine, dup_used=used, stream=bs.cuda_stream)
         elif lens[me]:
             mine.fill_(-1)  # no build rows in this range: every ref kMiss

@@ -161,6 +161,10 @@ class HashTable:
         the build skips its key-range reduction."""
         check(self._L.hj_build_key_range(self._h, int(lo), int(hi)))
 
+    def dense(self) -> None:
+        """hj_build_dense: direct-addressed over the key_range whatever the density."""
+        check(self._L.hj_build_dense(self._h))
+
     def key_base(self, base: int) -> None:
         """hj_build_key_base: this int32 table's build keys are offsets from `base`; once
         built, the table is keyed by base + offset and takes int64 probe keys (a

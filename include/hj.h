@@ -150,6 +150,12 @@ hj_status hj_build_finish(hj_table* t, int partition);
  * reference sizes its table from the row count, new_map_3.rs:162). */
 hj_status hj_build_key_range(hj_table* t, int64_t key_lo, int64_t key_hi);
 
+/* Optional, after hj_build_key_range and before the barrier: the table takes the
+ * direct-addressed layout over that key range whatever its density (a sparse piece of the
+ * sharded-build plan still exports refs, hj_table_dense_export). The range must fit the
+ * direct-addressed layout (< 2^28 values). */
+hj_status hj_build_dense(hj_table* t);
+
 /* The build keys (an HJ_INT32 table) are int32 offsets v from key_base: the table is keyed
  * by key_base + v in the int64 domain, and once built it takes int64 keys in every probe
  * and lookup. Only a direct-addressed table can be re-keyed this way (it stores no keys,

@@ -35,6 +35,9 @@ def _keys(kind, rng, nb, np_):
     elif kind == "clustered":  # build keys at both ends of the range: middle pieces empty
         bk = np.concatenate([rng.integers(0, 1000, nb // 2), rng.integers(7 * nb, 7 * nb + 1000, nb - nb // 2)])
         pk = rng.integers(-10, 7 * nb + 1010, np_)
+    elif kind == "sparse_piece":  # one piece holds a handful of rows over its whole key range
+        bk = np.concatenate([rng.integers(0, 1000, nb - 7), rng.integers(7 * nb, 7 * nb + 1000, 7)])
+        pk = np.concatenate([rng.choice(bk, np_ // 2), rng.integers(-10, 7 * nb + 1010, np_ - np_ // 2)])
     else:
         bk = rng.integers(0, nb + nb // 2, nb) + off
         pk = rng.integers(-1000, nb * 2, np_) + off
@@ -143,7 +146,7 @@ def _threaded_join(world, comm, rank, bk, pk, out, errs):
 
 
 @pytest.mark.parametrize("world", [2, 4, 8])
-@pytest.mark.parametrize("kind", ["dense", "dups", "clustered"])
+@pytest.mark.parametrize("kind", ["dense", "dups", "clustered", "sparse_piece"])
 def test_sharded_build_threads(dfp, oracle_mod, world, kind):
     rng = np.random.default_rng(world * 10 + len(kind))
     bk, pk = _keys(kind, rng, 120_000, 400_000)
