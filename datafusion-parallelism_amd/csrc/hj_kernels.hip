@@ -3629,11 +3629,13 @@ hipError_t launch_probe_sliced(int key_bytes, const TableView& tv, const void* k
                             : (const void*)sl_lookup_kernel<false, kSlOwnWin>;
     e = hipFuncSetAttribute(lk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)tab_lds);
     if (e != hipSuccess) return e;
-    // (slice, tile range) work items: about 1024 of them, so that the resident workgroups
-    // (one per CU at 128 KB slices) run several rounds and the tail stays short
+    // (slice, tile range) work items: about 768 of them, so that the resident workgroups
+    // (one per CU at 128 KB slices) run several rounds and the tail stays short; more items
+    // load each slice image more often (profiles/r03_lookup_items.txt: C2 768 vs 1024 items
+    // +0.5 % in three alternating pairs, C3 +0.7 %, C2h the same one part per slice)
     static const uint32_t target = [] {
         const char* ev = getenv("DFP_HJ_SLICED_ITEMS");
-        return ev ? (uint32_t)std::max(1, atoi(ev)) : 1024u;
+        return ev ? (uint32_t)std::max(1, atoi(ev)) : 768u;
     }();
     for (uint32_t pass = 0; pass < npass; ++pass) {
         const uint32_t s0 = pass * (uint32_t)kSlMaxSlices;
