@@ -389,6 +389,26 @@ def _spawn_ranks(n: int) -> int:
     return rc
 
 
+def _median(xs):
+    return round(float(np.median(xs)), 4) if xs else None
+
+
+def stage_fields(job) -> dict:
+    """Per-step stage times of a job's timed steps (medians, ms): build_ms (the device build
+    span: the local build, or the multi-GPU build side - plan, exchange, local build,
+    gathers - on its stream), probe_ms, exchange_ms, and host_ms_per_step (host time
+    inside the join call per step; None for a job that does not record it)."""
+    return {"build_ms": _median(job.build_ms), "probe_ms": _median(job.probe_ms),
+            "exchange_ms": _median(getattr(job, "exchange_ms", [])),
+            "host_ms_per_step": _median(getattr(job, "host_ms", []))}
+
+
+def _clear_stage_lists(job) -> None:
+    for name in ("probe_ms", "build_ms", "exchange_ms", "host_ms", "step_ms"):
+        if hasattr(job, name):
+            getattr(job, name).clear()
+
+
 class DryRunJob:
     """--dry-run: the launcher, rendezvous, timing and reporting skeleton on the CPU (gloo),
     with a stand-in step (no GPU, no join): for tests of the multi-rank plumbing on a
@@ -398,16 +418,26 @@ class DryRunJob:
     pipelined = False
 
     def __init__(self):
-        self.probe_ms, self.build_ms, self.exchange_ms = [], [], []
+        self.probe_ms, self.build_ms, self.exchange_ms, self.host_ms = [], [], [], []
         self.matches = 0
-        self.x = torch.arange(1 << 16, dtype=torch.int64)
+        g = torch.Generator().manual_seed(1)
+        self.bk = torch.randint(0, 1 << 20, (1 << 16,), generator=g)
+        self.pk = torch.randint(0, 1 << 21, (1 << 17,), generator=g)
 
     def step(self):
+        # stand-ins timed like the real jobs' stages: a "build" (sort of the build keys) and
+        # a "probe" (binary search of the probe keys); host time = the whole step call
+        h0 = time.perf_counter()
         t0 = time.perf_counter()
-        self.matches = int((self.x & 1).sum())
-        self.probe_ms.append((time.perf_counter() - t0) * 1e3)
-        self.build_ms.append(0.0)
+        sk, _ = torch.sort(self.bk)
+        t1 = time.perf_counter()
+        pos = torch.searchsorted(sk, self.pk).clamp_(max=sk.numel() - 1)
+        self.matches = int((sk[pos] == self.pk).sum())
+        t2 = time.perf_counter()
+        self.build_ms.append((t1 - t0) * 1e3)
+        self.probe_ms.append((t2 - t1) * 1e3)
         self.exchange_ms.append(0.0)
+        self.host_ms.append((time.perf_counter() - h0) * 1e3)
 
     def collect(self):
         pass
@@ -424,6 +454,7 @@ def dry_run(args, json_out):
     job = DryRunJob()
     for _ in range(args.warmup):
         job.step()
+    _clear_stage_lists(job)
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
@@ -442,7 +473,8 @@ def dry_run(args, json_out):
                           "warmup": args.warmup, "ms_per_step": round(float(el.item()) / args.steps * 1e3, 4),
                           "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "int64",
                           "data": "dry-run (CPU, gloo: launcher and timing skeleton only, not a measurement)",
-                          "ranks_reporting": int(ranks.item()), "config": {"workload": "dry run"}}),
+                          "ranks_reporting": int(ranks.item()), "config": {"workload": "dry run"},
+                          **stage_fields(job)}),
               file=json_out, flush=True)
     if world > 1:
         dist.destroy_process_group()
@@ -543,8 +575,7 @@ def main():
                 job.collect()
         torch.cuda.synchronize(dev)
         job.collect()
-        job.probe_ms.clear()
-        job.build_ms.clear()
+        _clear_stage_lists(job)
         # the local job's steps overlap one step's host work with the previous step's
         # device work (SingleGpuJoin.step); the exchange jobs synchronize inside a step
         barrier()
@@ -645,6 +676,10 @@ def main():
         if use_dist:
             line["exchange_ms"] = round(float(np.median(job.exchange_ms)), 4)
             line["plan"] = plan
+            line["host_ms_per_step"] = _median(getattr(job, "host_ms", []))
+            line["build_ms_source"] = ("HIP events on the build stream around the build side (plan, exchange, "
+                                       "local build" + (", table gathers)" if plan == "sharded" else ")"))
+            line["probe_ms_source"] = "HIP events on the probe stream, launch to end (with any wait for its table)"
         if weak is not None:
             line["weak"] = weak
         print(json.dumps(line), file=json_out, flush=True)
@@ -665,7 +700,7 @@ class DistJob:
         self.dj, self.bk, self.pk, self.dev = dj, bk, pk, dev
         self.bbase = bbase
         self.pbase = pbase
-        self.probe_ms, self.build_ms, self.exchange_ms = [], [], []
+        self.probe_ms, self.build_ms, self.exchange_ms, self.host_ms, self.step_ms = [], [], [], [], []
         self.matches = 0
         self.cap = pk.numel()
         self.kernel_desc = ("one-pass region partition (both sides) + RCCL point-to-point exchange + local build + "
@@ -681,15 +716,22 @@ class DistJob:
 
             # the plan and the build side on their own stream, beside the probe side's partition
             self.bstream = concurrent_stream(dev)
+        # the inputs exist once this event fires: the build stream waits for it, not for
+        # the previous step's probe on the current stream
+        self.ready = torch.cuda.Event()
+        self.ready.record()
 
     pipelined = True  # step k is collected (its pair count read) after step k + 1 is enqueued
 
     def step(self):
-        ev = {k: torch.cuda.Event(enable_timing=True) for k in ("start", "partitioned", "exchanged", "end")}
+        ev = {k: torch.cuda.Event(enable_timing=True)
+              for k in ("start", "build_start", "build_end", "partitioned", "exchanged", "probe_start", "end")}
         self.dj.events = ev
         ev["start"].record()
+        h0 = time.perf_counter()
         table, result = self.dj.join(self.bk, self.bbase, self.pk, self.pbase, self.cap, check=False,
-                                     build_stream=self.bstream)
+                                     build_stream=self.bstream, inputs_ready=self.ready)
+        self.host_ms.append((time.perf_counter() - h0) * 1e3)
         ev["end"].record()
         self.dj.events = None
         prev, self._pending = self._pending, (table, result, ev)
@@ -706,9 +748,11 @@ class DistJob:
         b, _ = result()
         self.matches = int(b.numel())
         ev["end"].synchronize()
-        self.probe_ms.append(ev["start"].elapsed_time(ev["end"]))
+        # both probe events on the probe's (current) stream; the build span on the build stream
+        self.probe_ms.append(ev["probe_start"].elapsed_time(ev["end"]))
+        self.step_ms.append(ev["start"].elapsed_time(ev["end"]))
         self.exchange_ms.append(ev["partitioned"].elapsed_time(ev["exchanged"]))
-        self.build_ms.append(0.0)
+        self.build_ms.append(ev["build_start"].elapsed_time(ev["build_end"]))
         table.close()
 
     def finish(self):
@@ -728,7 +772,7 @@ class ShardedJob:
 
     def __init__(self, dj, bk, pk, bbase, pbase, dev):
         self.dj, self.bk, self.pk, self.bbase, self.pbase, self.dev = dj, bk, pk, bbase, pbase, dev
-        self.probe_ms, self.build_ms, self.exchange_ms = [], [], []
+        self.probe_ms, self.build_ms, self.exchange_ms, self.host_ms = [], [], [], []
         self.matches = 0
         self.cap = pk.numel()
         from datafusion_parallelism_amd.distributed import concurrent_stream
@@ -737,13 +781,18 @@ class ShardedJob:
         self.kernel_desc = ("sharded build: range exchange of the build side (RCCL), local build of the rank's key "
                             "range, all_gather of the table pieces, sliced probe of the local rows")
         self._pending = None
+        self.ready = torch.cuda.Event()  # the inputs exist: the build stream waits for this only
+        self.ready.record()
 
     def step(self):
-        ev = {k: torch.cuda.Event(enable_timing=True) for k in ("partitioned", "exchanged", "start", "end")}
+        ev = {k: torch.cuda.Event(enable_timing=True)
+              for k in ("build_start", "partitioned", "exchanged", "build_end", "probe_start", "end")}
         self.dj.events = ev
         cur = torch.cuda.current_stream(self.dev)
+        h0 = time.perf_counter()
         table, result = self.dj.join_sharded(self.bk, self.bbase, self.pk, self.pbase, self.cap,
-                                             build_stream=self.bstream)
+                                             build_stream=self.bstream, inputs_ready=self.ready)
+        self.host_ms.append((time.perf_counter() - h0) * 1e3)
         self.dj.events = None
         ev["end"].record(cur)
         prev, self._pending = self._pending, (table, result, ev)
@@ -759,9 +808,11 @@ class ShardedJob:
         b, _ = result()
         self.matches = int(b.numel())
         ev["end"].synchronize()
+        # the build side (plan, exchange, local build, gathers) on the build stream; the
+        # probe from its launch to its end on the probe stream (with any wait for the table)
         self.exchange_ms.append(ev["partitioned"].elapsed_time(ev["exchanged"]))
-        self.probe_ms.append(ev["exchanged"].elapsed_time(ev["end"]))
-        self.build_ms.append(0.0)
+        self.build_ms.append(ev["build_start"].elapsed_time(ev["build_end"]))
+        self.probe_ms.append(ev["probe_start"].elapsed_time(ev["end"]))
         table.close()
 
     def finish(self):
@@ -783,7 +834,7 @@ class BroadcastJob:
 
     def __init__(self, dj, bk, pk, pbase, dev):
         self.dj, self.bk, self.pk, self.pbase, self.dev = dj, bk, pk, pbase, dev
-        self.probe_ms, self.build_ms, self.exchange_ms = [], [], []
+        self.probe_ms, self.build_ms, self.exchange_ms, self.host_ms = [], [], [], []
         self.matches = 0
         n = pk.numel()
         self.ws = torch.empty(HashTable.workspace_bytes(n), dtype=torch.uint8, device=dev)
@@ -822,6 +873,7 @@ class BroadcastJob:
         ev = self.evs[self.k & 1]
         slot = self.k & 1
         self.k += 1
+        h0 = time.perf_counter()
         with torch.cuda.stream(self.cstream):
             ev[0].record(self.cstream)
             # the global key range (hj_key_minmax + one all-reduce; the host waits for this
@@ -845,6 +897,7 @@ class BroadcastJob:
         t.probe_async(self.pk.data_ptr(), self.pk.numel(), self.ob.data_ptr(), self.op.data_ptr(), self.cap,
                       self.d_total.data_ptr(), self.ws.data_ptr(), cur.cuda_stream, probe_base=self.pbase)
         ev[3].record(cur)
+        self.host_ms.append((time.perf_counter() - h0) * 1e3)
         self.collect()
         self.prev = (t, ev)
 

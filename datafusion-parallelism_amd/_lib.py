@@ -87,6 +87,8 @@ SIGNATURES = [
     ("hj_probe_workspace_bytes", I64, [I64]),
     ("hj_set_probe_mode", I32, [I32]),
     ("hj_set_build_mode", I32, [I32]),
+    ("hj_set_device_budget", I64, [I64]),
+    ("hj_table_device_bytes", I32, [P, ctypes.POINTER(ctypes.c_int64)]),
     ("hj_probe_async", I32, [P, P, P, I64, I64, P, P, I64, P, P, P]),
     ("hj_probe_async_ids", I32, [P, P, P, I64, P, I64, P, P, I64, P, P, P]),
     ("hj_probe_async_base", I32, [P, P, P, I64, I64, U32, P, P, I64, P, P, P]),

@@ -218,6 +218,23 @@ int build_mode_raw() {
 // histogram + scan + staged-scatter partition for it (the tile-local one is the default)
 int build_mode() { return build_mode_raw() == 1 ? 1 : 0; }
 bool frag_build_mode() { return build_mode_raw() == 0; }
+// Per-table device budget in bytes (0 = none): a one-device table whose build would hold
+// more than this (staged input, table, duplicate segments, build scratch) refuses with
+// HJ_ERR_OOM, the signal for a planner to shard the build over several GPUs. Stands in
+// for the capacity of one GPU's HBM (C5: a build side larger than one GPU). Set with
+// hj_set_device_budget or DFP_HJ_DEVICE_BUDGET_BYTES.
+std::atomic<int64_t> g_budget{-1};
+int64_t device_budget() {
+    int64_t b = g_budget.load(std::memory_order_relaxed);
+    if (b < 0) {
+        const char* e = getenv("DFP_HJ_DEVICE_BUDGET_BYTES");
+        b = e ? std::max<int64_t>(0, atoll(e)) : 0;
+        int64_t unset = -1;
+        g_budget.compare_exchange_strong(unset, b, std::memory_order_relaxed);
+        b = g_budget.load(std::memory_order_relaxed);
+    }
+    return b;
+}
 double load_factor() {
     const char* e = getenv("DFP_HJ_LOAD_FACTOR");
     double lf = e ? atof(e) : kDefaultLoadFactor;
@@ -290,6 +307,9 @@ struct hj_table {
     // multi-GPU facade: shards on several devices behind this handle (hj_build_begin_multi)
     MultiTable* multi = nullptr;
     std::vector<std::tuple<int, void*, size_t>> multi_bufs;  // (device, block, bytes) the shards borrow
+    // device bytes the table holds (allocs + scratch) and their peak: the device budget's
+    // measure (hj_set_device_budget)
+    int64_t live_bytes = 0, peak_bytes = 0;
 };
 
 namespace {
@@ -313,16 +333,26 @@ hipError_t wait_mailbox(int64_t* mm, int64_t seq, const int64_t* d_minmax, hipSt
 
 hj_status dev_alloc(hj_table* t, std::vector<std::pair<void*, size_t>>& list, void** p, size_t bytes) {
     if (bytes == 0) bytes = 64;
+    const int64_t budget = device_budget();
+    if (budget > 0 && t->live_bytes + (int64_t)bytes > budget)
+        return fail(HJ_ERR_OOM, "device budget: this build needs more than " + std::to_string(budget) +
+                                    " bytes of one device (DFP_HJ_DEVICE_BUDGET_BYTES / hj_set_device_budget); "
+                                    "shard it over several GPUs (hj_build_begin_multi, radix plan)");
     hipError_t e;
     *p = cache_alloc(t->device, bytes, &e);
     if (*p == nullptr) return fail(HJ_ERR_OOM, std::string("device allocation: ") + hipGetErrorString(e));
     list.emplace_back(*p, bytes);
+    t->live_bytes += (int64_t)bytes;
+    t->peak_bytes = std::max(t->peak_bytes, t->live_bytes);
     return HJ_OK;
 }
 
 // only once no queued work uses the blocks any more
 void free_list(hj_table* t, std::vector<std::pair<void*, size_t>>& list) {
-    for (auto& pb : list) cache_free(t->device, pb.first, pb.second);
+    for (auto& pb : list) {
+        cache_free(t->device, pb.first, pb.second);
+        t->live_bytes -= (int64_t)pb.second;
+    }
     list.clear();
 }
 
@@ -1285,6 +1315,18 @@ hj_status hj_build_append(hj_table* t, int partition, const void* keys, const ui
         hs.voff = validity_offset;
         hs.ids = ids;
     } else {
+        // staged copies count toward the device budget
+        const int64_t staged = n * t->key_bytes + (validity ? (((validity_offset & 7) + n + 7) >> 3) : 0) +
+                               (ids ? n * 8 : 0);
+        {
+            std::lock_guard<std::mutex> g(t->mu);
+            const int64_t budget = device_budget();
+            if (budget > 0 && t->live_bytes + staged > budget)
+                return fail(HJ_ERR_OOM, "device budget: staging this build input exceeds " + std::to_string(budget) +
+                                            " bytes of one device (DFP_HJ_DEVICE_BUDGET_BYTES); shard the build");
+            t->live_bytes += staged;
+            t->peak_bytes = std::max(t->peak_bytes, t->live_bytes);
+        }
         void* dk = nullptr;
         HIP_TRY(hipMalloc(&dk, (size_t)n * t->key_bytes));
         hs.owned.push_back(dk);
@@ -1549,6 +1591,25 @@ int hj_set_build_mode(int mode) {
     const int old = build_mode_raw();
     g_build_mode.store(mode, std::memory_order_relaxed);
     return old;
+}
+
+int64_t hj_set_device_budget(int64_t bytes) {
+    const int64_t old = device_budget();
+    g_budget.store(bytes < 0 ? 0 : bytes, std::memory_order_relaxed);
+    return old;
+}
+
+hj_status hj_table_device_bytes(const hj_table* t, int64_t* peak_per_device) {
+    if (t == nullptr || peak_per_device == nullptr) return fail(HJ_ERR_INVALID, "null table/out");
+    if (t->multi) {  // the largest shard: each shard is one device's table
+        int64_t mx = 0;
+        for (const hj_table* sh : t->multi->shards)
+            if (sh != nullptr) mx = std::max(mx, sh->peak_bytes);
+        *peak_per_device = mx;
+        return HJ_OK;
+    }
+    *peak_per_device = t->peak_bytes;
+    return HJ_OK;
 }
 
 int hj_set_probe_mode(int mode) {

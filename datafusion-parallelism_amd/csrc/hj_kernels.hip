@@ -2706,6 +2706,7 @@ constexpr int kRpTile = kRpThreads * kRpIters;  // rows per tile
 constexpr int kRpSlots = kRpIters * (kRpThreads / 64);  // (iteration, wave) counts per destination
 static_assert(kRpSlots % 64 == 0, "the per-destination scan gives each lane whole slots");
 constexpr unsigned kRpSpinLimit = 1u << 22;
+constexpr unsigned long long kRpPoison = 1ull << 60;  // offset published by a tile whose look-back gave up
 // diagnostic builds only (tools/lib_variants.py with DFP_HJ_ABLATIONS, DFP_RP_ABL; wrong output): 1 no look-back wait, 2 no
 // stores, 4 no ids. The wait costs about half the kernel (355 -> 180 us for 10^8 rows
 // with the filter); batching 2-16 look-back windows per flag round trip, longer spin
@@ -2796,6 +2797,7 @@ part_regions_kernel(const void* __restrict__ keys, const uint8_t* __restrict__ v
         bool done = t == 0;
         int64_t j0 = t - 1;  // window: tiles j0 - k
         unsigned spins = 0;
+        bool failed = false;
         while (__ballot(!done) != 0) {
             const int64_t j = j0 - k;
             unsigned long long f = kFlagIncl;  // before tile 0: an inclusive zero
@@ -2810,6 +2812,7 @@ part_regions_kernel(const void* __restrict__ keys, const uint8_t* __restrict__ v
             if (__ballot(wait) != 0) {
                 if (++spins > kRpSpinLimit) {  // never expected: report, do not hang
                     if (lane == 0) atomicOr(err, 1ull);
+                    failed = true;
                     break;
                 }
                 __builtin_amdgcn_s_sleep(1);
@@ -2821,6 +2824,11 @@ part_regions_kernel(const void* __restrict__ keys, const uint8_t* __restrict__ v
             if (incl_m) done = true;
             j0 -= per;
         }
+        // a tile that gave up publishes a poisoned offset (>= 2^60 rows): its own rows are
+        // not stored (pos >= cap), every later tile's offset and the region counts come out
+        // above any region size, and hj_partition_regions' contract makes a count above
+        // region_rows the caller's error signal (the error word says the same)
+        if (failed) excl = kRpPoison;
         if (k == 0) {
             if (t > 0) flag_store(flags + t * nparts + d, kFlagIncl | (excl + tot));
             s_off[d] = excl;

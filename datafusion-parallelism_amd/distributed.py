@@ -367,6 +367,21 @@ def _exchange_cols(cols: list[torch.Tensor], m: list[list[int]], group=None, asy
     return outs, []
 
 
+def check_counts(m: list[list[int]], cap: int, me: int = 0) -> None:
+    """A region partition's counts (count matrix m: row s = rank s's counts) must be sane
+    before anything is exchanged: hj_partition_regions reports a failed look-back (never
+    expected) by counts of 2^60 or more, and a count above the region size means rows were
+    not written. This rank's row is checked against its own region size `cap`, every row
+    against the poison bound (each rank sees the same matrix, so all ranks raise together
+    instead of exchanging wrong regions)."""
+    for s, row in enumerate(m):
+        for d, c in enumerate(row):
+            if c < 0 or c >= 1 << 59 or (s == me and c > cap):
+                raise HjError(_lib.HJ_ERR_HIP, f"region partition of rank {s}: count {c} for destination {d} "
+                                               f"outside [0, {cap if s == me else '2^59'}] (device look-back "
+                                               f"failure or region overflow)")
+
+
 def exchange_regions(cols: list[torch.Tensor], cap: int, m: list[list[int]], group=None, async_op: bool = False):
     """Exchange per-destination regions (gpu_partition_regions' layout) with point-to-point
     sends and receives (RCCL ncclSend/ncclRecv in one group; xGMI links are point to point,
@@ -377,6 +392,7 @@ def exchange_regions(cols: list[torch.Tensor], cap: int, m: list[list[int]], gro
     split from the count matrix)."""
     me = dist.get_rank(group)
     world = len(m)
+    check_counts(m, cap, me)
     recv = [m[s][me] for s in range(world)]
     if world == 1:
         return [c[:recv[0]] for c in cols], []
@@ -498,7 +514,11 @@ class DistributedHashJoin:
         self.chunks = max(1, int(chunks))
         self.compress_keys = compress_keys
         self.runtime_filter = runtime_filter
-        self.events: dict | None = None  # {"partitioned", "exchanged"}: torch.cuda.Event recorded by join()
+        # optional stage events (bench): torch.cuda.Event objects recorded by join() /
+        # join_sharded() when present: "build_start" / "build_end" bracket the build side on
+        # its stream, "partitioned" / "exchanged" the exchange, "probe_start" the probe's
+        # launch on the probe stream
+        self.events: dict | None = None
         # prepare()'s key-range reads and its host read run on this stream when set. Only for
         # callers whose build keys are complete with respect to it (inputs resident before a
         # pipeline of joins starts): the next join's plan is then read while the previous
@@ -558,6 +578,13 @@ class DistributedHashJoin:
             plan.key_offset = gmin + 2**31
         return plan
 
+    def _mark(self, name: str, stream=None) -> None:
+        """Record stage event `name` (if the caller asked for it) on `stream` (default: the
+        current stream)."""
+        ev = self.events
+        if ev is not None and name in ev:
+            ev[name].record(stream)
+
     def _partition(self, keys: torch.Tensor, id_base: int, id_dtype: torch.dtype, key_offset: int | None,
                    spec: PartSpec | None = None):
         """-> per-destination regions (keys, ids, counts, cap) of gpu_partition_regions."""
@@ -609,21 +636,38 @@ class DistributedHashJoin:
                                  key_range=plan.local_key_range(self.rank, self.world))
         return self.local_build_fn(bk, bi)
 
+    @staticmethod
+    def _order_build_stream(build_stream, cur, inputs_ready) -> None:
+        """The side stream must not read the inputs before their producers wrote them: it
+        waits for `inputs_ready` (an event the caller recorded after producing the keys),
+        else for everything enqueued on the current stream so far (safe, but it then also
+        waits for a previous join's probe there)."""
+        if build_stream is None or cur is None:
+            return
+        if inputs_ready is not None:
+            build_stream.wait_event(inputs_ready)
+        else:
+            build_stream.wait_stream(cur)
+
     def join(self, build_keys: torch.Tensor, build_base: int, probe_keys: torch.Tensor, probe_base: int,
-             capacity_hint: int | None = None, check: bool = True, build_stream: torch.cuda.Stream | None = None):
+             capacity_hint: int | None = None, check: bool = True, build_stream: torch.cuda.Stream | None = None,
+             inputs_ready: torch.cuda.Event | None = None):
         """The radix plan, one pass per side: plan (one host read), both sides partitioned
         into per-destination regions, ONE count exchange for both (one host read), the
         build side's regions exchanged and built (asynchronously: a direct-addressed build
         overlaps the probe side's exchange), the probe side's exchanged and probed once.
         build_stream: the plan and the build side (partition, exchange, local build) run
         there, beside the probe side's partition on the current stream; the probe waits for
-        the table only (its build event).
+        the table only (its build event). The side stream first waits for `inputs_ready`
+        (recorded by the caller once the keys exist), or without it for the current stream.
         -> (table, result): result() waits and yields this rank's pairs (canonical for
         its keys); close the table afterwards."""
         ev = self.events  # optional stage events (bench): partitioned, exchanged
         cur = torch.cuda.current_stream(probe_keys.device) if probe_keys.is_cuda else None
+        self._order_build_stream(build_stream, cur, inputs_ready)
         bside = torch.cuda.stream(build_stream) if build_stream is not None else contextlib.nullcontext()
         with bside:
+            self._mark("build_start")
             plan = self.prepare(build_keys, probe_keys, build_base)
             # build ids leave the partition as int64 (the table's id type: no widening pass; the
             # build side is the small one, 4 more bytes per row on the wire)
@@ -642,12 +686,14 @@ class DistributedHashJoin:
             if check and plan.build_rows is not None:
                 check_ids(bi, plan.build_rows, "received build ids")
             table = self._local_table(bk, bi, plan)
+            self._mark("build_end")
         (pk, pi), works = exchange_regions([pk_r, pi_r], pcap, mp(), self.group, async_op=True)
         for wk in works:
             if wk is not None:
                 wk.wait()
         if ev is not None:
             ev["exchanged"].record()
+        self._mark("probe_start")
         result = self._probe_chunk(table, pk, pi, [], capacity_hint)
         return table, result
 
@@ -702,14 +748,19 @@ class DistributedHashJoin:
         """The sharded-build plan needs a direct-addressed build domain split by key range
         (prepare's range map; one rank: the whole range), build ids held in place of rows
         (< 2^31 rows) and every piece's segment offsets, rebased, inside the packed refs'
-        27 bits (2·B + 2·G + 2 < 2^27)."""
+        27 bits (2·B + 2·G + 2 < 2^27). The gathered table is one direct-addressed array
+        over the whole build key range, so that range must also be within the widest
+        direct-addressed range (DENSE_MAX_RANGE, as broadcast_key_plan requires): a wider
+        one would be refused by hj_table_wrap_dense after the exchange."""
         if plan.build_lo is None or plan.build_rows is None or plan.build_id_dtype != torch.int32:
             return False
-        dense = (plan.build_hi - plan.build_lo + 1) <= 8 * plan.build_rows
+        rng = plan.build_hi - plan.build_lo + 1
+        dense = rng <= DENSE_FACTOR * plan.build_rows and rng <= DENSE_MAX_RANGE
         return dense and (world == 1 or plan.spec.by_range) and 2 * plan.build_rows + 2 * world + 2 < 2**27
 
     def join_sharded(self, build_keys: torch.Tensor, build_base: int, probe_keys: torch.Tensor, probe_base: int,
-                     capacity_hint: int | None = None, build_stream: torch.cuda.Stream | None = None):
+                     capacity_hint: int | None = None, build_stream: torch.cuda.Stream | None = None,
+                     inputs_ready: torch.cuda.Event | None = None):
         """The sharded-build broadcast plan: the build side goes through the radix plan's
         range partition and exchange, each rank builds the direct-addressed table of its
         own contiguous key range (global build ids in place of rows), the ranks all-gather
@@ -720,22 +771,22 @@ class DistributedHashJoin:
         the broadcast plan's whole build and B·4 bytes of keys. The ranks' outputs in rank
         order are the canonical output. build_stream: the build side (plan, partition,
         exchange, local build, gather) runs there and the probe on the current stream
-        waits for the gathered table only. Falls back to run_broadcast's shape (whole
+        waits for the gathered table only (the side stream first waits for `inputs_ready`,
+        or without it for the current stream). Falls back to run_broadcast's shape (whole
         build per rank) when sharded_ok is false.
         -> (table, result): result() waits and yields this rank's pairs; close the table
         afterwards."""
         cur = torch.cuda.current_stream(probe_keys.device)
+        self._order_build_stream(build_stream, cur, inputs_ready)
         bs = build_stream or cur
-        ev = self.events  # optional (bench): "partitioned" / "exchanged" = start / end of the build side
         with torch.cuda.stream(bs):
-            if ev is not None:
-                ev["partitioned"].record(bs)
+            self._mark("build_start", bs)
             plan = self.prepare(build_keys, probe_keys, build_base)
             if not self.sharded_ok(plan, self.world):
                 return self._broadcast_table(build_keys, probe_keys, probe_base, capacity_hint, bs, cur)
             table = self._gather_pieces(build_keys, build_base, plan, probe_keys.dtype, bs)
-            if ev is not None:
-                ev["exchanged"].record(bs)
+            self._mark("build_end", bs)
+        self._mark("probe_start", cur)
         result = self._probe_own(table, probe_keys, probe_base, capacity_hint, cur)
         return table, result
 
@@ -743,7 +794,9 @@ class DistributedHashJoin:
         dev = build_keys.device
         W, me = self.world, self.rank
         bk_r, bi_r, bc, bcap = self._partition(build_keys, build_base, torch.int64, plan.key_offset, plan.spec)
+        self._mark("partitioned", bs)
         bk, bi = self._exchange_build(bk_r, bi_r, bc, bcap)
+        self._mark("exchanged", bs)
         # every rank's key range, as the partition's range map cut it (they tile the domain)
         rngs = [plan.local_key_range(d, W) for d in range(W)]
         lens = [0 if r is None else r[1] - r[0] + 1 for r in rngs]
@@ -795,6 +848,7 @@ class DistributedHashJoin:
         """The build side's regions to their owners -> (keys, ids) this rank received."""
         if self.world == 1:
             n = int(host_read_async(bc)()[0])
+            check_counts([[n]], bcap)
             return bk_r[:n], bi_r[:n]
         (bk, bi), _ = exchange_regions([bk_r, bi_r], bcap, _count_matrix(bc, self.group), self.group)
         return bk, bi
@@ -862,17 +916,21 @@ class DistributedHashJoin:
     def _broadcast_table(self, build_keys, probe_keys, probe_base, capacity_hint, bs, cur):
         """Fallback of join_sharded: every rank builds the whole gathered build side."""
         dev = build_keys.device
+        self._mark("partitioned", bs)
         sizes = gather_sizes(build_keys.numel(), dev, self.group)
         if self.world > 1:
             g = torch.empty(sum(sizes), dtype=build_keys.dtype, device=dev)
             dist.all_gather(list(torch.split(g, sizes)), build_keys, group=self.group)
         else:
             g = build_keys
+        self._mark("exchanged", bs)
         table = HashTable(1, "int64" if g.dtype == torch.int64 else "int32", dev.index or 0)
         table.append(0, g)
         table.finish(0)
         table._keep.append(g)
+        self._mark("build_end", bs)
         with torch.cuda.stream(cur):
+            self._mark("probe_start", cur)
             result = self._probe_own(table, probe_keys, probe_base, capacity_hint, cur)
         return table, result
 

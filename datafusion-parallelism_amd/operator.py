@@ -209,9 +209,11 @@ class GpuIndexLookup:
 class _SharedBuild:
     """State shared by all partitions of one build (JoinStateInstances)."""
 
-    def __init__(self, parallelism: int, device: int):
+    def __init__(self, parallelism: int, device: int, devices: Sequence[int] | None = None, plan: str = "auto"):
         self.parallelism = parallelism
-        self.device = device
+        self.device = devices[0] if devices else device
+        self.devices = list(devices) if devices else None
+        self.plan = plan
         self.lock = threading.Lock()
         self.table: HashTable | None = None
         self.key_type: str | None = None
@@ -230,7 +232,10 @@ class _SharedBuild:
         with self.lock:
             if self.table is None:
                 self.key_type = key_type
-                self.table = HashTable(self.parallelism, key_type, self.device)
+                # one table on one GPU, or one table over a node's GPUs (hj_build_begin_multi:
+                # broadcast or radix shards behind the same build / probe calls)
+                self.table = HashTable(self.parallelism, key_type, self.device, devices=self.devices,
+                                       plan=self.plan)
             elif key_type != self.key_type:
                 raise HjError(HJ_ERR_INVALID, "all build batches must have the same key type")
             return self.table
@@ -249,6 +254,9 @@ class _SharedBuild:
                     ncol = len(parts[0][0])
                     cols = [DeviceColumn.concat([p[0][j] for p in parts]) for j in range(ncol)]
                     self.record_batch = DeviceRecordBatch(schema, cols, sum(p[1] for p in parts))
+                    # the per-batch columns are no longer needed (the table keeps the key
+                    # tensors it borrows alive itself): drop them, keep the row counts
+                    self.batches = [[(None, n) for _, n in part] for part in self.batches]
                 else:
                     dev = torch.device("cuda", self.device)
                     empty = [DeviceColumn.from_arrow(pa.array([], type=f.type), dev) for f in schema]
@@ -268,13 +276,21 @@ class BuildImplementation:
     """src/operator/build_implementation.rs:20-112 with the `Gpu` arm only."""
 
     def __init__(self, build_implementation_version: JoinReplacement, parallelism: int,
-                 input_schema: pa.Schema | None = None, device: int = 0):
+                 input_schema: pa.Schema | None = None, device: int = 0, devices: Sequence[int] | None = None,
+                 plan: str = "auto"):
+        """devices: build one table over these GPUs of the node (hj_build_begin_multi;
+        DataFusion runs every partition in one process, so the in-process multi-GPU table
+        is the drop-in's node-wide form); plan "auto" | "broadcast" | "radix" (the build
+        side sharded by key hash, 1/G per GPU: builds larger than one GPU). Batches and
+        probe keys live on devices[0]; the table moves rows to the other GPUs itself."""
         if build_implementation_version is not JoinReplacement.Gpu:
             raise NotImplementedError(
                 f"{build_implementation_version} is one of the reference's CPU strategies; this package "
                 "implements JoinReplacement.Gpu")
+        if devices is not None and len(devices) < 1:
+            raise HjError(HJ_ERR_INVALID, "devices must name at least one GPU")
         self.parallelism = parallelism
-        self._shared = _SharedBuild(parallelism, device)
+        self._shared = _SharedBuild(parallelism, device, devices, plan)
         self._shared.schema = input_schema
 
     def build_side(self, partition: int, stream: Iterable[pa.RecordBatch], build_expressions: Sequence[str | int],
@@ -469,7 +485,8 @@ class ParallelHashJoin:
     def __init__(self, left: list[list[pa.RecordBatch]], right: list[list[pa.RecordBatch]],
                  on: Sequence[tuple[str, str]], join_type: JoinType | str = JoinType.Inner, device: int = 0,
                  replacement: JoinReplacement = JoinReplacement.Gpu, filter: JoinFilter | None = None,
-                 right_schema: pa.Schema | None = None):
+                 right_schema: pa.Schema | None = None, devices: Sequence[int] | None = None, plan: str = "auto"):
+        """devices / plan: one build table over several GPUs (BuildImplementation)."""
         if len(on) < 1:
             raise HjError(HJ_ERR_INVALID, "an equi-join needs at least one (left, right) key pair")
         self.join_type = JoinType.parse(join_type)
@@ -480,7 +497,7 @@ class ParallelHashJoin:
         self.on = list(on)
         self.filter = filter
         self.right_schema = right_schema or next((b.schema for part in self.right for b in part), None)
-        self._build = BuildImplementation(replacement, n, device=device)
+        self._build = BuildImplementation(replacement, n, device=device, devices=devices, plan=plan)
         self._finalizer = _Finalizer(n)
 
     def execute(self, partition: int) -> list[pa.RecordBatch]:

@@ -103,6 +103,17 @@ def _producer_stream(keys, device: int) -> int | None:
     return None
 
 
+def set_device_budget(nbytes: int) -> int:
+    """hj_set_device_budget: per-table device byte budget of later builds (0 = none); a
+    one-device build above it raises HjError(HJ_ERR_OOM). -> the previous budget."""
+    return _lib.load().hj_set_device_budget(int(nbytes))
+
+
+def is_budget_error(e: Exception) -> bool:
+    """The HjError a build raises when it exceeds the device budget."""
+    return isinstance(e, _lib.HjError) and e.status == _lib.HJ_ERR_OOM and "device budget" in str(e)
+
+
 class HashTable:
     """One shared build table for `parallelism` partitions (hj_build_begin .. finish)."""
 
@@ -217,6 +228,13 @@ class HashTable:
     def build_ns(self) -> int:
         """Device time of the build (HIP events), no device work."""
         return self._L.hj_table_build_ns(self._h)
+
+    def device_bytes(self) -> int:
+        """Peak device bytes the build held (the device budget's measure; a multi-GPU
+        table: its largest shard's)."""
+        v = ctypes.c_int64()
+        check(self._L.hj_table_device_bytes(self._h, ctypes.byref(v)))
+        return v.value
 
     def stats(self) -> dict:
         s = _lib.HjTableStats()

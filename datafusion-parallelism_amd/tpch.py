@@ -295,6 +295,41 @@ def multi_join(devices: list[int], plan: str = "radix"):
     return join
 
 
+def planned_join(devices: list[int], plan: str = "radix"):
+    """A join_fn that builds each join on one GPU while its build fits the device budget
+    (hj_set_device_budget / DFP_HJ_DEVICE_BUDGET_BYTES), and shards a build that does not
+    over `devices` with the radix plan (every shard a one-device table of about 1/G of the
+    build): C5's premise, a build side larger than one GPU, at any scale. join.log records
+    one (build rows, "one-gpu" | plan, peak device bytes of the table) per join."""
+    from ._lib import HjError
+    from .table import is_budget_error
+
+    log: list[tuple[int, str, int]] = []
+
+    def join(build: torch.Tensor, probe: torch.Tensor):
+        dev = probe.device
+        try:
+            with HashTable(1, "int64", dev.index or 0) as t:
+                t.build(build.contiguous())
+                peak = t.device_bytes()
+                b, p = t.probe(probe.contiguous(), device_output=True)
+            log.append((int(build.numel()), "one-gpu", peak))
+            return b, p.to(torch.int64)
+        except HjError as e:
+            if not is_budget_error(e):
+                raise
+        with HashTable(1, "int64", devices=list(devices), plan=plan) as t:
+            t.append(0, build.contiguous())
+            t.finish(0)
+            peak = t.device_bytes()
+            b, p = t.probe(probe.contiguous(), device_output=True)
+        log.append((int(build.numel()), plan, peak))
+        return b, p.to(torch.int64)
+
+    join.log = log
+    return join
+
+
 def q9(t: Tables, color_flag: str = "green", join_fn=None) -> list[tuple[str, int, int]]:
     """-> [(nation, o_year, sum_profit in 1e-4 units)] ordered by nation, o_year desc.
     join_fn: as q3's."""

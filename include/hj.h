@@ -144,9 +144,11 @@ hj_status hj_build_finish(hj_table* t, int partition);
 /* Optional, before the barrier: every valid build key lies in [key_lo, key_hi] (the caller
  * knows the range, e.g. from an exchange plan's global min/max). The build then skips its
  * key-range reduction and the host's wait for it, and takes its layout from this range
- * (direct-addressed when it spans at most 8x the build rows). A key outside the range may
- * be lost (a direct-addressed table has no slot for it): the caller's guarantee is the
- * contract. New (the
+ * (direct-addressed when it spans at most 8x the build rows). The caller's guarantee is the
+ * contract and is not checked on the device: a valid build key outside [key_lo, key_hi]
+ * is UNDEFINED BEHAVIOUR (the direct-addressed build indexes its histograms and the table
+ * by key - key_lo, so such a key can write out of bounds). Pass a range derived from the
+ * keys themselves (hj_key_minmax, or an exchange plan's global min/max). New (the
  * reference sizes its table from the row count, new_map_3.rs:162). */
 hj_status hj_build_key_range(hj_table* t, int64_t key_lo, int64_t key_hi);
 
@@ -295,6 +297,22 @@ int hj_set_probe_mode(int mode);
  * settable with DFP_HJ_DENSE=0 (hashed) and DFP_HJ_FRAG_BUILD=0 (mode 2). */
 int hj_set_build_mode(int mode);
 
+/* Per-table device budget for later builds of this process, in bytes (0 = none; also
+ * DFP_HJ_DEVICE_BUDGET_BYTES). A one-device table whose build would hold more device
+ * memory than this - staged input copies, the table, duplicate segments and the build's
+ * scratch - fails its hj_build_append / hj_build_finish with HJ_ERR_OOM ("device budget"),
+ * so that a planner can shard the build over several GPUs instead (hj_build_begin_multi,
+ * HJ_MULTI_RADIX: every shard is a one-device table of about 1/G of the build, each under
+ * the budget). It stands in for one GPU's HBM capacity when a build side larger than one
+ * GPU (BASELINE configs[4], the reference's SF300 Q9 on 8 GPUs) is rehearsed at a smaller
+ * scale. Returns the previous budget. New (the reference's CPU build grows its tables
+ * without bound, new_map_3.rs:325-411). */
+int64_t hj_set_device_budget(int64_t bytes);
+
+/* Peak device bytes a built table held during its build (the budget's measure); for a
+ * multi-GPU table, the largest shard's. */
+hj_status hj_table_device_bytes(const hj_table* t, int64_t* peak_per_device);
+
 /* Makes `stream` wait for the build of `t` (for probes on other streams). */
 hj_status hj_table_stream_wait(const hj_table* t, void* stream);
 
@@ -347,7 +365,11 @@ hj_status hj_partition_rows(hj_key_type key_type, const void* keys,
  * tiles gives each tile's offset in each region), and a region is a contiguous send
  * buffer for one peer, so no grouped copy precedes the exchange. counts[d] is exact even
  * when it exceeds region_rows (rows past the region are not written): region_rows >= n
- * always suffices. workspace: hj_partition_regions_workspace_bytes(n, nparts). */
+ * always suffices. workspace: hj_partition_regions_workspace_bytes(n, nparts).
+ * Failure on the device: a tile whose look-back wait exceeds its spin limit (never
+ * expected) sets the error word (workspace bytes 8..15) and makes every affected count
+ * >= 2^60, so a caller that reads the counts for its exchange must treat any count above
+ * n as an error (the Python plans raise HJ_ERR_HIP); the output is then invalid. */
 int64_t hj_partition_regions_workspace_bytes(int64_t n, int nparts);
 hj_status hj_partition_regions(hj_key_type key_type, const void* keys,
                                const uint8_t* validity, int64_t validity_offset,

@@ -25,6 +25,18 @@ def test_gpus_2_without_launcher_spawns_two_ranks():
     assert d["n_gpus"] == 2 and d["ranks_reporting"] == 2
     assert d["steps"] == 2 and d["warmup"] == 1
     assert "dry-run" in d["data"]
+    # the stage fields the N > 1 lines carry: a measured build span (no literal 0.0) and
+    # the host time per step
+    assert d["build_ms"] is not None and d["build_ms"] > 0
+    assert d["probe_ms"] is not None and d["probe_ms"] > 0
+    assert d["host_ms_per_step"] is not None and d["host_ms_per_step"] > 0
+
+
+def test_no_literal_zero_build_ms():
+    """No job in bench.py appends a placeholder build time."""
+    with open(os.path.join(ROOT, "bench.py")) as f:
+        src = f.read()
+    assert "build_ms.append(0.0)" not in src
 
 
 def test_world_size_mismatch_is_an_error():

@@ -200,6 +200,45 @@ def test_choose_plan():
     assert DistributedHashJoin.choose_plan(10**7, 10**8, 1) == "broadcast"
 
 
+def test_check_counts_rejects_poisoned_counts():
+    """A failed look-back in hj_partition_regions makes counts >= 2^60: every rank raises
+    (poison bound on every row); a rank's own count above its region size raises too."""
+    from datafusion_parallelism_amd import HjError
+    from datafusion_parallelism_amd.distributed import check_counts
+
+    check_counts([[3, 4], [10, 0]], 7, me=0)  # rank 1's 10 is within its own (larger) region
+    with pytest.raises(HjError):
+        check_counts([[3, 4], [-1, 0]], 7, me=0)
+    with pytest.raises(HjError):
+        check_counts([[3, 4], [1 << 60, 0]], 7, me=0)
+    with pytest.raises(HjError):
+        check_counts([[3, 9]], 7, me=0)
+
+
+def test_sharded_ok_boundaries():
+    """sharded_ok: a direct-addressed build domain within the widest dense range
+    (DENSE_MAX_RANGE), u32 build ids and packed segment offsets; a range one value past
+    DENSE_MAX_RANGE (dense by the 8 x rows criterion) takes the fallback instead of an
+    exchange whose gathered table hj_table_wrap_dense would refuse."""
+    from datafusion_parallelism_amd.distributed import (DENSE_MAX_RANGE, DistributedHashJoin, ExchangePlan,
+                                                        PartSpec)
+
+    def plan(rng, rows, by_range=True, ids=torch.int32):
+        return ExchangePlan(build_id_dtype=ids, spec=PartSpec(by_range, 0, rng - 1), build_rows=rows,
+                            build_lo=0, build_hi=rng - 1)
+
+    ok = DistributedHashJoin.sharded_ok
+    rows = 40_000_000  # 8 x rows > DENSE_MAX_RANGE, 2 x rows + 2G + 2 < 2^27
+    assert ok(plan(DENSE_MAX_RANGE, rows), 8)
+    assert not ok(plan(DENSE_MAX_RANGE + 1, rows), 8)
+    assert ok(plan(8 * 1000, 1000), 4) and not ok(plan(8 * 1000 + 1, 1000), 4)  # density
+    assert not ok(plan(1000, 1000, by_range=False), 2) and ok(plan(1000, 1000, by_range=False), 1)
+    assert not ok(plan(1000, 1000, ids=torch.int64), 2)
+    big = (2**27 - 2 * 8 - 2) // 2  # packed refs: 2B + 2G + 2 < 2^27
+    assert ok(plan(big, big - 1), 8) and not ok(plan(big, big), 8)
+    assert not ok(ExchangePlan(), 1)  # empty build side
+
+
 def _plan_worker(rank, world, port, shards, rows, q):
     sys.path.insert(0, ROOT)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))

@@ -89,6 +89,57 @@ def test_operator_matches_oracle_parallel(dfp, oracle_mod):
     assert got == want
 
 
+@pytest.mark.parametrize("plan", ["radix", "broadcast"])
+def test_operator_multi_gpu_table_matches_oracle(dfp, oracle_mod, plan):
+    """ParallelHashJoin(devices=...) — the drop-in's node-wide form (one process runs every
+    partition, build_implementation.rs:34-48, parallel_hash_join.rs:140-167): the shared
+    build table of 8 concurrent partitions is one table over 4 GPUs (hj_build_begin_multi;
+    [0] * 4 on this one-GPU box), and every probe partition's batches are probed through it.
+    Joined rows equal the oracle's pairs; each probe batch's pairs come out in canonical
+    order (the multi table merges its shards' pairs)."""
+    from datafusion_parallelism_amd.operator import ParallelHashJoin
+
+    rng = np.random.default_rng(23)
+    bk = rng.integers(-3000, 4000, 24000)
+    pk = rng.integers(-5000, 6000, 30000)
+    bnull = rng.random(len(bk)) < 0.05
+    pnull = rng.random(len(pk)) < 0.03
+    build = pa.RecordBatch.from_pydict({"k": pa.array(bk, mask=bnull), "bid": np.arange(len(bk))})
+    probe = pa.RecordBatch.from_pydict({"k": pa.array(pk, mask=pnull), "pid": np.arange(len(pk))})
+    bparts = split(pa.Table.from_batches([build]).to_batches(max_chunksize=1000), 8)
+    pparts = split(pa.Table.from_batches([probe]).to_batches(max_chunksize=1000), 8)
+    join = ParallelHashJoin(bparts, pparts, on=[("k", "k")], devices=[0] * 4, plan=plan)
+    out = join.collect()
+    for rb in out:  # per batch: probe rows ascending, build rows of one probe row descending
+        pid = np.asarray(rb.column("pid"))
+        bid = np.asarray(rb.column("bid"))
+        same = pid[1:] == pid[:-1]
+        assert np.all(pid[1:] >= pid[:-1]) and np.all(bid[1:][same] < bid[:-1][same])
+    res = pa.Table.from_batches(out)
+    got = sorted(zip(res.column("bid").to_pylist(), res.column("pid").to_pylist()))
+    ob, op = oracle_mod.inner_join(bk, pk, ~bnull, ~pnull)
+    want = sorted(zip(ob.tolist(), op.tolist()))
+    assert got == want and len(got) > 0
+
+
+def test_build_implementation_multi_gpu_lookup(dfp):
+    """BuildImplementation(devices=...): get_iter on the node-wide table keeps the chain
+    order (newest first) and the partition-state rule."""
+    from datafusion_parallelism_amd import HjError
+    from datafusion_parallelism_amd.operator import BuildImplementation, JoinReplacement
+
+    class Collect:
+        def call(self, lookup, record_batch):
+            return [list(lookup.get_iter(k)) for k in (1, 2, 7)], record_batch.num_rows
+
+    bi = BuildImplementation(JoinReplacement.Gpu, 1, devices=[0, 0], plan="radix")
+    batches = [pa.RecordBatch.from_pydict({"id": pa.array(v, pa.int64())}) for v in ([1, 2, 3], [2, 4, 5], [1, 6, 7])]
+    its, n = bi.build_side(0, batches, ["id"], Collect())
+    assert its == [[6, 0], [3, 1], [8]] and n == 9  # version10/build_implementation.rs:98-178
+    with pytest.raises(HjError, match="State already consumed for partition 0"):
+        bi.build_side(0, batches, ["id"], Collect())
+
+
 def test_build_side_state_consumed(dfp):
     """src/operator/version10/build_implementation.rs:32-33: a partition's state can be
     taken once."""

@@ -34,7 +34,15 @@ def main():
     ap.add_argument("--shards", type=int, default=0,
                     help="one-GPU plans with every join on a table of this many radix shards on GPU 0 "
                          "(hj_build_begin_multi on [0] * K: C4/C5's sharded builds in one process)")
+    ap.add_argument("--budget", type=int, default=0,
+                    help="one-GPU plans under a per-table device budget in bytes (hj_set_device_budget): a join "
+                         "whose build exceeds it is sharded over --shards (default 8) radix shards on GPU 0 "
+                         "(tpch.planned_join); the line lists each join's plan and peak device bytes")
     a = ap.parse_args()
+    if a.budget:
+        from datafusion_parallelism_amd.table import set_device_budget
+
+        set_device_budget(a.budget)
     rank, world = 0, 1
     if a.dist:
         if "RANK" not in os.environ:  # one rank without a launcher
@@ -57,11 +65,18 @@ def main():
             fn = tpch.q3_dist if q == "q3" else tpch.q9_dist
         else:
             fn = tpch.q3 if q == "q3" else tpch.q9
-            if a.shards:
+            jf = None
+            if a.budget:
+                jf = tpch.planned_join([0] * (a.shards or 8))
+            elif a.shards:
                 jf = tpch.multi_join([0] * a.shards)
+            if jf is not None:
                 base = fn
                 fn = lambda tt, base=base, jf=jf: base(tt, join_fn=jf)  # noqa: E731
         r = fn(t)  # warm-up
+        if a.budget:
+            joins = [{"build_rows": n, "plan": p, "peak_device_bytes": b} for n, p, b in jf.log]
+            jf.log.clear()
         times = []
         for _ in range(a.reps):
             if a.dist:
@@ -85,7 +100,9 @@ def main():
             "what": f"TPC-H-shaped {q.upper()} on {world} GPU(s), tables resident in HBM"
                     + (" (multi-GPU plan: broadcast + RCCL shuffles)" if a.dist else ""),
             "query": q, "sf": sf, "n_gpus": world,
-            "plan": "dist" if a.dist else (f"{a.shards} radix shards on one GPU" if a.shards else "single"),
+            "plan": "dist" if a.dist else (
+                f"device budget {a.budget} B: one GPU per join, {a.shards or 8} radix shards on one GPU above it"
+                if a.budget else f"{a.shards} radix shards on one GPU" if a.shards else "single"),
             "lineitem_rows": nl,
             "query_ms_min": round(best * 1e3, 3), "query_ms_median": round(sorted(times)[len(times) // 2] * 1e3, 3),
             "lineitem_mrows_s": round(nl / best / 1e6, 1),
@@ -94,6 +111,8 @@ def main():
             line.update(groups=r.groups, top1=[r.l_orderkey[0], r.revenue[0], r.o_orderdate[0]] if r.l_orderkey else None)
         else:
             line.update(groups=len(r), first=list(r[0]) if r else None)
+        if a.budget:
+            line["joins"] = joins
         if rank == 0:
             print(json.dumps(line), flush=True)
         del t
