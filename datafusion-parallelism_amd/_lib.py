@@ -57,6 +57,13 @@ class HjPartSpec(ctypes.Structure):
     _fields_ = [("by_range", ctypes.c_int), ("key_lo", ctypes.c_int64), ("key_hi", ctypes.c_int64)]
 
 
+class HjDistInfo(ctypes.Structure):
+    _fields_ = [("build_rows", ctypes.c_int64), ("recv_rows", ctypes.c_int64), ("sharded", ctypes.c_int)]
+
+
+HJ_COMM_ID_BYTES = 128
+
+
 # (name, restype, argtypes) of every entry point declared in include/hj.h
 P, I64, I32, U32, U64 = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_uint32, ctypes.c_uint64
 PP = ctypes.POINTER(ctypes.c_void_p)
@@ -110,6 +117,10 @@ SIGNATURES = [
     ("hj_equal_pairs_workspace_bytes", I64, [I64]),
     ("hj_filter_equal_pairs", I32, [I32, ctypes.POINTER(HjKeyColumn), ctypes.POINTER(HjKeyColumn), P, P, I64, P, P,
                                     P, P, P]),
+    ("hj_comm_unique_id", I32, [P]),
+    ("hj_comm_create", I32, [I32, I32, P, I32, PP]),
+    ("hj_comm_free", None, [P]),
+    ("hj_dist_build_sharded", I32, [P, I32, P, P, I64, I64, I64, P, PP, ctypes.POINTER(HjDistInfo)]),
     ("hj_gen_perm_keys", I32, [P, I64, I64, I64, P]),
     ("hj_gen_uniform_keys", I32, [P, I64, U64, I64, P]),
     ("hj_gen_exponential_keys", I32, [P, I32, I32]),

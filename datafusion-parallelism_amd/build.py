@@ -1,7 +1,8 @@
 """Build the in-tree C-ABI library ``lib/libdfp_hj.so`` (gfx950 code objects).
 
 The kernels are compiled by ``hipcc --offload-arch=gfx950``; the host layer by g++.
-The library links the HIP runtime that PyTorch-ROCm ships (``torch/lib/libamdhip64.so``)
+The library links the HIP runtime and RCCL that PyTorch-ROCm ships (``torch/lib/libamdhip64.so``,
+``torch/lib/librccl.so``, SONAME ``librccl.so.1`` as /opt/rocm's)
 so that a process which also uses torch for device memory, streams and
 ``torch.distributed`` holds exactly one HIP/HSA runtime. (``/opt/rocm``'s runtime has
 SONAME ``libamdhip64.so.7``; torch's has none, so linking the ROCm one would load a
@@ -24,8 +25,8 @@ INCLUDE = os.path.join(os.path.dirname(HERE), "include")
 ARCH = "gfx950"
 
 SOURCES_HIP = ["hj_kernels.hip", "hj_columns.hip", "hj_keys.hip"]
-SOURCES_CPP = ["hj_api.cpp"]
-HEADERS = ["hj_device.h", "hj_launch.h", "hj_util.h"]
+SOURCES_CPP = ["hj_api.cpp", "hj_dist.cpp"]
+HEADERS = ["hj_device.h", "hj_launch.h", "hj_util.h", "hj_host.h"]
 
 
 def torch_lib_dir() -> str:
@@ -83,7 +84,7 @@ def build(force: bool = False, verbose: bool = False, defines: tuple[str, ...] =
     with ThreadPoolExecutor(max_workers=len(cmds)) as ex:
         list(ex.map(lambda c: _run(c, verbose), cmds))
     tmp = out + ".tmp"
-    _run(["g++", "-shared", "-o", tmp, *objs, f"-L{tlib}", "-lamdhip64", f"-Wl,-rpath,{tlib}",
+    _run(["g++", "-shared", "-o", tmp, *objs, f"-L{tlib}", "-lamdhip64", "-lrccl", f"-Wl,-rpath,{tlib}",
           "-Wl,--no-undefined", "-lpthread"], verbose)
     os.replace(tmp, out)
     return out

@@ -38,6 +38,7 @@
 
 #include "../../include/hj.h"
 #include "hj_device.h"
+#include "hj_host.h"
 #include "hj_launch.h"
 
 using namespace dfp;
@@ -310,7 +311,23 @@ struct hj_table {
     // device bytes the table holds (allocs + scratch) and their peak: the device budget's
     // measure (hj_set_device_budget)
     int64_t live_bytes = 0, peak_bytes = 0;
+    std::vector<hj_table*> owned_tables;  // freed with this table (hj_dist.cpp's local pieces)
 };
+
+namespace dfp {
+namespace host {
+hj_status set_error(hj_status st, const std::string& msg) { return fail(st, msg); }
+void* dev_block(int dev, size_t bytes) {
+    hipError_t e;
+    return cache_alloc(dev, bytes ? bytes : 64, &e);
+}
+void free_block(int dev, void* p, size_t bytes) { cache_free(dev, p, bytes ? bytes : 64); }
+void table_adopt_block(hj_table* t, int dev, void* p, size_t bytes) {
+    t->multi_bufs.emplace_back(dev, p, bytes ? bytes : 64);
+}
+void table_adopt_table(hj_table* t, hj_table* other) { t->owned_tables.push_back(other); }
+}  // namespace host
+}  // namespace dfp
 
 namespace {
 
@@ -1820,6 +1837,7 @@ void hj_table_free(hj_table* t) {
     free_list(t, t->scratch);
     delete t->multi;  // its shards first: they borrow multi_bufs
     for (auto& b : t->multi_bufs) cache_free(std::get<0>(b), std::get<1>(b), std::get<2>(b));
+    for (hj_table* o : t->owned_tables) hj_table_free(o);
     for (auto& part : t->parts)
         for (auto& hs : part) {
             for (void* p : hs.owned) (void)hipFree(p);

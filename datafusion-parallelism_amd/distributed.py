@@ -452,6 +452,54 @@ def all_to_all_rows(keys_by_dest: torch.Tensor, ids_by_dest: torch.Tensor, count
     return rk, ri, st
 
 
+class NativeComm:
+    """An hj_comm — RCCL behind the C ABI (hj_dist.cpp) — for the ranks of `group`: rank 0
+    makes the 128-byte unique id (hj_comm_unique_id), the group broadcasts it (the
+    out-of-band channel a Rust host would provide itself), every rank creates the
+    communicator on its GPU (hj_comm_create, collective)."""
+
+    def __init__(self, device: torch.device, group=None):
+        L = _lib.load()
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        self.device = device
+        idb = torch.zeros(_lib.HJ_COMM_ID_BYTES, dtype=torch.uint8)
+        if self.rank == 0:
+            check(L.hj_comm_unique_id(idb.data_ptr()))
+        if self.world > 1:
+            src = dist.get_global_rank(group, 0) if group is not None else 0
+            t = idb.to(device) if dist.get_backend(group) == "nccl" else idb
+            dist.broadcast(t, src=src, group=group)
+            idb = t.cpu()
+        h = ctypes.c_void_p()
+        check(L.hj_comm_create(self.rank, self.world, idb.data_ptr(), device.index or 0, ctypes.byref(h)))
+        self._h = h
+
+    def build_sharded(self, keys: torch.Tensor, build_base: int, stream: int, valid: torch.Tensor | None = None,
+                      valid_offset: int = 0):
+        """hj_dist_build_sharded on this rank's build keys (enqueued on `stream`) -> (the
+        whole build side's table, HjDistInfo)."""
+        L = _lib.load()
+        kt = HJ_INT64 if keys.dtype == torch.int64 else HJ_INT32
+        h = ctypes.c_void_p()
+        info = _lib.HjDistInfo()
+        check(L.hj_dist_build_sharded(self._h, kt, keys.data_ptr() if keys.numel() else None,
+                                      None if valid is None else valid.data_ptr(), valid_offset, keys.numel(),
+                                      build_base, stream or None, ctypes.byref(h), ctypes.byref(info)))
+        return HashTable.from_handle(h, keys.device.index or 0, kt, keep=[keys, valid]), info
+
+    def close(self):
+        if getattr(self, "_h", None):
+            _lib.load().hj_comm_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 DENSE_FACTOR = 8                 # hj_api.cpp kDenseFactor: direct-addressed when range <= 8 x rows
 DENSE_MAX_RANGE = 131071 << 11   # kMaxChunks << kDenseShift: the widest direct-addressed range
 
@@ -504,8 +552,15 @@ class DistributedHashJoin:
 
     def __init__(self, group=None, partition_fn: Callable | None = None, local_join_fn: Callable | None = None,
                  chunks: int = 1, local_build_fn: Callable | None = None, compress_keys: bool = True,
-                 runtime_filter: bool = True):
+                 runtime_filter: bool = True, native: bool | None = None):
+        """native: run the sharded-build plan's build side through hj_dist_build_sharded
+        (RCCL inside the library: one C call per step) instead of the torch.distributed
+        steps below; None = when the group's backend is nccl (RCCL) and the world is a
+        power of two."""
         self.group = group
+        self.native = native
+        self._comm: NativeComm | None = None
+        self.last_native = False  # the latest join_sharded ran the C entry point
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
         self.partition_fn = partition_fn or gpu_radix_partition
@@ -779,6 +834,17 @@ class DistributedHashJoin:
         cur = torch.cuda.current_stream(probe_keys.device)
         self._order_build_stream(build_stream, cur, inputs_ready)
         bs = build_stream or cur
+        self.last_native = self._use_native(build_keys)
+        if self.last_native:
+            # the whole build side in one C call (hj_dist_build_sharded: RCCL inside)
+            if getattr(self, "_comm", None) is None:
+                self._comm = NativeComm(build_keys.device, self.group)
+            with torch.cuda.stream(bs):
+                self._mark("build_start", bs)
+                table, _ = self._comm.build_sharded(build_keys, build_base, bs.cuda_stream)
+                self._mark("build_end", bs)
+            self._mark("probe_start", cur)
+            return table, self._probe_own(table, probe_keys, probe_base, capacity_hint, cur)
         with torch.cuda.stream(bs):
             self._mark("build_start", bs)
             plan = self.prepare(build_keys, probe_keys, build_base)
@@ -789,6 +855,22 @@ class DistributedHashJoin:
         self._mark("probe_start", cur)
         result = self._probe_own(table, probe_keys, probe_base, capacity_hint, cur)
         return table, result
+
+    def _use_native(self, build_keys: torch.Tensor) -> bool:
+        native = getattr(self, "native", None)
+        if native is not None:
+            return bool(native)
+        if not build_keys.is_cuda or self.partition_fn is not gpu_radix_partition:
+            return False
+        if type(self)._exchange_build is not DistributedHashJoin._exchange_build:  # test doubles
+            return False
+        return dist.get_backend(self.group) == "nccl" and (self.world & (self.world - 1)) == 0
+
+    def close(self) -> None:
+        """Release the native communicator (if one was made)."""
+        if self._comm is not None:
+            self._comm.close()
+            self._comm = None
 
     def _gather_pieces(self, build_keys, build_base, plan: ExchangePlan, probe_dtype, bs):
         dev = build_keys.device

@@ -356,6 +356,18 @@ class HashTable:
         self._keep = [refs, dup_rows]
         return self
 
+    @classmethod
+    def from_handle(cls, handle: ctypes.c_void_p, device: int, key_type: str | int, keep=()) -> "HashTable":
+        """Adopt a built table handle another entry point returned (hj_dist_build_sharded);
+        `keep`: tensors its build still reads, kept alive until close()."""
+        self = cls.__new__(cls)
+        self._L = _lib.load()
+        kt = key_type if isinstance(key_type, int) else (HJ_INT64 if key_type == "int64" else HJ_INT32)
+        self.key_type, self.parallelism, self.device, self.devices = kt, 1, device, None
+        self._h = handle
+        self._keep = list(keep)
+        return self
+
     @staticmethod
     def rebase_dups(refs: torch.Tensor, base: int, packed: bool, stream: int = 0) -> None:
         """hj_dense_rebase_dups on a (view of a) u32 refs tensor."""

@@ -36,7 +36,7 @@ typedef enum hj_status {
     HJ_ERR_INVALID = 1,   /* bad argument / state (DataFusionError::Internal) */
     HJ_ERR_OOM = 2,       /* device allocation failed */
     HJ_ERR_HIP = 3,       /* HIP runtime error */
-    HJ_ERR_RCCL = 4,      /* reserved for the multi-GPU exchange */
+    HJ_ERR_RCCL = 4,      /* RCCL failure in a multi-process step (hj_comm_*, hj_dist_*) */
     HJ_ERR_CAPACITY = 5,  /* output buffer too small; *count holds the size needed */
     HJ_ERR_NO_DEVICE = 6  /* no GPU: the HIP path cannot run (there is no CPU fallback) */
 } hj_status;
@@ -467,6 +467,60 @@ hj_status hj_filter_equal_pairs(int ncols, const hj_key_column* build_cols,
                                 const uint32_t* probe_idx, int64_t n, uint64_t* out_build,
                                 uint32_t* out_probe, int64_t* d_count, void* workspace,
                                 void* stream);
+
+/* ---- multi-process, one GPU per process: RCCL behind the ABI --------------------
+ * The reference runs one process; a node of GPUs driven as one process per GPU (the
+ * Rust host launching a rank per device) needs the exchange steps of the multi-GPU plans
+ * here, not in the host language. A communicator is RCCL's (ncclCommInitRank over xGMI);
+ * its 128-byte unique id is made by one rank (hj_comm_unique_id) and handed to every rank
+ * by the caller (any out-of-band channel: the launcher's store, a socket, an MPI bcast).
+ * The radix precedent is the shard function of
+ * src/utils/partitioned_concurrent_self_hash_join_map.rs:13-16; the operator seam that a
+ * per-rank plan sits behind is BuildImplementation::build_side
+ * (src/operator/build_implementation.rs:50-112). */
+typedef struct hj_comm hj_comm;
+#define HJ_COMM_ID_BYTES 128
+hj_status hj_comm_unique_id(uint8_t id[HJ_COMM_ID_BYTES]);
+/* Collective: every rank of `world` calls it with the same id; binds the communicator to
+ * `device`. */
+hj_status hj_comm_create(int rank, int world, const uint8_t id[HJ_COMM_ID_BYTES], int device,
+                         hj_comm** out);
+void hj_comm_free(hj_comm* c);
+
+typedef struct hj_dist_info {
+    int64_t build_rows;  /* global build rows (the ranks' build_base + n, max) */
+    int64_t recv_rows;   /* build rows this rank received and built */
+    int sharded;         /* 1: sharded build; 0: every rank built the whole build side */
+} hj_dist_info;
+
+/* The sharded-build plan's build side, one collective call per step on every rank.
+ * Rank r holds build rows [build_base, build_base + n) of the global build column (the
+ * ranks' ranges tile [0, B) in rank order); the returned table holds the WHOLE build side
+ * and is probed by this rank's own probe rows with hj_probe_async_base(t, ..., probe_base,
+ * ...): build_idx = global build row, probe_idx = probe_base + row, and the ranks' outputs
+ * in rank order are the single-GPU canonical output. Steps, all enqueued on `stream` (the
+ * host waits for three small reads: the plan, the count matrix, the duplicate-segment
+ * sizes):
+ *   1 global key range and build rows (hj_key_minmax, one grouped all-reduce);
+ *   2 when the build key domain is dense (range <= 8 x rows, within the direct-addressed
+ *     layout), with < 2^31 rows and a power-of-two world: every valid row to the rank that
+ *     owns its contiguous key range (hj_partition_regions by range, keys as int32 offsets
+ *     when the range spans < 2^32 values, global ids), point-to-point exchange
+ *     (ncclSend/ncclRecv in one group);
+ *   3 a direct-addressed build of the rank's own key range (global ids in place of rows),
+ *     its refs all-gathered into one array over the whole domain, the duplicate segments
+ *     all-gathered end to end and re-pointed (hj_dense_rebase_dups), wrapped as one
+ *     probe-only table (hj_table_wrap_dense);
+ *   otherwise (sparse domain, >= 2^31 rows, other worlds) every rank all-gathers the valid
+ *   build rows with their global ids and builds the whole table.
+ * Probes on any stream wait for the table by themselves. Free it with hj_table_free. The
+ * inputs must be complete in `stream`'s order. Per-call scratch is released at a later
+ * call on the same communicator once its work has finished (or at hj_comm_free). New (the
+ * reference has no multi-process path). */
+hj_status hj_dist_build_sharded(hj_comm* c, hj_key_type key_type, const void* keys,
+                                const uint8_t* validity, int64_t validity_offset, int64_t n,
+                                int64_t build_base, void* stream, hj_table** out,
+                                hj_dist_info* info);
 
 /* ---- synthetic generators of SURVEY.md §8(d) on the device (bench inputs) ----- */
 /* out[i] = (i * mul) mod range  (unique build keys when gcd(mul, range) = 1);

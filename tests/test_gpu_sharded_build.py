@@ -53,26 +53,74 @@ def _init_one_rank():
     dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
 
 
+@pytest.mark.parametrize("native", [True, False])
 @pytest.mark.parametrize("kind", ["dense", "dense_far", "dups", "sparse"])
-def test_sharded_build_one_rank(dfp, oracle_mod, kind):
+def test_sharded_build_one_rank(dfp, oracle_mod, kind, native):
+    """native: the build side through the C entry point hj_dist_build_sharded (RCCL inside
+    the library, the path a Rust host drives); else the torch.distributed steps."""
     from datafusion_parallelism_amd.distributed import DistributedHashJoin
 
     _init_one_rank()
+    dj = None
     try:
         rng = np.random.default_rng(11)
         bk, pk = _keys(kind, rng, 150_000, 500_000)
-        dj = DistributedHashJoin()
+        dj = DistributedHashJoin(native=native)
         side = torch.cuda.Stream()
-        table, result = dj.join_sharded(torch.from_numpy(bk).cuda(), 0, torch.from_numpy(pk).cuda(), 7,
-                                        build_stream=side)
+        for _ in range(2):  # the second step reuses the communicator (and its deferred scratch)
+            table, result = dj.join_sharded(torch.from_numpy(bk).cuda(), 0, torch.from_numpy(pk).cuda(), 7,
+                                            build_stream=side)
+            assert dj.last_native == native
+            try:
+                b, p = result()
+            finally:
+                table.close()
+            ob, op = oracle_mod.inner_join(bk, pk)
+            assert np.array_equal(b.cpu().numpy().astype(np.uint64), ob)
+            assert np.array_equal(p.cpu().numpy().astype(np.uint32), op + 7)
+    finally:
+        if dj is not None:
+            dj.close()
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("kind", ["dense", "dups", "sparse"])
+@pytest.mark.parametrize("key_type", ["int64", "int32"])
+def test_native_build_sharded_nulls_and_base(dfp, oracle_mod, kind, key_type):
+    """hj_dist_build_sharded directly (one rank): a validity bitmap with an offset, a
+    nonzero build_base (global ids = base + row), int32 and int64 keys; the table probed
+    with hj_probe_async_base equals the oracle with the ids shifted."""
+    from datafusion_parallelism_amd import HashTable
+    from datafusion_parallelism_amd.distributed import NativeComm
+
+    _init_one_rank()
+    comm = None
+    try:
+        rng = np.random.default_rng(5)
+        bk, pk = _keys(kind, rng, 100_000, 300_000)
+        if key_type == "int32":
+            if kind == "sparse":
+                bk, pk = (bk % (2**31)).astype(np.int32), (pk % (2**31)).astype(np.int32)
+            else:
+                bk, pk = bk.astype(np.int32), pk.astype(np.int32)
+        valid = rng.random(bk.size + 3) > 0.1  # bit 3 is row 0
+        bits = torch.from_numpy(np.packbits(valid, bitorder="little")).cuda()
+        comm = NativeComm(torch.device("cuda", 0))
+        s = torch.cuda.current_stream()
+        table, info = comm.build_sharded(torch.from_numpy(bk).cuda(), 1000, s.cuda_stream, valid=bits,
+                                         valid_offset=3)
+        assert info.build_rows == 1000 + bk.size and info.sharded == (kind != "sparse")
         try:
-            b, p = result()
+            b, p = table.probe(torch.from_numpy(pk).cuda(), device_output=True)
+            assert isinstance(table, HashTable)
         finally:
             table.close()
-        ob, op = oracle_mod.inner_join(bk, pk)
-        assert np.array_equal(b.cpu().numpy().astype(np.uint64), ob)
-        assert np.array_equal(p.cpu().numpy().astype(np.uint32), op + 7)
+        ob, op = oracle_mod.inner_join(bk, pk, valid[3:], None)
+        assert np.array_equal(b.cpu().numpy().astype(np.uint64), ob + 1000)
+        assert np.array_equal(p.cpu().numpy().astype(np.uint32), op)
     finally:
+        if comm is not None:
+            comm.close()
         dist.destroy_process_group()
 
 

@@ -9,7 +9,7 @@ export TMPDIR=/tmp
 O=gpurun_out/r04s1; mkdir -p $O
 step() { local t=$1; shift; echo "== $*"; timeout -k 10 $t "$@" || { echo "FAILED($?): $*"; exit 1; }; }
 PT="python3 -u -m pytest -x -q --timeout 300 --timeout-method thread"
-step 600 $PT tests/test_gpu_operator.py tests/test_gpu_tpch.py -k "budget or multi_gpu or sf300" > $O/new_tests.log 2>&1
+step 600 $PT tests/test_gpu_sharded_build.py tests/test_gpu_operator.py tests/test_gpu_tpch.py -k "budget or multi_gpu or sf300 or one_rank or native" > $O/new_tests.log 2>&1
 tail -2 $O/new_tests.log
 step 900 $PT tests -m gpu > $O/tests.log 2>&1
 tail -2 $O/tests.log
