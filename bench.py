@@ -504,6 +504,9 @@ def main():
                     help="multi-GPU plan for the strong-scaling line (auto: broadcast when B*G < B+P)")
     ap.add_argument("--no-weak", action="store_true",
                     help="multi-GPU: skip the weak-scaling extra (a config-sized join per rank, radix exchange)")
+    ap.add_argument("--native", default="auto", choices=["auto", "on", "off"],
+                    help="multi-GPU sharded plan: its build side through the C entry point hj_dist_build_sharded "
+                         "(RCCL inside the library; auto = on RCCL groups) or the torch.distributed steps (off)")
     ap.add_argument("--dry-run", action="store_true",
                     help="CPU/gloo: run the multi-rank launcher and timing skeleton without a GPU (tests)")
     args = ap.parse_args()
@@ -547,7 +550,8 @@ def main():
     else:
         from datafusion_parallelism_amd.distributed import DistributedHashJoin
 
-        dj = DistributedHashJoin(chunks=args.chunks, compress_keys=not args.no_compress_keys)
+        dj = DistributedHashJoin(chunks=args.chunks, compress_keys=not args.no_compress_keys,
+                                 native={"auto": None, "on": True, "off": False}[args.native])
         plan = args.plan if args.plan != "auto" else DistributedHashJoin.choose_plan(gB, gP, world)
         if args.plan == "auto" and plan == "broadcast":
             # the broadcast side's sharded form: each rank builds 1/G of the table and the
@@ -676,6 +680,8 @@ def main():
         if use_dist:
             line["exchange_ms"] = round(float(np.median(job.exchange_ms)), 4)
             line["plan"] = plan
+            if plan == "sharded":
+                line["native_build_side"] = bool(getattr(dj, "last_native", False))
             line["host_ms_per_step"] = _median(getattr(job, "host_ms", []))
             line["build_ms_source"] = ("HIP events on the build stream around the build side (plan, exchange, "
                                        "local build" + (", table gathers)" if plan == "sharded" else ")"))

@@ -17,6 +17,8 @@ for pl in sharded radix broadcast; do
   step 300 python3 bench.py --force-dist --plan $pl --no-cpu-baseline --steps 20 --warmup 5 > $O/bench_$pl.json 2> $O/bench_$pl.err
   cat $O/bench_$pl.json
 done
+step 300 python3 bench.py --force-dist --plan sharded --native off --no-cpu-baseline --steps 20 --warmup 5 > $O/bench_sharded_py.json 2> $O/bench_sharded_py.err
+cat $O/bench_sharded_py.json
 step 300 python3 bench.py --no-cpu-baseline > $O/bench_c2.json 2> $O/bench_c2.err
 cat $O/bench_c2.json
 step 600 python3 tools/bench_tpch.py --reps 3 q9:300 > $O/tpch_single.json 2> $O/tpch_single.err
