@@ -1326,6 +1326,11 @@ constexpr int kSlHistBins = 4096;                       // per-tile slice histog
 constexpr int kSlMaxSlices = kSlHistBins - 1;           // slices per pass: key ranges up to ~2^27 values
 constexpr int kSlOwnWin = 2048;        // flattened segment positions per owner window (32 per lane)
 constexpr int kSlOwnWinHashed = 1024;  // hashed slices: 16 per lane (u64 entries)
+// the emission's waves own 2048-row ranges of a tile: the partition counts each range's
+// entries (wcnt) so that a tile whose entries all hit one unique row each (no correction
+// flag from the lookup) needs no count pass in the emission
+constexpr int kSlRanges = 8;
+constexpr int kSlRangeRows = kSlTile / kSlRanges;  // 2048
 static_assert(kSlWidthLogMax + kSlTileLog <= 32, "entry = offset << tile bits | row");
 static_assert(kSlWidthLogMax <= 16 && kSlTileLog <= 16, "key offsets and rows leave as u16");
 
@@ -1348,12 +1353,15 @@ sl_partition_kernel(int64_t dmin, uint64_t drange, uint32_t wlog, uint32_t nslic
                     int64_t tile_off, int64_t row_base, uint32_t* __restrict__ tile_base,
                     unsigned long long* __restrict__ hdr,  // probe: workspace header (error word at [1]); build: null
                     unsigned long long* __restrict__ tcnt,      // probe: the tile's entry count; build: null
-                    uint32_t* __restrict__ tent) {  // probe: entries of the tile so far (earlier passes: append after them)
+                    uint32_t* __restrict__ tent,  // probe: entries of the tile so far (earlier passes: append after them)
+                    uint16_t* __restrict__ wcnt,  // probe: entries per 2048-row range of the tile (kSlRanges u16)
+                    uint32_t* __restrict__ tflag) {  // probe: the lookup's correction flag, zeroed by pass 0
     __shared__ __attribute__((aligned(16))) uint32_t s_ent[kSlTile];
     __shared__ __attribute__((aligned(16))) uint32_t s_hist[kSlHistBins];  // bins 0..nslices (<= kSlMaxSlices + 1)
-    // the scan's wave totals alias the entry staging area (free until the scatter), so the
-    // workgroup stays within 80 KB: two per CU
+    // the scan's wave totals and the per-range entry counts alias the entry staging area
+    // (free until the scatter), so the workgroup stays within 80 KB: two per CU
     uint32_t* s_w = s_ent;
+    uint32_t* s_wc = s_ent + kSlThreads / 64;
     const int64_t tile = blockIdx.x;          // tile of this key array
     const int64_t gtile = tile + tile_off;    // its output region (the build partitions several arrays)
     const int64_t tile0 = tile * kSlTile;
@@ -1362,6 +1370,7 @@ sl_partition_kernel(int64_t dmin, uint64_t drange, uint32_t wlog, uint32_t nslic
     // tile's entries of the earlier passes (hdr == null marks a later pass)
     const uint32_t ebase = (tent != nullptr && hdr == nullptr) ? tent[gtile] : 0u;
     for (uint32_t b = threadIdx.x; b < kSlHistBins; b += kSlThreads) s_hist[b] = 0;
+    if (threadIdx.x < kSlRanges) s_wc[threadIdx.x] = 0;
     // probe: zero the workspace header incl. the error word (no memset launch)
     if (hdr != nullptr && blockIdx.x == 0 && threadIdx.x == 0) hdr[0] = hdr[1] = 0;
     __syncthreads();
@@ -1382,11 +1391,24 @@ sl_partition_kernel(int64_t dmin, uint64_t drange, uint32_t wlog, uint32_t nslic
             e[g][q] = ((uint32_t)(idx & ((1u << wlog) - 1)) << kSlTileLog) | (uint32_t)(loc0 + q);
             sr[g][q] = ok ? (sl << kSlTileLog) | atomicAdd(&s_hist[sl], 1u) : 0xFFFFFFFFu;
         }
+        if (wcnt != nullptr) {  // probe: entries per emission range (a wave's rows of one group share a range)
+            uint32_t ws = 0;    // the wave's entries in group g: scalar popcounts of the entry ballots
+#pragma unroll
+            for (int q = 0; q < 4; ++q) ws += (uint32_t)__popcll(__ballot(sr[g][q] != 0xFFFFFFFFu));
+            if ((threadIdx.x & 63) == 0 && ws) atomicAdd(&s_wc[(g * (kSlThreads * 4) + threadIdx.x * 4) / kSlRangeRows], ws);
+        }
     }
     __syncthreads();
+    // the range counts leave s_ent before the scan's barriers (its wave totals use s_ent[0, 16))
+    const uint32_t my_wc = (wcnt != nullptr && threadIdx.x < kSlRanges) ? s_wc[threadIdx.x] : 0u;
     // exclusive scan of the bins, four per thread
     uint32_t tot;
     hist_excl_scan(s_hist, s_w, &tot);
+    if (wcnt != nullptr && threadIdx.x < kSlRanges) {
+        uint16_t* wc = wcnt + gtile * kSlRanges + threadIdx.x;
+        *wc = (uint16_t)((ebase ? *wc : 0u) + my_wc);
+        if (threadIdx.x == 0 && hdr != nullptr) tflag[gtile] = 0u;  // pass 0: no correction seen yet
+    }
     uint16_t* to = toff + gtile * (int64_t)nbins;
     for (uint32_t b = threadIdx.x; b < nbins; b += kSlThreads) to[b] = (uint16_t)(ebase + s_hist[b]);
     if (tile_base != nullptr && threadIdx.x == 0) tile_base[gtile] = (uint32_t)(row_base + tile0);  // build only
@@ -2027,8 +2049,10 @@ template <bool HASHED, int W>
 __global__ void __launch_bounds__(kSlThreads)
 sl_lookup_kernel(TableView tv, uint32_t wlog, uint32_t nslices, int64_t ntiles, uint32_t parts,
                  const void* __restrict__ ko, uint32_t* __restrict__ res, const uint16_t* __restrict__ toff,
-                 unsigned long long* __restrict__ tcnt, uint32_t soff) {  // soff: first slice of this pass (hashed)
+                 unsigned long long* __restrict__ tcnt, uint32_t soff,  // soff: first slice of this pass (hashed)
+                 uint32_t* __restrict__ tflag) {  // tiles with an entry of a missing or duplicated key: 1
     extern __shared__ __attribute__((aligned(16))) uint32_t s_tab[];  // dense: 2^wlog refs; hashed: 2048 buckets
+    __shared__ uint8_t s_odd[kSlThreads];  // per wave, by rank: the fragment holds an entry of count != 1
     __shared__ uint32_t s_base[kSlThreads];
     __shared__ uint32_t s_lane[kSlThreads];  // per wave: tile lane of each non-empty segment, by rank
     // per wave, by rank: dense, the correction running sum at each fragment's start;
@@ -2124,6 +2148,8 @@ sl_lookup_kernel(TableView tv, uint32_t wlog, uint32_t nslices, int64_t ntiles, 
         // Hashed (half the entries of a uniform probe side miss): the running sum of every
         // row, recorded at each fragment's last position instead.
         scst[lane] = 0;
+        uint8_t* sodd = s_odd + wave * 64;
+        sodd[lane] = 0;
         uint32_t corr_run = 0;
         // the 64 tiles' regions as buffers (wave-uniform bases): 32-bit offsets, and an
         // out-of-range offset turns a position past R into a dropped access
@@ -2212,6 +2238,7 @@ sl_lookup_kernel(TableView tv, uint32_t wlog, uint32_t nslices, int64_t ntiles, 
                 __builtin_amdgcn_raw_buffer_store_b32(v, rres, (int)(o * 4), 0, 0);
                 if constexpr (HASHED) {
                     uint32_t d = c - 1u;  // kOob: c = 1
+                    if (d != 0) sodd[off[u] >> 26] = 1;  // the emission's count-free path is off for its tile
                     if (d != 0xFFFFFFFFu && d >= kBigCorr) {
                         atomicAdd(&tcnt[tc + slane[off[u] >> 26]], (unsigned long long)d);
                         d = 0;
@@ -2224,6 +2251,7 @@ sl_lookup_kernel(TableView tv, uint32_t wlog, uint32_t nslices, int64_t ntiles, 
                 // a fragment start (start mask bit) records the running sum before it
                 const bool odd = o != kOob && c != 1;
                 if (__ballot(odd) != 0) {
+                    if (odd) sodd[off[u] >> 26] = 1;  // the emission's count-free path is off for its tile
                     uint32_t d = odd ? c - 1u : 0u;
                     if (d != 0xFFFFFFFFu && d >= kBigCorr) {  // a huge duplicate: straight to its tile
                         atomicAdd(&tcnt[tc + slane[off[u] >> 26]], (unsigned long long)d);
@@ -2249,6 +2277,7 @@ sl_lookup_kernel(TableView tv, uint32_t wlog, uint32_t nslices, int64_t ntiles, 
                 cr = (int)(nxt - scst[rank]);
             }
             if (cr != 0) atomicAdd(&tcnt[tc + lane], (unsigned long long)(long long)cr);
+            if (sodd[rank]) atomicOr(&tflag[tc + lane], 1u);
         }
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         __builtin_amdgcn_wave_barrier();
@@ -2387,7 +2416,9 @@ __global__ void __launch_bounds__(kSlEmitThreads, 4)  // two workgroups per CU: 
 sl_emit_kernel(TableView tv, const uint32_t* __restrict__ tent, const uint16_t* __restrict__ rl,
                const uint32_t* __restrict__ res, const uint32_t* __restrict__ probe_ids, uint32_t pbase,
                const unsigned long long* __restrict__ tcnt, int64_t ntiles, uint64_t* __restrict__ out_b,
-               uint32_t* __restrict__ out_p, int64_t cap, int64_t* __restrict__ d_total) {
+               uint32_t* __restrict__ out_p, int64_t cap, int64_t* __restrict__ d_total,
+               const uint16_t* __restrict__ wcnt,     // entries per 2048-row range (null: always count)
+               const uint32_t* __restrict__ tflag) {  // the lookup's correction flag per tile
     __shared__ __attribute__((aligned(16))) uint32_t s_ref[kSlTile];  // the tile's refs, kMiss = none
     __shared__ unsigned long long s_w[kSlEmitThreads / 64];
     __shared__ unsigned long long s_pre[kSlEmitThreads / 64];
@@ -2397,6 +2428,9 @@ sl_emit_kernel(TableView tv, const uint32_t* __restrict__ tent, const uint16_t* 
     uint2 e4[U];
     uint4 r4[U];
     uint32_t cnt = 0;
+    // count-free tiles: every entry's key had exactly one row (no correction flag), so a
+    // wave's pair count is its range's entry count and a row's count is 0 (kMiss) or 1
+    uint32_t nflag = 1, nwc = 0;
     // Persistent: workgroup b takes tiles b, b + grid, ...; the next tile's entries are
     // loaded while this tile's pairs are counted and written. All loads of a tile are
     // issued at once, after its entry count. A tile's output offset is the sum of the
@@ -2410,6 +2444,10 @@ sl_emit_kernel(TableView tv, const uint32_t* __restrict__ tent, const uint16_t* 
     };
     auto fetch = [&](int64_t t) {
         cnt = DFP_ABL(2) ? 0u : tent[t];  // the tile's entries over every pass
+        if (wcnt != nullptr) {
+            nflag = tflag[t];
+            nwc = wcnt[t * kSlRanges + wave];
+        }
         const uint16_t* te = rl + t * kSlTile;
         const uint32_t* tr = res + t * kSlTile;
 #pragma unroll
@@ -2445,17 +2483,23 @@ sl_emit_kernel(TableView tv, const uint32_t* __restrict__ tent, const uint16_t* 
             if (i + 3 < cnt) s_ref[e4[u].y >> 16] = r4[u].w;
         }
         __syncthreads();
+        const bool fast = wcnt != nullptr && nflag == 0;  // this tile's (read before the prefetch)
+        const uint32_t fast_wc = nwc;
         const int64_t next = tile + gridDim.x;
         if (next < ntiles) fetch(next);
-        // pass 1: this wave's pair count
+        // pass 1: this wave's pair count (a count-free tile: its entries in the wave's range)
         const int row_w = wave * kSlWaveRows;
-        uint32_t lsum = 0;  // < 32 rows x < 2^26 rows each
+        if (fast) {
+            if (lane == 0) s_w[wave] = fast_wc;
+        } else {
+            uint32_t lsum = 0;  // < 32 rows x < 2^26 rows each
 #pragma unroll 8
-        for (int k = 0; k < kSlWaveRows; k += 64) lsum += sl_count(tv, s_ref[row_w + k + lane]);
-        // wave total in u64: two 32-bit halves of the per-lane sums
-        const unsigned long long wsum = (unsigned long long)wave_sum_dpp(lsum & 0xFFFFu) +
-                                        ((unsigned long long)wave_sum_dpp(lsum >> 16) << 16);
-        if (lane == 0) s_w[wave] = wsum;
+            for (int k = 0; k < kSlWaveRows; k += 64) lsum += sl_count(tv, s_ref[row_w + k + lane]);
+            // wave total in u64: two 32-bit halves of the per-lane sums
+            const unsigned long long wsum = (unsigned long long)wave_sum_dpp(lsum & 0xFFFFu) +
+                                            ((unsigned long long)wave_sum_dpp(lsum >> 16) << 16);
+            if (lane == 0) s_w[wave] = wsum;
+        }
         __syncthreads();
         unsigned long long pos = base, tile_total = 0;
         for (int w = 0; w < kSlEmitThreads / 64; ++w) {
@@ -2470,8 +2514,28 @@ sl_emit_kernel(TableView tv, const uint32_t* __restrict__ tent, const uint16_t* 
             // max-scan of start markers), so every store instruction writes one
             // contiguous run and the duplicate segments are read in parallel.
             uint32_t* own = s_own[wave];
+            if (fast) {
+                // count-free tile: one pair per hit row, the prefix a popcount of the hit mask
+#pragma unroll 4
+                for (int k = 0; k < kSlWaveRows; k += 64) {
+                    const int loc = row_w + k + lane;
+                    const uint32_t r = s_ref[loc];
+                    const unsigned long long hit = __ballot(r != kMiss);
+                    if (r != kMiss) {
+                        const uint32_t below = __builtin_amdgcn_mbcnt_hi(
+                            (uint32_t)(hit >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)hit, 0u));
+                        const unsigned long long o = pos + below;
+                        const int64_t row = tile0 + loc;
+                        if (o < (unsigned long long)cap) {
+                            out_b[o] = HAS_ROW_IDS ? tv.row_ids[r] : (uint64_t)r;
+                            out_p[o] = HAS_PROBE_IDS ? probe_ids[row] : (uint32_t)row + pbase;
+                        }
+                    }
+                    pos += (uint32_t)__builtin_popcountll(hit);
+                }
+            }
 #pragma unroll 2
-            for (int k = 0; k < kSlWaveRows; k += 64) {
+            for (int k = 0; !fast && k < kSlWaveRows; k += 64) {
                 const int loc = row_w + k + lane;
                 const uint32_t r = s_ref[loc];
                 const uint32_t c = sl_count(tv, r);
@@ -3255,7 +3319,8 @@ hipError_t launch_build_frag(int key_bytes, const Segment* h_segs, int nseg, con
 #define DFP_BLP(KT, HV)                                                                                          \
     sl_partition_kernel<KT, HV><<<(unsigned)nt, kSlThreads, 0, s>>>(g.dmin, drange, wlog, nblk, sg.keys, sg.valid, \
                                                                    sg.voff, sg.n, vec, ko, rl, toff, 0, t0,          \
-                                                                   sg.row_base, tile_base, nullptr, nullptr, nullptr)
+                                                                   sg.row_base, tile_base, nullptr, nullptr, nullptr, \
+                                                                   nullptr, nullptr)
         if (key_bytes == 8) {
             if (sg.valid) DFP_BLP(int64_t, true); else DFP_BLP(int64_t, false);
         } else {
@@ -3495,6 +3560,8 @@ struct SlicedWs {
     void* ko;
     uint16_t* rl;
     uint32_t* res;
+    uint16_t* wcnt;   // entries per 2048-row range of a tile (kSlRanges per tile)
+    uint32_t* tflag;  // the lookup's correction flag per tile
     int64_t bytes;
 };
 SlicedWs sliced_ws_layout(void* base, int64_t n) {
@@ -3507,6 +3574,8 @@ SlicedWs sliced_ws_layout(void* base, int64_t n) {
     w.ko = (void*)p;                  p = al256(p + 8 * nt * kSlTile);
     w.rl = (uint16_t*)p;              p = al256(p + 2 * nt * kSlTile);
     w.res = (uint32_t*)p;             p = al256(p + 4 * nt * kSlTile);
+    w.wcnt = (uint16_t*)p;            p = al256(p + 2 * kSlRanges * (nt + 2));
+    w.tflag = (uint32_t*)p;           p = al256(p + 4 * (nt + 2));
     w.bytes = (int64_t)(p - (uintptr_t)base) + 256;
     return w;
 }
@@ -3669,7 +3738,7 @@ hipError_t launch_probe_sliced(int key_bytes, const TableView& tv, const void* k
 #define DFP_SLP(KT, HV)                                                                                      \
     sl_partition_kernel<KT, HV><<<(unsigned)nt, kSlThreads, 0, s>>>(dmin_p, drange_p, wlog, nsl, keys, valid, voff, n, \
                                                                    vec, (uint16_t*)w.ko, w.rl, w.toff, sl_nt, 0, 0,   \
-                                                                   nullptr, h, w.tcnt, w.tent)
+                                                                   nullptr, h, w.tcnt, w.tent, w.wcnt, w.tflag)
             if (key_bytes == 8) {
                 if (valid) DFP_SLP(int64_t, true); else DFP_SLP(int64_t, false);
             } else {
@@ -3691,16 +3760,17 @@ hipError_t launch_probe_sliced(int key_bytes, const TableView& tv, const void* k
         }
         if (hashed)
             sl_lookup_kernel<true, kSlOwnWinHashed><<<nsl * parts, kSlThreads, tab_lds, s>>>(
-                tp, wlog, nsl, nt, parts, w.ko, w.res, w.toff, w.tcnt, s0);
+                tp, wlog, nsl, nt, parts, w.ko, w.res, w.toff, w.tcnt, s0, w.tflag);
         else
             sl_lookup_kernel<false, kSlOwnWin><<<nsl * parts, kSlThreads, tab_lds, s>>>(tp, wlog, nsl, nt, parts, w.ko,
-                                                                                      w.res, w.toff, w.tcnt, 0u);
+                                                                                      w.res, w.toff, w.tcnt, 0u, w.tflag);
     }
     const bool ri = tv.row_ids != nullptr, pi = probe_ids != nullptr;
     const unsigned egrid = (unsigned)std::min<int64_t>(nt, (int64_t)sl_emit_wgs_per_cu() * sl_num_cus());
 #define DFP_SLE(RI, PI)                                                                                           \
     sl_emit_kernel<RI, PI><<<egrid, kSlEmitThreads, 0, s>>>(tv, w.tent, w.rl, w.res, probe_ids, pbase, w.tcnt, nt,   \
-                                                           out_b, out_p, cap, d_total)
+                                                           out_b, out_p, cap, d_total, hashed ? nullptr : w.wcnt,  \
+                                                           w.tflag)
     if (ri && pi) DFP_SLE(true, true);
     else if (ri) DFP_SLE(true, false);
     else if (pi) DFP_SLE(false, true);

@@ -106,7 +106,10 @@ def test_operator_multi_gpu_table_matches_oracle(dfp, oracle_mod, plan):
     pnull = rng.random(len(pk)) < 0.03
     build = pa.RecordBatch.from_pydict({"k": pa.array(bk, mask=bnull), "bid": np.arange(len(bk))})
     probe = pa.RecordBatch.from_pydict({"k": pa.array(pk, mask=pnull), "pid": np.arange(len(pk))})
-    bparts = split(pa.Table.from_batches([build]).to_batches(max_chunksize=1000), 8)
+    # build partitions of consecutive batches: the canonical build index (partition 0's
+    # batches, then partition 1's, ...) is then the bid column
+    bb = pa.Table.from_batches([build]).to_batches(max_chunksize=1000)
+    bparts = [bb[3 * p:3 * (p + 1)] for p in range(8)]
     pparts = split(pa.Table.from_batches([probe]).to_batches(max_chunksize=1000), 8)
     join = ParallelHashJoin(bparts, pparts, on=[("k", "k")], devices=[0] * 4, plan=plan)
     out = join.collect()
