@@ -1119,6 +1119,12 @@ hj_status multi_probe(const hj_table* t, const void* keys, const uint8_t* valid,
             hipStream_t sg = m->streams[g];
             Part& P = parts[g];
             P.n = cnt[g];
+            if (dev == d && !force_stage()) {  // a shard on the batch's device probes its region in place
+                P.k = (const char*)ok + off * kb;
+                P.ids = oi + off;
+                off += P.n;
+                continue;
+            }
             HIP_TRY(hipSetDevice(dev));
             MT_ALLOC(kd, void*, dev, (size_t)P.n * kb);
             MT_ALLOC(id, uint32_t*, dev, (size_t)P.n * 4);

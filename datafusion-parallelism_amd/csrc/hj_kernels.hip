@@ -1354,8 +1354,7 @@ sl_partition_kernel(int64_t dmin, uint64_t drange, uint32_t wlog, uint32_t nslic
                     unsigned long long* __restrict__ hdr,  // probe: workspace header (error word at [1]); build: null
                     unsigned long long* __restrict__ tcnt,      // probe: the tile's entry count; build: null
                     uint32_t* __restrict__ tent,  // probe: entries of the tile so far (earlier passes: append after them)
-                    uint16_t* __restrict__ wcnt,  // probe: entries per 2048-row range of the tile (kSlRanges u16)
-                    uint32_t* __restrict__ tflag) {  // probe: the lookup's correction flag, zeroed by pass 0
+                    uint16_t* __restrict__ wcnt) {  // probe: entries per 2048-row range of the tile (kSlRanges u16)
     __shared__ __attribute__((aligned(16))) uint32_t s_ent[kSlTile];
     __shared__ __attribute__((aligned(16))) uint32_t s_hist[kSlHistBins];  // bins 0..nslices (<= kSlMaxSlices + 1)
     // the scan's wave totals and the per-range entry counts alias the entry staging area
@@ -1407,7 +1406,6 @@ sl_partition_kernel(int64_t dmin, uint64_t drange, uint32_t wlog, uint32_t nslic
     if (wcnt != nullptr && threadIdx.x < kSlRanges) {
         uint16_t* wc = wcnt + gtile * kSlRanges + threadIdx.x;
         *wc = (uint16_t)((ebase ? *wc : 0u) + my_wc);
-        if (threadIdx.x == 0 && hdr != nullptr) tflag[gtile] = 0u;  // pass 0: no correction seen yet
     }
     uint16_t* to = toff + gtile * (int64_t)nbins;
     for (uint32_t b = threadIdx.x; b < nbins; b += kSlThreads) to[b] = (uint16_t)(ebase + s_hist[b]);
@@ -2034,6 +2032,12 @@ __device__ __forceinline__ uint32_t lds_bucket_ref(const uint4* __restrict__ img
 }
 
 constexpr uint32_t kBigCorr = 1u << 16;  // counts - 1 from here on correct the tile count directly
+// a tile's pair count (tcnt) is < 2^45 (16384 rows x < 2^31 build rows); the dense lookup
+// adds kOddFlag once per fragment with an entry of a missing or duplicated key (at most
+// 4095 slices x 3 passes of a direct-addressed range: the flag bits never wrap to 0)
+constexpr int kOddShift = 46;
+constexpr unsigned long long kOddFlag = 1ull << kOddShift;
+constexpr unsigned long long kCountMask = kOddFlag - 1;
 
 // Timing ablations (wrong pairs by design) exist only in a diagnostic build of the
 // library (tools/build_ablation.py defines DFP_HJ_ABLATIONS); the product library folds
@@ -2049,10 +2053,9 @@ template <bool HASHED, int W>
 __global__ void __launch_bounds__(kSlThreads)
 sl_lookup_kernel(TableView tv, uint32_t wlog, uint32_t nslices, int64_t ntiles, uint32_t parts,
                  const void* __restrict__ ko, uint32_t* __restrict__ res, const uint16_t* __restrict__ toff,
-                 unsigned long long* __restrict__ tcnt, uint32_t soff,  // soff: first slice of this pass (hashed)
-                 uint32_t* __restrict__ tflag) {  // tiles with an entry of a missing or duplicated key: 1
+                 unsigned long long* __restrict__ tcnt, uint32_t soff) {  // soff: first slice of this pass (hashed)
     extern __shared__ __attribute__((aligned(16))) uint32_t s_tab[];  // dense: 2^wlog refs; hashed: 2048 buckets
-    __shared__ uint8_t s_odd[kSlThreads];  // per wave, by rank: the fragment holds an entry of count != 1
+    __shared__ uint8_t s_odd[HASHED ? 1 : kSlThreads];  // dense, per wave by rank: the fragment holds an entry of count != 1
     __shared__ uint32_t s_base[kSlThreads];
     __shared__ uint32_t s_lane[kSlThreads];  // per wave: tile lane of each non-empty segment, by rank
     // per wave, by rank: dense, the correction running sum at each fragment's start;
@@ -2148,8 +2151,8 @@ sl_lookup_kernel(TableView tv, uint32_t wlog, uint32_t nslices, int64_t ntiles, 
         // Hashed (half the entries of a uniform probe side miss): the running sum of every
         // row, recorded at each fragment's last position instead.
         scst[lane] = 0;
-        uint8_t* sodd = s_odd + wave * 64;
-        sodd[lane] = 0;
+        uint8_t* sodd = s_odd + (HASHED ? 0 : wave * 64);
+        if constexpr (!HASHED) sodd[lane] = 0;
         uint32_t corr_run = 0;
         // the 64 tiles' regions as buffers (wave-uniform bases): 32-bit offsets, and an
         // out-of-range offset turns a position past R into a dropped access
@@ -2238,7 +2241,6 @@ sl_lookup_kernel(TableView tv, uint32_t wlog, uint32_t nslices, int64_t ntiles, 
                 __builtin_amdgcn_raw_buffer_store_b32(v, rres, (int)(o * 4), 0, 0);
                 if constexpr (HASHED) {
                     uint32_t d = c - 1u;  // kOob: c = 1
-                    if (d != 0) sodd[off[u] >> 26] = 1;  // the emission's count-free path is off for its tile
                     if (d != 0xFFFFFFFFu && d >= kBigCorr) {
                         atomicAdd(&tcnt[tc + slane[off[u] >> 26]], (unsigned long long)d);
                         d = 0;
@@ -2276,8 +2278,11 @@ sl_lookup_kernel(TableView tv, uint32_t wlog, uint32_t nslices, int64_t ntiles, 
                 const uint32_t nxt = rank + 1 < nranks ? scst[rank + 1] : corr_run;
                 cr = (int)(nxt - scst[rank]);
             }
-            if (cr != 0) atomicAdd(&tcnt[tc + lane], (unsigned long long)(long long)cr);
-            if (sodd[rank]) atomicOr(&tflag[tc + lane], 1u);
+            // dense: a fragment with a missing or duplicated key also turns off its tile's
+            // count-free emission (kOddFlag above the count bits, one atomic for both)
+            const unsigned long long add =
+                (unsigned long long)(long long)cr + (!HASHED && sodd[rank] ? kOddFlag : 0ull);
+            if (add != 0) atomicAdd(&tcnt[tc + lane], add);
         }
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         __builtin_amdgcn_wave_barrier();
@@ -2417,8 +2422,7 @@ sl_emit_kernel(TableView tv, const uint32_t* __restrict__ tent, const uint16_t* 
                const uint32_t* __restrict__ res, const uint32_t* __restrict__ probe_ids, uint32_t pbase,
                const unsigned long long* __restrict__ tcnt, int64_t ntiles, uint64_t* __restrict__ out_b,
                uint32_t* __restrict__ out_p, int64_t cap, int64_t* __restrict__ d_total,
-               const uint16_t* __restrict__ wcnt,     // entries per 2048-row range (null: always count)
-               const uint32_t* __restrict__ tflag) {  // the lookup's correction flag per tile
+               const uint16_t* __restrict__ wcnt) {  // entries per 2048-row range (null: always count)
     __shared__ __attribute__((aligned(16))) uint32_t s_ref[kSlTile];  // the tile's refs, kMiss = none
     __shared__ unsigned long long s_w[kSlEmitThreads / 64];
     __shared__ unsigned long long s_pre[kSlEmitThreads / 64];
@@ -2439,13 +2443,13 @@ sl_emit_kernel(TableView tv, const uint32_t* __restrict__ tent, const uint16_t* 
     // load per thread), so no scan launch runs between S2 and S3.
     auto count_sum = [&](int64_t lo, int64_t hi) -> unsigned long long {  // this thread's share
         unsigned long long v = 0;
-        for (int64_t j = lo + threadIdx.x; j < hi; j += kSlEmitThreads) v += tcnt[j];
+        for (int64_t j = lo + threadIdx.x; j < hi; j += kSlEmitThreads) v += tcnt[j] & kCountMask;
         return v;
     };
     auto fetch = [&](int64_t t) {
         cnt = DFP_ABL(2) ? 0u : tent[t];  // the tile's entries over every pass
         if (wcnt != nullptr) {
-            nflag = tflag[t];
+            nflag = (uint32_t)(tcnt[t] >> kOddShift);  // the lookup's flag: some entry's count != 1
             nwc = wcnt[t * kSlRanges + wave];
         }
         const uint16_t* te = rl + t * kSlTile;
@@ -3320,7 +3324,7 @@ hipError_t launch_build_frag(int key_bytes, const Segment* h_segs, int nseg, con
     sl_partition_kernel<KT, HV><<<(unsigned)nt, kSlThreads, 0, s>>>(g.dmin, drange, wlog, nblk, sg.keys, sg.valid, \
                                                                    sg.voff, sg.n, vec, ko, rl, toff, 0, t0,          \
                                                                    sg.row_base, tile_base, nullptr, nullptr, nullptr, \
-                                                                   nullptr, nullptr)
+                                                                   nullptr)
         if (key_bytes == 8) {
             if (sg.valid) DFP_BLP(int64_t, true); else DFP_BLP(int64_t, false);
         } else {
@@ -3561,7 +3565,6 @@ struct SlicedWs {
     uint16_t* rl;
     uint32_t* res;
     uint16_t* wcnt;   // entries per 2048-row range of a tile (kSlRanges per tile)
-    uint32_t* tflag;  // the lookup's correction flag per tile
     int64_t bytes;
 };
 SlicedWs sliced_ws_layout(void* base, int64_t n) {
@@ -3575,7 +3578,6 @@ SlicedWs sliced_ws_layout(void* base, int64_t n) {
     w.rl = (uint16_t*)p;              p = al256(p + 2 * nt * kSlTile);
     w.res = (uint32_t*)p;             p = al256(p + 4 * nt * kSlTile);
     w.wcnt = (uint16_t*)p;            p = al256(p + 2 * kSlRanges * (nt + 2));
-    w.tflag = (uint32_t*)p;           p = al256(p + 4 * (nt + 2));
     w.bytes = (int64_t)(p - (uintptr_t)base) + 256;
     return w;
 }
@@ -3738,7 +3740,7 @@ hipError_t launch_probe_sliced(int key_bytes, const TableView& tv, const void* k
 #define DFP_SLP(KT, HV)                                                                                      \
     sl_partition_kernel<KT, HV><<<(unsigned)nt, kSlThreads, 0, s>>>(dmin_p, drange_p, wlog, nsl, keys, valid, voff, n, \
                                                                    vec, (uint16_t*)w.ko, w.rl, w.toff, sl_nt, 0, 0,   \
-                                                                   nullptr, h, w.tcnt, w.tent, w.wcnt, w.tflag)
+                                                                   nullptr, h, w.tcnt, w.tent, w.wcnt)
             if (key_bytes == 8) {
                 if (valid) DFP_SLP(int64_t, true); else DFP_SLP(int64_t, false);
             } else {
@@ -3760,17 +3762,16 @@ hipError_t launch_probe_sliced(int key_bytes, const TableView& tv, const void* k
         }
         if (hashed)
             sl_lookup_kernel<true, kSlOwnWinHashed><<<nsl * parts, kSlThreads, tab_lds, s>>>(
-                tp, wlog, nsl, nt, parts, w.ko, w.res, w.toff, w.tcnt, s0, w.tflag);
+                tp, wlog, nsl, nt, parts, w.ko, w.res, w.toff, w.tcnt, s0);
         else
             sl_lookup_kernel<false, kSlOwnWin><<<nsl * parts, kSlThreads, tab_lds, s>>>(tp, wlog, nsl, nt, parts, w.ko,
-                                                                                      w.res, w.toff, w.tcnt, 0u, w.tflag);
+                                                                                      w.res, w.toff, w.tcnt, 0u);
     }
     const bool ri = tv.row_ids != nullptr, pi = probe_ids != nullptr;
     const unsigned egrid = (unsigned)std::min<int64_t>(nt, (int64_t)sl_emit_wgs_per_cu() * sl_num_cus());
 #define DFP_SLE(RI, PI)                                                                                           \
     sl_emit_kernel<RI, PI><<<egrid, kSlEmitThreads, 0, s>>>(tv, w.tent, w.rl, w.res, probe_ids, pbase, w.tcnt, nt,   \
-                                                           out_b, out_p, cap, d_total, hashed ? nullptr : w.wcnt,  \
-                                                           w.tflag)
+                                                           out_b, out_p, cap, d_total, hashed ? nullptr : w.wcnt)
     if (ri && pi) DFP_SLE(true, true);
     else if (ri) DFP_SLE(true, false);
     else if (pi) DFP_SLE(false, true);
