@@ -3768,10 +3768,16 @@ hipError_t launch_probe_sliced(int key_bytes, const TableView& tv, const void* k
                                                                                       w.res, w.toff, w.tcnt, 0u);
     }
     const bool ri = tv.row_ids != nullptr, pi = probe_ids != nullptr;
+    // DFP_HJ_COUNT_FREE=0: every tile takes the emission's count pass (A/B of the count-free path)
+    static const bool count_free = [] {
+        const char* e = getenv("DFP_HJ_COUNT_FREE");
+        return !(e != nullptr && e[0] == '0');
+    }();
     const unsigned egrid = (unsigned)std::min<int64_t>(nt, (int64_t)sl_emit_wgs_per_cu() * sl_num_cus());
 #define DFP_SLE(RI, PI)                                                                                           \
     sl_emit_kernel<RI, PI><<<egrid, kSlEmitThreads, 0, s>>>(tv, w.tent, w.rl, w.res, probe_ids, pbase, w.tcnt, nt,   \
-                                                           out_b, out_p, cap, d_total, hashed ? nullptr : w.wcnt)
+                                                           out_b, out_p, cap, d_total,                      \
+                                                           hashed || !count_free ? nullptr : w.wcnt)
     if (ri && pi) DFP_SLE(true, true);
     else if (ri) DFP_SLE(true, false);
     else if (pi) DFP_SLE(false, true);
