@@ -1371,7 +1371,11 @@ sl_partition_kernel(int64_t dmin, uint64_t drange, uint32_t wlog, uint32_t nslic
     for (uint32_t b = threadIdx.x; b < kSlHistBins; b += kSlThreads) s_hist[b] = 0;
     if (threadIdx.x < kSlRanges) s_wc[threadIdx.x] = 0;
     // probe: zero the workspace header incl. the error word (no memset launch)
-    if (hdr != nullptr && blockIdx.x == 0 && threadIdx.x == 0) hdr[0] = hdr[1] = 0;
+    // (and the emission's tile counter after the tile counts: one tile per workgroup here)
+    if (hdr != nullptr && blockIdx.x == 0 && threadIdx.x == 0) {
+        hdr[0] = hdr[1] = 0;
+        tcnt[gridDim.x] = 0;
+    }
     __syncthreads();
     // per row: entry (offset << 14 | row) and (slice << 14 | rank in slice), ~0 = no entry
     uint32_t e[kSlGroups][4], sr[kSlGroups][4];
@@ -2031,6 +2035,12 @@ __device__ __forceinline__ uint32_t lds_bucket_ref(const uint4* __restrict__ img
     return ref;
 }
 
+// Measured (r04) and not kept: the hashed slice image re-laid as quad arrays (low key
+// halves, high halves, key 4 + meta, refs: one quad read per lane on 16 of a bank row's
+// 256 B instead of 4 of them) with three quad reads and a dependent ref read per entry
+// — C2h lookup 770 -> 830 us: the lookup is bound by its per-row dependency chains, not
+// by LDS bank conflicts, and the extra dependent read lengthens every chain.
+
 constexpr uint32_t kBigCorr = 1u << 16;  // counts - 1 from here on correct the tile count directly
 // a tile's pair count (tcnt) is < 2^45 (16384 rows x < 2^31 build rows); the dense lookup
 // adds kOddFlag once per fragment with an entry of a missing or duplicated key (at most
@@ -2045,8 +2055,39 @@ constexpr unsigned long long kCountMask = kOddFlag - 1;
 #ifdef DFP_HJ_ABLATIONS
 __constant__ int kAblDev;
 #define DFP_ABL(bit) (kAblDev & (bit))
+// per-workgroup timeline of the last sliced lookup / emission (diagnostic build only):
+// [4 * blockIdx + 0..3] = start, after its first phase (lookup: slice image loaded),
+// end (wall clock, 100 MHz), hardware id (xcc << 16 | se << 8 | cu)
+__device__ unsigned long long g_dbg_lk_ts[4 * 65536];
+__device__ unsigned long long g_dbg_em_ts[4 * 65536];
+__device__ __forceinline__ unsigned long long dbg_hwid() {
+    const unsigned cu = __builtin_amdgcn_s_getreg(GETREG_IMMED(HW_ID_CU_ID_SIZE - 1, HW_ID_CU_ID_OFFSET, HW_ID));
+    const unsigned se = __builtin_amdgcn_s_getreg(GETREG_IMMED(HW_ID_SE_ID_SIZE - 1, HW_ID_SE_ID_OFFSET, HW_ID));
+    const unsigned xcc = __builtin_amdgcn_s_getreg(GETREG_IMMED(3, 0, 20));
+    return ((unsigned long long)xcc << 16) | (se << 8) | cu;
+}
+#define DFP_DBG_TS(arr, slot, v) \
+    do { if (threadIdx.x == 0 && blockIdx.x < 65536) arr[4 * blockIdx.x + (slot)] = (v); } while (0)
+// the sliced lookup's per-phase shader cycles summed over every wave of the last launches
+// (DFP_HJ_ABLATE bit 256 turns it on: it adds an s_waitcnt vmcnt(0) before the row work):
+// [0] block setup, [1] entry loads issued, [2] wait for them, [3] rows, [4] block end,
+// [5] blocks, [6] windows
+__device__ unsigned long long g_dbg_lk_ph[8];
+#define DFP_PH_DECL unsigned long long ph_t = 0, ph_acc[7] = {0, 0, 0, 0, 0, 0, 0}; \
+    const bool ph_on = DFP_ABL(256) != 0; if (ph_on) ph_t = clock64()
+#define DFP_PH(i) do { if (ph_on) { const unsigned long long t_ = clock64(); ph_acc[i] += t_ - ph_t; ph_t = t_; } } while (0)
+#define DFP_PH_WAIT() do { if (ph_on) asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); } while (0)
+#define DFP_PH_CNT(i) do { if (ph_on) ph_acc[i] += 1; } while (0)
+#define DFP_PH_FLUSH() do { if (ph_on && (threadIdx.x & 63) == 0) \
+    for (int i_ = 0; i_ < 7; ++i_) atomicAdd(&g_dbg_lk_ph[i_], ph_acc[i_]); } while (0)
 #else
 #define DFP_ABL(bit) 0
+#define DFP_DBG_TS(arr, slot, v) do { } while (0)
+#define DFP_PH_DECL do { } while (0)
+#define DFP_PH(i) do { } while (0)
+#define DFP_PH_WAIT() do { } while (0)
+#define DFP_PH_CNT(i) do { } while (0)
+#define DFP_PH_FLUSH() do { } while (0)
 #endif
 
 template <bool HASHED, int W>
@@ -2063,6 +2104,7 @@ sl_lookup_kernel(TableView tv, uint32_t wlog, uint32_t nslices, int64_t ntiles, 
     __shared__ uint32_t s_cst[kSlThreads];
     __shared__ uint32_t s_end[HASHED ? kSlThreads : 1];  // hashed, per wave: end position of each fragment, by rank
     __shared__ unsigned long long s_mask[kSlThreads / 64][W / 64];
+    DFP_DBG_TS(g_dbg_lk_ts, 0, wall_clock64());
     const uint32_t item = DFP_ABL(128) ? blockIdx.x : xcd_item(blockIdx.x, gridDim.x);
     const uint32_t s = item % nslices, part = item / nslices;
     uint32_t sbase = 0;  // hashed: first bucket of the slice
@@ -2093,6 +2135,7 @@ sl_lookup_kernel(TableView tv, uint32_t wlog, uint32_t nslices, int64_t ntiles, 
         for (uint32_t i = done + threadIdx.x; i < len; i += kSlThreads) s_tab[i] = dense[base + i];
     }
     __syncthreads();
+    DFP_DBG_TS(g_dbg_lk_ts, 1, wall_clock64());
     // part boundaries on 64-tile blocks (the transposed bounds' granule)
     const int64_t nblk = (ntiles + 63) / 64;
     const int64_t ta = nblk * part / parts * 64, tb = min<int64_t>(nblk * (part + 1) / parts * 64, ntiles);
@@ -2126,7 +2169,9 @@ sl_lookup_kernel(TableView tv, uint32_t wlog, uint32_t nslices, int64_t ntiles, 
     };
     uint32_t nst, nlen;
     bounds(ta + (int64_t)wave * 64, &nst, &nlen);
+    DFP_PH_DECL;
     for (int64_t tc = ta + (int64_t)wave * 64; tc < tb; tc += kStep) {
+        DFP_PH_CNT(5);
         const uint32_t st = nst, len = nlen;
         bounds(tc + kStep, &nst, &nlen);
         const uint32_t incl = wave_incl_scan_dpp(len);
@@ -2163,19 +2208,34 @@ sl_lookup_kernel(TableView tv, uint32_t wlog, uint32_t nslices, int64_t ntiles, 
         const __amdgpu_buffer_rsrc_t rres =
             __builtin_amdgcn_make_buffer_rsrc((void*)(res + tcu * kSlTile), 0, 64 * kSlTile * 4, 0x00020000);
         uint32_t kb = 0;  // segments started before the current row
+        DFP_PH(0);
         for (uint32_t w0 = 0; w0 < R; w0 += W) {
+            DFP_PH_CNT(6);
             if (lane < W / 64) smask[lane] = 0;
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
             __builtin_amdgcn_wave_barrier();
             if (len != 0 && excl >= w0 && excl < w0 + W) atomicOr(&smask[(excl - w0) >> 6], 1ull << ((excl - w0) & 63));
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
             __builtin_amdgcn_wave_barrier();
-            uint32_t off[W / 64];  // the entry's index (or kOob) | owner rank << 26
+            // Measured (r04) and not kept, C2 serialized (tools/lookup_ablate.py, lookup with
+            // its stores / entry loads / table reads removed: 138 / 122 / 129 / 113 us with
+            // none of the three): every row's start mask from one LDS read, the owners' bases
+            // and the entry loads in branch-free groups of 8 rows, and the refs stored one
+            // window late (after the next window's loads): 146 us (104 without stores) —
+            // a shorter skeleton, but the stores then cost 41 us; the 2048-position form of it
+            // spills. The hashed analogue (first bucket lines of two rows read together, the
+            // correction scans interleaved): C2h 56.8K -> 55.5K Mrows/s.
+            constexpr int NU = W / 64;  // rows of 64 positions per window
+            uint32_t off[NU];      // the entry's index (or kOob) | owner rank << 26
             uint32_t off_end = 0;  // hashed: bit u = this lane's position u ends its fragment
             using EV = typename std::conditional<HASHED, unsigned long long, uint32_t>::type;
-            EV ev[W / 64];
+            EV ev[NU];
+            // Measured (r04): reading every row's start mask at once (one LDS read, then
+            // v_readlane per row) and the owners' bases in batches of 8 rows took the C2
+            // lookup 133 -> 150 us (128 VGPRs, spills); the per-row LDS round trips below
+            // overlap across the 16 waves of the CU.
 #pragma unroll
-            for (int u = 0; u < W / 64; ++u) {
+            for (int u = 0; u < NU; ++u) {
                 off[u] = kOob;
                 if (w0 + u * 64 >= R) continue;  // uniform: past the run
                 const uint32_t r = w0 + u * 64 + lane;
@@ -2199,16 +2259,20 @@ sl_lookup_kernel(TableView tv, uint32_t wlog, uint32_t nslices, int64_t ntiles, 
                         uint2, __builtin_amdgcn_raw_buffer_load_b64(rko, (int)(o * 8), 0, 0));
                     ev[u] = ((unsigned long long)v.y << 32) | v.x;
                 } else {
-                    ev[u] = __builtin_amdgcn_raw_buffer_load_b16(rko, (int)(o * 2), 0, 0);
+                    // ablation 1024: no entry loads (wrong pairs)
+                    ev[u] = DFP_ABL(1024) ? (r & 0x7FFF) : __builtin_amdgcn_raw_buffer_load_b16(rko, (int)(o * 2), 0, 0);
                 }
                 off[u] = o | ((k & 63) << 26);  // the owner's rank (its tile lane: slane, read only for a correction)
             }
+            DFP_PH(1);
+            DFP_PH_WAIT();
+            DFP_PH(2);
+            if constexpr (HASHED) {
 #pragma unroll
-            for (int u = 0; u < W / 64; ++u) {
-                if (w0 + u * 64 >= R) continue;  // uniform: past the run
-                const uint32_t o = off[u] & kOobMask;
-                uint32_t v, c;  // ref and its row count (kCountUnknown: in its segment header)
-                if constexpr (HASHED) {
+                for (int u = 0; u < NU; ++u) {
+                    if (w0 + u * 64 >= R) continue;  // uniform: past the run
+                    const uint32_t o = off[u] & kOobMask;
+                    uint32_t v, c;  // ref and its row count (kCountUnknown: in its segment header)
                     const unsigned long long sk = ev[u];
                     if (o == kOob) {
                         v = kMiss;  // no store, no correction
@@ -2222,24 +2286,15 @@ sl_lookup_kernel(TableView tv, uint32_t wlog, uint32_t nslices, int64_t ntiles, 
                     } else {
                         v = lds_bucket_ref(reinterpret_cast<const uint4*>(s_tab), tv.nb, sbase, cmask, sk, &c);
                     }
-                } else {
-                    v = s_tab[ev[u] & ((1u << wlog) - 1)];
-                    c = 1;
-                    if (o != kOob && (v == kMiss || (v & kDupFlag))) {
-                        const uint32_t c4 = tv.off_mask == kPackedMask ? ((v >> 27) & 15u) : 0u;
-                        c = v == kMiss ? 0u : c4 ? c4 : kCountUnknown;
+                    // counts not inline: read from the segment header in a wave-uniform branch
+                    // that waits there. Merged into the common path, that load's wait was an
+                    // s_waitcnt vmcnt(0) on every row — for the previous rows' ref stores (loads
+                    // and stores share vmcnt): one store round trip per 64 entries.
+                    if (__ballot(c == kCountUnknown) != 0) {
+                        if (c == kCountUnknown) c = tv.dup_rows[v & tv.off_mask];
+                        asm volatile("" : "+v"(c));
                     }
-                }
-                // counts not inline: read from the segment header in a wave-uniform branch
-                // that waits there. Merged into the common path, that load's wait was an
-                // s_waitcnt vmcnt(0) on every row — for the previous rows' ref stores (loads
-                // and stores share vmcnt): one store round trip per 64 entries.
-                if (__ballot(c == kCountUnknown) != 0) {
-                    if (c == kCountUnknown) c = tv.dup_rows[v & tv.off_mask];
-                    asm volatile("" : "+v"(c));
-                }
-                __builtin_amdgcn_raw_buffer_store_b32(v, rres, (int)(o * 4), 0, 0);
-                if constexpr (HASHED) {
+                    __builtin_amdgcn_raw_buffer_store_b32(v, rres, (int)(o * 4), 0, 0);
                     uint32_t d = c - 1u;  // kOob: c = 1
                     if (d != 0xFFFFFFFFu && d >= kBigCorr) {
                         atomicAdd(&tcnt[tc + slane[off[u] >> 26]], (unsigned long long)d);
@@ -2248,24 +2303,46 @@ sl_lookup_kernel(TableView tv, uint32_t wlog, uint32_t nslices, int64_t ntiles, 
                     corr_run += wave_incl_scan_dpp(d);
                     if (off_end & (1u << u)) scst[off[u] >> 26] = corr_run;
                     corr_run = (uint32_t)__builtin_amdgcn_readlane((int)corr_run, 63);
-                    continue;
                 }
-                // a fragment start (start mask bit) records the running sum before it
-                const bool odd = o != kOob && c != 1;
-                if (__ballot(odd) != 0) {
-                    if (odd) sodd[off[u] >> 26] = 1;  // the emission's count-free path is off for its tile
-                    uint32_t d = odd ? c - 1u : 0u;
-                    if (d != 0xFFFFFFFFu && d >= kBigCorr) {  // a huge duplicate: straight to its tile
-                        atomicAdd(&tcnt[tc + slane[off[u] >> 26]], (unsigned long long)d);
-                        d = 0;
+            } else {
+#pragma unroll
+                for (int u = 0; u < NU; ++u) {
+                    if (w0 + u * 64 >= R) continue;  // uniform: past the run
+                    const uint32_t o = off[u] & kOobMask;
+                    // ablation 2048: no table read (wrong pairs)
+                    const uint32_t v = DFP_ABL(2048) ? ev[u] : s_tab[ev[u] & ((1u << wlog) - 1)];
+                    uint32_t c = 1;  // ref and its row count (kCountUnknown: in its segment header)
+                    if (o != kOob && (v == kMiss || (v & kDupFlag))) {
+                        const uint32_t c4 = tv.off_mask == kPackedMask ? ((v >> 27) & 15u) : 0u;
+                        c = v == kMiss ? 0u : c4 ? c4 : kCountUnknown;
                     }
-                    const uint32_t ci = wave_incl_scan_dpp(d) + corr_run;
-                    if ((smask[u] >> lane) & 1ull) scst[off[u] >> 26] = ci - d;
-                    corr_run = (uint32_t)__builtin_amdgcn_readlane((int)ci, 63);
-                } else if (corr_run != 0) {  // uniform
-                    if ((smask[u] >> lane) & 1ull) scst[off[u] >> 26] = corr_run;
+                    // counts not inline: read from the segment header in a wave-uniform branch
+                    // that waits there. Merged into the common path, that load's wait was an
+                    // s_waitcnt vmcnt(0) on every row — for the previous rows' ref stores (loads
+                    // and stores share vmcnt): one store round trip per 64 entries.
+                    if (__ballot(c == kCountUnknown) != 0) {
+                        if (c == kCountUnknown) c = tv.dup_rows[v & tv.off_mask];
+                        asm volatile("" : "+v"(c));
+                    }
+                    if (!DFP_ABL(512)) __builtin_amdgcn_raw_buffer_store_b32(v, rres, (int)(o * 4), 0, 0);  // 512: no stores
+                    // a fragment start (start mask bit) records the running sum before it
+                    const bool odd = o != kOob && c != 1;
+                    if (__ballot(odd) != 0) {
+                        if (odd) sodd[off[u] >> 26] = 1;  // the emission's count-free path is off for its tile
+                        uint32_t d = odd ? c - 1u : 0u;
+                        if (d != 0xFFFFFFFFu && d >= kBigCorr) {  // a huge duplicate: straight to its tile
+                            atomicAdd(&tcnt[tc + slane[off[u] >> 26]], (unsigned long long)d);
+                            d = 0;
+                        }
+                        const uint32_t ci = wave_incl_scan_dpp(d) + corr_run;
+                        if ((smask[u] >> lane) & 1ull) scst[off[u] >> 26] = ci - d;
+                        corr_run = (uint32_t)__builtin_amdgcn_readlane((int)ci, 63);
+                    } else if (corr_run != 0) {  // uniform
+                        if ((smask[u] >> lane) & 1ull) scst[off[u] >> 26] = corr_run;
+                    }
                 }
             }
+            DFP_PH(3);
         }
         // one atomic per tile that has a correction (64 contiguous counters)
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -2286,7 +2363,14 @@ sl_lookup_kernel(TableView tv, uint32_t wlog, uint32_t nslices, int64_t ntiles, 
         }
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         __builtin_amdgcn_wave_barrier();
+        DFP_PH(4);
     }
+    DFP_PH_FLUSH();
+#ifdef DFP_HJ_ABLATIONS
+    __syncthreads();
+    DFP_DBG_TS(g_dbg_lk_ts, 2, wall_clock64());
+    DFP_DBG_TS(g_dbg_lk_ts, 3, dbg_hwid());
+#endif
 }
 
 // S1 of the hashed sliced probe: per 16384-row tile, the valid rows sorted by slice
@@ -2308,7 +2392,10 @@ hs_partition_kernel(uint32_t nb, uint32_t slog, uint32_t s0, uint32_t nslices, c
     const uint32_t nbins = nslices + 1;
     const bool probe = tcnt != nullptr;  // else the hashed frag build's partition of one build segment
     const bool later = probe && hdr == nullptr;
-    if (probe && !later && blockIdx.x == 0 && threadIdx.x == 0) hdr[0] = hdr[1] = 0;  // workspace header (error word)
+    if (probe && !later && blockIdx.x == 0 && threadIdx.x == 0) {
+        hdr[0] = hdr[1] = 0;  // workspace header (error word)
+        tcnt[ntiles] = 0;     // the emission's tile counter
+    }
     int64_t k[kSlGroups][4], nk[kSlGroups][4];
     auto load = [&](int64_t t, int64_t (&dst)[kSlGroups][4]) {
 #pragma unroll
@@ -2422,11 +2509,13 @@ sl_emit_kernel(TableView tv, const uint32_t* __restrict__ tent, const uint16_t* 
                const uint32_t* __restrict__ res, const uint32_t* __restrict__ probe_ids, uint32_t pbase,
                const unsigned long long* __restrict__ tcnt, int64_t ntiles, uint64_t* __restrict__ out_b,
                uint32_t* __restrict__ out_p, int64_t cap, int64_t* __restrict__ d_total,
-               const uint16_t* __restrict__ wcnt) {  // entries per 2048-row range (null: always count)
+               const uint16_t* __restrict__ wcnt,  // entries per 2048-row range (null: always count)
+               unsigned long long* __restrict__ dyn) {  // tile counter (zeroed by S1), null: static tiles
     __shared__ __attribute__((aligned(16))) uint32_t s_ref[kSlTile];  // the tile's refs, kMiss = none
     __shared__ unsigned long long s_w[kSlEmitThreads / 64];
     __shared__ unsigned long long s_pre[kSlEmitThreads / 64];
     __shared__ uint32_t s_own[kSlEmitThreads / 64][64];  // per wave: owner markers of one output window
+    __shared__ int64_t s_nxt;                              // dyn: the tile after the next one
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     constexpr int U = kSlTile / (kSlEmitThreads * 4);  // 8 x (4 rows + 4 refs) per thread
     uint2 e4[U];
@@ -2435,7 +2524,10 @@ sl_emit_kernel(TableView tv, const uint32_t* __restrict__ tent, const uint16_t* 
     // count-free tiles: every entry's key had exactly one row (no correction flag), so a
     // wave's pair count is its range's entry count and a row's count is 0 (kMiss) or 1
     uint32_t nflag = 1, nwc = 0;
-    // Persistent: workgroup b takes tiles b, b + grid, ...; the next tile's entries are
+    // Persistent: workgroup b takes tile b, then tiles b + grid, b + 2 grid, ... (static)
+    // or, with dyn, the grid + i-th tile for the i-th draw of the tile counter (every
+    // workgroup's tiles still ascend, and a slow CU takes fewer tiles: the static grid's
+    // workgroups ended 110-153 us into a 154 us C2 emission); the next tile's entries are
     // loaded while this tile's pairs are counted and written. All loads of a tile are
     // issued at once, after its entry count. A tile's output offset is the sum of the
     // pair counts (tcnt, final once S2 is done) of the tiles below it: the first tile's
@@ -2463,17 +2555,26 @@ sl_emit_kernel(TableView tv, const uint32_t* __restrict__ tent, const uint16_t* 
             }
         }
     };
+    DFP_DBG_TS(g_dbg_em_ts, 0, wall_clock64());
     int64_t tile = blockIdx.x;
     if (tile < ntiles) fetch(tile);
     unsigned long long base = 0;  // the current tile's output offset
+    int64_t next;                 // this workgroup's next tile
     {
         const unsigned long long v = wave_sum<unsigned long long>(count_sum(0, min<int64_t>(tile, ntiles)));
         if (lane == 0) s_pre[wave] = v;
+        if (dyn != nullptr && threadIdx.x == 0) s_nxt = (int64_t)gridDim.x + (int64_t)atomicAdd(dyn, 1ull);
         __syncthreads();
         for (int w = 0; w < kSlEmitThreads / 64; ++w) base += s_pre[w];
+        next = dyn != nullptr ? s_nxt : tile + gridDim.x;
         __syncthreads();
     }
-    for (; tile < ntiles; tile += gridDim.x) {
+    DFP_DBG_TS(g_dbg_em_ts, 1, wall_clock64());
+    while (tile < ntiles) {
+        // dyn: draw the tile after the next one now; its value is needed only at the end
+        // of this tile, so the atomic's round trip hides behind the tile's work
+        unsigned long long draw = 0;
+        if (dyn != nullptr && threadIdx.x == 0 && next < ntiles) draw = atomicAdd(dyn, 1ull);
         const int64_t tile0 = tile * kSlTile;
         for (int i = threadIdx.x * 4; i < kSlTile; i += kSlEmitThreads * 4)
             *reinterpret_cast<uint4*>(s_ref + i) = make_uint4(kMiss, kMiss, kMiss, kMiss);
@@ -2489,7 +2590,6 @@ sl_emit_kernel(TableView tv, const uint32_t* __restrict__ tent, const uint16_t* 
         __syncthreads();
         const bool fast = wcnt != nullptr && nflag == 0;  // this tile's (read before the prefetch)
         const uint32_t fast_wc = nwc;
-        const int64_t next = tile + gridDim.x;
         if (next < ntiles) fetch(next);
         // pass 1: this wave's pair count (a count-free tile: its entries in the wave's range)
         const int row_w = wave * kSlWaveRows;
@@ -2563,6 +2663,10 @@ sl_emit_kernel(TableView tv, const uint32_t* __restrict__ tent, const uint16_t* 
                     total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
                     const uint32_t excl = incl - c;
                     uint32_t carry = 0;
+                    // Measured (r04) and not kept: each window's pairs stored one window later
+                    // (the next window's segment read issued first, two register sets): C3
+                    // emission 666 -> 676 us — the compiler's in-order vmcnt waits still put a
+                    // store round trip in every iteration.
                     for (uint32_t w0 = 0; w0 < total; w0 += 64) {
                         own[lane] = 0;
                         __builtin_amdgcn_wave_barrier();
@@ -2593,10 +2697,35 @@ sl_emit_kernel(TableView tv, const uint32_t* __restrict__ tent, const uint16_t* 
         // only now: a wait on them would also wait for the next tile's entries in flight)
         const unsigned long long pre = wave_sum<unsigned long long>(next < ntiles ? count_sum(tile, next) : 0ull);
         if (lane == 0) s_pre[wave] = pre;
-        __syncthreads();  // s_ref, s_w and s_pre are rewritten for the next tile
+        if (dyn != nullptr && threadIdx.x == 0) s_nxt = next < ntiles ? (int64_t)gridDim.x + (int64_t)draw : ntiles;
+        __syncthreads();  // s_ref, s_w, s_pre and s_nxt are rewritten for the next tile
         for (int w = 0; w < kSlEmitThreads / 64; ++w) base += s_pre[w];
+        tile = next;
+        next = dyn != nullptr ? s_nxt : next + gridDim.x;
     }
+    DFP_DBG_TS(g_dbg_em_ts, 2, wall_clock64());
+    DFP_DBG_TS(g_dbg_em_ts, 3, dbg_hwid());
 }
+
+#ifdef DFP_HJ_ABLATIONS
+// diagnostic build only: copy the last sliced lookup's (which = 0) or emission's (1)
+// per-workgroup timeline (4 u64 per workgroup, see g_dbg_lk_ts) to host memory
+extern "C" __attribute__((visibility("default"))) int hj_debug_timeline(int which, unsigned long long* host, int nblocks) {
+    const size_t bytes = sizeof(unsigned long long) * 4 * (size_t)std::min(nblocks, 65536);
+    return which == 0 ? (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_dbg_lk_ts), bytes)
+                      : (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_dbg_em_ts), bytes);
+}
+// diagnostic build only: the lookup's phase cycle sums (g_dbg_lk_ph, 8 u64); reset = 1
+// zeroes them after the copy
+extern "C" __attribute__((visibility("default"))) int hj_debug_lookup_phases(unsigned long long* host, int reset) {
+    int e = (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_dbg_lk_ph), 8 * sizeof(unsigned long long));
+    if (e == 0 && reset) {
+        static const unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        e = (int)hipMemcpyToSymbol(HIP_SYMBOL(g_dbg_lk_ph), z, sizeof(z));
+    }
+    return e;
+}
+#endif
 
 // ---------------------------------------------------------------------------
 // table queries (not on the hot path)
@@ -3696,16 +3825,20 @@ hipError_t launch_probe_sliced(int key_bytes, const TableView& tv, const void* k
 #ifdef DFP_HJ_ABLATIONS
     // diagnostic build only (wrong pairs): emit 1 no stores, 2 no entries, 8 no duplicate
     // segment reads; lookup 4 no bucket lookup (hashed), 128 plain item order
-    static const bool abl_set = [] {
+    {  // re-read per call, so that a tool can switch ablations between probes
+        static int abl_last = -1;
         const char* ev = getenv("DFP_HJ_ABLATE");
         const int v = ev ? atoi(ev) : 0;
-        return hipMemcpyToSymbol(HIP_SYMBOL(kAblDev), &v, sizeof(v)) == hipSuccess;
-    }();
-    (void)abl_set;
+        if (v != abl_last && hipMemcpyToSymbol(HIP_SYMBOL(kAblDev), &v, sizeof(v)) == hipSuccess) abl_last = v;
+    }
 #endif
     const size_t tab_lds = hashed ? (sizeof(Bucket) << kHsSliceLog) : (sizeof(uint32_t) << wlog);
-    const void* lk = hashed ? (const void*)sl_lookup_kernel<true, kSlOwnWinHashed>
-                            : (const void*)sl_lookup_kernel<false, kSlOwnWin>;
+    // dense lookup window: 2048 positions (32 per lane) or DFP_HJ_SL_DENSE_WIN=1024
+    // (measured equal on C2 and C3, r04)
+    static const bool dense_w1024 = sl_env_int("DFP_HJ_SL_DENSE_WIN", kSlOwnWin) == 1024;
+    const void* lk = hashed        ? (const void*)sl_lookup_kernel<true, kSlOwnWinHashed>
+                     : dense_w1024 ? (const void*)sl_lookup_kernel<false, 1024>
+                                   : (const void*)sl_lookup_kernel<false, kSlOwnWin>;
     e = hipFuncSetAttribute(lk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)tab_lds);
     if (e != hipSuccess) return e;
     // (slice, tile range) work items: about 768 of them, so that the resident workgroups
@@ -3763,12 +3896,20 @@ hipError_t launch_probe_sliced(int key_bytes, const TableView& tv, const void* k
         if (hashed)
             sl_lookup_kernel<true, kSlOwnWinHashed><<<nsl * parts, kSlThreads, tab_lds, s>>>(
                 tp, wlog, nsl, nt, parts, w.ko, w.res, w.toff, w.tcnt, s0);
+        else if (dense_w1024)
+            sl_lookup_kernel<false, 1024><<<nsl * parts, kSlThreads, tab_lds, s>>>(tp, wlog, nsl, nt, parts, w.ko, w.res,
+                                                                                 w.toff, w.tcnt, 0u);
         else
             sl_lookup_kernel<false, kSlOwnWin><<<nsl * parts, kSlThreads, tab_lds, s>>>(tp, wlog, nsl, nt, parts, w.ko,
                                                                                       w.res, w.toff, w.tcnt, 0u);
     }
     const bool ri = tv.row_ids != nullptr, pi = probe_ids != nullptr;
     // DFP_HJ_COUNT_FREE=0: every tile takes the emission's count pass (A/B of the count-free path)
+    // DFP_HJ_EMIT_DYN=0: the emission's static tile schedule (A/B of the tile counter)
+    static const bool emit_dyn = [] {
+        const char* e = getenv("DFP_HJ_EMIT_DYN");
+        return !(e != nullptr && e[0] == '0');
+    }();
     static const bool count_free = [] {
         const char* e = getenv("DFP_HJ_COUNT_FREE");
         return !(e != nullptr && e[0] == '0');
@@ -3777,7 +3918,8 @@ hipError_t launch_probe_sliced(int key_bytes, const TableView& tv, const void* k
 #define DFP_SLE(RI, PI)                                                                                           \
     sl_emit_kernel<RI, PI><<<egrid, kSlEmitThreads, 0, s>>>(tv, w.tent, w.rl, w.res, probe_ids, pbase, w.tcnt, nt,   \
                                                            out_b, out_p, cap, d_total,                      \
-                                                           hashed || !count_free ? nullptr : w.wcnt)
+                                                           hashed || !count_free ? nullptr : w.wcnt,          \
+                                                           emit_dyn ? w.tcnt + nt : nullptr)
     if (ri && pi) DFP_SLE(true, true);
     else if (ri) DFP_SLE(true, false);
     else if (pi) DFP_SLE(false, true);
