@@ -678,7 +678,7 @@ def main():
             "cpu_baseline": cpu,
         }
         if use_dist:
-            line["exchange_ms"] = round(float(np.median(job.exchange_ms)), 4)
+            line["exchange_ms"] = _median(job.exchange_ms)
             line["plan"] = plan
             if plan == "sharded":
                 line["native_build_side"] = bool(getattr(dj, "last_native", False))
@@ -801,7 +801,9 @@ class ShardedJob:
         self.host_ms.append((time.perf_counter() - h0) * 1e3)
         self.dj.events = None
         ev["end"].record(cur)
-        prev, self._pending = self._pending, (table, result, ev)
+        # the native build side (hj_dist_build_sharded: one C call) records no partition /
+        # exchange events: its exchange is inside build_ms
+        prev, self._pending = self._pending, (table, result, ev, bool(getattr(self.dj, "last_native", False)))
         if prev is not None:
             self._collect(*prev)
 
@@ -810,13 +812,14 @@ class ShardedJob:
             pending, self._pending = self._pending, None
             self._collect(*pending)
 
-    def _collect(self, table, result, ev):
+    def _collect(self, table, result, ev, native):
         b, _ = result()
         self.matches = int(b.numel())
         ev["end"].synchronize()
         # the build side (plan, exchange, local build, gathers) on the build stream; the
         # probe from its launch to its end on the probe stream (with any wait for the table)
-        self.exchange_ms.append(ev["partitioned"].elapsed_time(ev["exchanged"]))
+        if not native:
+            self.exchange_ms.append(ev["partitioned"].elapsed_time(ev["exchanged"]))
         self.build_ms.append(ev["build_start"].elapsed_time(ev["build_end"]))
         self.probe_ms.append(ev["probe_start"].elapsed_time(ev["end"]))
         table.close()

@@ -644,7 +644,7 @@ chunk_build_kernel(uint32_t nb, uint32_t clog2, uint32_t nchunks, const uint32_t
             }
         };
         if (in_regs) {
-    #pragma unroll
+#pragma unroll
             for (int u = 0; u < kChunkRegRows; ++u)
                 if (rslot[u] >= 0) place(rslot[u], rrow[u]);
         } else {
@@ -666,10 +666,10 @@ chunk_build_kernel(uint32_t nb, uint32_t clog2, uint32_t nchunks, const uint32_t
             const unsigned n = d_cnt[li], off = d_off[li];
             if (n <= (unsigned)kSmallSeg) {
                 uint32_t v[16];
-    #pragma unroll
+#pragma unroll
                 for (int i = 0; i < 16; ++i) v[i] = (i < (int)n) ? dup_rows[off + 1 + i] : 0u;
                 sort16_desc(v);
-    #pragma unroll
+#pragma unroll
                 for (int i = 0; i < 16; ++i)
                     if (i < (int)n) dup_rows[off + 1 + i] = v[i];
             }
@@ -1379,28 +1379,55 @@ sl_partition_kernel(int64_t dmin, uint64_t drange, uint32_t wlog, uint32_t nslic
     __syncthreads();
     // per row: entry (offset << 14 | row) and (slice << 14 | rank in slice), ~0 = no entry
     uint32_t e[kSlGroups][4], sr[kSlGroups][4];
+    // the next group's keys load while this group's rows are ranked (one load round trip
+    // per tile instead of one per group; two groups of keys fit the 64-register budget).
+    // A whole aligned tile takes straight 16-byte loads with no branch between the groups
+    // (a branch would make the next group's loads wait at its join).
+    auto groups = [&](auto full_tag) {
+        constexpr bool FULL = decltype(full_tag)::value;
+        int64_t kn[4];
+        auto load_group = [&](int g, int64_t (&dst)[4]) {
+            const int loc0 = g * (kSlThreads * 4) + threadIdx.x * 4;
+            if constexpr (FULL && sizeof(K) == 8) {
+                const v2i64* p = reinterpret_cast<const v2i64*>(reinterpret_cast<const K*>(keys) + tile0 + loc0);
+                const v2i64 a = p[0], b = p[1];
+                dst[0] = a.x; dst[1] = a.y; dst[2] = b.x; dst[3] = b.y;
+            } else if constexpr (FULL) {
+                const int4 a = *reinterpret_cast<const int4*>(reinterpret_cast<const K*>(keys) + tile0 + loc0);
+                dst[0] = a.x; dst[1] = a.y; dst[2] = a.z; dst[3] = a.w;
+            } else if (nt & 1) {
+                load4<K, true>(keys, tile0 + loc0, n, vec, dst);
+            } else {
+                load4<K>(keys, tile0 + loc0, n, vec, dst);
+            }
+        };
+        load_group(0, kn);
 #pragma unroll
-    for (int g = 0; g < kSlGroups; ++g) {
-        const int loc0 = g * (kSlThreads * 4) + threadIdx.x * 4;
-        int64_t k[4];
-        if (nt & 1) load4<K, true>(keys, tile0 + loc0, n, vec, k);
-        else load4<K>(keys, tile0 + loc0, n, vec, k);
+        for (int g = 0; g < kSlGroups; ++g) {
+            const int loc0 = g * (kSlThreads * 4) + threadIdx.x * 4;
+            int64_t k[4];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int64_t row = tile0 + loc0 + q;
-            const uint64_t idx = (uint64_t)k[q] - (uint64_t)dmin;
-            const bool ok = row < n && (!HAS_VALID || bit_valid(valid, voff, row)) && idx < drange;
-            const uint32_t sl = (uint32_t)(idx >> wlog);
-            e[g][q] = ((uint32_t)(idx & ((1u << wlog) - 1)) << kSlTileLog) | (uint32_t)(loc0 + q);
-            sr[g][q] = ok ? (sl << kSlTileLog) | atomicAdd(&s_hist[sl], 1u) : 0xFFFFFFFFu;
+            for (int q = 0; q < 4; ++q) k[q] = kn[q];
+            if (g + 1 < kSlGroups) load_group(g + 1, kn);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int64_t row = tile0 + loc0 + q;
+                const uint64_t idx = (uint64_t)k[q] - (uint64_t)dmin;
+                const bool ok = row < n && (!HAS_VALID || bit_valid(valid, voff, row)) && idx < drange;
+                const uint32_t sl = (uint32_t)(idx >> wlog);
+                e[g][q] = ((uint32_t)(idx & ((1u << wlog) - 1)) << kSlTileLog) | (uint32_t)(loc0 + q);
+                sr[g][q] = ok ? (sl << kSlTileLog) | atomicAdd(&s_hist[sl], 1u) : 0xFFFFFFFFu;
+            }
+            if (wcnt != nullptr) {  // probe: entries per emission range (a wave's rows of one group share a range)
+                uint32_t ws = 0;    // the wave's entries in group g: scalar popcounts of the entry ballots
+#pragma unroll
+                for (int q = 0; q < 4; ++q) ws += (uint32_t)__popcll(__ballot(sr[g][q] != 0xFFFFFFFFu));
+                if ((threadIdx.x & 63) == 0 && ws) atomicAdd(&s_wc[(g * (kSlThreads * 4) + threadIdx.x * 4) / kSlRangeRows], ws);
+            }
         }
-        if (wcnt != nullptr) {  // probe: entries per emission range (a wave's rows of one group share a range)
-            uint32_t ws = 0;    // the wave's entries in group g: scalar popcounts of the entry ballots
-#pragma unroll
-            for (int q = 0; q < 4; ++q) ws += (uint32_t)__popcll(__ballot(sr[g][q] != 0xFFFFFFFFu));
-            if ((threadIdx.x & 63) == 0 && ws) atomicAdd(&s_wc[(g * (kSlThreads * 4) + threadIdx.x * 4) / kSlRangeRows], ws);
-        }
-    }
+    };
+    if (vec && tile0 + kSlTile <= n && !(nt & 1)) groups(std::true_type{});
+    else groups(std::false_type{});
     __syncthreads();
     // the range counts leave s_ent before the scan's barriers (its wave totals use s_ent[0, 16))
     const uint32_t my_wc = (wcnt != nullptr && threadIdx.x < kSlRanges) ? s_wc[threadIdx.x] : 0u;
@@ -2092,7 +2119,9 @@ __device__ unsigned long long g_dbg_lk_ph[8];
 
 template <bool HASHED, int W>
 __global__ void __launch_bounds__(kSlThreads)
-sl_lookup_kernel(TableView tv, uint32_t wlog, uint32_t nslices, int64_t ntiles, uint32_t parts,
+sl_lookup_kernel(TableView tv, uint32_t wlog, uint32_t nslices, int64_t ntiles, uint32_t parts, uint32_t s1,
+                 uint32_t parts2,  // slices [0, s1): `parts` items each; [s1, nslices): `parts2` smaller ones, last
+                 int early,        // 1: each wave sets up its first block and issues its entry loads before the image barrier
                  const void* __restrict__ ko, uint32_t* __restrict__ res, const uint16_t* __restrict__ toff,
                  unsigned long long* __restrict__ tcnt, uint32_t soff) {  // soff: first slice of this pass (hashed)
     extern __shared__ __attribute__((aligned(16))) uint32_t s_tab[];  // dense: 2^wlog refs; hashed: 2048 buckets
@@ -2105,8 +2134,23 @@ sl_lookup_kernel(TableView tv, uint32_t wlog, uint32_t nslices, int64_t ntiles, 
     __shared__ uint32_t s_end[HASHED ? kSlThreads : 1];  // hashed, per wave: end position of each fragment, by rank
     __shared__ unsigned long long s_mask[kSlThreads / 64][W / 64];
     DFP_DBG_TS(g_dbg_lk_ts, 0, wall_clock64());
-    const uint32_t item = DFP_ABL(128) ? blockIdx.x : xcd_item(blockIdx.x, gridDim.x);
-    const uint32_t s = item % nslices, part = item / nslices;
+    // Items: the first s1 slices in `parts` parts each, then the rest in `parts2` smaller
+    // ones; every XCD runs its share of the first stage before its share of the second
+    // (block b on XCD b % 8 as b / 8-th), so the last round is of small items (the even
+    // split left 0.59 of a round: CUs 13 % idle, r04 timelines)
+    const uint32_t n1 = s1 * parts;
+    uint32_t s, part, np;  // slice, part, parts of this slice
+    if (blockIdx.x < n1) {
+        const uint32_t item = DFP_ABL(128) ? blockIdx.x : xcd_item(blockIdx.x, n1);
+        s = item % s1;
+        part = item / s1;
+        np = parts;
+    } else {
+        const uint32_t item = DFP_ABL(128) ? blockIdx.x - n1 : xcd_item(blockIdx.x - n1, gridDim.x - n1);
+        s = s1 + item % (nslices - s1);
+        part = item / (nslices - s1);
+        np = parts2;
+    }
     uint32_t sbase = 0;  // hashed: first bucket of the slice
     // the slice's image: whole 1 KB pieces by LDS DMA (global_load_lds_dwordx4, one wave
     // instruction per piece, every piece of a wave in flight at once, no VGPR round trip),
@@ -2134,11 +2178,21 @@ sl_lookup_kernel(TableView tv, uint32_t wlog, uint32_t nslices, int64_t ntiles, 
         const uint32_t done = dma(reinterpret_cast<const uint4*>(dense + base), len >> 2) * 4;
         for (uint32_t i = done + threadIdx.x; i < len; i += kSlThreads) s_tab[i] = dense[base + i];
     }
-    __syncthreads();
+    // The image is needed only from the first row lookup on: with `early`, each wave sets
+    // up its first block and issues that window's entry loads while the image loads, and
+    // meets the barrier there (every wave exactly once: a wave without blocks at the end).
+    bool img_ready = early == 0;
+    if (img_ready) __syncthreads();
+    auto wait_image = [&]() {
+        if (!img_ready) {
+            __syncthreads();
+            img_ready = true;
+        }
+    };
     DFP_DBG_TS(g_dbg_lk_ts, 1, wall_clock64());
     // part boundaries on 64-tile blocks (the transposed bounds' granule)
     const int64_t nblk = (ntiles + 63) / 64;
-    const int64_t ta = nblk * part / parts * 64, tb = min<int64_t>(nblk * (part + 1) / parts * 64, ntiles);
+    const int64_t ta = nblk * part / np * 64, tb = min<int64_t>(nblk * (part + 1) / np * 64, ntiles);
     const int64_t nbins = nslices + 1;
     // per wave: the non-empty segments' bases (tile-relative position - excl) by rank, and
     // one 64-bit start mask per 64-position row of the window
@@ -2264,6 +2318,7 @@ sl_lookup_kernel(TableView tv, uint32_t wlog, uint32_t nslices, int64_t ntiles, 
                 }
                 off[u] = o | ((k & 63) << 26);  // the owner's rank (its tile lane: slane, read only for a correction)
             }
+            wait_image();
             DFP_PH(1);
             DFP_PH_WAIT();
             DFP_PH(2);
@@ -2365,6 +2420,7 @@ sl_lookup_kernel(TableView tv, uint32_t wlog, uint32_t nslices, int64_t ntiles, 
         __builtin_amdgcn_wave_barrier();
         DFP_PH(4);
     }
+    wait_image();  // a wave without blocks still meets the image barrier
     DFP_PH_FLUSH();
 #ifdef DFP_HJ_ABLATIONS
     __syncthreads();
@@ -3883,6 +3939,31 @@ hipError_t launch_probe_sliced(int key_bytes, const TableView& tv, const void* k
         }
         uint32_t parts = std::max<uint32_t>(1, (target + nsl - 1) / nsl);
         parts = (uint32_t)std::min<int64_t>(parts, (nt + 63) / 64);
+        // the last round of small items: the slices beyond whole rounds of `parts` items
+        // over the CUs split so that they fill about one round (DFP_HJ_SL_TAIL=0: even split)
+        uint32_t s1 = nsl, parts2 = parts;
+        {
+            static const bool tail_on = [] {
+                const char* ev = getenv("DFP_HJ_SL_TAIL");
+                return !(ev != nullptr && ev[0] == '0');
+            }();
+            const uint32_t cus = (uint32_t)sl_num_cus();
+            const uint32_t rounds = nsl * parts / cus;
+            const uint32_t a = rounds * cus / parts;  // slices in the whole rounds
+            if (tail_on && rounds >= 1 && a < nsl && a > 0) {
+                const uint32_t p2 = std::min<uint32_t>(cus / (nsl - a), (uint32_t)std::min<int64_t>(8 * parts, (nt + 63) / 64));
+                if (p2 > parts) {
+                    s1 = a;
+                    parts2 = p2;
+                }
+            }
+        }
+        const unsigned lgrid = s1 * parts + (nsl - s1) * parts2;
+        // DFP_HJ_SL_EARLY=0: the image barrier right after the image load (A/B)
+        static const int early = [] {
+            const char* ev = getenv("DFP_HJ_SL_EARLY");
+            return (ev != nullptr && ev[0] == '0') ? 0 : 1;
+        }();
         if (pass == 0 && built != nullptr) {  // S1 reads no table memory: the build may still be running
             e = hipStreamWaitEvent(s, built, 0);
             if (e != hipSuccess) return e;
@@ -3894,14 +3975,14 @@ hipError_t launch_probe_sliced(int key_bytes, const TableView& tv, const void* k
             tp.drange = std::min<uint64_t>(tv.drange - lo, (uint64_t)nsl << wlog);
         }
         if (hashed)
-            sl_lookup_kernel<true, kSlOwnWinHashed><<<nsl * parts, kSlThreads, tab_lds, s>>>(
-                tp, wlog, nsl, nt, parts, w.ko, w.res, w.toff, w.tcnt, s0);
+            sl_lookup_kernel<true, kSlOwnWinHashed><<<lgrid, kSlThreads, tab_lds, s>>>(
+                tp, wlog, nsl, nt, parts, s1, parts2, early, w.ko, w.res, w.toff, w.tcnt, s0);
         else if (dense_w1024)
-            sl_lookup_kernel<false, 1024><<<nsl * parts, kSlThreads, tab_lds, s>>>(tp, wlog, nsl, nt, parts, w.ko, w.res,
-                                                                                 w.toff, w.tcnt, 0u);
+            sl_lookup_kernel<false, 1024><<<lgrid, kSlThreads, tab_lds, s>>>(tp, wlog, nsl, nt, parts, s1, parts2, early,
+                                                                           w.ko, w.res, w.toff, w.tcnt, 0u);
         else
-            sl_lookup_kernel<false, kSlOwnWin><<<nsl * parts, kSlThreads, tab_lds, s>>>(tp, wlog, nsl, nt, parts, w.ko,
-                                                                                      w.res, w.toff, w.tcnt, 0u);
+            sl_lookup_kernel<false, kSlOwnWin><<<lgrid, kSlThreads, tab_lds, s>>>(tp, wlog, nsl, nt, parts, s1, parts2,
+                                                                                early, w.ko, w.res, w.toff, w.tcnt, 0u);
     }
     const bool ri = tv.row_ids != nullptr, pi = probe_ids != nullptr;
     // DFP_HJ_COUNT_FREE=0: every tile takes the emission's count pass (A/B of the count-free path)

@@ -61,6 +61,7 @@ def main():
         sf = float(sf)
         t = tpch.generate(sf, dev, q9=(q == "q9"), rank=rank, world=world)
         torch.cuda.synchronize()
+        torch.cuda.empty_cache()  # the generator's temporaries back to the device (the library allocates its own)
         if a.dist:
             fn = tpch.q3_dist if q == "q3" else tpch.q9_dist
         else:
