@@ -1614,12 +1614,46 @@ dense_frag_build_kernel(ChunkGeom g, uint32_t nblk, int64_t ntiles, const uint16
     uint32_t rrow[RR];
     int ridx[RR];
     if (in_regs) {
+        // the RR positions' owner tiles by binary searches in lock step (power-of-two steps
+        // over s_to, one LDS read per position per step, the RR reads of a step independent):
+        // one LDS round trip per step instead of one per step and position
+        int own[RR];
+#pragma unroll
+        for (int u = 0; u < RR; ++u) own[u] = 0;
+        int top = 1;
+        while (top < (int)ntiles) top <<= 1;
+        for (int step = top >> 1; step > 0; step >>= 1) {
+#pragma unroll
+            for (int u = 0; u < RR; ++u) {
+                const uint32_t r = u * T + threadIdx.x;
+                // branch-free (a branch around the read serializes the positions' reads):
+                // s_to[ntiles] = R stops every position below R at the last tile
+                const int cand = own[u] + step;
+                const uint32_t v = s_to[min(cand, (int)ntiles)];
+                own[u] = v <= r ? cand : own[u];
+            }
+        }
+        // the entries, branch-free too (positions past R read entry 0 of tile 0 and drop it)
+        uint32_t pos[RR], tb[RR];
 #pragma unroll
         for (int u = 0; u < RR; ++u) {
             const uint32_t r = u * T + threadIdx.x;
-            ridx[u] = -1;
-            rrow[u] = 0;
-            if (r < R) fetch(r, &ridx[u], &rrow[u]);
+            const uint32_t in = 0u - (uint32_t)(r < R);  // masks, not selects: no branch around a read
+            const int o = (int)((uint32_t)own[u] & in);
+            pos[u] = (s_pb[o] + r) & in;
+            tb[u] = tile_base[o];
+        }
+#pragma unroll
+        for (int u = 0; u < RR; ++u) {
+            const uint32_t r = u * T + threadIdx.x;
+            const int i = (int)ko[pos[u]];
+            const uint32_t rw = tb[u] + rl[pos[u]];
+            ridx[u] = r < R ? i : -1;
+            rrow[u] = rw;
+        }
+        if (ids32 != nullptr) {  // uniform
+#pragma unroll
+            for (int u = 0; u < RR; ++u) rrow[u] = ridx[u] >= 0 ? (uint32_t)ids32[rrow[u]] : 0u;
         }
 #pragma unroll
         for (int u = 0; u < RR; ++u)
