@@ -1896,12 +1896,39 @@ hashed_frag_build_kernel(uint32_t nb, uint32_t clog2, uint32_t s0, uint32_t nsl,
     // pass A: claim slots; the claiming insert stores its row (final for a single-row key)
     if (in_regs) {
         unsigned long long rk[RR];
+        // owner tiles by lock-step binary searches and branch-free gathers, as the dense
+        // frag build does (one LDS round trip per search step for all RR positions)
+        int own[RR];
+#pragma unroll
+        for (int u = 0; u < RR; ++u) own[u] = 0;
+        int top = 1;
+        while (top < (int)ntiles) top <<= 1;
+        for (int step = top >> 1; step > 0; step >>= 1) {
+#pragma unroll
+            for (int u = 0; u < RR; ++u) {
+                const uint32_t r = u * T + threadIdx.x;
+                const int cand = own[u] + step;
+                const uint32_t v = s_to[min(cand, (int)ntiles)];  // s_to[ntiles] = R
+                own[u] = v <= r ? cand : own[u];
+            }
+        }
+        uint32_t pos[RR], tb[RR];
 #pragma unroll
         for (int u = 0; u < RR; ++u) {
             const uint32_t r = u * T + threadIdx.x;
-            rk[u] = 0;
-            rrow[u] = 0;
-            if (r < R) fetch(r, &rk[u], &rrow[u]);
+            const uint32_t in = 0u - (uint32_t)(r < R);  // positions past R read entry 0 and drop it
+            const int o = (int)((uint32_t)own[u] & in);
+            pos[u] = (s_pb[o] + r) & in;
+            tb[u] = tile_base[o];
+        }
+#pragma unroll
+        for (int u = 0; u < RR; ++u) {
+            rk[u] = ko[pos[u]];
+            rrow[u] = tb[u] + rl[pos[u]];
+        }
+        if (ids32 != nullptr) {  // uniform
+#pragma unroll
+            for (int u = 0; u < RR; ++u) rrow[u] = u * T + threadIdx.x < R ? (uint32_t)ids32[rrow[u]] : 0u;
         }
 #pragma unroll
         for (int u = 0; u < RR; ++u) {
