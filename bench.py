@@ -36,6 +36,9 @@ import datafusion_parallelism_amd as dfp  # noqa: E402
 from datafusion_parallelism_amd.table import HashTable  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+# DFP_BENCH_STEP_EVENTS=0: no timing events around each pipelined probe (probe_ms_in_step
+# then null): a default event's system-scope release writes the L2 back between steps
+STEP_EVENTS = os.environ.get("DFP_BENCH_STEP_EVENTS", "1") != "0"
 PERM_MUL = 7368787
 MIX_MUL = 0x9E3779B97F4A7C15  # odd: multiplication mod 2^64 is a bijection of int64
 MIX_MUL_I64 = MIX_MUL - (1 << 64)
@@ -157,10 +160,12 @@ class SingleGpuJoin:
             t.stream_wait(s.cuda_stream)  # probe_ms times the probe alone
         ev = self.evs[self.k & 1]
         self.k += 1
-        ev[0].record(s)
+        if STEP_EVENTS:
+            ev[0].record(s)
         t.probe_async(self.pk.data_ptr(), self.pk.numel(), self.ob.data_ptr(), self.op.data_ptr(), self.cap,
                       self.d_total.data_ptr(), self.ws.data_ptr(), s.cuda_stream)
-        ev[1].record(s)
+        if STEP_EVENTS:
+            ev[1].record(s)
         self.collect()
         self.prev = (t, ev)
 
@@ -171,10 +176,11 @@ class SingleGpuJoin:
         if self.prev is None:
             return
         t, ev = self.prev
-        ev[1].synchronize()
-        self.probe_ms.append(ev[0].elapsed_time(ev[1]))
+        if STEP_EVENTS:
+            ev[1].synchronize()
+            self.probe_ms.append(ev[0].elapsed_time(ev[1]))
         self.build_ms.append(t.build_ns() / 1e6)
-        t.close()
+        t.close()  # waits for the table's probes (the library's probe-end event)
         self.prev = None
 
     def finish(self):

@@ -30,6 +30,7 @@
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
+#include <map>
 #include <mutex>
 #include <string>
 #include <tuple>
@@ -92,6 +93,19 @@ struct BuildResources {
 std::mutex g_pool_mu;
 std::unordered_map<int, std::vector<BuildResources>> g_pool;
 
+// Release scope of the events that only order this device's own streams (the probe-end
+// events; DFP_HJ_EV_SCOPE=1 also the build events): a default event's system-scope release
+// writes the L2 back after every probe (measured: DESIGN.md §4.7)
+int ev_scope() {
+    static const int v = [] {
+        const char* e = getenv("DFP_HJ_EV_SCOPE");
+        return e ? atoi(e) : 0;
+    }();
+    return v;
+}
+unsigned probe_ev_flags() { return hipEventDisableTiming | (ev_scope() >= 1 ? hipEventReleaseToDevice : 0u); }
+unsigned build_ev_flags() { return ev_scope() >= 2 ? hipEventReleaseToDevice : hipEventDefault; }
+
 bool acquire_resources(int dev, BuildResources* r) {
     {
         std::lock_guard<std::mutex> g(g_pool_mu);
@@ -103,8 +117,9 @@ bool acquire_resources(int dev, BuildResources* r) {
         }
     }
     return hipStreamCreateWithFlags(&r->stream, hipStreamNonBlocking) == hipSuccess &&
-           hipEventCreate(&r->ev0) == hipSuccess && hipEventCreate(&r->ev1) == hipSuccess &&
-           hipEventCreateWithFlags(&r->evp, hipEventDisableTiming) == hipSuccess &&
+           hipEventCreateWithFlags(&r->ev0, build_ev_flags()) == hipSuccess &&
+           hipEventCreateWithFlags(&r->ev1, build_ev_flags()) == hipSuccess &&
+           hipEventCreateWithFlags(&r->evp, probe_ev_flags()) == hipSuccess &&
            hipHostMalloc((void**)&r->h_minmax, 4 * sizeof(int64_t), hipHostMallocCoherent | hipHostMallocMapped) ==
                hipSuccess &&
            hipHostGetDevicePointer((void**)&r->d_mbox, r->h_minmax, 0) == hipSuccess;
@@ -122,7 +137,8 @@ void release_resources(int dev, const BuildResources& r) {
 // (hj_table_free contract).
 struct DevCache {
     std::mutex mu;
-    std::unordered_map<uint64_t, std::vector<void*>> bins;  // key = device << 48 | size class
+    std::map<uint64_t, std::vector<void*>> bins;  // key = device << 48 | size class (ordered: best fit)
+    std::unordered_map<void*, size_t> cls;        // size class of every block handed out
     size_t cached_bytes = 0;
 };
 DevCache g_cache;
@@ -138,16 +154,34 @@ size_t size_class(size_t bytes) {
     return (bytes + step - 1) / step * step;
 }
 
+// Blocks of 64 MiB and more may also come from a cached block up to 1/4 larger (best fit):
+// multi-GB scratch of slightly different sizes (each join of a query, each probe batch)
+// reuses the same blocks instead of piling up until an allocation fails and the whole
+// cache is released (the 8-shard SF300 Q9 on one GPU spent seconds there).
+constexpr size_t kBestFitMin = size_t(64) << 20;
+
 void* cache_alloc(int dev, size_t bytes, hipError_t* err) {
     const size_t c = size_class(bytes);
     const uint64_t key = ((uint64_t)dev << 48) | c;
     {
         std::lock_guard<std::mutex> g(g_cache.mu);
         auto it = g_cache.bins.find(key);
+        if ((it == g_cache.bins.end() || it->second.empty()) && c >= kBestFitMin) {
+            for (it = g_cache.bins.lower_bound(key);
+                 it != g_cache.bins.end() && (it->first >> 48) == (uint64_t)dev &&
+                 (it->first & ((1ull << 48) - 1)) <= c + c / 4;
+                 ++it)
+                if (!it->second.empty()) break;
+            if (it != g_cache.bins.end() && ((it->first >> 48) != (uint64_t)dev ||
+                                             (it->first & ((1ull << 48) - 1)) > c + c / 4))
+                it = g_cache.bins.end();
+        }
         if (it != g_cache.bins.end() && !it->second.empty()) {
             void* p = it->second.back();
             it->second.pop_back();
-            g_cache.cached_bytes -= c;
+            const size_t bc = (size_t)(it->first & ((1ull << 48) - 1));
+            g_cache.cached_bytes -= bc;
+            g_cache.cls[p] = bc;
             *err = hipSuccess;
             return p;
         }
@@ -166,13 +200,21 @@ void* cache_alloc(int dev, size_t bytes, hipError_t* err) {
         }
         *err = hipMalloc(&p, c);
     }
-    return *err == hipSuccess ? p : nullptr;
+    if (*err != hipSuccess) return nullptr;
+    std::lock_guard<std::mutex> g(g_cache.mu);
+    g_cache.cls[p] = c;
+    return p;
 }
 
 void cache_free(int dev, void* p, size_t bytes) {
     if (p == nullptr) return;
-    const size_t c = size_class(bytes);
     std::lock_guard<std::mutex> g(g_cache.mu);
+    size_t c = size_class(bytes);
+    auto it = g_cache.cls.find(p);  // a best-fit block goes back to its own class
+    if (it != g_cache.cls.end()) {
+        c = it->second;
+        g_cache.cls.erase(it);
+    }
     g_cache.bins[((uint64_t)dev << 48) | c].push_back(p);
     g_cache.cached_bytes += c;
 }
@@ -738,7 +780,7 @@ hj_status note_probe(const hj_table* t, hipStream_t s) {
             return HJ_OK;
         }
     hipEvent_t ev = t->res.evp;
-    if (!t->probe_evs.empty()) HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    if (!t->probe_evs.empty()) HIP_TRY(hipEventCreateWithFlags(&ev, probe_ev_flags()));
     t->probe_evs.emplace_back(s, ev);
     HIP_TRY(hipEventRecord(ev, s));
     return HJ_OK;
