@@ -36,9 +36,11 @@ import datafusion_parallelism_amd as dfp  # noqa: E402
 from datafusion_parallelism_amd.table import HashTable  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
-# DFP_BENCH_STEP_EVENTS=0: no timing events around each pipelined probe (probe_ms_in_step
-# then null): a default event's system-scope release writes the L2 back between steps
-STEP_EVENTS = os.environ.get("DFP_BENCH_STEP_EVENTS", "1") != "0"
+# The single-GPU job's timed steps record no timing events: a torch event's system-scope
+# release writes the L2 back between two probes (C2 0.620 -> 0.612 ms per step,
+# profiles/r04_step_events_ab.txt); probe_ms_in_step comes from an instrumented pass after
+# the timed loop. DFP_BENCH_STEP_EVENTS=1: events around every timed probe (rounds 1-3).
+STEP_EVENTS = os.environ.get("DFP_BENCH_STEP_EVENTS", "0") == "1"
 PERM_MUL = 7368787
 MIX_MUL = 0x9E3779B97F4A7C15  # odd: multiplication mod 2^64 is a bijection of int64
 MIX_MUL_I64 = MIX_MUL - (1 << 64)
@@ -136,6 +138,7 @@ class SingleGpuJoin:
         self.probe_ms = []
         self.build_ms = []
         self.matches = 0
+        self.step_events = STEP_EVENTS
 
     def _alloc(self):
         self.ob = torch.empty(self.cap, dtype=torch.int64, device=self.dev)
@@ -160,11 +163,11 @@ class SingleGpuJoin:
             t.stream_wait(s.cuda_stream)  # probe_ms times the probe alone
         ev = self.evs[self.k & 1]
         self.k += 1
-        if STEP_EVENTS:
+        if self.step_events:
             ev[0].record(s)
         t.probe_async(self.pk.data_ptr(), self.pk.numel(), self.ob.data_ptr(), self.op.data_ptr(), self.cap,
                       self.d_total.data_ptr(), self.ws.data_ptr(), s.cuda_stream)
-        if STEP_EVENTS:
+        if self.step_events:
             ev[1].record(s)
         self.collect()
         self.prev = (t, ev)
@@ -176,7 +179,7 @@ class SingleGpuJoin:
         if self.prev is None:
             return
         t, ev = self.prev
-        if STEP_EVENTS:
+        if self.step_events:
             ev[1].synchronize()
             self.probe_ms.append(ev[0].elapsed_time(ev[1]))
         self.build_ms.append(t.build_ns() / 1e6)
@@ -188,6 +191,12 @@ class SingleGpuJoin:
         self.matches = int(self.d_total.item())
         if self.matches > self.cap:
             raise RuntimeError("output capacity too small")
+        if not self.step_events:  # probe_ms_in_step: a few pipelined steps with events, untimed
+            build_ms, self.probe_ms, self.step_events = self.build_ms, [], True
+            for _ in range(6):
+                self.step()
+            self.collect()
+            self.build_ms = build_ms
         # after the timed loop: the probe alone on a finished table (the roofline's
         # launch time; inside the pipeline a probe also waits for the end of its build)
         t = HashTable(1, "int64", self.dev.index or 0)

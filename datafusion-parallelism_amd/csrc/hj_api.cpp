@@ -244,7 +244,6 @@ constexpr double kDefaultLoadFactor = 0.5;
 
 // Table layout: 0 auto (direct-addressed when the key range is at most kDenseFactor x the
 // build rows, else hashed buckets), 1 hashed always. DFP_HJ_DENSE=0 selects 1.
-constexpr uint64_t kDenseFactor = 8;
 std::atomic<int> g_build_mode{-1};
 int build_mode_raw() {
     int m = g_build_mode.load(std::memory_order_relaxed);
@@ -277,6 +276,16 @@ int64_t device_budget() {
         b = g_budget.load(std::memory_order_relaxed);
     }
     return b;
+}
+// DFP_HJ_SPEC_BUILD=0: the host reads the build's key range before it launches the build
+// (rounds 1-3; the device idles for the mailbox round trip between the reduction and the
+// partition)
+bool spec_build_on() {
+    static const bool v = [] {
+        const char* e = getenv("DFP_HJ_SPEC_BUILD");
+        return !(e != nullptr && e[0] == '0');
+    }();
+    return v;
 }
 double load_factor() {
     const char* e = getenv("DFP_HJ_LOAD_FACTOR");
@@ -354,6 +363,16 @@ struct hj_table {
     // measure (hj_set_device_budget)
     int64_t live_bytes = 0, peak_bytes = 0;
     std::vector<hj_table*> owned_tables;  // freed with this table (hj_dist.cpp's local pieces)
+    // build with the key range left on the device (SpecGeo, build_attempt): the host has not
+    // read the range yet; ensure_geometry reads it before any use of the table's geometry
+    std::atomic<bool> spec_pending{false};
+    std::mutex spec_mu;
+    int64_t spec_seq = 0;
+    uint32_t spec_cap = 0;
+    const int64_t* spec_mm = nullptr;  // the reduction's result in device memory (scratch)
+    std::vector<Segment> spec_segs;    // the build's segments, for a build in another layout
+    bool mm_known = false;             // the key range read after a speculative build
+    int64_t mm_lo = 0, mm_hi = 0;
 };
 
 namespace dfp {
@@ -448,7 +467,8 @@ hj_status build_attempt(hj_table* t, const std::vector<Segment>& segs, double lf
     d_minmax = (int64_t*)p;
     // few segments: the key-range kernel publishes them and zeroes the counters (no
     // reduction when the caller gave the range)
-    const bool minmax = total > 0 && build_mode() == 0 && !t->has_range;
+    const bool need_range = total > 0 && build_mode() == 0 && !t->has_range;
+    const bool minmax = need_range && !t->mm_known;  // the reduction runs (not read back yet)
     const bool by_arg = minmax && segs.size() <= (size_t)kArgSegs;
     if (!by_arg) {
         if (!segs.empty())
@@ -456,28 +476,61 @@ hj_status build_attempt(hj_table* t, const std::vector<Segment>& segs, double lf
         HIP_TRY(hipMemsetAsync(ctr, 0, sizeof(BuildCounters), s));
     }
 
+    std::vector<int64_t> seg_n(segs.size());
+    for (size_t i = 0; i < segs.size(); ++i) seg_n[i] = segs[i].n;
+    const int64_t ftiles = frag_build_tiles(seg_n.data(), (int)segs.size());
+    // Speculative dense frag build: the kernels take the range from the reduction's result
+    // in device memory (SpecGeo), so the build runs on with no host round trip between the
+    // reduction and the partition; the grid and the blocks cover the widest range the frag
+    // build takes (kDenseFactor x rows, <= kMaxLevel1Bins blocks). The host reads the range
+    // when the table is first used (ensure_geometry); a range that takes another layout
+    // (the kernels then wrote nothing) is built there.
+    const bool packed_ok = (uint64_t)(2 * total + 2) < (1ull << 27);  // every dup_rows offset fits
+    const uint32_t spec_cap =
+        (uint32_t)std::min<uint64_t>(kMaxLevel1Bins, (kDenseFactor * (uint64_t)total + kDenseBlockValues - 1) /
+                                                         kDenseBlockValues);
+    const ChunkGeom spec_g{0, 0, spec_cap << kDenseBlockShift, kDenseShift, 0, 1, packed_ok ? 1 : 0};
+    const bool spec = minmax && spec_build_on() && !t->has_base && !t->force_dense && t->multi == nullptr &&
+                      device_budget() <= 0 && frag_build_mode() && spec_cap > 0 && frag_build_ok(spec_g, ftiles);
     // layout: a dense key range gets the direct-addressed table (one u32 ref per key value)
     ChunkGeom g{};
     bool dense = false;
-    if (minmax || (t->has_range && total > 0 && (build_mode() == 0 || t->force_dense))) {
+    if (need_range || (t->has_range && total > 0 && (build_mode() == 0 || t->force_dense))) {
         int64_t mm[2] = {t->range_lo, t->range_hi};
+        if (t->mm_known) {
+            mm[0] = t->mm_lo;
+            mm[1] = t->mm_hi;
+        }
         if (minmax) {
             int64_t* mb = t->res.h_minmax;
             const int64_t seq = ++t->res.mb_seq;
             HIP_TRY(launch_key_minmax(t->key_bytes, segs.data(), d_segs, (int)segs.size(), by_arg ? ctr : nullptr,
                                       total, d_minmax, t->res.d_mbox, seq, s));
-            HIP_TRY(wait_mailbox(mb, seq, d_minmax, s));
-            mm[0] = mb[0];
-            mm[1] = mb[1];
+            if (spec) {
+                t->spec_seq = seq;
+                t->spec_cap = spec_cap;
+                t->spec_mm = d_minmax;
+                t->spec_segs = segs;
+                mm[0] = 1;  // not read: the geometry below is spec_g's
+                mm[1] = 0;
+            } else {
+                HIP_TRY(wait_mailbox(mb, seq, d_minmax, s));
+                mm[0] = mb[0];
+                mm[1] = mb[1];
+            }
         }
-        if (mm[0] <= mm[1]) {
+        if (spec) {
+            dense = true;
+            g = spec_g;
+            t->dmin = 0;
+            t->drange = 0;
+        } else if (mm[0] <= mm[1]) {
             const uint64_t range = (uint64_t)mm[1] - (uint64_t)mm[0] + 1;
             const uint64_t nch = (range + (1u << kDenseShift) - 1) >> kDenseShift;
             if (range != 0 && (range <= kDenseFactor * (uint64_t)total || t->force_dense) &&
                 nch <= (uint64_t)kMaxChunks) {
                 dense = true;
-                const bool packed = (uint64_t)(2 * total + 2) < (1ull << 27);  // every dup_rows offset fits
-                g = ChunkGeom{0, 0, (uint32_t)nch, kDenseShift, mm[0], 1, packed ? 1 : 0};
+                g = ChunkGeom{0, 0, (uint32_t)nch, kDenseShift, mm[0], 1, packed_ok ? 1 : 0};
                 t->dmin = mm[0];
                 t->drange = range;
             }
@@ -513,9 +566,6 @@ hj_status build_attempt(hj_table* t, const std::vector<Segment>& segs, double lf
     t->nb = g.nb;
     const uint64_t nchunks = g.nchunks;
     // dense builds that fit the tile-local partition skip the histogram/scan/scatter path
-    std::vector<int64_t> seg_n(segs.size());
-    for (size_t i = 0; i < segs.size(); ++i) seg_n[i] = segs[i].n;
-    const int64_t ftiles = frag_build_tiles(seg_n.data(), (int)segs.size());
     const bool frag = dense && total > 0 && frag_build_mode() && frag_build_ok(g, ftiles);
     // hashed tables: the frag build unless mode 2 keeps the histogram path (DFP_HJ_FRAG_BUILD=0)
     const bool hfrag = !dense && total > 0 && build_mode_raw() != 2 && hashed_frag_ok(g, ftiles);
@@ -577,9 +627,13 @@ hj_status build_attempt(hj_table* t, const std::vector<Segment>& segs, double lf
         const int cus = prop ? prop->multiProcessorCount : 256;
         if (frag) {
             HIP_TRY(launch_build_frag(t->key_bytes, segs.data(), (int)segs.size(), g, ftiles, fscr, d_tb, ids32,
-                                      t->dense, t->dup_rows, fbig, ctr, d_segs, total, ids_as_rows, cus, s));
+                                      t->dense, t->dup_rows, fbig, ctr, d_segs, total, ids_as_rows, cus,
+                                      spec ? SpecGeo{(const long long*)d_minmax, (uint64_t)total, spec_cap}
+                                           : SpecGeo{nullptr, 0, 0},
+                                      s));
             // a direct-addressed build cannot overflow (no retry): nothing to read back, the
             // build stays asynchronous; consumers wait on its completion event
+            if (spec) t->spec_pending.store(true, std::memory_order_release);
             return HJ_OK;
         }
         HIP_TRY(launch_build_hashed_frag(t->key_bytes, segs.data(), (int)segs.size(), g, ftiles, fscr, d_tb, ids32,
@@ -648,6 +702,71 @@ hj_status build_attempt(hj_table* t, const std::vector<Segment>& segs, double lf
 
 hj_status run_multi_build_entry(hj_table* t, const std::vector<Segment>& segs, const std::vector<HostSeg*>& hsegs);
 
+// build attempts until no chunk overflows (halving the load factor each time)
+hj_status build_attempts(hj_table* t, const std::vector<Segment>& segs) {
+    double lf = load_factor();
+    for (int attempt = 0;; ++attempt) {
+        bool retry = false;
+        hj_status st = build_attempt(t, segs, lf, &retry);
+        if (st != HJ_OK) return st;
+        if (!retry) return HJ_OK;
+        // a chunk overflowed (adversarial key distribution): halve the load and rebuild
+        if (attempt >= 4) return fail(HJ_ERR_INVALID, "build: a table chunk overflowed at every load factor");
+        lf *= 0.5;
+        HIP_TRY(hipEventRecord(t->res.ev0, t->bstream));
+    }
+}
+
+// The geometry of a speculative build (build_attempt): the key range from the mailbox.
+// When it takes the dense frag layout the kernels have built the table; otherwise they
+// wrote nothing, and the table is built here in its layout (the range now known), on the
+// build stream, with ev1 recorded again after it.
+hj_status ensure_geometry(const hj_table* ct) {
+    hj_table* t = const_cast<hj_table*>(ct);
+    // settled: by the build, or by another caller (whose build may have failed)
+    auto settled = [t]() { return t->build_st == HJ_OK ? HJ_OK : fail(t->build_st, t->build_err); };
+    if (!t->spec_pending.load(std::memory_order_acquire)) return settled();
+    std::lock_guard<std::mutex> g(t->spec_mu);
+    if (!t->spec_pending.load(std::memory_order_relaxed)) return settled();
+    HIP_TRY(hipSetDevice(t->device));
+    int64_t* mb = t->res.h_minmax;
+    HIP_TRY(wait_mailbox(mb, t->spec_seq, t->spec_mm, t->bstream));
+    const int64_t mn = mb[0], mx = mb[1];
+    if (spec_dense_blocks(mn, mx, (uint64_t)t->total_rows, t->spec_cap) != 0) {
+        const uint64_t range = (uint64_t)mx - (uint64_t)mn + 1;
+        t->dmin = mn;
+        t->drange = range;
+        t->nchunks = (uint32_t)((range + (1u << kDenseShift) - 1) >> kDenseShift);
+        t->spec_pending.store(false, std::memory_order_release);
+        return HJ_OK;
+    }
+    // another layout: drain the (idle) speculative kernels, release their blocks, build
+    HIP_TRY(hipStreamSynchronize(t->bstream));
+    free_list(t, t->allocs);
+    free_list(t, t->scratch);
+    t->dense = nullptr;
+    t->tbl = nullptr;
+    t->dup_rows = nullptr;
+    t->row_ids = nullptr;
+    t->ctr = nullptr;
+    t->mm_known = true;
+    t->mm_lo = mn;
+    t->mm_hi = mx;
+    hj_status st = build_attempts(t, t->spec_segs);
+    if (st == HJ_OK && hipEventRecord(t->res.ev1, t->bstream) != hipSuccess)
+        st = fail(HJ_ERR_HIP, "hipEventRecord failed");
+    t->build_ns = -1;
+    if (st != HJ_OK) {  // the table is unusable from here on
+        (void)hipStreamSynchronize(t->bstream);
+        t->build_st = st;
+        t->build_err = g_err;
+    }
+    // only now: a concurrent caller that saw the flag waits on spec_mu until the table
+    // (and ev1) are complete; one that sees it clear reads the finished geometry
+    t->spec_pending.store(false, std::memory_order_release);
+    return st;
+}
+
 // The device build, run once by the last partition to arrive at the barrier.
 hj_status run_build(hj_table* t) {
     HIP_TRY(hipSetDevice(t->device));
@@ -677,17 +796,8 @@ hj_status run_build(hj_table* t) {
         for (auto& hs : t->parts[p])
             if (hs.ready) HIP_TRY(hipStreamWaitEvent(s, hs.ready, 0));
     HIP_TRY(hipEventRecord(t->res.ev0, s));
-    double lf = load_factor();
-    for (int attempt = 0;; ++attempt) {
-        bool retry = false;
-        hj_status st = build_attempt(t, segs, lf, &retry);
-        if (st != HJ_OK) return st;
-        if (!retry) break;
-        // a chunk overflowed (adversarial key distribution): halve the load and rebuild
-        if (attempt >= 4) return fail(HJ_ERR_INVALID, "build: a table chunk overflowed at every load factor");
-        lf *= 0.5;
-        HIP_TRY(hipEventRecord(t->res.ev0, s));
-    }
+    hj_status bst = build_attempts(t, segs);
+    if (bst != HJ_OK) return bst;
     // ev1 marks the table complete: probes and queries on other streams wait on it
     // (hipStreamWaitEvent, no host synchronisation); build_ns is read when first asked
     HIP_TRY(hipEventRecord(t->res.ev1, s));
@@ -722,7 +832,7 @@ hj_status check_table(const hj_table* t) {
     if (t == nullptr) return fail(HJ_ERR_INVALID, "null table");
     if (!t->built) return fail(HJ_ERR_INVALID, "table is not built: every partition must call hj_build_finish");
     if (t->build_st != HJ_OK) return fail(t->build_st, t->build_err);
-    return HJ_OK;
+    return ensure_geometry(t);
 }
 
 TableView view_of(const hj_table* t) {
@@ -800,6 +910,7 @@ hj_status probe_impl(const hj_table* t, const void* keys, const uint8_t* valid, 
                      const uint32_t* probe_ids, uint32_t pbase, int64_t n, uint64_t* out_b, uint32_t* out_p,
                      int64_t cap, int64_t* d_total, void* ws, hipStream_t s) {
     hj_status st = check_probe_args(n, pbase, cap, ws);
+    if (st == HJ_OK) st = ensure_geometry(t);
     if (st != HJ_OK) return st;
     // the probe orders itself after the build (on another stream) at its first table read
     HIP_TRY(launch_probe(t->key_bytes, view_of(t), keys, valid, voff, probe_ids, pbase, n, out_b, out_p, cap, d_total, ws,
@@ -1432,6 +1543,9 @@ hj_status hj_build_finish(hj_table* t, int partition) {
     if (t->arrived == t->parallelism) {
         // last arriver finalises (InitializeLast::initialize_or_wait)
         hj_status st = run_build(t);
+        // borrowed input (no HJ_BORROW_KEEP) must be read before this returns: a
+        // speculative build's geometry is settled now (a build in another layout reads it)
+        if (st == HJ_OK && t->sync_finish) st = ensure_geometry(t);
         // a failed build may have queued work on its stream before the error (ev1 is not
         // recorded then): drain it, so that hj_table_free returns idle blocks to the cache
         if (st != HJ_OK) (void)hipStreamSynchronize(t->bstream);

@@ -138,4 +138,28 @@ struct ChunkGeom {
     int packed;  // dense refs carry small counts (kPackedMask)
 };
 
+// A key range of at most kDenseFactor x rows takes the direct-addressed layout.
+constexpr uint64_t kDenseFactor = 8;
+constexpr uint64_t kDenseBlockValues = 8192;  // a frag-build block: 4 chunks of 2^kDenseShift values
+
+// Build with the key range left on the device (hj_api.cpp build_attempt): the dense frag
+// build is launched before the host knows the range, its kernels read the range the
+// reduction left in device memory (mm = {min, max}) and resolve the geometry themselves.
+// spec_dense_blocks = the 8192-value blocks a direct-addressed table over [mn, mx] spans,
+// or 0 when that range takes another layout (no valid key, wider than kDenseFactor x rows
+// or than `cap` blocks): the kernels then do nothing and the host builds once it has read
+// the range. Host and device evaluate this one function, so they agree on the outcome.
+struct SpecGeo {
+    const long long* mm;  // null: the geometry came from the host
+    uint64_t rows;
+    uint32_t cap;
+};
+__host__ __device__ inline uint32_t spec_dense_blocks(int64_t mn, int64_t mx, uint64_t rows, uint32_t cap) {
+    if (mn > mx) return 0u;
+    const uint64_t range = (uint64_t)mx - (uint64_t)mn + 1;  // 0: the whole int64 domain
+    if (range == 0 || range > kDenseFactor * rows) return 0u;
+    const uint64_t nblk = (range + kDenseBlockValues - 1) / kDenseBlockValues;
+    return nblk <= cap ? (uint32_t)nblk : 0u;
+}
+
 }  // namespace dfp

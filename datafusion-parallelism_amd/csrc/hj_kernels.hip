@@ -1354,8 +1354,17 @@ sl_partition_kernel(int64_t dmin, uint64_t drange, uint32_t wlog, uint32_t nslic
                     unsigned long long* __restrict__ hdr,  // probe: workspace header (error word at [1]); build: null
                     unsigned long long* __restrict__ tcnt,      // probe: the tile's entry count; build: null
                     uint32_t* __restrict__ tent,  // probe: entries of the tile so far (earlier passes: append after them)
-                    uint16_t* __restrict__ wcnt) {  // probe: entries per 2048-row range of the tile (kSlRanges u16)
+                    uint16_t* __restrict__ wcnt,  // probe: entries per 2048-row range of the tile (kSlRanges u16)
+                    SpecGeo sg) {  // build with the key range on the device (mm null: dmin, drange, nslices given)
     __shared__ __attribute__((aligned(16))) uint32_t s_ent[kSlTile];
+    if (sg.mm != nullptr) {  // (uniform) the geometry from the reduction's result; none: another layout
+        const long long mn = sg.mm[0], mx = sg.mm[1];
+        const uint32_t nb = spec_dense_blocks(mn, mx, sg.rows, sg.cap);
+        if (nb == 0) return;
+        dmin = mn;
+        nslices = nb;
+        drange = (uint64_t)nb << wlog;
+    }
     __shared__ __attribute__((aligned(16))) uint32_t s_hist[kSlHistBins];  // bins 0..nslices (<= kSlMaxSlices + 1)
     // the scan's wave totals and the per-range entry counts alias the entry staging area
     // (free until the scatter), so the workgroup stays within 80 KB: two per CU
@@ -1487,10 +1496,16 @@ sl_partition_kernel(int64_t dmin, uint64_t drange, uint32_t wlog, uint32_t nslic
 constexpr int kSlTrChunk = 64;  // slices per block: grid = tile blocks x slice chunks
 __global__ void __launch_bounds__(256)
 sl_toff_transpose_kernel(const uint16_t* __restrict__ toff, uint32_t nbins, int64_t ntiles,
-                         uint16_t* __restrict__ toffT) {
+                         uint16_t* __restrict__ toffT, SpecGeo sg) {
     __shared__ uint16_t s_t[64][kSlTrChunk + 2];
+    if (sg.mm != nullptr) {  // (uniform) bins from the reduction's result; the grid covers the widest
+        const uint32_t nb = spec_dense_blocks(sg.mm[0], sg.mm[1], sg.rows, sg.cap);
+        if (nb == 0) return;
+        nbins = nb + 1;
+    }
     const uint32_t nch = (nbins + kSlTrChunk - 1) / kSlTrChunk;
     const int64_t b = blockIdx.x / nch;
+    if (b * 64 >= ntiles) return;  // (uniform) past the tiles: a grid sized for more bins
     const uint32_t c0 = (blockIdx.x % nch) * kSlTrChunk;
     const uint32_t cw = min<uint32_t>(kSlTrChunk, nbins - c0);
     for (uint32_t i = threadIdx.x; i < 64 * kSlTrChunk; i += 256) {
@@ -1530,10 +1545,17 @@ dense_frag_build_kernel(ChunkGeom g, uint32_t nblk, int64_t ntiles, const uint16
                         const uint16_t* __restrict__ ko, const uint16_t* __restrict__ rl,
                         const uint32_t* __restrict__ tile_base, const uint64_t* __restrict__ ids32,
                         uint32_t* __restrict__ dense, uint32_t* __restrict__ dup_rows, BigSeg* __restrict__ big,
-                        BuildCounters* ctr, unsigned long long* __restrict__ spill, uint32_t run) {
+                        BuildCounters* ctr, unsigned long long* __restrict__ spill, uint32_t run, SpecGeo sg) {
     constexpr uint32_t GV = kDenseSub << kDenseBlockShift;  // 8192 values per block
+    static_assert(GV == kDenseBlockValues, "frag-build blocks");
     constexpr uint32_t NSUB = GV / kDenseSub;
     __shared__ uint32_t refs[GV];
+    if (sg.mm != nullptr) {  // (uniform) blocks from the reduction's result; the grid covers `cap`
+        const uint32_t nb = spec_dense_blocks(sg.mm[0], sg.mm[1], sg.rows, sg.cap);
+        if (blockIdx.x >= nb) return;
+        g.dmin = sg.mm[0];
+        nblk = nb;
+    }
     __shared__ uint32_t d_off[kDenseSub], d_cur[kDenseSub], d_cnt[kDenseSub];
     __shared__ uint32_t s_to[kFragMaxTiles + 1];  // exclusive position of each tile's fragment
     __shared__ uint32_t s_pb[kFragMaxTiles];      // fragment position - s_to (region offset)
@@ -2755,6 +2777,11 @@ sl_emit_kernel(TableView tv, const uint32_t* __restrict__ tent, const uint16_t* 
                     pos += (uint32_t)__builtin_popcountll(hit);
                 }
             }
+            // Measured (r04) and not kept: counted tiles in batches of 4 steps whose duplicate
+            // segment reads (up to 8 output windows) were all issued before any of their
+            // stores — C3 emission 666 -> 670 us: the segment reads are bound by the rate of
+            // random line reads into dup_rows (30 MB, Infinity-Cache resident), not by one
+            // round trip per window.
 #pragma unroll 2
             for (int k = 0; !fast && k < kSlWaveRows; k += 64) {
                 const int loc = row_w + k + lane;
@@ -3548,7 +3575,9 @@ uint32_t frag_threads() {  // read per build, so that tests can run both forms i
 hipError_t launch_build_frag(int key_bytes, const Segment* h_segs, int nseg, const ChunkGeom& g, int64_t ftiles,
                              void* scratch, uint32_t* tile_base, const uint64_t* ids32, uint32_t* dense,
                              uint32_t* dup_rows, BigSeg* big, BuildCounters* ctr, const Segment* d_segs, int64_t total,
-                             bool ids_as_rows, int big_grid, hipStream_t s) {
+                             bool ids_as_rows, int big_grid, const SpecGeo& spec, hipStream_t s) {
+    // spec.mm: the grid and the scratch cover g's `cap` blocks; the kernels take theirs from
+    // the key range in device memory (SpecGeo)
     const uint32_t nblk = dense_blocks(g.nchunks), nbins = nblk + 1;
     constexpr uint32_t GV = kDenseSub << kDenseBlockShift;
     const uint32_t wlog = 31 - __builtin_clz(GV);
@@ -3558,6 +3587,12 @@ hipError_t launch_build_frag(int key_bytes, const Segment* h_segs, int nseg, con
     uint16_t* rl = (uint16_t*)p;   p = a256(p + 2 * ftiles * kSlTile);
     uint16_t* toff = (uint16_t*)p; p = a256(p + 2 * ftiles * nbins);
     uint16_t* toffT = (uint16_t*)p; p = a256(p + 2 * ((ftiles + 63) & ~(int64_t)63) * nbins);
+    // Measured (r04) and not kept: the partition writing the bounds in the 64-tile layout
+    // itself (no transpose launch): its scattered 2-byte stores cost the partition what the
+    // launch costs (C2 build partition 38 -> 48 us against an 8 us transpose); the key-range
+    // partials folded by every partition block instead of minmax_final_kernel: the build
+    // partition 38 -> 44 us against a 5.5 us launch, and the probe's partition (the same
+    // kernel) 218 -> 224 us.
     unsigned long long* spill = (unsigned long long*)p;  // total rows at most
     int64_t t0 = 0;
     for (int i = 0; i < nseg; ++i) {
@@ -3570,7 +3605,7 @@ hipError_t launch_build_frag(int key_bytes, const Segment* h_segs, int nseg, con
     sl_partition_kernel<KT, HV><<<(unsigned)nt, kSlThreads, 0, s>>>(g.dmin, drange, wlog, nblk, sg.keys, sg.valid, \
                                                                    sg.voff, sg.n, vec, ko, rl, toff, 0, t0,          \
                                                                    sg.row_base, tile_base, nullptr, nullptr, nullptr, \
-                                                                   nullptr)
+                                                                   nullptr, spec)
         if (key_bytes == 8) {
             if (sg.valid) DFP_BLP(int64_t, true); else DFP_BLP(int64_t, false);
         } else {
@@ -3580,15 +3615,15 @@ hipError_t launch_build_frag(int key_bytes, const Segment* h_segs, int nseg, con
         t0 += nt;
     }
     sl_toff_transpose_kernel<<<(unsigned)((ftiles + 63) / 64 * ((nblk + kSlTrChunk) / kSlTrChunk)), 256, 0, s>>>(
-        toff, nbins, ftiles, toffT);
+        toff, nbins, ftiles, toffT, spec);
     if (frag_threads() != 1024)
         dense_frag_build_kernel<512, 16><<<nblk, 512, 0, s>>>(g, nblk, ftiles, toffT, ko, rl, tile_base,
                                                              ids_as_rows ? ids32 : nullptr, dense, dup_rows, big, ctr,
-                                                             spill, frag_run());
+                                                             spill, frag_run(), spec);
     else
         dense_frag_build_kernel<1024, 8><<<nblk, 1024, 0, s>>>(g, nblk, ftiles, toffT, ko, rl, tile_base,
                                                                ids_as_rows ? ids32 : nullptr, dense, dup_rows, big, ctr,
-                                                               spill, frag_run());
+                                                               spill, frag_run(), spec);
     dup_sort_big_kernel<<<big_grid, kBigThreads, 0, s>>>(dup_rows, big, ctr, d_segs, nseg, total, key_bytes,
                                                          ids_as_rows);
     return hipGetLastError();
@@ -3659,7 +3694,7 @@ hipError_t launch_build_hashed_frag(int key_bytes, const Segment* h_segs, int ns
             t0 += nt;
         }
         sl_toff_transpose_kernel<<<(unsigned)((ftiles + 63) / 64 * ((nbins + kSlTrChunk - 1) / kSlTrChunk)), 256, 0,
-                                   s>>>(toff, nbins, ftiles, toffT);
+                                   s>>>(toff, nbins, ftiles, toffT, SpecGeo{});
         if ((e = chk("toff transpose")) != hipSuccess) return e;
         hashed_frag_build_kernel<T, RR><<<nsl, T, lds, s>>>(g.nb, g.clog2, s0, nsl, ftiles, toffT, ko, rl, tile_base,
                                                            ids_as_rows ? ids32 : nullptr, tbl, dup_rows, big, ctr,
@@ -3990,7 +4025,7 @@ hipError_t launch_probe_sliced(int key_bytes, const TableView& tv, const void* k
 #define DFP_SLP(KT, HV)                                                                                      \
     sl_partition_kernel<KT, HV><<<(unsigned)nt, kSlThreads, 0, s>>>(dmin_p, drange_p, wlog, nsl, keys, valid, voff, n, \
                                                                    vec, (uint16_t*)w.ko, w.rl, w.toff, sl_nt, 0, 0,   \
-                                                                   nullptr, h, w.tcnt, w.tent, w.wcnt)
+                                                                   nullptr, h, w.tcnt, w.tent, w.wcnt, SpecGeo{})
             if (key_bytes == 8) {
                 if (valid) DFP_SLP(int64_t, true); else DFP_SLP(int64_t, false);
             } else {

@@ -48,7 +48,7 @@ int64_t frag_build_scratch_bytes(const ChunkGeom& g, int64_t ftiles, int64_t tot
 hipError_t launch_build_frag(int key_bytes, const Segment* h_segs, int nseg, const ChunkGeom& g, int64_t ftiles,
                              void* scratch, uint32_t* tile_base, const uint64_t* ids32, uint32_t* dense,
                              uint32_t* dup_rows, BigSeg* big, BuildCounters* ctr, const Segment* d_segs, int64_t total,
-                             bool ids_as_rows, int big_grid, hipStream_t s);
+                             bool ids_as_rows, int big_grid, const SpecGeo& spec, hipStream_t s);
 // Hashed builds of chunks <= 1024 buckets and <= kFragMaxTiles tiles: the probe's hashed
 // partition on the build keys (1024-bucket slices, passes of <= 2047 slices), then one
 // workgroup per slice gathers its rows from the tiles' fragments and builds the slice's

@@ -815,3 +815,84 @@ def test_range_free_dense_build(dfp, oracle_mod, case):
     assert st["buckets"] == 0, "a direct-addressed table"
     ob, op = oracle_mod.inner_join(bk, pk, None if bvalid is None else np.asarray(bvalid, bool))
     assert_same(b, p, ob, op)
+
+
+# ---- the speculative build (the key range stays on the device) --------------------
+
+@pytest.mark.parametrize("case", ["dense_edge", "hashed_edge", "wide", "all_null", "single_key", "int32"])
+def test_spec_build_layouts(dfp, oracle_mod, case):
+    """hj_build_finish launches the dense frag build before the host has read the key range
+    (its kernels resolve the geometry from the reduction's result in device memory); the
+    host reads the range when the table is first used, and a range that takes another
+    layout is built then. At the layout edges — a range of exactly 8 x rows (dense) and one
+    value more (hashed), keys over the whole int64 domain, every key null, one key value,
+    int32 keys — the table takes the layout the range gives and the oracle's pairs."""
+    rng = np.random.default_rng(hash(case) & 0xFFFF)
+    n = 100_000
+    bvalid = None
+    key_type = "int64"
+    want_dense = True
+    if case == "dense_edge":
+        bk = rng.integers(0, 8 * n, n) - 12345
+        bk[:2] = [-12345, 8 * n - 1 - 12345]
+    elif case == "hashed_edge":
+        bk = rng.integers(0, 8 * n + 1, n) - 12345
+        bk[:2] = [-12345, 8 * n - 12345]
+        want_dense = False
+    elif case == "wide":
+        bk = rng.integers(I64_MIN, np.iinfo(np.int64).max, n, dtype=np.int64)
+        want_dense = False
+    elif case == "all_null":
+        bk = rng.integers(0, 1000, n)
+        bvalid = np.zeros(n, bool)
+        want_dense = None
+    elif case == "single_key":
+        bk = np.full(n, 77, np.int64)
+    else:
+        bk = rng.integers(-2**31, 2**31 - 8 * n, 1)[0] + rng.integers(0, 4 * n, n)
+        key_type = "int32"
+    bk = np.asarray(bk, np.int64 if key_type == "int64" else np.int32)
+    pk = np.concatenate([rng.choice(bk, 50_000), rng.integers(int(bk.min()) - 10, int(bk.min()) + 4 * n, 50_000)])
+    pk = pk.astype(bk.dtype)
+    b, p, st = gpu_join(dfp, bk, pk, bvalid=bvalid, key_type=key_type)
+    if want_dense is not None:
+        assert (st["buckets"] == 0) == want_dense, st
+    ob, op = oracle_mod.inner_join(bk, pk, None if bvalid is None else bvalid)
+    assert_same(b, p, ob, op)
+
+
+@pytest.mark.parametrize("case", ["dense", "hashed"])
+def test_spec_build_concurrent_first_probes(dfp, oracle_mod, case):
+    """Several threads probe a freshly built table at once (the operator's partitions do):
+    the first caller settles a speculative build — for wide keys by building the hashed
+    table — and the others wait for it; every probe gives the oracle's pairs."""
+    import threading
+
+    rng = np.random.default_rng(11 if case == "dense" else 12)
+    n = 200_000
+    bk = (rng.integers(0, 4 * n, n) if case == "dense"
+          else rng.integers(I64_MIN, np.iinfo(np.int64).max, n, dtype=np.int64)).astype(np.int64)
+    pks = [np.concatenate([rng.choice(bk, 40_000), rng.integers(0, 4 * n, 40_000)]).astype(np.int64)
+           for _ in range(4)]
+    want = [oracle_mod.inner_join(bk, pk) for pk in pks]
+    for _ in range(3):
+        with dfp.HashTable(1, "int64", 0) as t:
+            t.append(0, torch.from_numpy(bk).cuda())
+            t.finish(0)
+            got, errs = [None] * 4, []
+
+            def run(i):
+                try:
+                    got[i] = t.probe(torch.from_numpy(pks[i]).cuda())
+                except Exception as e:  # noqa: BLE001 - reported below
+                    errs.append(e)
+
+            th = [threading.Thread(target=run, args=(i,)) for i in range(4)]
+            for x in th:
+                x.start()
+            for x in th:
+                x.join()
+            assert not errs, errs
+            for (b, p), (ob, op) in zip(got, want):
+                assert_same(b, p, ob, op)
+            assert (t.stats()["buckets"] == 0) == (case == "dense")
