@@ -16,7 +16,8 @@ import os
 import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "lib", "libdfp_hj.so")
+# DFP_HJ_LIB: a diagnostic build of the same library (tools/lib_variants.py) in its place
+LIB_PATH = os.environ.get("DFP_HJ_LIB") or os.path.join(HERE, "lib", "libdfp_hj.so")
 
 HJ_OK, HJ_ERR_INVALID, HJ_ERR_OOM, HJ_ERR_HIP, HJ_ERR_RCCL, HJ_ERR_CAPACITY, HJ_ERR_NO_DEVICE = range(7)
 HJ_INT32, HJ_INT64 = 0, 1

@@ -2128,6 +2128,9 @@ hashed_frag_build_kernel(uint32_t nb, uint32_t clog2, uint32_t s0, uint32_t nsl,
 //          bucket's line in LDS (exact compare of stored keys, linear probing inside the
 //          chunk, as lookup4); key 0 reads the side bucket.
 constexpr int kHsSliceLog = 11;  // buckets per hashed slice: 2^11 x 64 B = 128 KB of LDS
+#ifndef DFP_HL_DEFER
+#define DFP_HL_DEFER 0
+#endif
 
 // ref of stored key sk (!= 0) in the LDS image of a hashed slice whose first bucket is
 // sbase; linear probing wraps inside the key's chunk (cmask), as the table was built
@@ -2145,6 +2148,13 @@ __device__ __forceinline__ uint32_t lds_bucket_ref(const uint4* __restrict__ img
     return ref;
 }
 
+// Measured (r04) and not kept: every hashed row branch-free (selects, stores dropped by an
+// out-of-range offset, the rare rows deferred to a pass after the window, two rows per
+// scheduling region; 108 VGPRs): C2h lookup 771 -> 1107 us.
+// Measured (r04) and not kept: the home bucket's compares alone, with a duplicated key's
+// inline count and the probe past a bucket an insert passed full in wave-uniform branches
+// (fewer instructions per row): C2h lookup 771 -> 917 us — the per-row ballots split the
+// unrolled rows into separate blocks, so no row's LDS reads overlap another's work.
 // Measured (r04) and not kept: the hashed slice image re-laid as quad arrays (low key
 // halves, high halves, key 4 + meta, refs: one quad read per lane on 16 of a bank row's
 // 256 B instead of 4 of them) with three quad reads and a dependent ref read per entry
@@ -2406,6 +2416,9 @@ sl_lookup_kernel(TableView tv, uint32_t wlog, uint32_t nslices, int64_t ntiles, 
             DFP_PH_WAIT();
             DFP_PH(2);
             if constexpr (HASHED) {
+#if DFP_HL_DEFER
+                uint32_t hl_unk = 0;  // bit u: row u's count is in its segment header
+#endif
 #pragma unroll
                 for (int u = 0; u < NU; ++u) {
                     if (w0 + u * 64 >= R) continue;  // uniform: past the run
@@ -2428,10 +2441,17 @@ sl_lookup_kernel(TableView tv, uint32_t wlog, uint32_t nslices, int64_t ntiles, 
                     // that waits there. Merged into the common path, that load's wait was an
                     // s_waitcnt vmcnt(0) on every row — for the previous rows' ref stores (loads
                     // and stores share vmcnt): one store round trip per 64 entries.
+#if DFP_HL_DEFER
+                    // a count in its segment header: the row's correction goes to its tile's
+                    // count after the window (no per-row branch)
+                    hl_unk |= (uint32_t)(c == kCountUnknown) << u;
+                    c = c == kCountUnknown ? 1u : c;
+#else
                     if (__ballot(c == kCountUnknown) != 0) {
                         if (c == kCountUnknown) c = tv.dup_rows[v & tv.off_mask];
                         asm volatile("" : "+v"(c));
                     }
+#endif
                     __builtin_amdgcn_raw_buffer_store_b32(v, rres, (int)(o * 4), 0, 0);
                     uint32_t d = c - 1u;  // kOob: c = 1
                     if (d != 0xFFFFFFFFu && d >= kBigCorr) {
@@ -2442,6 +2462,18 @@ sl_lookup_kernel(TableView tv, uint32_t wlog, uint32_t nslices, int64_t ntiles, 
                     if (off_end & (1u << u)) scst[off[u] >> 26] = corr_run;
                     corr_run = (uint32_t)__builtin_amdgcn_readlane((int)corr_run, 63);
                 }
+#if DFP_HL_DEFER
+                if (__ballot(hl_unk != 0) != 0) {  // rare: keys of more than 63 rows
+                    for (int u = 0; u < NU; ++u) {
+                        if (!((hl_unk >> u) & 1u)) continue;
+                        uint32_t c;
+                        const uint32_t v =
+                            lds_bucket_ref(reinterpret_cast<const uint4*>(s_tab), tv.nb, sbase, cmask, ev[u], &c);
+                        c = tv.dup_rows[v & tv.off_mask];
+                        atomicAdd(&tcnt[tc + slane[off[u] >> 26]], (unsigned long long)((long long)c - 1));
+                    }
+                }
+#endif
             } else {
 #pragma unroll
                 for (int u = 0; u < NU; ++u) {
