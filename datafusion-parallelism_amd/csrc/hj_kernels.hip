@@ -1563,6 +1563,7 @@ dense_frag_build_kernel(ChunkGeom g, uint32_t nblk, int64_t ntiles, const uint16
     __shared__ unsigned long long s_w[T / 64];
     __shared__ unsigned long long s_base, s_sp;
     __shared__ uint32_t s_carry;
+    __shared__ uint32_t s_qo[NSUB + 1], s_qc[NSUB];  // spilled rows: each duplicate sub-range's start, fill
     // key block (slice): runs of `run` consecutive blocks per XCD (blocks are dispatched
     // round-robin over the 8 XCDs), so that the blocks resident on one XCD at once read
     // adjacent fragments of each tile (shared lines in that XCD's L2) while the runs still
@@ -1605,40 +1606,13 @@ dense_frag_build_kernel(ChunkGeom g, uint32_t nblk, int64_t ntiles, const uint16
         if (R) atomicAdd(&ctr->n_valid, (unsigned long long)R);
     }
     __syncthreads();
-    // position r -> (key index in the block, row value)
-    auto fetch = [&](uint32_t r, int* idx, uint32_t* row) {
-        int lo = 0, hi = (int)ntiles - 1;  // largest tile with s_to[tile] <= r (skips empty ones)
-        while (lo < hi) {
-            const int mid = (lo + hi + 1) >> 1;
-            if (s_to[mid] <= r) lo = mid; else hi = mid - 1;
-        }
-        const uint32_t pos = s_pb[lo] + r;
-        *idx = (int)ko[pos];
-        const uint32_t rw = tile_base[lo] + rl[pos];
-        *row = ids32 ? (uint32_t)ids32[rw] : rw;
-    };
-    const bool in_regs = R <= (uint32_t)(T * RR);
-    if (threadIdx.x < NSUB) s_dup[threadIdx.x] = in_regs ? 0u : 1u;  // more rows than the registers hold
-    if (threadIdx.x == 0 && !in_regs) s_sp = atomicAdd(&ctr->spill_used, (unsigned long long)R);
-    __syncthreads();
-    // a block with more rows than the registers hold gathers them once into the spill
-    // pool (key index << 32 | row); its duplicate passes then stream them from there
-    unsigned long long* sp = spill + (in_regs ? 0ull : s_sp);
-    if (!in_regs) {
-        for (uint32_t r = threadIdx.x; r < R; r += T) {
-            int i;
-            uint32_t rw;
-            fetch(r, &i, &rw);
-            sp[r] = ((unsigned long long)(uint32_t)i << 32) | rw;
-        }
-        __syncthreads();
-    }
-    uint32_t rrow[RR];
-    int ridx[RR];
-    if (in_regs) {
-        // the RR positions' owner tiles by binary searches in lock step (power-of-two steps
-        // over s_to, one LDS read per position per step, the RR reads of a step independent):
-        // one LDS round trip per step instead of one per step and position
+    // positions r0 + u * T + thread (u < RR) -> (key index in the block or -1 past R, row
+    // value): the owner tiles by binary searches in lock step (power-of-two steps over s_to,
+    // one LDS read per position per step, the RR reads of a step independent: one LDS round
+    // trip per step instead of one per step and position), then the entries, branch-free
+    // (a branch around a read serializes the positions' reads; positions past R read entry
+    // 0 of tile 0 and drop it)
+    auto gather = [&](uint32_t r0, int (&gi)[RR], uint32_t (&gr)[RR]) {
         int own[RR];
 #pragma unroll
         for (int u = 0; u < RR; ++u) own[u] = 0;
@@ -1647,19 +1621,17 @@ dense_frag_build_kernel(ChunkGeom g, uint32_t nblk, int64_t ntiles, const uint16
         for (int step = top >> 1; step > 0; step >>= 1) {
 #pragma unroll
             for (int u = 0; u < RR; ++u) {
-                const uint32_t r = u * T + threadIdx.x;
-                // branch-free (a branch around the read serializes the positions' reads):
+                const uint32_t r = r0 + u * T + threadIdx.x;
                 // s_to[ntiles] = R stops every position below R at the last tile
                 const int cand = own[u] + step;
                 const uint32_t v = s_to[min(cand, (int)ntiles)];
                 own[u] = v <= r ? cand : own[u];
             }
         }
-        // the entries, branch-free too (positions past R read entry 0 of tile 0 and drop it)
         uint32_t pos[RR], tb[RR];
 #pragma unroll
         for (int u = 0; u < RR; ++u) {
-            const uint32_t r = u * T + threadIdx.x;
+            const uint32_t r = r0 + u * T + threadIdx.x;
             const uint32_t in = 0u - (uint32_t)(r < R);  // masks, not selects: no branch around a read
             const int o = (int)((uint32_t)own[u] & in);
             pos[u] = (s_pb[o] + r) & in;
@@ -1667,16 +1639,77 @@ dense_frag_build_kernel(ChunkGeom g, uint32_t nblk, int64_t ntiles, const uint16
         }
 #pragma unroll
         for (int u = 0; u < RR; ++u) {
-            const uint32_t r = u * T + threadIdx.x;
+            const uint32_t r = r0 + u * T + threadIdx.x;
             const int i = (int)ko[pos[u]];
             const uint32_t rw = tb[u] + rl[pos[u]];
-            ridx[u] = r < R ? i : -1;
-            rrow[u] = rw;
+            gi[u] = r < R ? i : -1;
+            gr[u] = rw;
         }
         if (ids32 != nullptr) {  // uniform
 #pragma unroll
-            for (int u = 0; u < RR; ++u) rrow[u] = ridx[u] >= 0 ? (uint32_t)ids32[rrow[u]] : 0u;
+            for (int u = 0; u < RR; ++u) gr[u] = gi[u] >= 0 ? (uint32_t)ids32[gr[u]] : 0u;
         }
+    };
+    const bool in_regs = R <= (uint32_t)(T * RR);
+    if (threadIdx.x < NSUB) s_dup[threadIdx.x] = in_regs ? 0u : 1u;  // more rows than the registers hold
+    if (threadIdx.x == 0 && !in_regs) s_sp = atomicAdd(&ctr->spill_used, 2ull * R);
+    if (threadIdx.x <= NSUB) s_qo[threadIdx.x] = 0;
+    __syncthreads();
+    // a block with more rows than the registers hold gathers them once into the spill
+    // pool (key index << 32 | row), then files them by duplicate sub-range (a second copy
+    // in the pool): each sub-range's duplicate passes stream its own rows only (they
+    // streamed every row of the block once per sub-range: C3's build 310 -> 268 us)
+    unsigned long long* sp = spill + (in_regs ? 0ull : s_sp);
+    if (!in_regs) {
+        const int lane = threadIdx.x & 63;
+        uint32_t qn[NSUB];
+#pragma unroll
+        for (uint32_t q = 0; q < NSUB; ++q) qn[q] = 0;
+        for (uint32_t r0 = 0; r0 < R; r0 += T * RR) {
+            int gi[RR];
+            uint32_t gr[RR];
+            gather(r0, gi, gr);
+#pragma unroll
+            for (int u = 0; u < RR; ++u) {
+                if (gi[u] >= 0) sp[r0 + u * T + threadIdx.x] = ((unsigned long long)(uint32_t)gi[u] << 32) | gr[u];
+#pragma unroll
+                for (uint32_t q = 0; q < NSUB; ++q) qn[q] += (uint32_t)(gi[u] >= 0 && (uint32_t)gi[u] / kDenseSub == q);
+            }
+        }
+#pragma unroll
+        for (uint32_t q = 0; q < NSUB; ++q)
+            if (qn[q]) atomicAdd(&s_qo[q + 1], qn[q]);
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            for (uint32_t q = 0; q < NSUB; ++q) {
+                s_qo[q + 1] += s_qo[q];
+                s_qc[q] = s_qo[q];
+            }
+        }
+        __syncthreads();
+        unsigned long long* sp2 = sp + R;
+        for (uint32_t r0 = 0; r0 < R; r0 += T) {
+            const uint32_t r = r0 + threadIdx.x;
+            const unsigned long long v = r < R ? sp[r] : 0ull;
+            const uint32_t q = (uint32_t)(v >> 32) / kDenseSub;
+#pragma unroll
+            for (uint32_t qq = 0; qq < NSUB; ++qq) {
+                const unsigned long long m = __ballot(r < R && q == qq);
+                if (m == 0) continue;  // uniform
+                uint32_t base = 0;
+                if (lane == 0) base = atomicAdd(&s_qc[qq], (uint32_t)__popcll(m));
+                base = (uint32_t)__shfl((int)base, 0, 64);
+                if (r < R && q == qq)
+                    sp2[base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] = v;
+            }
+        }
+        __syncthreads();
+        sp = sp2;  // by sub-range: sub-range q's rows at [s_qo[q], s_qo[q + 1])
+    }
+    uint32_t rrow[RR];
+    int ridx[RR];
+    if (in_regs) {
+        gather(0, ridx, rrow);
 #pragma unroll
         for (int u = 0; u < RR; ++u)
             if (ridx[u] >= 0 && atomicExch(&refs[ridx[u]], rrow[u]) != kMiss) s_dup[ridx[u] / kDenseSub] = 1u;
@@ -1694,10 +1727,7 @@ dense_frag_build_kernel(ChunkGeom g, uint32_t nblk, int64_t ntiles, const uint16
             for (int u = 0; u < RR; ++u)
                 if (ridx[u] >= lo && ridx[u] < hi) atomicAdd(&refs[ridx[u]], 1u);
         } else {
-            for (uint32_t r = threadIdx.x; r < R; r += T) {
-                const int i = (int)(sp[r] >> 32);
-                if (i >= lo && i < hi) atomicAdd(&refs[i], 1u);
-            }
+            for (uint32_t r = s_qo[q] + threadIdx.x; r < s_qo[q + 1]; r += T) atomicAdd(&refs[(int)(sp[r] >> 32)], 1u);
         }
         __syncthreads();
         for (uint32_t i = threadIdx.x; i < kDenseSub; i += T) {
@@ -1743,10 +1773,9 @@ dense_frag_build_kernel(ChunkGeom g, uint32_t nblk, int64_t ntiles, const uint16
             for (int u = 0; u < RR; ++u)
                 if (ridx[u] >= lo && ridx[u] < hi) place(ridx[u], rrow[u]);
         } else {
-            for (uint32_t r = threadIdx.x; r < R; r += T) {
+            for (uint32_t r = s_qo[q] + threadIdx.x; r < s_qo[q + 1]; r += T) {
                 const unsigned long long v = sp[r];
-                const int i = (int)(v >> 32);
-                if (i >= lo && i < hi) place(i, (uint32_t)v);
+                place((int)(v >> 32), (uint32_t)v);
             }
         }
         __syncthreads();
@@ -2128,9 +2157,6 @@ hashed_frag_build_kernel(uint32_t nb, uint32_t clog2, uint32_t s0, uint32_t nsl,
 //          bucket's line in LDS (exact compare of stored keys, linear probing inside the
 //          chunk, as lookup4); key 0 reads the side bucket.
 constexpr int kHsSliceLog = 11;  // buckets per hashed slice: 2^11 x 64 B = 128 KB of LDS
-#ifndef DFP_HL_DEFER
-#define DFP_HL_DEFER 0
-#endif
 
 // ref of stored key sk (!= 0) in the LDS image of a hashed slice whose first bucket is
 // sbase; linear probing wraps inside the key's chunk (cmask), as the table was built
@@ -2148,6 +2174,8 @@ __device__ __forceinline__ uint32_t lds_bucket_ref(const uint4* __restrict__ img
     return ref;
 }
 
+// Measured (r04) and not kept: a count in its segment header deferred to a pass after the
+// window (no per-row ballot): C2h lookup 771 -> 771 us.
 // Measured (r04) and not kept: every hashed row branch-free (selects, stores dropped by an
 // out-of-range offset, the rare rows deferred to a pass after the window, two rows per
 // scheduling region; 108 VGPRs): C2h lookup 771 -> 1107 us.
@@ -2416,9 +2444,6 @@ sl_lookup_kernel(TableView tv, uint32_t wlog, uint32_t nslices, int64_t ntiles, 
             DFP_PH_WAIT();
             DFP_PH(2);
             if constexpr (HASHED) {
-#if DFP_HL_DEFER
-                uint32_t hl_unk = 0;  // bit u: row u's count is in its segment header
-#endif
 #pragma unroll
                 for (int u = 0; u < NU; ++u) {
                     if (w0 + u * 64 >= R) continue;  // uniform: past the run
@@ -2441,17 +2466,10 @@ sl_lookup_kernel(TableView tv, uint32_t wlog, uint32_t nslices, int64_t ntiles, 
                     // that waits there. Merged into the common path, that load's wait was an
                     // s_waitcnt vmcnt(0) on every row — for the previous rows' ref stores (loads
                     // and stores share vmcnt): one store round trip per 64 entries.
-#if DFP_HL_DEFER
-                    // a count in its segment header: the row's correction goes to its tile's
-                    // count after the window (no per-row branch)
-                    hl_unk |= (uint32_t)(c == kCountUnknown) << u;
-                    c = c == kCountUnknown ? 1u : c;
-#else
                     if (__ballot(c == kCountUnknown) != 0) {
                         if (c == kCountUnknown) c = tv.dup_rows[v & tv.off_mask];
                         asm volatile("" : "+v"(c));
                     }
-#endif
                     __builtin_amdgcn_raw_buffer_store_b32(v, rres, (int)(o * 4), 0, 0);
                     uint32_t d = c - 1u;  // kOob: c = 1
                     if (d != 0xFFFFFFFFu && d >= kBigCorr) {
@@ -2462,18 +2480,6 @@ sl_lookup_kernel(TableView tv, uint32_t wlog, uint32_t nslices, int64_t ntiles, 
                     if (off_end & (1u << u)) scst[off[u] >> 26] = corr_run;
                     corr_run = (uint32_t)__builtin_amdgcn_readlane((int)corr_run, 63);
                 }
-#if DFP_HL_DEFER
-                if (__ballot(hl_unk != 0) != 0) {  // rare: keys of more than 63 rows
-                    for (int u = 0; u < NU; ++u) {
-                        if (!((hl_unk >> u) & 1u)) continue;
-                        uint32_t c;
-                        const uint32_t v =
-                            lds_bucket_ref(reinterpret_cast<const uint4*>(s_tab), tv.nb, sbase, cmask, ev[u], &c);
-                        c = tv.dup_rows[v & tv.off_mask];
-                        atomicAdd(&tcnt[tc + slane[off[u] >> 26]], (unsigned long long)((long long)c - 1));
-                    }
-                }
-#endif
             } else {
 #pragma unroll
                 for (int u = 0; u < NU; ++u) {
@@ -3583,7 +3589,7 @@ bool frag_build_ok(const ChunkGeom& g, int64_t ftiles) {
 int64_t frag_build_scratch_bytes(const ChunkGeom& g, int64_t ftiles, int64_t total) {
     const int64_t nbins = dense_blocks(g.nchunks) + 1;
     return 2 * ftiles * kSlTile + 2 * ftiles * kSlTile + 2 * ftiles * nbins + 2 * ((ftiles + 63) & ~(int64_t)63) * nbins +
-           8 * total + 6 * 256;
+           16 * total + 6 * 256;  // spill pool: the spilled rows twice (gathered, then by sub-range)
 }
 
 // dense frag build: consecutive key blocks per XCD run (DFP_HJ_FRAG_RUN; 1 = plain order)
@@ -3625,7 +3631,7 @@ hipError_t launch_build_frag(int key_bytes, const Segment* h_segs, int nseg, con
     // partials folded by every partition block instead of minmax_final_kernel: the build
     // partition 38 -> 44 us against a 5.5 us launch, and the probe's partition (the same
     // kernel) 218 -> 224 us.
-    unsigned long long* spill = (unsigned long long*)p;  // total rows at most
+    unsigned long long* spill = (unsigned long long*)p;  // 2 x total rows at most
     int64_t t0 = 0;
     for (int i = 0; i < nseg; ++i) {
         const Segment& sg = h_segs[i];
