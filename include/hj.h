@@ -138,7 +138,11 @@ hj_status hj_build_append(hj_table* t, int partition, const void* keys,
  * returns the table is read-only and may be probed concurrently. A direct-addressed
  * build runs on asynchronously when no input was borrowed without HJ_BORROW_KEEP: every
  * later call on the table (probe, lookup, stats) waits for it on the device, and
- * hj_table_stream_wait orders any other stream after it. */
+ * hj_table_stream_wait orders any other stream after it. With the key range left on the
+ * device (the default speculative build; DFP_HJ_SPEC_BUILD=0 turns it off) the layout is
+ * settled by the first call that uses the table: a build side whose key range takes the
+ * hashed layout is built then, so an error of that build (HJ_ERR_OOM, ...) is returned by
+ * that call and by every later one. */
 hj_status hj_build_finish(hj_table* t, int partition);
 
 /* Optional, before the barrier: every valid build key lies in [key_lo, key_hi] (the caller
