@@ -103,12 +103,10 @@ int ev_scope() {
     }();
     return v;
 }
-// 1: device-scope release; 3: no system-scope fence at all (probe-end events only)
-unsigned probe_ev_flags() {
-    return hipEventDisableTiming | (ev_scope() == 3 ? hipEventDisableSystemFence
-                                                    : ev_scope() >= 1 ? hipEventReleaseToDevice : 0u);
-}
-unsigned build_ev_flags() { return ev_scope() == 2 ? hipEventReleaseToDevice : hipEventDefault; }
+// (measured: probe-end events without any system-scope fence changed nothing either,
+// profiles/r04_nontemporal_ab.txt)
+unsigned probe_ev_flags() { return hipEventDisableTiming | (ev_scope() >= 1 ? hipEventReleaseToDevice : 0u); }
+unsigned build_ev_flags() { return ev_scope() >= 2 ? hipEventReleaseToDevice : hipEventDefault; }
 
 bool acquire_resources(int dev, BuildResources* r) {
     {

@@ -1345,7 +1345,7 @@ __device__ __forceinline__ void hist_excl_scan(uint32_t* s_hist, uint32_t* s_w, 
     __syncthreads();
 }
 
-template <typename K, bool HAS_VALID, bool NTK = false>  // NTK: nontemporal key loads (whole tiles)
+template <typename K, bool HAS_VALID>
 __global__ void __launch_bounds__(kSlThreads, 8)  // 8 waves per SIMD = two workgroups per CU: <= 64 VGPRs
 sl_partition_kernel(int64_t dmin, uint64_t drange, uint32_t wlog, uint32_t nslices, const void* __restrict__ keys,
                     const uint8_t* __restrict__ valid, int64_t voff, int64_t n, bool vec,
@@ -1399,14 +1399,7 @@ sl_partition_kernel(int64_t dmin, uint64_t drange, uint32_t wlog, uint32_t nslic
             const int loc0 = g * (kSlThreads * 4) + threadIdx.x * 4;
             if constexpr (FULL && sizeof(K) == 8) {
                 const v2i64* p = reinterpret_cast<const v2i64*>(reinterpret_cast<const K*>(keys) + tile0 + loc0);
-                v2i64 a, b;
-                if constexpr (NTK) {
-                    a = __builtin_nontemporal_load(p);
-                    b = __builtin_nontemporal_load(p + 1);
-                } else {
-                    a = p[0];
-                    b = p[1];
-                }
+                const v2i64 a = p[0], b = p[1];
                 dst[0] = a.x; dst[1] = a.y; dst[2] = b.x; dst[3] = b.y;
             } else if constexpr (FULL) {
                 const int4 a = *reinterpret_cast<const int4*>(reinterpret_cast<const K*>(keys) + tile0 + loc0);
@@ -2687,7 +2680,7 @@ __device__ __forceinline__ uint32_t sl_count(const TableView& tv, uint32_t r) {
 constexpr int kSlEmitThreads = 512;
 constexpr int kSlWaveRows = kSlTile / (kSlEmitThreads / 64);  // 2048
 
-template <bool HAS_ROW_IDS, bool HAS_PROBE_IDS, bool NTS = false>  // NTS: nontemporal pair stores
+template <bool HAS_ROW_IDS, bool HAS_PROBE_IDS>
 __global__ void __launch_bounds__(kSlEmitThreads, 4)  // two workgroups per CU: <= 128 VGPRs
 sl_emit_kernel(TableView tv, const uint32_t* __restrict__ tent, const uint16_t* __restrict__ rl,
                const uint32_t* __restrict__ res, const uint32_t* __restrict__ probe_ids, uint32_t pbase,
@@ -2701,14 +2694,11 @@ sl_emit_kernel(TableView tv, const uint32_t* __restrict__ tent, const uint16_t* 
     __shared__ uint32_t s_own[kSlEmitThreads / 64][64];  // per wave: owner markers of one output window
     __shared__ int64_t s_nxt;                              // dyn: the tile after the next one
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    // Measured (r04) and not kept: nontemporal pair stores (C2 162.4K -> 140.8K Mrows/s) and
+    // nontemporal probe-key loads in the partition (-3.5 %), profiles/r04_nontemporal_ab.txt
     auto put = [&](unsigned long long o, uint64_t b, uint32_t p) {
-        if constexpr (NTS) {
-            __builtin_nontemporal_store(b, out_b + o);
-            __builtin_nontemporal_store(p, out_p + o);
-        } else {
-            out_b[o] = b;
-            out_p[o] = p;
-        }
+        out_b[o] = b;
+        out_p[o] = p;
     };
     constexpr int U = kSlTile / (kSlEmitThreads * 4);  // 8 x (4 rows + 4 refs) per thread
     uint2 e4[U];
@@ -4028,12 +4018,6 @@ hipError_t launch_probe_sliced(int key_bytes, const TableView& tv, const void* k
         const char* ev = getenv("DFP_HJ_SL_NT");
         return ev ? atoi(ev) : 0;
     }();
-    // DFP_HJ_SL_NTIO (A/B): bit 0 nontemporal probe-key loads of whole tiles (int64 keys, no
-    // nulls), bit 1 nontemporal pair stores (no id arrays)
-    static const int sl_ntio = [] {
-        const char* ev = getenv("DFP_HJ_SL_NTIO");
-        return ev ? atoi(ev) : 0;
-    }();
 #ifdef DFP_HJ_ABLATIONS
     // diagnostic build only (wrong pairs): emit 1 no stores, 2 no entries, 8 no duplicate
     // segment reads; lookup 4 no bucket lookup (hashed), 128 plain item order
@@ -4082,14 +4066,12 @@ hipError_t launch_probe_sliced(int key_bytes, const TableView& tv, const void* k
             const uint64_t lo = (uint64_t)s0 << wlog;
             const int64_t dmin_p = (int64_t)((uint64_t)tv.dmin + lo);
             const uint64_t drange_p = std::min<uint64_t>(tv.drange - lo, (uint64_t)nsl << wlog);
-#define DFP_SLP(KT, HV, ...)                                                                                 \
-    sl_partition_kernel<KT, HV, ##__VA_ARGS__><<<(unsigned)nt, kSlThreads, 0, s>>>(dmin_p, drange_p, wlog, nsl, keys, valid, voff, n, \
+#define DFP_SLP(KT, HV)                                                                                      \
+    sl_partition_kernel<KT, HV><<<(unsigned)nt, kSlThreads, 0, s>>>(dmin_p, drange_p, wlog, nsl, keys, valid, voff, n, \
                                                                    vec, (uint16_t*)w.ko, w.rl, w.toff, sl_nt, 0, 0,   \
                                                                    nullptr, h, w.tcnt, w.tent, w.wcnt, SpecGeo{})
             if (key_bytes == 8) {
-                if (valid) DFP_SLP(int64_t, true);
-                else if (sl_ntio & 1) DFP_SLP(int64_t, false, true);
-                else DFP_SLP(int64_t, false);
+                if (valid) DFP_SLP(int64_t, true); else DFP_SLP(int64_t, false);
             } else {
                 if (valid) DFP_SLP(int32_t, true); else DFP_SLP(int32_t, false);
             }
@@ -4154,15 +4136,14 @@ hipError_t launch_probe_sliced(int key_bytes, const TableView& tv, const void* k
         return !(e != nullptr && e[0] == '0');
     }();
     const unsigned egrid = (unsigned)std::min<int64_t>(nt, (int64_t)sl_emit_wgs_per_cu() * sl_num_cus());
-#define DFP_SLE(RI, PI, ...)                                                                                      \
-    sl_emit_kernel<RI, PI, ##__VA_ARGS__><<<egrid, kSlEmitThreads, 0, s>>>(tv, w.tent, w.rl, w.res, probe_ids, pbase, w.tcnt, nt,   \
+#define DFP_SLE(RI, PI)                                                                                           \
+    sl_emit_kernel<RI, PI><<<egrid, kSlEmitThreads, 0, s>>>(tv, w.tent, w.rl, w.res, probe_ids, pbase, w.tcnt, nt,   \
                                                            out_b, out_p, cap, d_total,                      \
                                                            hashed || !count_free ? nullptr : w.wcnt,          \
                                                            emit_dyn ? w.tcnt + nt : nullptr)
     if (ri && pi) DFP_SLE(true, true);
     else if (ri) DFP_SLE(true, false);
     else if (pi) DFP_SLE(false, true);
-    else if (sl_ntio & 2) DFP_SLE(false, false, true);
     else DFP_SLE(false, false);
 #undef DFP_SLE
     return hipGetLastError();
