@@ -605,6 +605,8 @@ def main():
             if per_step_sync:
                 torch.cuda.synchronize(dev)
                 job.collect()
+        if hasattr(job, "drain"):  # a prefetched native build side: inside the timed region
+            job.drain()
         torch.cuda.synchronize(dev)
         barrier()
         elapsed = time.perf_counter() - t_start
@@ -755,7 +757,8 @@ class DistJob:
         self.host_ms.append((time.perf_counter() - h0) * 1e3)
         ev["end"].record()
         self.dj.events = None
-        prev, self._pending = self._pending, (table, result, ev)
+        native = bool(getattr(self.dj, "last_native", False))
+        prev, self._pending = self._pending, (table, result, ev, native)
         if prev is not None:
             self._collect(*prev)
 
@@ -765,9 +768,17 @@ class DistJob:
         pending, self._pending = self._pending, None
         self._collect(*pending)
 
-    def _collect(self, table, result, ev):
+    def _collect(self, table, result, ev, native=False):
         b, _ = result()
         self.matches = int(b.numel())
+        del b, _
+        if native:  # hj_dist_join_radix: the job's own stage events (build side, exchange, probe)
+            bms, xms, pms = result.job.times()
+            self.build_ms.append(bms)
+            self.exchange_ms.append(xms)
+            self.probe_ms.append(pms)
+            table.close()
+            return
         ev["end"].synchronize()
         # both probe events on the probe's (current) stream; the build span on the build stream
         self.probe_ms.append(ev["probe_start"].elapsed_time(ev["end"]))
@@ -802,8 +813,12 @@ class ShardedJob:
         self.kernel_desc = ("sharded build: range exchange of the build side (RCCL), local build of the rank's key "
                             "range, all_gather of the table pieces, sliced probe of the local rows")
         self._pending = None
+        self._next = None  # the next step's native build side, started during this step's probe
         self.ready = torch.cuda.Event()  # the inputs exist: the build stream waits for this only
         self.ready.record()
+
+    def _start(self):
+        return self.dj.start_sharded(self.bk, self.bbase, self.bstream, self.ready, self.pk.dtype)
 
     def step(self):
         ev = {k: torch.cuda.Event(enable_timing=True)
@@ -811,8 +826,13 @@ class ShardedJob:
         self.dj.events = ev
         cur = torch.cuda.current_stream(self.dev)
         h0 = time.perf_counter()
+        pending, self._next = self._next or self._start(), None
         table, result = self.dj.join_sharded(self.bk, self.bbase, self.pk, self.pbase, self.cap,
-                                             build_stream=self.bstream, inputs_ready=self.ready)
+                                             build_stream=self.bstream, inputs_ready=self.ready, pending=pending)
+        if self.dj.last_native:
+            # step k + 1's build side, queued now: the worker's host reads wait while the device
+            # runs this step's probe (the build keys are resident and unchanged between steps)
+            self._next = self._start()
         self.host_ms.append((time.perf_counter() - h0) * 1e3)
         self.dj.events = None
         ev["end"].record(cur)
@@ -833,13 +853,25 @@ class ShardedJob:
         ev["end"].synchronize()
         # the build side (plan, exchange, local build, gathers) on the build stream; the
         # probe from its launch to its end on the probe stream (with any wait for the table)
-        if not native:
+        if native:  # the build side ran as a job: its table's build time spans it (plan to gathers)
+            self.build_ms.append(table.build_ns() / 1e6)
+        else:
             self.exchange_ms.append(ev["partitioned"].elapsed_time(ev["exchanged"]))
-        self.build_ms.append(ev["build_start"].elapsed_time(ev["build_end"]))
+            self.build_ms.append(ev["build_start"].elapsed_time(ev["build_end"]))
         self.probe_ms.append(ev["probe_start"].elapsed_time(ev["end"]))
         table.close()
 
+    def drain(self):
+        """The prefetched build side (the step after the last): finish its job."""
+        if self._next is not None:
+            nxt, self._next = self._next, None
+            t, _ = nxt.table()
+            nxt.close()
+            torch.cuda.current_stream(self.dev).synchronize()
+            t.close()
+
     def finish(self):
+        self.drain()
         self.collect()
 
 

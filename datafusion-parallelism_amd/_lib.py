@@ -121,13 +121,37 @@ SIGNATURES = [
     ("hj_comm_unique_id", I32, [P]),
     ("hj_comm_create", I32, [I32, I32, P, I32, PP]),
     ("hj_comm_free", None, [P]),
-    ("hj_dist_build_sharded", I32, [P, I32, P, P, I64, I64, I64, P, PP, ctypes.POINTER(HjDistInfo)]),
+    ("hj_dist_build_sharded", I32, [P, I32, P, P, I64, I64, I64, I32, P, PP, ctypes.POINTER(HjDistInfo)]),
+    ("hj_dist_build_sharded_async", I32, [P, I32, P, P, I64, I64, I64, I32, P, PP]),
+    ("hj_dist_join_radix", I32, [P, I32, P, P, I64, I64, I64, I32, P, P, I64, I64, I64, P, PP]),
+    ("hj_dist_job_wait", I32, [P, ctypes.POINTER(HjDistInfo)]),
+    ("hj_dist_job_table", I32, [P, PP, ctypes.POINTER(HjDistInfo)]),
+    ("hj_dist_job_pairs", I32, [P, PP, PP, ctypes.POINTER(ctypes.c_int64)]),
+    ("hj_dist_job_times", I32, [P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
+                                ctypes.POINTER(ctypes.c_double)]),
+    ("hj_dist_job_free", None, [P]),
     ("hj_gen_perm_keys", I32, [P, I64, I64, I64, P]),
     ("hj_gen_uniform_keys", I32, [P, I64, U64, I64, P]),
     ("hj_gen_exponential_keys", I32, [P, I32, I32]),
 ]
 
+# the test library's extra entry points (lib/libdfp_hj_commtest.so: the thread transport)
+COMMTEST_PATH = os.path.join(HERE, "lib", "libdfp_hj_commtest.so")
+COMMTEST_SIGNATURES = [
+    ("hj_test_hub_create", P, [I32, ctypes.c_double]),
+    ("hj_test_hub_free", None, [P]),
+    ("hj_test_comm_create", I32, [P, I32, I32, PP]),
+    ("hj_test_comm_fail_at", None, [P, I32, I32]),
+]
+
 _lib = None
+
+
+def _bind(L: ctypes.CDLL, sigs) -> None:
+    for name, res, args in sigs:
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
 
 
 def load() -> ctypes.CDLL:
@@ -139,17 +163,26 @@ def load() -> ctypes.CDLL:
         raise ImportError(f"{LIB_PATH} is missing: run `python __graft_entry__.py build` "
                           "(or datafusion-parallelism_amd/build.py). There is no CPU fallback.")
     L = ctypes.CDLL(LIB_PATH)
-    for name, res, args in SIGNATURES:
-        f = getattr(L, name)
-        f.restype = res
-        f.argtypes = args
+    _bind(L, SIGNATURES)
     _lib = L
     return L
 
 
-def check(status: int) -> None:
+def load_commtest() -> ctypes.CDLL:
+    """The test library (the product's entry points + the in-process thread transport).
+    Tests only: a handle made by one library must not be passed to the other."""
+    if not os.path.exists(COMMTEST_PATH):
+        raise ImportError(f"{COMMTEST_PATH} is missing: run `python __graft_entry__.py build`")
+    L = ctypes.CDLL(COMMTEST_PATH)
+    _bind(L, SIGNATURES + COMMTEST_SIGNATURES)
+    return L
+
+
+def check(status: int, L: ctypes.CDLL | None = None) -> None:
+    """Raise HjError for a non-OK status; the message from library `L` (the one that
+    failed: its hj_last_error is thread-local to it), default the product library."""
     if status != HJ_OK:
-        msg = load().hj_last_error()
+        msg = (L or load()).hj_last_error()
         raise HjError(status, msg.decode() if msg else "")
 
 

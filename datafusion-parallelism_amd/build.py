@@ -26,7 +26,11 @@ ARCH = "gfx950"
 
 SOURCES_HIP = ["hj_kernels.hip", "hj_columns.hip", "hj_keys.hip"]
 SOURCES_CPP = ["hj_api.cpp", "hj_dist.cpp"]
-HEADERS = ["hj_device.h", "hj_launch.h", "hj_util.h", "hj_host.h"]
+HEADERS = ["hj_device.h", "hj_launch.h", "hj_util.h", "hj_host.h", "hj_comm.h"]
+# test library: the product objects + the in-process thread transport for hj_comm
+# (tests/test_gpu_dist_threads.py); never part of libdfp_hj.so
+COMMTEST_LIB = os.path.join(LIBDIR, "libdfp_hj_commtest.so")
+SOURCES_COMMTEST = ["hj_comm_threads.cpp"]
 
 
 def torch_lib_dir() -> str:
@@ -39,11 +43,11 @@ def torch_lib_dir() -> str:
     return d
 
 
-def _stale(lib: str = LIB) -> bool:
+def _stale(lib: str = LIB, extra: tuple[str, ...] = ()) -> bool:
     if not os.path.exists(lib):
         return True
     t = os.path.getmtime(lib)
-    deps = [os.path.join(CSRC, f) for f in SOURCES_HIP + SOURCES_CPP + HEADERS]
+    deps = [os.path.join(CSRC, f) for f in SOURCES_HIP + SOURCES_CPP + HEADERS + list(extra)]
     deps += [os.path.join(INCLUDE, "hj.h"), __file__]
     return any(os.path.getmtime(d) > t for d in deps)
 
@@ -90,5 +94,28 @@ def build(force: bool = False, verbose: bool = False, defines: tuple[str, ...] =
     return out
 
 
+def build_commtest(force: bool = False, verbose: bool = False) -> str:
+    """lib/libdfp_hj_commtest.so: the product library's objects (built first) plus the
+    thread transport (hj_test_* entry points). Test infrastructure only."""
+    build(force=force, verbose=verbose)
+    if not force and not _stale(COMMTEST_LIB, tuple(SOURCES_COMMTEST)):
+        return COMMTEST_LIB
+    rocm = os.environ.get("ROCM_PATH", "/opt/rocm")
+    tlib = torch_lib_dir()
+    objdir = os.path.join(HERE, "build")
+    objs = [os.path.join(objdir, src + ".o") for src in SOURCES_HIP + SOURCES_CPP]
+    for src in SOURCES_COMMTEST:
+        obj = os.path.join(objdir, src + ".o")
+        _run(["g++", "-O2", "-fPIC", "-std=c++17", "-D__HIP_PLATFORM_AMD__", "-I", INCLUDE,
+              "-I", os.path.join(rocm, "include"), "-c", os.path.join(CSRC, src), "-o", obj], verbose)
+        objs.append(obj)
+    tmp = COMMTEST_LIB + ".tmp"
+    _run(["g++", "-shared", "-o", tmp, *objs, f"-L{tlib}", "-lamdhip64", "-lrccl", f"-Wl,-rpath,{tlib}",
+          "-Wl,--no-undefined", "-lpthread"], verbose)
+    os.replace(tmp, COMMTEST_LIB)
+    return COMMTEST_LIB
+
+
 if __name__ == "__main__":
     print(build(force="--force" in sys.argv, verbose=True))
+    print(build_commtest(verbose=True))

@@ -365,6 +365,7 @@ struct hj_table {
     // measure (hj_set_device_budget)
     int64_t live_bytes = 0, peak_bytes = 0;
     std::vector<hj_table*> owned_tables;  // freed with this table (hj_dist.cpp's local pieces)
+    hipEvent_t ext_ev0 = nullptr;         // table_set_start_event: the build time's start (owned)
     // build with the key range left on the device (SpecGeo, build_attempt): the host has not
     // read the range yet; ensure_geometry reads it before any use of the table's geometry
     std::atomic<bool> spec_pending{false};
@@ -389,6 +390,11 @@ void table_adopt_block(hj_table* t, int dev, void* p, size_t bytes) {
     t->multi_bufs.emplace_back(dev, p, bytes ? bytes : 64);
 }
 void table_adopt_table(hj_table* t, hj_table* other) { t->owned_tables.push_back(other); }
+void table_set_start_event(hj_table* t, hipEvent_t ev) {
+    if (t->ext_ev0) (void)hipEventDestroy(t->ext_ev0);
+    t->ext_ev0 = ev;
+    t->build_ns = -1;
+}
 }  // namespace host
 }  // namespace dfp
 
@@ -817,7 +823,7 @@ int64_t build_time_ns(hj_table* t) {
     if (t->build_ns < 0) {
         float ms = 0;
         if (hipEventSynchronize(t->res.ev1) != hipSuccess ||
-            hipEventElapsedTime(&ms, t->res.ev0, t->res.ev1) != hipSuccess)
+            hipEventElapsedTime(&ms, t->ext_ev0 ? t->ext_ev0 : t->res.ev0, t->res.ev1) != hipSuccess)
             return -1;
         t->build_ns = (int64_t)(ms * 1e6);
     }
@@ -2002,6 +2008,7 @@ void hj_table_free(hj_table* t) {
     delete t->multi;  // its shards first: they borrow multi_bufs
     for (auto& b : t->multi_bufs) cache_free(std::get<0>(b), std::get<1>(b), std::get<2>(b));
     for (hj_table* o : t->owned_tables) hj_table_free(o);
+    if (t->ext_ev0) (void)hipEventDestroy(t->ext_ev0);
     for (auto& part : t->parts)
         for (auto& hs : part) {
             for (void* p : hs.owned) (void)hipFree(p);

@@ -21,6 +21,9 @@ void free_block(int dev, void* p, size_t bytes);
 void table_adopt_block(hj_table* t, int dev, void* p, size_t bytes);
 // the table frees `other` when it is freed (a piece whose arrays were copied out)
 void table_adopt_table(hj_table* t, hj_table* other);
+// the table's build time runs from `ev` (a timing event the caller recorded where the
+// work the table stands for began, e.g. a multi-GPU build side); the table owns it
+void table_set_start_event(hj_table* t, hipEvent_t ev);
 
 }  // namespace host
 }  // namespace dfp

@@ -452,45 +452,156 @@ def all_to_all_rows(keys_by_dest: torch.Tensor, ids_by_dest: torch.Tensor, count
     return rk, ri, st
 
 
-class NativeComm:
-    """An hj_comm — RCCL behind the C ABI (hj_dist.cpp) — for the ranks of `group`: rank 0
-    makes the 128-byte unique id (hj_comm_unique_id), the group broadcasts it (the
-    out-of-band channel a Rust host would provide itself), every rank creates the
-    communicator on its GPU (hj_comm_create, collective)."""
+def check_l(L, status: int) -> None:
+    check(status, L)
 
-    def __init__(self, device: torch.device, group=None):
-        L = _lib.load()
+
+class _DevArray:
+    """A device buffer owned by a native job, exported to torch without a copy
+    (``__cuda_array_interface__``): the tensor torch.as_tensor makes holds this object,
+    which holds the job, so the job's memory lives as long as the tensor."""
+
+    def __init__(self, ptr: int, n: int, typestr: str, owner):
+        self.owner = owner
+        self.__cuda_array_interface__ = {"shape": (n,), "typestr": typestr, "data": (ptr or 0, False),
+                                         "version": 2}
+
+
+def _tensor_of(ptr: int, n: int, dtype: torch.dtype, device: torch.device, owner) -> torch.Tensor:
+    if n == 0 or not ptr:
+        return torch.empty(0, dtype=dtype, device=device)
+    ts = {torch.int64: "<i8", torch.int32: "<i4"}[dtype]
+    return torch.as_tensor(_DevArray(ptr, n, ts, owner), device=device)
+
+
+class NativeJob:
+    """An hj_dist_job (one multi-GPU plan step queued on the communicator's worker thread):
+    the caller's thread returns at once; table() / pairs() wait for the job's host steps."""
+
+    def __init__(self, L, handle: ctypes.c_void_p, device: torch.device, keep=(), key_type: int = HJ_INT64):
+        self._L, self._h, self.device, self._keep, self.key_type = L, handle, device, list(keep), key_type
+
+    def wait(self):
+        info = _lib.HjDistInfo()
+        check_l(self._L, self._L.hj_dist_job_wait(self._h, ctypes.byref(info)))
+        return info
+
+    def table(self):
+        """The job's table (the sharded build side: the whole build side) -> (HashTable,
+        HjDistInfo); the table keeps the job's inputs alive."""
+        h = ctypes.c_void_p()
+        info = _lib.HjDistInfo()
+        check_l(self._L, self._L.hj_dist_job_table(self._h, ctypes.byref(h), ctypes.byref(info)))
+        return HashTable.from_handle(h, self.device.index or 0, self.key_type, keep=self._keep, lib=self._L), info
+
+    def pairs(self):
+        """A radix job's pairs -> (build_idx int64 [u64 values], probe_idx int32 [u32
+        values]) as device tensors over the job's buffers (no copy)."""
+        b, p, n = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_int64()
+        check_l(self._L, self._L.hj_dist_job_pairs(self._h, ctypes.byref(b), ctypes.byref(p), ctypes.byref(n)))
+        return (_tensor_of(b.value, n.value, torch.int64, self.device, self),
+                _tensor_of(p.value, n.value, torch.int32, self.device, self))
+
+    def times(self) -> tuple[float, float, float]:
+        """(build_ms, exchange_ms, probe_ms) of the finished job's device stages."""
+        v = [ctypes.c_double() for _ in range(3)]
+        check_l(self._L, self._L.hj_dist_job_times(self._h, *[ctypes.byref(x) for x in v]))
+        return tuple(x.value for x in v)
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._L.hj_dist_job_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class _JobRef:
+    """What join() returns in place of a table on the native radix path: close() drops this
+    reference only; the job (and the pairs' buffers) is freed once no result tensor refers
+    to it."""
+
+    def __init__(self, job):
+        self.job = job
+
+    def close(self):
+        self.job = None
+
+
+class NativeComm:
+    """An hj_comm — the multi-GPU plans behind the C ABI (hj_dist.cpp, RCCL inside) — for
+    the ranks of `group`: rank 0 makes the 128-byte unique id (hj_comm_unique_id), the group
+    broadcasts it (the out-of-band channel a Rust host would provide itself), every rank
+    creates the communicator on its GPU (hj_comm_create, collective). `lib` / `handle`:
+    an already-made communicator of another library build (tests: the thread transport)."""
+
+    def __init__(self, device: torch.device, group=None, lib=None, handle=None):
+        self.device = device
+        if handle is not None:
+            self._L, self._h = lib, handle
+            return
+        L = self._L = _lib.load()
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
-        self.device = device
         idb = torch.zeros(_lib.HJ_COMM_ID_BYTES, dtype=torch.uint8)
         if self.rank == 0:
-            check(L.hj_comm_unique_id(idb.data_ptr()))
+            check_l(L, L.hj_comm_unique_id(idb.data_ptr()))
         if self.world > 1:
             src = dist.get_global_rank(group, 0) if group is not None else 0
             t = idb.to(device) if dist.get_backend(group) == "nccl" else idb
             dist.broadcast(t, src=src, group=group)
             idb = t.cpu()
         h = ctypes.c_void_p()
-        check(L.hj_comm_create(self.rank, self.world, idb.data_ptr(), device.index or 0, ctypes.byref(h)))
+        check_l(L, L.hj_comm_create(self.rank, self.world, idb.data_ptr(), device.index or 0, ctypes.byref(h)))
         self._h = h
 
-    def build_sharded(self, keys: torch.Tensor, build_base: int, stream: int, valid: torch.Tensor | None = None,
-                      valid_offset: int = 0):
-        """hj_dist_build_sharded on this rank's build keys (enqueued on `stream`) -> (the
-        whole build side's table, HjDistInfo)."""
-        L = _lib.load()
-        kt = HJ_INT64 if keys.dtype == torch.int64 else HJ_INT32
+    @staticmethod
+    def _kt(t: torch.Tensor | torch.dtype) -> int:
+        dt = t if isinstance(t, torch.dtype) else t.dtype
+        return HJ_INT64 if dt == torch.int64 else HJ_INT32
+
+    def build_sharded_async(self, keys: torch.Tensor, build_base: int, stream: int, valid: torch.Tensor | None = None,
+                            valid_offset: int = 0, probe_dtype: torch.dtype | None = None) -> NativeJob:
+        """hj_dist_build_sharded_async on this rank's build keys (enqueued on `stream` by the
+        worker) -> a NativeJob whose table() is the whole build side's table, keyed in the
+        probe keys' type (default: the build keys')."""
         h = ctypes.c_void_p()
-        info = _lib.HjDistInfo()
-        check(L.hj_dist_build_sharded(self._h, kt, keys.data_ptr() if keys.numel() else None,
-                                      None if valid is None else valid.data_ptr(), valid_offset, keys.numel(),
-                                      build_base, stream or None, ctypes.byref(h), ctypes.byref(info)))
-        return HashTable.from_handle(h, keys.device.index or 0, kt, keep=[keys, valid]), info
+        pkt = self._kt(probe_dtype or keys.dtype)
+        check_l(self._L, self._L.hj_dist_build_sharded_async(self._h, self._kt(keys), keys.data_ptr() if keys.numel() else None,
+                                                  None if valid is None else valid.data_ptr(), valid_offset,
+                                                  keys.numel(), build_base, pkt, stream or None, ctypes.byref(h)))
+        return NativeJob(self._L, h, keys.device, keep=[keys, valid], key_type=pkt)
+
+    def build_sharded(self, keys: torch.Tensor, build_base: int, stream: int, valid: torch.Tensor | None = None,
+                      valid_offset: int = 0, probe_dtype: torch.dtype | None = None):
+        """The same, waiting -> (the whole build side's table, HjDistInfo)."""
+        job = self.build_sharded_async(keys, build_base, stream, valid, valid_offset, probe_dtype)
+        try:
+            return job.table()
+        finally:
+            job.close()
+
+    def join_radix(self, build_keys: torch.Tensor, build_base: int, probe_keys: torch.Tensor, probe_base: int,
+                   stream: int, build_valid: torch.Tensor | None = None, build_valid_offset: int = 0,
+                   probe_valid: torch.Tensor | None = None, probe_valid_offset: int = 0) -> NativeJob:
+        """hj_dist_join_radix: one radix-plan step -> a NativeJob whose pairs() are this
+        rank's share of the join (global ids)."""
+        h = ctypes.c_void_p()
+        check_l(self._L, self._L.hj_dist_join_radix(
+            self._h, self._kt(build_keys), build_keys.data_ptr() if build_keys.numel() else None,
+            None if build_valid is None else build_valid.data_ptr(), build_valid_offset, build_keys.numel(), build_base,
+            self._kt(probe_keys), probe_keys.data_ptr() if probe_keys.numel() else None,
+            None if probe_valid is None else probe_valid.data_ptr(), probe_valid_offset, probe_keys.numel(), probe_base,
+            stream or None, ctypes.byref(h)))
+        return NativeJob(self._L, h, probe_keys.device, keep=[build_keys, probe_keys, build_valid, probe_valid])
 
     def close(self):
         if getattr(self, "_h", None):
-            _lib.load().hj_comm_free(self._h)
+            self._L.hj_comm_free(self._h)
             self._h = None
 
     def __del__(self):
@@ -560,7 +671,7 @@ class DistributedHashJoin:
         self.group = group
         self.native = native
         self._comm: NativeComm | None = None
-        self.last_native = False  # the latest join_sharded ran the C entry point
+        self.last_native = False  # the latest join / join_sharded ran the C entry point
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
         self.partition_fn = partition_fn or gpu_radix_partition
@@ -717,6 +828,10 @@ class DistributedHashJoin:
         (recorded by the caller once the keys exist), or without it for the current stream.
         -> (table, result): result() waits and yields this rank's pairs (canonical for
         its keys); close the table afterwards."""
+        if self._use_native(build_keys) and self.compress_keys and self.runtime_filter:
+            # (the C plan always narrows keys and filters probe rows by the build range)
+            return self._join_native(build_keys, build_base, probe_keys, probe_base)
+        self.last_native = False
         ev = self.events  # optional stage events (bench): partitioned, exchanged
         cur = torch.cuda.current_stream(probe_keys.device) if probe_keys.is_cuda else None
         self._order_build_stream(build_stream, cur, inputs_ready)
@@ -751,6 +866,24 @@ class DistributedHashJoin:
         self._mark("probe_start")
         result = self._probe_chunk(table, pk, pi, [], capacity_hint)
         return table, result
+
+    def _join_native(self, build_keys, build_base, probe_keys, probe_base):
+        """The radix plan through the C entry point hj_dist_join_radix (RCCL inside the
+        library): one job on the communicator's worker; the build side's kernels and the
+        collectives on its side stream, the probe side's on the current stream. -> (job,
+        result) as join()'s: result() waits and yields this rank's pairs (device tensors
+        over the job's buffers, valid while they are referenced)."""
+        self.last_native = True
+        if getattr(self, "_comm", None) is None:
+            self._comm = NativeComm(probe_keys.device, self.group)
+        cur = torch.cuda.current_stream(probe_keys.device)
+        job = self._comm.join_radix(build_keys, build_base, probe_keys, probe_base, cur.cuda_stream)
+
+        def result(total=None):
+            return job.pairs()  # tensors over the job's buffers: they keep the job alive
+
+        result.job = job
+        return _JobRef(job), result
 
     def run(self, build_keys: torch.Tensor, build_base: int, probe_keys: torch.Tensor, probe_base: int,
             capacity_hint: int | None = None):
@@ -815,7 +948,7 @@ class DistributedHashJoin:
 
     def join_sharded(self, build_keys: torch.Tensor, build_base: int, probe_keys: torch.Tensor, probe_base: int,
                      capacity_hint: int | None = None, build_stream: torch.cuda.Stream | None = None,
-                     inputs_ready: torch.cuda.Event | None = None):
+                     inputs_ready: torch.cuda.Event | None = None, pending=None):
         """The sharded-build broadcast plan: the build side goes through the radix plan's
         range partition and exchange, each rank builds the direct-addressed table of its
         own contiguous key range (global build ids in place of rows), the ranks all-gather
@@ -828,23 +961,22 @@ class DistributedHashJoin:
         exchange, local build, gather) runs there and the probe on the current stream
         waits for the gathered table only (the side stream first waits for `inputs_ready`,
         or without it for the current stream). Falls back to run_broadcast's shape (whole
-        build per rank) when sharded_ok is false.
+        build per rank) when sharded_ok is false. On the native path the build side is a
+        job on the communicator's worker (start_sharded; `pending`: a job the caller started
+        earlier for these build keys).
         -> (table, result): result() waits and yields this rank's pairs; close the table
         afterwards."""
         cur = torch.cuda.current_stream(probe_keys.device)
-        self._order_build_stream(build_stream, cur, inputs_ready)
-        bs = build_stream or cur
-        self.last_native = self._use_native(build_keys)
-        if self.last_native:
-            # the whole build side in one C call (hj_dist_build_sharded: RCCL inside)
-            if getattr(self, "_comm", None) is None:
-                self._comm = NativeComm(build_keys.device, self.group)
-            with torch.cuda.stream(bs):
-                self._mark("build_start", bs)
-                table, _ = self._comm.build_sharded(build_keys, build_base, bs.cuda_stream)
-                self._mark("build_end", bs)
+        if pending is None:
+            pending = self.start_sharded(build_keys, build_base, build_stream, inputs_ready, probe_keys.dtype)
+        if pending is not None:  # the native build side (a job queued on the communicator's worker)
+            self.last_native = True
+            table, _ = pending.table()  # waits for the job's host steps only
+            pending.close()
             self._mark("probe_start", cur)
             return table, self._probe_own(table, probe_keys, probe_base, capacity_hint, cur)
+        self.last_native = False
+        bs = build_stream or cur
         with torch.cuda.stream(bs):
             self._mark("build_start", bs)
             plan = self.prepare(build_keys, probe_keys, build_base)
@@ -855,6 +987,23 @@ class DistributedHashJoin:
         self._mark("probe_start", cur)
         result = self._probe_own(table, probe_keys, probe_base, capacity_hint, cur)
         return table, result
+
+    def start_sharded(self, build_keys: torch.Tensor, build_base: int, build_stream: torch.cuda.Stream | None = None,
+                      inputs_ready: torch.cuda.Event | None = None, probe_dtype: torch.dtype | None = None):
+        """Queue the sharded plan's build side as a native job (hj_dist_build_sharded_async:
+        the communicator's worker runs its host steps, the caller's thread returns at once)
+        -> a NativeJob to hand to join_sharded(pending=...), or None when the native path
+        is off (join_sharded then runs the torch.distributed steps itself). A caller that
+        pipelines steps starts step k + 1's build side before step k's probe: its host
+        reads then wait on the worker while the device runs the probe."""
+        if not self._use_native(build_keys):
+            return None
+        cur = torch.cuda.current_stream(build_keys.device)
+        self._order_build_stream(build_stream, cur, inputs_ready)
+        bs = build_stream or cur
+        if getattr(self, "_comm", None) is None:
+            self._comm = NativeComm(build_keys.device, self.group)
+        return self._comm.build_sharded_async(build_keys, build_base, bs.cuda_stream, probe_dtype=probe_dtype)
 
     def _use_native(self, build_keys: torch.Tensor) -> bool:
         native = getattr(self, "native", None)

@@ -357,11 +357,12 @@ class HashTable:
         return self
 
     @classmethod
-    def from_handle(cls, handle: ctypes.c_void_p, device: int, key_type: str | int, keep=()) -> "HashTable":
+    def from_handle(cls, handle: ctypes.c_void_p, device: int, key_type: str | int, keep=(), lib=None) -> "HashTable":
         """Adopt a built table handle another entry point returned (hj_dist_build_sharded);
-        `keep`: tensors its build still reads, kept alive until close()."""
+        `keep`: tensors its build still reads, kept alive until close(); `lib`: the library
+        that made it (tests: the thread-transport build), default the product library."""
         self = cls.__new__(cls)
-        self._L = _lib.load()
+        self._L = lib or _lib.load()
         kt = key_type if isinstance(key_type, int) else (HJ_INT64 if key_type == "int64" else HJ_INT32)
         self.key_type, self.parallelism, self.device, self.devices = kt, 1, device, None
         self._h = handle

@@ -491,40 +491,102 @@ hj_status hj_comm_create(int rank, int world, const uint8_t id[HJ_COMM_ID_BYTES]
                          hj_comm** out);
 void hj_comm_free(hj_comm* c);
 
+/* The multi-GPU plans run as JOBS on the communicator's worker thread: an entry point
+ * below enqueues the job and returns; the job's host steps (its small reads of the plan,
+ * the count matrices and segment sizes, each waiting for its own stream only) run on the
+ * worker, in submission order, so the caller's thread never waits for them until it asks
+ * for the job's result. Every rank submits the same sequence of jobs (the collectives
+ * inside must match). Failures are collective: each host read carries every rank's status
+ * word and the buffers later collectives need are sized before it, so a rank that fails
+ * locally still completes the collectives and every rank's job returns an error (a peer's
+ * failure as HJ_ERR_RCCL "a peer rank failed during ..."). The one exception is an
+ * allocation failure of the radix plan's received probe rows (sized after the last status
+ * exchange): that rank aborts the communicator (unusable afterwards; its peers' jobs then
+ * fail in RCCL). Inputs must stay valid until the job's device work has finished (the
+ * table's or the pairs' consumers wait for it). Call a communicator's entry points from one
+ * thread at a time. New (the reference has no multi-process path; its partitions' builds
+ * are concurrent futures, src/operator/parallel_hash_join_executor.rs:86-122). */
+typedef struct hj_dist_job hj_dist_job;
+
 typedef struct hj_dist_info {
     int64_t build_rows;  /* global build rows (the ranks' build_base + n, max) */
     int64_t recv_rows;   /* build rows this rank received and built */
-    int sharded;         /* 1: sharded build; 0: every rank built the whole build side */
+    int sharded;         /* 1: sharded build / radix shard; 0: every rank built the whole build side */
 } hj_dist_info;
 
-/* The sharded-build plan's build side, one collective call per step on every rank.
+/* The sharded-build plan's build side, one job per step on every rank.
  * Rank r holds build rows [build_base, build_base + n) of the global build column (the
- * ranks' ranges tile [0, B) in rank order); the returned table holds the WHOLE build side
+ * ranks' ranges tile [0, B) in rank order); the job's table holds the WHOLE build side
  * and is probed by this rank's own probe rows with hj_probe_async_base(t, ..., probe_base,
  * ...): build_idx = global build row, probe_idx = probe_base + row, and the ranks' outputs
- * in rank order are the single-GPU canonical output. Steps, all enqueued on `stream` (the
- * host waits for three small reads: the plan, the count matrix, the duplicate-segment
- * sizes):
- *   1 global key range and build rows (hj_key_minmax, one grouped all-reduce);
+ * in rank order are the single-GPU canonical output. The table is keyed in
+ * `probe_key_type` (the probe keys' width; int32 and int64 build keys may be probed by
+ * either on a dense domain). Steps, all enqueued on `stream`:
+ *   1 global key range, build rows and statuses (hj_key_minmax, one grouped all-reduce);
  *   2 when the build key domain is dense (range <= 8 x rows, within the direct-addressed
  *     layout), with < 2^31 rows and a power-of-two world: every valid row to the rank that
  *     owns its contiguous key range (hj_partition_regions by range, keys as int32 offsets
- *     when the range spans < 2^32 values, global ids), point-to-point exchange
- *     (ncclSend/ncclRecv in one group);
+ *     when the range spans < 2^32 values, global ids), the count matrix all-gathered, a
+ *     point-to-point exchange (ncclSend/ncclRecv in one group);
  *   3 a direct-addressed build of the rank's own key range (global ids in place of rows),
  *     its refs all-gathered into one array over the whole domain, the duplicate segments
  *     all-gathered end to end and re-pointed (hj_dense_rebase_dups), wrapped as one
  *     probe-only table (hj_table_wrap_dense);
  *   otherwise (sparse domain, >= 2^31 rows, other worlds) every rank all-gathers the valid
- *   build rows with their global ids and builds the whole table.
- * Probes on any stream wait for the table by themselves. Free it with hj_table_free. The
- * inputs must be complete in `stream`'s order. Per-call scratch is released at a later
- * call on the same communicator once its work has finished (or at hj_comm_free). New (the
- * reference has no multi-process path). */
+ *   build rows with their global ids and builds the whole table (probe keys of the build
+ *   key type then).
+ * Probes on any stream wait for the table by themselves (hj_table_build_ns spans the whole
+ * build side). Per-job scratch is released by a later job once its work has finished (or
+ * at hj_comm_free). */
+hj_status hj_dist_build_sharded_async(hj_comm* c, hj_key_type key_type, const void* keys,
+                                      const uint8_t* validity, int64_t validity_offset, int64_t n,
+                                      int64_t build_base, hj_key_type probe_key_type, void* stream,
+                                      hj_dist_job** job);
+/* The same, waiting for the job: -> the table (free it with hj_table_free). */
 hj_status hj_dist_build_sharded(hj_comm* c, hj_key_type key_type, const void* keys,
                                 const uint8_t* validity, int64_t validity_offset, int64_t n,
-                                int64_t build_base, void* stream, hj_table** out,
-                                hj_dist_info* info);
+                                int64_t build_base, hj_key_type probe_key_type, void* stream,
+                                hj_table** out, hj_dist_info* info);
+
+/* The radix plan, one job per step on every rank (north_star's split: "the build side
+ * radix-partitions ... RCCL all-to-all"; the shard function's precedent is
+ * src/utils/partitioned_concurrent_self_hash_join_map.rs:13-16, its per-shard inserts
+ * 263-281). Rank r holds build rows [build_base, build_base + nb) and probe rows
+ * [probe_base, probe_base + np) of the global columns. Steps: the global build key range
+ * (one all-reduce, one read) -> runtime filter (probe rows outside it do not travel),
+ * contiguous key ranges per rank for a dense build domain (else mix64 hash bits), keys as
+ * int32 offsets when the range spans < 2^32 values; both sides partitioned into
+ * per-destination regions in one pass each; the build side's count matrix (one read), its
+ * point-to-point exchange and the local build (the rank's key range given, global ids in
+ * place of rows) on the communicator's side stream; the probe side's count matrix (one
+ * read), its exchange, and the probe of the received rows with their global u32 ids
+ * (probe_base + np <= 2^32) on `stream`. The job's pairs (hj_dist_job_pairs) are this
+ * rank's share of the join: probe rows in ascending global id, each probe row's build rows
+ * in the canonical (descending) order; the ranks' shares together are the whole join
+ * (a merge by probe id restores the single-GPU order). */
+hj_status hj_dist_join_radix(hj_comm* c, hj_key_type build_key_type, const void* build_keys,
+                             const uint8_t* build_validity, int64_t build_validity_offset,
+                             int64_t nb, int64_t build_base, hj_key_type probe_key_type,
+                             const void* probe_keys, const uint8_t* probe_validity,
+                             int64_t probe_validity_offset, int64_t np, int64_t probe_base,
+                             void* stream, hj_dist_job** job);
+
+/* Wait for the job's host steps (not for its device work); its status and info. */
+hj_status hj_dist_job_wait(hj_dist_job* job, hj_dist_info* info);
+/* Wait and take the job's table (the sharded build side; the radix plan's local shard,
+ * which a radix job's hj_dist_job_pairs re-probe then cannot use): the caller frees it. */
+hj_status hj_dist_job_table(hj_dist_job* job, hj_table** out, hj_dist_info* info);
+/* A radix job's pairs: waits for the probe, re-probes once with the exact size when the
+ * matches exceeded the received probe rows; device pointers owned by the job (valid until
+ * hj_dist_job_free). */
+hj_status hj_dist_job_pairs(hj_dist_job* job, const uint64_t** build_idx, const uint32_t** probe_idx,
+                            int64_t* count);
+/* Device times of a finished job's stages (waits for them), ms: a radix job's build side
+ * (plan to local build), exchange (the build side's exchange to the probe's start) and
+ * probe; a sharded job's build side in build_ms (0 for the others). NULL outputs skipped. */
+hj_status hj_dist_job_times(hj_dist_job* job, double* build_ms, double* exchange_ms, double* probe_ms);
+/* Waits for the job (host steps and device work) and releases it and what it owns. */
+void hj_dist_job_free(hj_dist_job* job);
 
 /* ---- synthetic generators of SURVEY.md §8(d) on the device (bench inputs) ----- */
 /* out[i] = (i * mul) mod range  (unique build keys when gcd(mul, range) = 1);
