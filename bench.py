@@ -19,6 +19,7 @@ on host cores over a bounded sample (rank 0, N = 1 only).
 from __future__ import annotations
 
 import argparse
+import collections
 import json
 import os
 import platform
@@ -522,6 +523,11 @@ def main():
     ap.add_argument("--native", default="auto", choices=["auto", "on", "off"],
                     help="multi-GPU sharded plan: its build side through the C entry point hj_dist_build_sharded "
                          "(RCCL inside the library; auto = on RCCL groups) or the torch.distributed steps (off)")
+    ap.add_argument("--comms", type=int, default=2,
+                    help="multi-GPU native plans: communicators used in turn (consecutive steps' host reads overlap)")
+    ap.add_argument("--build-priority", default="normal", choices=["normal", "high"],
+                    help="multi-GPU plans: the build side's stream at high HIP priority (its kernels are the critical "
+                         "path of the build side's host reads)")
     ap.add_argument("--dry-run", action="store_true",
                     help="CPU/gloo: run the multi-rank launcher and timing skeleton without a GPU (tests)")
     args = ap.parse_args()
@@ -566,7 +572,7 @@ def main():
         from datafusion_parallelism_amd.distributed import DistributedHashJoin
 
         dj = DistributedHashJoin(chunks=args.chunks, compress_keys=not args.no_compress_keys,
-                                 native={"auto": None, "on": True, "off": False}[args.native])
+                                 native={"auto": None, "on": True, "off": False}[args.native], comms=args.comms)
         plan = args.plan if args.plan != "auto" else DistributedHashJoin.choose_plan(gB, gP, world)
         if args.plan == "auto" and plan == "broadcast":
             # the broadcast side's sharded form: each rank builds 1/G of the table and the
@@ -574,7 +580,8 @@ def main():
             # sparse build domain)
             plan = "sharded"
         job = (BroadcastJob(dj, bk, pk, pbase, dev) if plan == "broadcast" else
-               ShardedJob(dj, bk, pk, bbase, pbase, dev) if plan == "sharded" else
+               ShardedJob(dj, bk, pk, bbase, pbase, dev, priority=-1 if args.build_priority == "high" else 0)
+               if plan == "sharded" else
                DistJob(dj, bk, pk, bbase, pbase, dev, same_stream=args.same_stream))
 
     def barrier():
@@ -768,6 +775,9 @@ class DistJob:
         pending, self._pending = self._pending, None
         self._collect(*pending)
 
+    def drain(self):
+        self.collect()
+
     def _collect(self, table, result, ev, native=False):
         b, _ = result()
         self.matches = int(b.numel())
@@ -802,18 +812,21 @@ class ShardedJob:
 
     pipelined = True
 
-    def __init__(self, dj, bk, pk, bbase, pbase, dev):
+    def __init__(self, dj, bk, pk, bbase, pbase, dev, priority=0):
         self.dj, self.bk, self.pk, self.bbase, self.pbase, self.dev = dj, bk, pk, bbase, pbase, dev
         self.probe_ms, self.build_ms, self.exchange_ms, self.host_ms = [], [], [], []
         self.matches = 0
         self.cap = pk.numel()
         from datafusion_parallelism_amd.distributed import concurrent_stream
 
-        self.bstream = concurrent_stream(dev)  # on another hardware queue than the probes'
+        self.bstream = concurrent_stream(dev, priority=priority)  # on another hardware queue than the probes'
         self.kernel_desc = ("sharded build: range exchange of the build side (RCCL), local build of the rank's key "
                             "range, all_gather of the table pieces, sliced probe of the local rows")
         self._pending = None
-        self._next = None  # the next step's native build side, started during this step's probe
+        # the next steps' native build sides (one per communicator), started during this
+        # step's probe: their host reads wait on the communicators' workers meanwhile
+        self._next = collections.deque()
+        self.depth = max(1, getattr(dj, "_ncomms", 1))
         self.ready = torch.cuda.Event()  # the inputs exist: the build stream waits for this only
         self.ready.record()
 
@@ -826,13 +839,14 @@ class ShardedJob:
         self.dj.events = ev
         cur = torch.cuda.current_stream(self.dev)
         h0 = time.perf_counter()
-        pending, self._next = self._next or self._start(), None
+        pending = self._next.popleft() if self._next else self._start()
         table, result = self.dj.join_sharded(self.bk, self.bbase, self.pk, self.pbase, self.cap,
                                              build_stream=self.bstream, inputs_ready=self.ready, pending=pending)
         if self.dj.last_native:
-            # step k + 1's build side, queued now: the worker's host reads wait while the device
-            # runs this step's probe (the build keys are resident and unchanged between steps)
-            self._next = self._start()
+            # the next steps' build sides, queued now: the workers' host reads wait while the
+            # device runs this step's probe (the build keys are resident and unchanged)
+            while len(self._next) < self.depth:
+                self._next.append(self._start())
         self.host_ms.append((time.perf_counter() - h0) * 1e3)
         self.dj.events = None
         ev["end"].record(cur)
@@ -862,12 +876,11 @@ class ShardedJob:
         table.close()
 
     def drain(self):
-        """The prefetched build side (the step after the last): finish its job."""
-        if self._next is not None:
-            nxt, self._next = self._next, None
+        """The prefetched build sides (the steps after the last): finish their jobs."""
+        while self._next:
+            nxt = self._next.popleft()
             t, _ = nxt.table()
             nxt.close()
-            torch.cuda.current_stream(self.dev).synchronize()
             t.close()
 
     def finish(self):

@@ -69,6 +69,7 @@ struct hj_dist_job {
     int64_t* d_total = nullptr;  // device
     int64_t* h_total = nullptr;  // pinned
     hipEvent_t ev_total = nullptr;
+    hipEvent_t ev_in = nullptr;  // the caller's stream at submission (the inputs are complete there)
     int64_t total = -1;
     // radix: timing events (build side start, exchange start, build side end, probe start,
     // probe end); null for a sharded build side (its table's build time covers it)
@@ -89,7 +90,12 @@ struct hj_comm {
     std::atomic<bool> aborted{false};
     int64_t* host = nullptr;  // pinned mailbox for the plan's small reads
     hipEvent_t ev = nullptr;  // marks a read's copy
-    hipStream_t side = nullptr;  // the radix plan's build side and its collectives (the probe side stays on the caller's)
+    // the jobs' device work runs on the communicator's own streams (after the caller's
+    // stream at submission): two communicators' jobs never share a stream, so their
+    // collectives cannot be ordered differently on different ranks
+    hipStream_t side = nullptr;   // the sharded plan; the radix plan's build-side partition and collectives
+    hipStream_t build = nullptr;  // the radix plan's local build
+    hipStream_t probe = nullptr;  // the radix plan's probe side
     std::vector<hipEvent_t> evs;  // cross-stream ordering events (reused)
     // scratch of earlier jobs: released once their end event has fired
     struct Deferred {

@@ -26,8 +26,11 @@
 #include <stdint.h>
 #include <string.h>
 
+#include <stdlib.h>
+
 #include <algorithm>
 #include <string>
+#include <thread>
 #include <utility>
 #include <vector>
 
@@ -172,13 +175,24 @@ void release_finished(hj_comm* c, bool wait) {
     c->deferred = std::move(keep);
 }
 
+// The worker waits for its reads by polling (it is the plan's critical path and has a core
+// to itself; a blocking wait adds the runtime's wake-up latency to every one of the plan's
+// host reads).
+hj_status spin_wait(hipEvent_t e) {
+    for (uint32_t i = 0;; ++i) {
+        const hipError_t q = hipEventQuery(e);
+        if (q == hipSuccess) return HJ_OK;
+        if (q != hipErrorNotReady) return set_error(HJ_ERR_HIP, std::string("hipEventQuery: ") + hipGetErrorString(q));
+        if ((i & 63) == 63) std::this_thread::yield();
+    }
+}
+
 // a small device array to the host mailbox, waiting for this stream's work up to here only
 hj_status read_host(hj_comm* c, const void* d, int64_t words, hipStream_t s) {
     if (words > kHostWords) return set_error(HJ_ERR_INVALID, "hj_dist: host read too large");
     HIP_OK(hipMemcpyAsync(c->host, d, (size_t)words * 8, hipMemcpyDeviceToHost, s));
     HIP_OK(hipEventRecord(c->ev, s));
-    HIP_OK(hipEventSynchronize(c->ev));
-    return HJ_OK;
+    return spin_wait(c->ev);
 }
 
 // host words -> device (a pinned staging area of their own: the copy is asynchronous)
@@ -344,7 +358,10 @@ struct ShardedArgs {
 hj_status run_sharded(hj_comm* c, const ShardedArgs& a, hj_dist_job* j, int64_t jobno) {
     const int W = c->world, me = c->rank;
     const int kb = a.kt == HJ_INT64 ? 8 : 4;
-    hipStream_t s = a.s;
+    // every step on the communicator's own stream, after the caller's inputs (ev_in: the
+    // caller's stream at submission); consumers wait for the table's completion event
+    hipStream_t s = c->side;
+    HIP_OK(hipStreamWaitEvent(s, j->ev_in, 0));
     Scratch scr(c, {s});
     LocalFail lf;
     hipEvent_t t0 = nullptr;  // the build side's start (the table's build time runs from it)
@@ -361,6 +378,34 @@ hj_status run_sharded(hj_comm* c, const ShardedArgs& a, hj_dist_job* j, int64_t 
         if (!p) lf.note_oom(what);
         return p;
     };
+
+    // One rank whose rows start at global row 0: the exchange is the identity and the
+    // gathered table is the rank's own build, so the build side is the single-GPU build
+    // of the input in place (its key range stays on the device: no partition, no copy, no
+    // host read). DFP_HJ_DIST_W1_IDENTITY=0 runs the whole plan at one rank instead (to
+    // price its machinery).
+    static const bool w1_identity = [] {
+        const char* e = getenv("DFP_HJ_DIST_W1_IDENTITY");
+        return !(e && e[0] == '0');
+    }();
+    if (W == 1 && a.base == 0 && a.pkt == a.kt && w1_identity && !injected(c, jobno, 0)) {
+        hj_table* t = nullptr;
+        ST_OK(hj_build_begin(c->device, 1, a.kt, a.n, &t));
+        hj_status st = hj_build_append(t, 0, a.keys, a.valid, a.voff, nullptr, a.n,
+                                       HJ_INPUT_DEVICE | HJ_BORROW | HJ_BORROW_KEEP, s);
+        if (st == HJ_OK) st = hj_build_finish(t, 0);
+        if (st != HJ_OK) {
+            hj_table_free(t);
+            return st;
+        }
+        j->info.build_rows = a.n;
+        j->info.recv_rows = a.n;
+        j->info.sharded = 1;
+        dfp::host::table_set_start_event(t, t0);
+        t0 = nullptr;
+        j->table = t;
+        return scr.defer();
+    }
 
     // 1. the global key range, build rows and status: [min | max, rows, failed]
     int64_t* mm = (int64_t*)scr.get(8 * 8);
@@ -603,21 +648,23 @@ struct RadixArgs {
 // domain (range <= 8 x rows) is split by contiguous key ranges (else by mix64 hash bits),
 // keys travel as int32 offsets when the range spans < 2^32 values, build ids as u64 and
 // held in place of rows (< 2^31 rows), probe ids as u32 = probe_base + row. Streams: the
-// caller's `s` runs the probe side's kernels (its partition, the probe); the
-// communicator's side stream the build side's kernels and every collective (one stream
-// for the collectives: each rank's GPU runs them in issue order).
+// communicator's probe stream runs the probe side's kernels (its partition, the probe),
+// its side stream the build side's partition and every collective (one stream for the
+// collectives: each rank's GPU runs them in issue order), its build stream the local build.
 hj_status run_radix(hj_comm* c, const RadixArgs& a, hj_dist_job* j, int64_t jobno) {
     const int W = c->world, me = c->rank;
     const int kb = a.kt == HJ_INT64 ? 8 : 4;
-    hipStream_t s = a.s, sd = c->side;
-    Scratch scr(c, {s, sd});
+    hipStream_t s = c->probe, sd = c->side, sb = c->build;
+    Scratch scr(c, {s, sd, sb});
     LocalFail lf;
     auto get = [&](size_t bytes, const char* what) -> void* {
         void* p = scr.get(bytes);
         if (!p) lf.note_oom(what);
         return p;
     };
-    ST_OK(join_streams(c, s, sd, 0));  // the inputs are complete in s's order
+    // the inputs are complete at the caller's stream's point of submission (ev_in)
+    HIP_OK(hipStreamWaitEvent(sd, j->ev_in, 0));
+    HIP_OK(hipStreamWaitEvent(s, j->ev_in, 0));
     HIP_OK(hipEventRecord(j->ev_t[0], sd));
 
     // 1. the plan: [min | max, rows, failed] of the build side
@@ -725,19 +772,21 @@ hj_status run_radix(hj_comm* c, const RadixArgs& a, hj_dist_job* j, int64_t jobn
         ST_OK(c->tr->group_end(sd));
     }
     j->info.recv_rows = Rb;
-    // 3. the local build (the rank's key range known: no reduction), on the side stream
+    // 3. the local build (the rank's key range known: no reduction), on its own stream: the
+    // collective stream goes on to the probe side's counts without waiting for it
     hj_table* t = nullptr;
     if (injected(c, jobno, 2)) lf.note(set_error(HJ_ERR_INVALID, "injected failure (test hook) at the local build"));
+    ST_OK(join_streams(c, sd, sb, 4));
     if (!lf.failed) {
         hj_status st = hj_build_begin(c->device, 1, lkt, Rb, &t);
         const uint32_t fl = HJ_INPUT_DEVICE | HJ_BORROW | HJ_BORROW_KEEP | (u31 ? HJ_IDS_U31 : 0);
-        if (st == HJ_OK) st = hj_build_append(t, 0, bk, nullptr, 0, bi, Rb, fl, sd);
+        if (st == HJ_OK) st = hj_build_append(t, 0, bk, nullptr, 0, bi, Rb, fl, sb);
         if (st == HJ_OK && Rb > 0 && !lempty) st = hj_build_key_range(t, llo - koff, lhi - koff);
         if (st == HJ_OK) st = hj_build_finish(t, 0);
         lf.note(st);
     }
     j->table = t;  // freed with the job (or taken by the caller)
-    HIP_OK(hipEventRecord(j->ev_t[2], sd));  // the build side's end (as enqueued)
+    HIP_OK(hipEventRecord(j->ev_t[2], sb));  // the build side's end
     // 4. the probe side's counts (+ every rank's status after its local build)
     {
         int64_t f = lf.failed ? 1 : 0;
@@ -778,7 +827,8 @@ hj_status run_radix(hj_comm* c, const RadixArgs& a, hj_dist_job* j, int64_t jobn
     ST_OK(join_streams(c, sd, s, 3));
     HIP_OK(hipEventRecord(j->ev_t[3], s));  // the probe's start
     // 5. the probe of the received rows with their global ids (on s; it waits for the
-    // table's build by itself)
+    // table's build by itself at its first table read: the sliced probe's partition of the
+    // received rows overlaps the local build)
     j->rn = Rp;
     j->out_cap = std::max<int64_t>(Rp, 1);
     void* ws = scr.get((size_t)hj_probe_workspace_bytes(Rp));
@@ -856,11 +906,14 @@ hj_status wait_job(hj_dist_job* j) {
     return HJ_OK;
 }
 
-hj_status new_job(hj_comm* c, bool join, hj_dist_job** out) {
+hj_status new_job(hj_comm* c, bool join, void* stream, hj_dist_job** out) {
     hj_dist_job* j = new hj_dist_job();
     j->comm = c;
     j->device = c->device;
-    bool ok = true;
+    // the caller's stream at submission: the job's device work follows it
+    bool ok = hipSetDevice(c->device) == hipSuccess &&
+              hipEventCreateWithFlags(&j->ev_in, hipEventDisableTiming) == hipSuccess &&
+              hipEventRecord(j->ev_in, (hipStream_t)stream) == hipSuccess;
     if (join) {  // the pairs' count word and the stage events
         ok = hipHostMalloc((void**)&j->h_total, 8, hipHostMallocDefault) == hipSuccess &&
              hipEventCreateWithFlags(&j->ev_total, hipEventDisableTiming) == hipSuccess;
@@ -886,10 +939,16 @@ namespace dfp {
 namespace comm {
 hj_status start(hj_comm* c) {
     HIP_OK(hipSetDevice(c->device));
+    // DFP_HJ_COMM_PRIORITY=-1: the plan's own streams at high priority (their kernels are
+    // the host chain's critical path; measured)
+    const char* pe = getenv("DFP_HJ_COMM_PRIORITY");
+    const int prio = pe ? atoi(pe) : 0;
     if (hipHostMalloc((void**)&c->host, 2 * kHostWords * 8, hipHostMallocDefault) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev, hipEventDisableTiming) != hipSuccess ||
-        hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess)
-        return set_error(HJ_ERR_HIP, "hj_comm: pinned mailbox / event / stream");
+        hipStreamCreateWithPriority(&c->side, hipStreamNonBlocking, prio) != hipSuccess ||
+        hipStreamCreateWithPriority(&c->build, hipStreamNonBlocking, prio) != hipSuccess ||
+        hipStreamCreateWithPriority(&c->probe, hipStreamNonBlocking, prio) != hipSuccess)
+        return set_error(HJ_ERR_HIP, "hj_comm: pinned mailbox / event / streams");
     c->evs.assign(kEvents, nullptr);
     for (auto& e : c->evs)
         if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess)
@@ -956,11 +1015,15 @@ void hj_comm_free(hj_comm* c) {
     if (c->worker.joinable()) c->worker.join();
     (void)hipSetDevice(c->device);
     if (c->side) (void)hipStreamSynchronize(c->side);
+    if (c->build) (void)hipStreamSynchronize(c->build);
+    if (c->probe) (void)hipStreamSynchronize(c->probe);
     release_finished(c, true);
     c->tr.reset();
     for (auto e : c->evs)
         if (e) (void)hipEventDestroy(e);
     if (c->side) (void)hipStreamDestroy(c->side);
+    if (c->build) (void)hipStreamDestroy(c->build);
+    if (c->probe) (void)hipStreamDestroy(c->probe);
     if (c->ev) (void)hipEventDestroy(c->ev);
     if (c->host) (void)hipHostFree(c->host);
     delete c;
@@ -978,7 +1041,7 @@ hj_status hj_dist_build_sharded_async(hj_comm* c, hj_key_type key_type, const vo
     if (n < 0 || build_base < 0 || voff < 0) return set_error(HJ_ERR_INVALID, "negative n/base/offset");
     if (n > 0 && keys == nullptr) return set_error(HJ_ERR_INVALID, "null keys");
     hj_dist_job* j = nullptr;
-    ST_OK(new_job(c, false, &j));
+    ST_OK(new_job(c, false, stream, &j));
     const ShardedArgs a{key_type, probe_key_type, keys, validity, voff, n, build_base, (hipStream_t)stream};
     const int64_t no = c->jobs++;
     j->fn = [c, a, no](hj_dist_job* jj) { return run_sharded(c, a, jj, no); };
@@ -1017,7 +1080,7 @@ hj_status hj_dist_join_radix(hj_comm* c, hj_key_type build_key_type, const void*
     if ((nb > 0 && build_keys == nullptr) || (np > 0 && probe_keys == nullptr))
         return set_error(HJ_ERR_INVALID, "null keys");
     hj_dist_job* j = nullptr;
-    ST_OK(new_job(c, true, &j));
+    ST_OK(new_job(c, true, stream, &j));
     const RadixArgs a{build_key_type, probe_key_type, build_keys, probe_keys, build_validity, probe_validity,
                       build_voff, nb, build_base, probe_voff, np, probe_base, (hipStream_t)stream};
     const int64_t no = c->jobs++;
@@ -1123,6 +1186,7 @@ void hj_dist_job_free(hj_dist_job* j) {
     for (auto e : j->ev_t)
         if (e) (void)hipEventDestroy(e);
     if (j->ev_total) (void)hipEventDestroy(j->ev_total);
+    if (j->ev_in) (void)hipEventDestroy(j->ev_in);
     if (j->h_total) (void)hipHostFree(j->h_total);
     delete j;
 }

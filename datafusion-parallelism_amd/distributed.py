@@ -242,7 +242,8 @@ class ExchangeStats:
 A2A_MAX_BYTES = 256 << 20
 
 
-def concurrent_stream(device, avoid: torch.cuda.Stream | None = None, tries: int = 8) -> torch.cuda.Stream:
+def concurrent_stream(device, avoid: torch.cuda.Stream | None = None, tries: int = 8,
+                      priority: int = 0) -> torch.cuda.Stream:
     """A torch pool stream whose work runs concurrently with `avoid` (default: the current
     stream). HIP multiplexes streams onto a few hardware queues (GPU_MAX_HW_QUEUES, 4 here)
     in creation order, and two streams on one queue run one after the other: a side stream
@@ -250,11 +251,11 @@ def concurrent_stream(device, avoid: torch.cuda.Stream | None = None, tries: int
     (seen in kernel traces: the plan's key-range read queued behind the previous probe).
     Tested, not assumed: a spin kernel on `avoid`, a tiny one on the candidate, and the
     candidate must finish while the spin still runs. -> the first candidate that does (else
-    the last one tried)."""
+    the last one tried). priority: the HIP stream priority (-1 high, 0 normal)."""
     avoid = avoid or torch.cuda.current_stream(device)
     cand = None
     for _ in range(tries):
-        cand = torch.cuda.Stream(device)
+        cand = torch.cuda.Stream(device, priority=priority)
         if cand.cuda_stream == avoid.cuda_stream:
             continue
         spin_done = torch.cuda.Event()
@@ -663,14 +664,19 @@ class DistributedHashJoin:
 
     def __init__(self, group=None, partition_fn: Callable | None = None, local_join_fn: Callable | None = None,
                  chunks: int = 1, local_build_fn: Callable | None = None, compress_keys: bool = True,
-                 runtime_filter: bool = True, native: bool | None = None):
-        """native: run the sharded-build plan's build side through hj_dist_build_sharded
-        (RCCL inside the library: one C call per step) instead of the torch.distributed
-        steps below; None = when the group's backend is nccl (RCCL) and the world is a
-        power of two."""
+                 runtime_filter: bool = True, native: bool | None = None, comms: int = 2):
+        """native: run the plans through the C entry points (hj_dist_build_sharded_async,
+        hj_dist_join_radix: RCCL inside the library, one job per step on a communicator's
+        worker thread) instead of the torch.distributed steps below; None = when the group's
+        backend is nccl (RCCL) and the world is a power of two. comms: native communicators
+        used in turn, one step each, so that consecutive steps' host reads overlap (each has
+        its own worker and streams)."""
         self.group = group
         self.native = native
         self._comm: NativeComm | None = None
+        self._comms: list[NativeComm] = []
+        self._ncomms = max(1, int(comms))
+        self._turn = 0
         self.last_native = False  # the latest join / join_sharded ran the C entry point
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
@@ -874,10 +880,9 @@ class DistributedHashJoin:
         result) as join()'s: result() waits and yields this rank's pairs (device tensors
         over the job's buffers, valid while they are referenced)."""
         self.last_native = True
-        if getattr(self, "_comm", None) is None:
-            self._comm = NativeComm(probe_keys.device, self.group)
         cur = torch.cuda.current_stream(probe_keys.device)
-        job = self._comm.join_radix(build_keys, build_base, probe_keys, probe_base, cur.cuda_stream)
+        job = self._next_comm(probe_keys.device).join_radix(build_keys, build_base, probe_keys, probe_base,
+                                                            cur.cuda_stream)
 
         def result(total=None):
             return job.pairs()  # tensors over the job's buffers: they keep the job alive
@@ -1001,9 +1006,20 @@ class DistributedHashJoin:
         cur = torch.cuda.current_stream(build_keys.device)
         self._order_build_stream(build_stream, cur, inputs_ready)
         bs = build_stream or cur
-        if getattr(self, "_comm", None) is None:
-            self._comm = NativeComm(build_keys.device, self.group)
-        return self._comm.build_sharded_async(build_keys, build_base, bs.cuda_stream, probe_dtype=probe_dtype)
+        return self._next_comm(build_keys.device).build_sharded_async(build_keys, build_base, bs.cuda_stream,
+                                                                      probe_dtype=probe_dtype)
+
+    def _next_comm(self, device) -> "NativeComm":
+        """The native communicator of the next step (created on first use, collectively:
+        every rank makes its communicators in the same order)."""
+        if not hasattr(self, "_comms"):  # test doubles that skip __init__
+            self._comms, self._ncomms, self._turn = [], 1, 0
+        if len(self._comms) < self._ncomms:
+            self._comms.append(NativeComm(device, self.group))
+            self._comm = self._comms[0]
+        c = self._comms[self._turn % len(self._comms)]
+        self._turn += 1
+        return c
 
     def _use_native(self, build_keys: torch.Tensor) -> bool:
         native = getattr(self, "native", None)
@@ -1016,10 +1032,11 @@ class DistributedHashJoin:
         return dist.get_backend(self.group) == "nccl" and (self.world & (self.world - 1)) == 0
 
     def close(self) -> None:
-        """Release the native communicator (if one was made)."""
-        if self._comm is not None:
-            self._comm.close()
-            self._comm = None
+        """Release the native communicators (if any were made)."""
+        for c in getattr(self, "_comms", []):
+            c.close()
+        self._comms = []
+        self._comm = None
 
     def _gather_pieces(self, build_keys, build_base, plan: ExchangePlan, probe_dtype, bs):
         dev = build_keys.device

@@ -504,7 +504,12 @@ void hj_comm_free(hj_comm* c);
  * exchange): that rank aborts the communicator (unusable afterwards; its peers' jobs then
  * fail in RCCL). Inputs must stay valid until the job's device work has finished (the
  * table's or the pairs' consumers wait for it). Call a communicator's entry points from one
- * thread at a time. New (the reference has no multi-process path; its partitions' builds
+ * thread at a time. A job's device work runs on the communicator's own streams, after the
+ * work enqueued on the caller's `stream` before the call (its inputs must be complete
+ * there); consumers wait for its results by themselves (a table's completion event, the
+ * pairs' read). Two communicators of the same ranks may run jobs concurrently (a caller
+ * that alternates steps between them overlaps one step's host reads with the next's): they
+ * share no stream. New (the reference has no multi-process path; its partitions' builds
  * are concurrent futures, src/operator/parallel_hash_join_executor.rs:86-122). */
 typedef struct hj_dist_job hj_dist_job;
 
@@ -521,7 +526,7 @@ typedef struct hj_dist_info {
  * ...): build_idx = global build row, probe_idx = probe_base + row, and the ranks' outputs
  * in rank order are the single-GPU canonical output. The table is keyed in
  * `probe_key_type` (the probe keys' width; int32 and int64 build keys may be probed by
- * either on a dense domain). Steps, all enqueued on `stream`:
+ * either on a dense domain). Steps:
  *   1 global key range, build rows and statuses (hj_key_minmax, one grouped all-reduce);
  *   2 when the build key domain is dense (range <= 8 x rows, within the direct-addressed
  *     layout), with < 2^31 rows and a power-of-two world: every valid row to the rank that
@@ -558,9 +563,9 @@ hj_status hj_dist_build_sharded(hj_comm* c, hj_key_type key_type, const void* ke
  * int32 offsets when the range spans < 2^32 values; both sides partitioned into
  * per-destination regions in one pass each; the build side's count matrix (one read), its
  * point-to-point exchange and the local build (the rank's key range given, global ids in
- * place of rows) on the communicator's side stream; the probe side's count matrix (one
- * read), its exchange, and the probe of the received rows with their global u32 ids
- * (probe_base + np <= 2^32) on `stream`. The job's pairs (hj_dist_job_pairs) are this
+ * place of rows) on the communicator's streams; the probe side's count matrix (one read),
+ * its exchange, and the probe of the received rows with their global u32 ids
+ * (probe_base + np <= 2^32). The job's pairs (hj_dist_job_pairs) are this
  * rank's share of the join: probe rows in ascending global id, each probe row's build rows
  * in the canonical (descending) order; the ranks' shares together are the whole join
  * (a merge by probe id restores the single-GPU order). */
