@@ -2550,6 +2550,14 @@ sl_lookup_kernel(TableView tv, uint32_t wlog, uint32_t nslices, int64_t ntiles, 
 #endif
 }
 
+// Measured (r05) and not kept: the dense lookup with L lanes per fragment (a lane group
+// owns a fragment whole: its entries walked L at a time, the correction in registers; no
+// flattening, masks or owner search) — C2 196 / 210 / 265 / 541 us at L = 4 / 8 / 16 / 64
+// against 127 us, C3 362-8185 against 268 (profiles/r05_lookup_lanes.txt): L-lane-wide
+// accesses touch 64 / L lines per instruction where the flattened rows touch one or two.
+// The lookup's time against fragment length (profiles/r05_lookup_fraglen.txt): about 45-50
+// us fixed plus 1.6-1.7 ns per entry at C2's geometry.
+
 // S1 of the hashed sliced probe: per 16384-row tile, the valid rows sorted by slice
 // (home bucket >> kHsSliceLog) in LDS; the tile's stored keys (u64) and rows in the
 // tile (u16) leave in slice order, with the tile's slice bounds (u16). Persistent, one

@@ -28,7 +28,9 @@ else:
     bk = torch.empty(B, dtype=torch.int64, device=dev)
     pk = torch.empty(P, dtype=torch.int64, device=dev)
     assert L.hj_gen_perm_keys(bk.data_ptr(), B, 7368787, B, None) == 0
-    assert L.hj_gen_uniform_keys(pk.data_ptr(), P, 0xC0FFEE, 2 * B, None) == 0
+    # --prange=F: probe keys uniform over F x B values (default 2: half the probe rows in range)
+    PR = float(next((a.split("=", 1)[1] for a in sys.argv if a.startswith("--prange=")), "2"))
+    assert L.hj_gen_uniform_keys(pk.data_ptr(), P, 0xC0FFEE, int(PR * B), None) == 0
     if MIX:
         bk.mul_(0x9E3779B97F4A7C15 - (1 << 64))
         pk.mul_(0x9E3779B97F4A7C15 - (1 << 64))
