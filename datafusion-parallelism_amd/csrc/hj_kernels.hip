@@ -2190,6 +2190,10 @@ __device__ __forceinline__ uint32_t lds_bucket_ref(const uint4* __restrict__ img
 // by LDS bank conflicts, and the extra dependent read lengthens every chain.
 
 constexpr uint32_t kBigCorr = 1u << 16;  // counts - 1 from here on correct the tile count directly
+#ifndef DFP_LK_GROUP
+#define DFP_LK_GROUP 4
+#endif
+constexpr int kLkGroup = DFP_LK_GROUP;  // dense lookup: rows per branch-free group (divides the window's rows)
 // a tile's pair count (tcnt) is < 2^45 (16384 rows x < 2^31 build rows); the dense lookup
 // adds kOddFlag once per fragment with an entry of a missing or duplicated key (at most
 // 4095 slices x 3 passes of a direct-addressed range: the flag bits never wrap to 0)
@@ -2387,10 +2391,10 @@ sl_lookup_kernel(TableView tv, uint32_t wlog, uint32_t nslices, int64_t ntiles, 
         for (uint32_t w0 = 0; w0 < R; w0 += W) {
             DFP_PH_CNT(6);
             if (lane < W / 64) smask[lane] = 0;
-            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront", "local");  // LDS only: no wait for the ref stores
             __builtin_amdgcn_wave_barrier();
             if (len != 0 && excl >= w0 && excl < w0 + W) atomicOr(&smask[(excl - w0) >> 6], 1ull << ((excl - w0) & 63));
-            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront", "local");  // LDS only: no wait for the ref stores
             __builtin_amdgcn_wave_barrier();
             // Measured (r04) and not kept, C2 serialized (tools/lookup_ablate.py, lookup with
             // its stores / entry loads / table reads removed: 138 / 122 / 129 / 113 us with
@@ -2409,8 +2413,48 @@ sl_lookup_kernel(TableView tv, uint32_t wlog, uint32_t nslices, int64_t ntiles, 
             // v_readlane per row) and the owners' bases in batches of 8 rows took the C2
             // lookup 133 -> 150 us (128 VGPRs, spills); the per-row LDS round trips below
             // overlap across the 16 waves of the CU.
+            if constexpr (!HASHED) {
+                // dense: rows in branch-free groups of kLkGroup (rows past the run read a zero
+                // mask and take the out-of-range offset), so that a group's mask reads, then its
+                // owners' base reads, then its entry loads issue together: two LDS round trips
+                // per group instead of per row (r05)
+#pragma unroll
+                for (int g0 = 0; g0 < NU; g0 += kLkGroup) {
+#pragma unroll
+                    for (int u = g0; u < g0 + kLkGroup; ++u) off[u] = kOob;
+                    if (w0 + g0 * 64 >= R) continue;  // uniform: past the run
+                    unsigned long long mu[kLkGroup];
+#pragma unroll
+                    for (int j = 0; j < kLkGroup; ++j) {
+                        const unsigned long long m = smask[g0 + j];  // the same word for every lane
+                        const uint32_t mlo = __builtin_amdgcn_readfirstlane((uint32_t)m);
+                        const uint32_t mhi = __builtin_amdgcn_readfirstlane((uint32_t)(m >> 32));
+                        mu[j] = ((unsigned long long)mhi << 32) | mlo;
+                    }
+                    uint32_t kk[kLkGroup], bs[kLkGroup];
+#pragma unroll
+                    for (int j = 0; j < kLkGroup; ++j) {
+                        const unsigned long long m1 = mu[j] >> 1;
+                        const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m1 >> 32),
+                                                                          __builtin_amdgcn_mbcnt_lo((uint32_t)m1, 0u));
+                        kk[j] = kb + (uint32_t)(mu[j] & 1) + below - 1;
+                        kb += (uint32_t)__builtin_popcountll(mu[j]);
+                    }
+#pragma unroll
+                    for (int j = 0; j < kLkGroup; ++j) bs[j] = sbs[kk[j] & 63];
+#pragma unroll
+                    for (int j = 0; j < kLkGroup; ++j) {
+                        const uint32_t r = w0 + (g0 + j) * 64 + lane;
+                        const uint32_t o = r < R ? bs[j] + r : kOob;
+                        // ablation 1024: no entry loads (wrong pairs)
+                        ev[g0 + j] = DFP_ABL(1024) ? (r & 0x7FFF) : __builtin_amdgcn_raw_buffer_load_b16(rko, (int)(o * 2), 0, 0);
+                        off[g0 + j] = o | ((kk[j] & 63) << 26);
+                    }
+                }
+            }
 #pragma unroll
             for (int u = 0; u < NU; ++u) {
+                if constexpr (!HASHED) break;  // (above)
                 off[u] = kOob;
                 if (w0 + u * 64 >= R) continue;  // uniform: past the run
                 const uint32_t r = w0 + u * 64 + lane;
@@ -2482,28 +2526,53 @@ sl_lookup_kernel(TableView tv, uint32_t wlog, uint32_t nslices, int64_t ntiles, 
                 }
             } else {
 #pragma unroll
-                for (int u = 0; u < NU; ++u) {
-                    if (w0 + u * 64 >= R) continue;  // uniform: past the run
+                for (int g0 = 0; g0 < NU; g0 += kLkGroup) {
+                  if (w0 + g0 * 64 >= R) continue;  // uniform: past the run
+                  uint32_t vv[kLkGroup];
+                  bool any = false;
+#pragma unroll
+                  for (int j = 0; j < kLkGroup; ++j) {
+                      const int u = g0 + j;
+                      const uint32_t o = off[u] & kOobMask;
+                      // ablation 2048: no table read (wrong pairs)
+                      vv[j] = DFP_ABL(2048) ? ev[u] : s_tab[ev[u] & ((1u << wlog) - 1)];
+                      if (!DFP_ABL(512)) __builtin_amdgcn_raw_buffer_store_b32(vv[j], rres, (int)(o * 4), 0, 0);  // 512: no stores
+                      any |= o != kOob && vv[j] >= kDupFlag;
+                  }
+                  // a missing or duplicated key (kMiss and kDupFlag refs have bit 31 set): its
+                  // count, the correction and the odd flag in a wave-uniform branch, so that a
+                  // group of single hits (every row of a unique-key build) pays compares and one
+                  // ballot (r05: the count chain ran on every row)
+                  if (__ballot(any) == 0) {
+                      if (corr_run != 0) {  // uniform
+#pragma unroll
+                          for (int j = 0; j < kLkGroup; ++j)
+                              if ((smask[g0 + j] >> lane) & 1ull) scst[off[g0 + j] >> 26] = corr_run;
+                      }
+                      continue;
+                  }
+#pragma unroll
+                  for (int j = 0; j < kLkGroup; ++j) {
+                    const int u = g0 + j;
                     const uint32_t o = off[u] & kOobMask;
-                    // ablation 2048: no table read (wrong pairs)
-                    const uint32_t v = DFP_ABL(2048) ? ev[u] : s_tab[ev[u] & ((1u << wlog) - 1)];
-                    uint32_t c = 1;  // ref and its row count (kCountUnknown: in its segment header)
-                    if (o != kOob && (v == kMiss || (v & kDupFlag))) {
-                        const uint32_t c4 = tv.off_mask == kPackedMask ? ((v >> 27) & 15u) : 0u;
-                        c = v == kMiss ? 0u : c4 ? c4 : kCountUnknown;
-                    }
-                    // counts not inline: read from the segment header in a wave-uniform branch
-                    // that waits there. Merged into the common path, that load's wait was an
-                    // s_waitcnt vmcnt(0) on every row — for the previous rows' ref stores (loads
-                    // and stores share vmcnt): one store round trip per 64 entries.
-                    if (__ballot(c == kCountUnknown) != 0) {
-                        if (c == kCountUnknown) c = tv.dup_rows[v & tv.off_mask];
-                        asm volatile("" : "+v"(c));
-                    }
-                    if (!DFP_ABL(512)) __builtin_amdgcn_raw_buffer_store_b32(v, rres, (int)(o * 4), 0, 0);  // 512: no stores
-                    // a fragment start (start mask bit) records the running sum before it
-                    const bool odd = o != kOob && c != 1;
-                    if (__ballot(odd) != 0) {
+                    const uint32_t v = vv[j];
+                    const bool special = o != kOob && v >= kDupFlag;
+                    if (__ballot(special) != 0) {
+                        uint32_t c = 1;  // row count (kCountUnknown: in its segment header)
+                        if (special) {
+                            const uint32_t c4 = tv.off_mask == kPackedMask ? ((v >> 27) & 15u) : 0u;
+                            c = v == kMiss ? 0u : c4 ? c4 : kCountUnknown;
+                        }
+                        // counts not inline: read from the segment header in a wave-uniform branch
+                        // that waits there. Merged into the common path, that load's wait was an
+                        // s_waitcnt vmcnt(0) on every row — for the previous rows' ref stores (loads
+                        // and stores share vmcnt): one store round trip per 64 entries.
+                        if (__ballot(c == kCountUnknown) != 0) {
+                            if (c == kCountUnknown) c = tv.dup_rows[v & tv.off_mask];
+                            asm volatile("" : "+v"(c));
+                        }
+                        // a fragment start (start mask bit) records the running sum before it
+                        const bool odd = special && c != 1;
                         if (odd) sodd[off[u] >> 26] = 1;  // the emission's count-free path is off for its tile
                         uint32_t d = odd ? c - 1u : 0u;
                         if (d != 0xFFFFFFFFu && d >= kBigCorr) {  // a huge duplicate: straight to its tile
@@ -2516,12 +2585,13 @@ sl_lookup_kernel(TableView tv, uint32_t wlog, uint32_t nslices, int64_t ntiles, 
                     } else if (corr_run != 0) {  // uniform
                         if ((smask[u] >> lane) & 1ull) scst[off[u] >> 26] = corr_run;
                     }
+                  }
                 }
             }
             DFP_PH(3);
         }
         // one atomic per tile that has a correction (64 contiguous counters)
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront", "local");  // LDS only: no wait for the ref stores
         __builtin_amdgcn_wave_barrier();
         if (len != 0) {
             int cr;
@@ -2537,7 +2607,7 @@ sl_lookup_kernel(TableView tv, uint32_t wlog, uint32_t nslices, int64_t ntiles, 
                 (unsigned long long)(long long)cr + (!HASHED && sodd[rank] ? kOddFlag : 0ull);
             if (add != 0) atomicAdd(&tcnt[tc + lane], add);
         }
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront", "local");  // LDS only: no wait for the ref stores
         __builtin_amdgcn_wave_barrier();
         DFP_PH(4);
     }
