@@ -77,6 +77,9 @@ struct hj_dist_job {
     const void* rk = nullptr;  // received probe keys / ids (job-owned blocks)
     const uint32_t* ri = nullptr;
     int64_t rn = 0;
+    bool base_mode = false;      // one-rank identity: a re-probe reads the caller's keys, ids pbase + row
+    const uint8_t* rv = nullptr;  // (its validity bitmap and offset)
+    int64_t rvoff = 0, pbase = 0;
     void* ws = nullptr;
     hipStream_t stream = nullptr;
     std::vector<std::pair<void*, size_t>> blocks;  // job-owned device blocks

@@ -329,6 +329,16 @@ struct LocalFail {
     }
 };
 
+// one rank: the exchange is the identity (DFP_HJ_DIST_W1_IDENTITY=0 runs the whole plan,
+// to price its machinery)
+bool w1_identity() {
+    static const bool v = [] {
+        const char* e = getenv("DFP_HJ_DIST_W1_IDENTITY");
+        return !(e && e[0] == '0');
+    }();
+    return v;
+}
+
 // test hook of the thread transport: a rank's plan fails at step `at` of job fail_at
 bool injected(hj_comm* c, int64_t job, int at) { return c->fail_at >= 0 && job == c->fail_at / 8 && at == c->fail_at % 8; }
 
@@ -384,11 +394,7 @@ hj_status run_sharded(hj_comm* c, const ShardedArgs& a, hj_dist_job* j, int64_t 
     // of the input in place (its key range stays on the device: no partition, no copy, no
     // host read). DFP_HJ_DIST_W1_IDENTITY=0 runs the whole plan at one rank instead (to
     // price its machinery).
-    static const bool w1_identity = [] {
-        const char* e = getenv("DFP_HJ_DIST_W1_IDENTITY");
-        return !(e && e[0] == '0');
-    }();
-    if (W == 1 && a.base == 0 && a.pkt == a.kt && w1_identity && !injected(c, jobno, 0)) {
+    if (W == 1 && a.base == 0 && a.pkt == a.kt && w1_identity() && !injected(c, jobno, 0)) {
         hj_table* t = nullptr;
         ST_OK(hj_build_begin(c->device, 1, a.kt, a.n, &t));
         hj_status st = hj_build_append(t, 0, a.keys, a.valid, a.voff, nullptr, a.n,
@@ -666,6 +672,51 @@ hj_status run_radix(hj_comm* c, const RadixArgs& a, hj_dist_job* j, int64_t jobn
     HIP_OK(hipStreamWaitEvent(sd, j->ev_in, 0));
     HIP_OK(hipStreamWaitEvent(s, j->ev_in, 0));
     HIP_OK(hipEventRecord(j->ev_t[0], sd));
+
+    // One rank whose build rows start at global row 0: both exchanges are the identity, so
+    // the join is the single-GPU build of the build keys in place (on the build stream) and
+    // the probe of the probe keys with ids probe_base + row — no partition, no host read.
+    if (W == 1 && a.bbase == 0 && a.pkt == a.kt && w1_identity() && !injected(c, jobno, 0)) {
+        HIP_OK(hipStreamWaitEvent(sb, j->ev_in, 0));
+        if (a.pbase < 0 || a.pbase + a.np > ((int64_t)1 << 32))
+            return set_error(HJ_ERR_INVALID, "hj_dist_join_radix: probe ids (probe_base + row) must fit 32 bits");
+        hj_table* t = nullptr;
+        ST_OK(hj_build_begin(c->device, 1, a.kt, a.nb, &t));
+        j->table = t;  // freed with the job
+        ST_OK(hj_build_append(t, 0, a.bkeys, a.bvalid, a.bvoff, nullptr, a.nb,
+                              HJ_INPUT_DEVICE | HJ_BORROW | HJ_BORROW_KEEP, sb));
+        ST_OK(hj_build_finish(t, 0));
+        HIP_OK(hipEventRecord(j->ev_t[2], sb));
+        j->info.build_rows = a.nb;
+        j->info.recv_rows = a.nb;
+        j->info.sharded = 1;
+        HIP_OK(hipEventRecord(j->ev_t[1], s));  // no exchange: an empty span on the probe stream
+        HIP_OK(hipEventRecord(j->ev_t[3], s));
+        j->out_cap = std::max<int64_t>(a.np, 1);
+        void* ws = scr.get((size_t)hj_probe_workspace_bytes(a.np));
+        uint64_t* ob = (uint64_t*)scr.get((size_t)j->out_cap * 8);
+        uint32_t* op = (uint32_t*)scr.get((size_t)j->out_cap * 4);
+        int64_t* dt = (int64_t*)scr.get(8);
+        if (!ws || !ob || !op || !dt) return set_error(HJ_ERR_OOM, "hj_dist: device allocation failed (probe output)");
+        // (the probe waits for the table's build by itself)
+        ST_OK(hj_probe_async_base(t, a.pkeys, a.pvalid, a.pvoff, a.np, (uint32_t)a.pbase, ob, op, j->out_cap, dt, ws, s));
+        HIP_OK(hipEventRecord(j->ev_t[4], s));
+        HIP_OK(hipMemcpyAsync(j->h_total, dt, 8, hipMemcpyDeviceToHost, s));
+        HIP_OK(hipEventRecord(j->ev_total, s));
+        j->out_b = ob;
+        j->out_p = op;
+        j->d_total = dt;
+        j->rk = a.pkeys;  // a re-probe reads the caller's probe keys (base mode)
+        j->rv = a.pvalid;
+        j->rvoff = a.pvoff;
+        j->pbase = a.pbase;
+        j->base_mode = true;
+        j->rn = a.np;
+        j->ws = ws;
+        j->stream = s;
+        for (void* p : {(void*)ob, (void*)op, (void*)dt, ws}) scr.give(j, p);
+        return scr.defer();
+    }
 
     // 1. the plan: [min | max, rows, failed] of the build side
     int64_t* mm = (int64_t*)scr.get(8 * 8);
@@ -1131,8 +1182,12 @@ hj_status hj_dist_job_pairs(hj_dist_job* j, const uint64_t** build_idx, const ui
             j->blocks.emplace_back(ob, (size_t)total * 8);
             j->blocks.emplace_back(op, (size_t)total * 4);
             if (j->table_taken) return set_error(HJ_ERR_INVALID, "hj_dist_job_pairs: re-probe needs the job's table");
-            ST_OK(hj_probe_async_ids(j->table, j->rk, nullptr, 0, j->ri, j->rn, (uint64_t*)ob, (uint32_t*)op, total,
-                                     j->d_total, j->ws, j->stream));
+            if (j->base_mode)
+                ST_OK(hj_probe_async_base(j->table, j->rk, j->rv, j->rvoff, j->rn, (uint32_t)j->pbase, (uint64_t*)ob,
+                                          (uint32_t*)op, total, j->d_total, j->ws, j->stream));
+            else
+                ST_OK(hj_probe_async_ids(j->table, j->rk, nullptr, 0, j->ri, j->rn, (uint64_t*)ob, (uint32_t*)op,
+                                         total, j->d_total, j->ws, j->stream));
             HIP_OK(hipMemcpyAsync(j->h_total, j->d_total, 8, hipMemcpyDeviceToHost, j->stream));
             HIP_OK(hipEventRecord(j->ev_total, j->stream));
             HIP_OK(hipEventSynchronize(j->ev_total));
@@ -1180,7 +1235,9 @@ void hj_dist_job_free(hj_dist_job* j) {
         j->cv.wait(g, [j] { return j->done; });
     }
     (void)hipSetDevice(j->device);
-    if (j->stream) (void)hipStreamSynchronize(j->stream);
+    // this job's own device work only (its probe stream is the communicator's: a later job's
+    // work may already be queued behind it there)
+    if (j->ev_total) (void)hipEventSynchronize(j->ev_total);
     if (j->table && !j->table_taken) hj_table_free(j->table);
     for (auto& b : j->blocks) dfp::host::free_block(j->device, b.first, b.second);
     for (auto e : j->ev_t)

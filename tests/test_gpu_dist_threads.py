@@ -208,18 +208,18 @@ def test_sharded_threads_int32_probe_of_int64_build(ctl, oracle_mod, world):
     assert np.array_equal(np.concatenate([o[0][1] for o in out]), op.astype(np.uint64))
 
 
-def _radix_rank(r, comm, world, bk, pk, key_dtype, steps=1):
+def _radix_rank(r, comm, world, bk, pk, key_dtype, steps=1, base=0):
     b0, b1 = _split(bk.size, world, r)
     p0, p1 = _split(pk.size, world, r)
     keys = torch.from_numpy(bk[b0:b1].astype(key_dtype)).cuda()
     probe = torch.from_numpy(pk[p0:p1].astype(key_dtype)).cuda()
     s = torch.cuda.Stream()
     torch.cuda.synchronize()
-    jobs = [comm.join_radix(keys, b0, probe, p0, s.cuda_stream) for _ in range(steps)]
+    jobs = [comm.join_radix(keys, base + b0, probe, p0, s.cuda_stream) for _ in range(steps)]
     res = []
     for job in jobs:
         b, p = job.pairs()
-        res.append((b.cpu().numpy().astype(np.uint64), p.cpu().numpy().astype(np.uint32)))
+        res.append((b.cpu().numpy().astype(np.uint64) - base, p.cpu().numpy().astype(np.uint32)))
         t = job.times()
         assert all(x >= 0 for x in t)
         del b, p
@@ -255,7 +255,7 @@ def test_radix_threads(ctl, oracle_mod, world, kind):
             assert np.all(np.diff(o[step][1].astype(np.int64)) >= 0)
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [1, 2, 4])
 def test_radix_threads_int32_and_empty(ctl, oracle_mod, world):
     """int32 keys; and a build side with no rows on some ranks (a rank with nothing)."""
     rng = np.random.default_rng(world)
@@ -277,6 +277,27 @@ def test_radix_threads_int32_and_empty(ctl, oracle_mod, world):
         ranks.close()
     assert all(e is None for e in errs), errs
     assert sum(o[0][0].size for o in out) == 0
+
+
+@pytest.mark.parametrize("base", [0, 5000])
+def test_radix_one_rank_paths(ctl, oracle_mod, base):
+    """One rank: base 0 takes the identity path (the build in place, the probe with
+    probe_base), a nonzero global build base the whole plan; both give the oracle's pairs,
+    also with duplicate-heavy keys (more pairs than probe rows: the job's re-probe)."""
+    rng = np.random.default_rng(base + 1)
+    bk = np.concatenate([rng.integers(0, 2000, 20_000), np.full(300, 77)]).astype(np.int64)
+    pk = np.concatenate([rng.integers(-10, 2010, 30_000), np.full(50, 77)]).astype(np.int64)
+    ranks = Ranks(ctl, 1)
+    try:
+        out, errs = ranks.run(lambda r, c: _radix_rank(r, c, 1, bk, pk, np.int64, steps=2, base=base))
+    finally:
+        ranks.close()
+    assert all(e is None for e in errs), errs
+    ob, op = oracle_mod.inner_join(bk, pk)
+    for step in range(2):
+        b, p = out[0][step]
+        assert b.size > pk.size  # the re-probe ran
+        assert np.array_equal(b, ob) and np.array_equal(p, op)
 
 
 @pytest.mark.parametrize("plan", ["sharded", "radix"])

@@ -896,3 +896,45 @@ def test_spec_build_concurrent_first_probes(dfp, oracle_mod, case):
             for (b, p), (ob, op) in zip(got, want):
                 assert_same(b, p, ob, op)
             assert (t.stats()["buckets"] == 0) == (case == "dense")
+
+
+@pytest.mark.parametrize("case", ["dense", "hashed"])
+def test_spec_build_two_partitions_first_probes(dfp, oracle_mod, case):
+    """The shape of the round-4 fault (gpurun_out/r04p): the operator's two
+    partitions each append half of the build side and call hj_build_finish (the last one
+    launches the speculative build), then both probe at once with device output and a
+    validity bitmap — composite keys are 64-bit hashes, so the table is hashed and the first
+    probe builds it while the other must wait for the settled geometry."""
+    import threading
+
+    rng = np.random.default_rng(21 if case == "dense" else 22)
+    n = 120_000
+    bk = (rng.integers(0, 4 * n, n) if case == "dense"
+          else rng.integers(I64_MIN, np.iinfo(np.int64).max, n, dtype=np.int64)).astype(np.int64)
+    pks = [np.concatenate([rng.choice(bk, 30_000), rng.integers(0, 4 * n, 30_000)]).astype(np.int64) for _ in range(2)]
+    pvalid = [rng.random(pk.size + 5) > 0.05 for pk in pks]  # bit 5 of the bitmap is row 0
+    want = [oracle_mod.inner_join(bk, pk, None, v[5:]) for pk, v in zip(pks, pvalid)]
+    halves = [bk[: n // 2], bk[n // 2:]]
+    for _ in range(3):
+        with dfp.HashTable(2, "int64", 0) as t:
+            got, errs = [None] * 2, []
+
+            def part(i):
+                try:
+                    t.append(i, torch.from_numpy(halves[i]).cuda())
+                    t.finish(i)
+                    bits = torch.from_numpy(np.packbits(pvalid[i], bitorder="little")).cuda()
+                    b, p = t.probe(torch.from_numpy(pks[i]).cuda(), valid=bits, device_output=True, valid_offset=5)
+                    got[i] = (b.cpu().numpy().astype(np.uint64), p.cpu().numpy().astype(np.uint32))
+                except Exception as e:  # noqa: BLE001 - reported below
+                    errs.append(e)
+
+            th = [threading.Thread(target=part, args=(i,)) for i in range(2)]
+            for x in th:
+                x.start()
+            for x in th:
+                x.join()
+            assert not errs, errs
+            for (b, p), (ob, op) in zip(got, want):
+                assert_same(b, p, ob, op)
+            assert (t.stats()["buckets"] == 0) == (case == "dense")
