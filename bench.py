@@ -599,6 +599,8 @@ def main():
             if per_step_sync:
                 torch.cuda.synchronize(dev)
                 job.collect()
+        if hasattr(job, "drain"):  # no native job in flight across torch's barrier below
+            job.drain()
         torch.cuda.synchronize(dev)
         job.collect()
         _clear_stage_lists(job)

@@ -749,7 +749,9 @@ hj_status ensure_geometry(const hj_table* ct) {
         return HJ_OK;
     }
     // another layout: drain the (idle) speculative kernels, release their blocks, build
+    // (the build time then runs from here: ev0 again)
     HIP_TRY(hipStreamSynchronize(t->bstream));
+    HIP_TRY(hipEventRecord(t->res.ev0, t->bstream));
     free_list(t, t->allocs);
     free_list(t, t->scratch);
     t->dense = nullptr;
@@ -1763,6 +1765,7 @@ hj_status hj_table_stats_get(const hj_table* t, hj_table_stats* out) {
 
 int64_t hj_table_build_ns(const hj_table* t) {
     if (t == nullptr || !t->built || t->build_st != HJ_OK) return -1;
+    if (t->multi == nullptr && ensure_geometry(t) != HJ_OK) return -1;  // a pending speculative build settles first
     if (t->multi) {
         int64_t ns = 0;
         for (hj_table* sh : t->multi->shards) ns = std::max(ns, hj_table_build_ns(sh));

@@ -2757,6 +2757,10 @@ __device__ __forceinline__ uint32_t sl_count(const TableView& tv, uint32_t r) {
 // cover one contiguous run (no LDS staging, no barriers in the emission).
 constexpr int kSlEmitThreads = 512;
 constexpr int kSlWaveRows = kSlTile / (kSlEmitThreads / 64);  // 2048
+// the count-free emission reads a wave's entry count as wcnt[tile * kSlRanges + wave]: one
+// partition range per emission wave
+static_assert(kSlEmitThreads / 64 == kSlRanges && kSlWaveRows == kSlRangeRows,
+              "emission waves and the partition's entry-count ranges must coincide");
 
 template <bool HAS_ROW_IDS, bool HAS_PROBE_IDS>
 __global__ void __launch_bounds__(kSlEmitThreads, 4)  // two workgroups per CU: <= 128 VGPRs
