@@ -142,6 +142,7 @@ COMMTEST_SIGNATURES = [
     ("hj_test_hub_free", None, [P]),
     ("hj_test_comm_create", I32, [P, I32, I32, PP]),
     ("hj_test_comm_fail_at", None, [P, I32, I32]),
+    ("hj_test_range_share", I32, [I64, I64, I32, I32, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)]),
 ]
 
 _lib = None

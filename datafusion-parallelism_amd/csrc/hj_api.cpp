@@ -30,9 +30,11 @@
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
+#include <deque>
 #include <map>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <tuple>
 #include <unordered_map>
 #include <vector>
@@ -775,6 +777,67 @@ hj_status ensure_geometry(const hj_table* ct) {
     // (and ev1) are complete; one that sees it clear reads the finished geometry
     t->spec_pending.store(false, std::memory_order_release);
     return st;
+}
+
+// The settler: a process-wide thread that settles speculative builds (ensure_geometry) as
+// soon as their key range lands, instead of at the table's first use. A range that takes
+// another layout (a hashed table: wide or sparse keys) is then rebuilt while the caller's
+// previous probe still runs, not on the first probe's critical path.
+// DFP_HJ_SETTLE=0 leaves the settle to the first use.
+struct Settler {
+    std::mutex mu;
+    std::condition_variable cv;
+    std::deque<hj_table*> q;
+    hj_table* busy = nullptr;
+};
+Settler& settler() {
+    static Settler* s = [] {
+        Settler* st = new Settler();  // never destroyed: its detached thread may outlive main
+        std::thread([st] {
+            for (;;) {
+                hj_table* t;
+                {
+                    std::unique_lock<std::mutex> g(st->mu);
+                    st->cv.wait(g, [st] { return !st->q.empty(); });
+                    t = st->q.front();
+                    st->q.pop_front();
+                    st->busy = t;
+                }
+                (void)ensure_geometry(t);  // a failure is recorded on the table (build_st)
+                {
+                    std::lock_guard<std::mutex> g(st->mu);
+                    st->busy = nullptr;
+                }
+                st->cv.notify_all();
+            }
+        }).detach();
+        return st;
+    }();
+    return *s;
+}
+bool settler_on() {
+    static const bool v = [] {
+        const char* e = getenv("DFP_HJ_SETTLE");
+        return !(e && e[0] == '0');
+    }();
+    return v;
+}
+void settler_enqueue(hj_table* t) {
+    Settler& st = settler();
+    {
+        std::lock_guard<std::mutex> g(st.mu);
+        st.q.push_back(t);
+    }
+    st.cv.notify_all();
+}
+// before a table is freed: out of the queue, and not being settled
+void settler_forget(hj_table* t) {
+    if (!settler_on()) return;
+    Settler& st = settler();
+    std::unique_lock<std::mutex> g(st.mu);
+    for (auto it = st.q.begin(); it != st.q.end();)
+        it = *it == t ? st.q.erase(it) : it + 1;
+    st.cv.wait(g, [&st, t] { return st.busy != t; });
 }
 
 // The device build, run once by the last partition to arrive at the barrier.
@@ -1565,6 +1628,7 @@ hj_status hj_build_finish(hj_table* t, int partition) {
         t->build_err = st == HJ_OK ? "" : g_err;
         t->built = true;
         t->cv.notify_all();
+        if (st == HJ_OK && t->spec_pending.load(std::memory_order_acquire) && settler_on()) settler_enqueue(t);
     } else {
         // a partition that never arrives would block the rest forever; like the
         // reference's "Possible deadlock" timeouts (src/utils/parallel_compaction_batch_list.rs:56-58)
@@ -1998,6 +2062,7 @@ hj_status hj_table_stream_wait(const hj_table* t, void* stream) {
 
 void hj_table_free(hj_table* t) {
     if (t == nullptr) return;
+    if (t->spec_seq != 0) settler_forget(t);
     (void)hipSetDevice(t->device);
     // the blocks return to the cache (reused by any stream): the build and the latest
     // probe must be done (earlier probes on other streams are the caller's to finish)

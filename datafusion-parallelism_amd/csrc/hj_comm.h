@@ -121,5 +121,8 @@ namespace comm {
 // finish a communicator made by hj_comm_create or the test library: pinned mailbox,
 // events, the worker thread. -> HJ_OK or an error (the communicator is then freed)
 hj_status start(hj_comm* c);
+// the rank's contiguous share [lo, hi] of the key range [gmin, gmax] under the partition
+// kernel's range map (hj_dist.cpp); false when empty
+bool range_share_of(int64_t gmin, int64_t gmax, int W, int r, int64_t* lo, int64_t* hi);
 }  // namespace comm
 }  // namespace dfp

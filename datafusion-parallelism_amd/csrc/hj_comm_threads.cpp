@@ -260,6 +260,13 @@ hj_status hj_test_comm_create(hj_test_hub* h, int rank, int device, hj_comm** ou
     return HJ_OK;
 }
 
+// host only (no GPU): the sharded plan's key-range share of rank r (hj_dist.cpp's
+// range_share), for the CPU test that checks it against the Python plan's
+// ExchangePlan.local_key_range; -> 1 and [*lo, *hi], or 0 when the share is empty
+int hj_test_range_share(int64_t gmin, int64_t gmax, int world, int rank, int64_t* lo, int64_t* hi) {
+    return dfp::comm::range_share_of(gmin, gmax, world, rank, lo, hi) ? 1 : 0;
+}
+
 // the rank's plan fails (locally) at step `step` (0 key range, 1 partition, 2 local build)
 // of its job number `job` (0-based, in submission order)
 void hj_test_comm_fail_at(hj_comm* c, int job, int step) {

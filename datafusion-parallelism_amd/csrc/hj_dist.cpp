@@ -988,6 +988,9 @@ hj_status check_comm(hj_comm* c) {
 
 namespace dfp {
 namespace comm {
+bool range_share_of(int64_t gmin, int64_t gmax, int W, int r, int64_t* lo, int64_t* hi) {
+    return range_share(gmin, gmax, W, r, lo, hi);
+}
 hj_status start(hj_comm* c) {
     HIP_OK(hipSetDevice(c->device));
     // DFP_HJ_COMM_PRIORITY=-1: the plan's own streams at high priority (their kernels are

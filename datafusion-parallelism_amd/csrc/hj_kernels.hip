@@ -4062,6 +4062,7 @@ uint32_t sl_slices(const TableView& tv) {
 // entries, and looks them up; one emission at the end). Every pass re-reads the probe
 // keys: auto takes up to kSlAutoPasses passes, a forced sliced probe any number.
 constexpr uint32_t kSlAutoPasses = 4;
+constexpr int64_t kSlMinTilesPerPart = 1536;  // lookup items: tiles per (slice, part) at least
 uint32_t sl_passes(uint32_t nsl) { return (nsl + kSlMaxSlices - 1) / kSlMaxSlices; }
 
 bool sl_auto(const TableView& tv, int64_t n) {
@@ -4161,6 +4162,10 @@ hipError_t launch_probe_sliced(int key_bytes, const TableView& tv, const void* k
         }
         uint32_t parts = std::max<uint32_t>(1, (target + nsl - 1) / nsl);
         parts = (uint32_t)std::min<int64_t>(parts, (nt + 63) / 64);
+        // at least ~1536 tiles per part: a smaller probe (a rank's share on N GPUs) loads each
+        // slice image fewer times (profiles/r05_lookup_items_small.txt: 1.25*10^7 rows over C2's
+        // table, one part per slice 24.4 us against 37.1 us at C2's three; C2 keeps three)
+        parts = std::max<uint32_t>(1, std::min<uint32_t>(parts, (uint32_t)(nt / kSlMinTilesPerPart)));
         // the last round of small items: the slices beyond whole rounds of `parts` items
         // over the CUs split so that they fill about one round (DFP_HJ_SL_TAIL=0: even split)
         uint32_t s1 = nsl, parts2 = parts;
