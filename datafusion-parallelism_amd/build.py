@@ -96,8 +96,9 @@ def build(force: bool = False, verbose: bool = False, defines: tuple[str, ...] =
 
 def build_commtest(force: bool = False, verbose: bool = False) -> str:
     """lib/libdfp_hj_commtest.so: the product library's objects (built first) plus the
-    thread transport (hj_test_* entry points). Test infrastructure only."""
-    build(force=force, verbose=verbose)
+    thread transport (hj_test_* entry points). Test infrastructure only. `force` relinks
+    this library; the product objects are rebuilt only when stale."""
+    build(verbose=verbose)
     if not force and not _stale(COMMTEST_LIB, tuple(SOURCES_COMMTEST)):
         return COMMTEST_LIB
     rocm = os.environ.get("ROCM_PATH", "/opt/rocm")
