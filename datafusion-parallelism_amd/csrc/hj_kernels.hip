@@ -2158,18 +2158,39 @@ hashed_frag_build_kernel(uint32_t nb, uint32_t clog2, uint32_t s0, uint32_t nsl,
 //          chunk, as lookup4); key 0 reads the side bucket.
 constexpr int kHsSliceLog = 11;  // buckets per hashed slice: 2^11 x 64 B = 128 KB of LDS
 
+// The LDS image of a hashed slice, bank-spread: quad q of the slice's bucket bl lies at
+// quad (q ^ ((bl >> 2) & 3)) of its 64-byte line. A ds_read_b128 serves 16 lanes per LDS
+// cycle; their bank slot is (4 * (bl % 4) + physical quad) of the 256-byte bank row, so
+// with every line in plain order, 16 lanes reading the same quad of random buckets meet on
+// 4 slots (about 6-way); the XOR by the next two bucket bits spreads them over all 16.
+// (r03 rotated by the bucket's low bits, which leaves the 4 slots as they were.)
+#ifndef DFP_HS_ROT
+#define DFP_HS_ROT 1
+#endif
+__device__ __forceinline__ uint32_t hs_quad_rot(uint32_t bl) { return DFP_HS_ROT ? (bl >> 2) & 3u : 0u; }
+__device__ __forceinline__ void lds_line(const uint4* __restrict__ img, uint32_t bl, uint4& a0, uint4& a1, uint4& a2,
+                                         uint4& a3) {
+    const uint4* p = img + (size_t)bl * 4;
+    const uint32_t r = hs_quad_rot(bl);
+    a0 = p[0 ^ r];
+    a1 = p[1 ^ r];
+    a2 = p[2 ^ r];
+    a3 = p[3 ^ r];
+}
+
 // ref of stored key sk (!= 0) in the LDS image of a hashed slice whose first bucket is
 // sbase; linear probing wraps inside the key's chunk (cmask), as the table was built
 __device__ __forceinline__ uint32_t lds_bucket_ref(const uint4* __restrict__ img, uint32_t nb, uint32_t sbase,
                                                    uint32_t cmask, unsigned long long sk, uint32_t* cnt) {
     uint32_t b = stored_bucket(sk, nb);
-    const uint4* p = img + (size_t)(b - sbase) * 4;
+    uint4 a0, a1, a2, a3;
+    lds_line(img, b - sbase, a0, a1, a2, a3);
     bool more;
-    uint32_t ref = scan_line(p[0], p[1], p[2], p[3], sk, &more, cnt);
+    uint32_t ref = scan_line(a0, a1, a2, a3, sk, &more, cnt);
     for (uint32_t probes = 0; more && probes < cmask; ++probes) {
         b = (b & ~cmask) | ((b + 1) & cmask);
-        const uint4* q = img + (size_t)(b - sbase) * 4;
-        ref = scan_line(q[0], q[1], q[2], q[3], sk, &more, cnt);
+        lds_line(img, b - sbase, a0, a1, a2, a3);
+        ref = scan_line(a0, a1, a2, a3, sk, &more, cnt);
     }
     return ref;
 }
@@ -2194,6 +2215,23 @@ constexpr uint32_t kBigCorr = 1u << 16;  // counts - 1 from here on correct the 
 #define DFP_LK_GROUP 4
 #endif
 constexpr int kLkGroup = DFP_LK_GROUP;  // dense lookup: rows per branch-free group (divides the window's rows)
+#ifndef DFP_HS_LK2  // hashed lookup: the common-path rows (r05); 0 restores the per-row path
+#define DFP_HS_LK2 1
+#endif
+#ifndef DFP_HS_DEFER  // hashed lookup: probes past a full home bucket queued per wave (r05)
+#define DFP_HS_DEFER 1
+#endif
+#ifndef DFP_HS_NOPROBE  // timing ablation (wrong pairs): no probe past a full bucket
+#define DFP_HS_NOPROBE 0
+#endif
+#ifndef DFP_HS_G1
+#define DFP_HS_G1 1
+#endif
+#ifndef DFP_HS_G2
+#define DFP_HS_G2 1
+#endif
+constexpr int kHsGroup1 = DFP_HS_G1;  // hashed lookup: rows per group of owner searches and entry loads
+constexpr int kHsGroup2 = DFP_HS_G2;  // hashed lookup: rows per group of bucket-line reads
 // a tile's pair count (tcnt) is < 2^45 (16384 rows x < 2^31 build rows); the dense lookup
 // adds kOddFlag once per fragment with an entry of a missing or duplicated key (at most
 // 4095 slices x 3 passes of a direct-addressed range: the flag bits never wrap to 0)
@@ -2258,6 +2296,10 @@ sl_lookup_kernel(TableView tv, uint32_t wlog, uint32_t nslices, int64_t ntiles, 
     __shared__ uint32_t s_cst[kSlThreads];
     __shared__ uint32_t s_end[HASHED ? kSlThreads : 1];  // hashed, per wave: end position of each fragment, by rank
     __shared__ unsigned long long s_mask[kSlThreads / 64][W / 64];
+    // hashed (DFP_HS_DEFER): per wave, the window's entries that must probe past a full home
+    // bucket, queued (stored key, entry index | owner rank << 26) and looked up 64 at a time
+    __shared__ unsigned long long s_dqk[HASHED && DFP_HS_DEFER ? kSlThreads : 1];
+    __shared__ uint32_t s_dqo[HASHED && DFP_HS_DEFER ? kSlThreads : 1];
     DFP_DBG_TS(g_dbg_lk_ts, 0, wall_clock64());
     // Items: the first s1 slices in `parts` parts each, then the rest in `parts2` smaller
     // ones; every XCD runs its share of the first stage before its share of the second
@@ -2281,12 +2323,15 @@ sl_lookup_kernel(TableView tv, uint32_t wlog, uint32_t nslices, int64_t ntiles, 
     // instruction per piece, every piece of a wave in flight at once, no VGPR round trip),
     // the rest (a table's last partial piece) by ordinary loads
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    // (hashed: LDS quad i holds source quad i ^ hs_quad_rot(i / 4), the bank-spread lines)
     auto dma = [&](const uint4* src, uint32_t nq) {  // nq uint4 of src -> s_tab
         const uint32_t npieces = nq >> 6;
-        for (uint32_t c = (uint32_t)wave; c < npieces; c += kSlThreads / 64)
+        for (uint32_t c = (uint32_t)wave; c < npieces; c += kSlThreads / 64) {
+            const uint32_t i = c * 64 + lane;
             __builtin_amdgcn_global_load_lds(
-                (const __attribute__((address_space(1))) void*)(src + c * 64 + lane),
+                (const __attribute__((address_space(1))) void*)(src + (HASHED ? i ^ hs_quad_rot(i >> 2) : i)),
                 (__attribute__((address_space(3))) void*)(reinterpret_cast<uint4*>(s_tab) + c * 64), 16, 0, 0);
+        }
         return npieces << 6;
     };
     if constexpr (HASHED) {
@@ -2294,7 +2339,7 @@ sl_lookup_kernel(TableView tv, uint32_t wlog, uint32_t nslices, int64_t ntiles, 
         const uint32_t nbk = min<uint32_t>(1u << kHsSliceLog, tv.nb - sbase);
         const uint4* src = reinterpret_cast<const uint4*>(tv.tbl + sbase);
         uint4* dst = reinterpret_cast<uint4*>(s_tab);
-        for (uint32_t i = dma(src, nbk * 4) + threadIdx.x; i < nbk * 4; i += kSlThreads) dst[i] = src[i];
+        for (uint32_t i = dma(src, nbk * 4) + threadIdx.x; i < nbk * 4; i += kSlThreads) dst[i] = src[i ^ hs_quad_rot(i >> 2)];
     } else {
         const uint64_t base = (uint64_t)s << wlog;
         const uint32_t len = (uint32_t)min<uint64_t>(1u << wlog, tv.drange - base);
@@ -2452,9 +2497,56 @@ sl_lookup_kernel(TableView tv, uint32_t wlog, uint32_t nslices, int64_t ntiles, 
                     }
                 }
             }
+#if DFP_HS_LK2
+            if constexpr (HASHED) {
+                // hashed: the dense path's row groups (mask reads, then owner bases and
+                // fragment ends, then the entry loads of kHsGroup1 rows issue together)
+#pragma unroll
+                for (int g0 = 0; g0 < NU; g0 += kHsGroup1) {
+#pragma unroll
+                    for (int u = g0; u < g0 + kHsGroup1; ++u) {
+                        off[u] = kOob;
+                        ev[u] = 0;
+                    }
+                    if (w0 + g0 * 64 >= R) continue;  // uniform: past the run
+                    unsigned long long mu[kHsGroup1];
+#pragma unroll
+                    for (int j = 0; j < kHsGroup1; ++j) {
+                        const unsigned long long m = smask[g0 + j];  // the same word for every lane
+                        const uint32_t mlo = __builtin_amdgcn_readfirstlane((uint32_t)m);
+                        const uint32_t mhi = __builtin_amdgcn_readfirstlane((uint32_t)(m >> 32));
+                        mu[j] = ((unsigned long long)mhi << 32) | mlo;
+                    }
+                    uint32_t kk[kHsGroup1], bs[kHsGroup1], en[kHsGroup1];
+#pragma unroll
+                    for (int j = 0; j < kHsGroup1; ++j) {
+                        const unsigned long long m1 = mu[j] >> 1;
+                        const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m1 >> 32),
+                                                                          __builtin_amdgcn_mbcnt_lo((uint32_t)m1, 0u));
+                        kk[j] = kb + (uint32_t)(mu[j] & 1) + below - 1;
+                        kb += (uint32_t)__builtin_popcountll(mu[j]);
+                    }
+#pragma unroll
+                    for (int j = 0; j < kHsGroup1; ++j) {
+                        bs[j] = sbs[kk[j] & 63];
+                        en[j] = send[kk[j] & 63];
+                    }
+#pragma unroll
+                    for (int j = 0; j < kHsGroup1; ++j) {
+                        const uint32_t r = w0 + (g0 + j) * 64 + lane;
+                        const uint32_t o = r < R ? bs[j] + r : kOob;
+                        if (r + 1 == en[j]) off_end |= 1u << (g0 + j);  // last position of its fragment
+                        const uint2 v = __builtin_bit_cast(
+                            uint2, __builtin_amdgcn_raw_buffer_load_b64(rko, (int)(o * 8), 0, 0));
+                        ev[g0 + j] = ((unsigned long long)v.y << 32) | v.x;
+                        off[g0 + j] = o | ((kk[j] & 63) << 26);
+                    }
+                }
+            }
+#endif
 #pragma unroll
             for (int u = 0; u < NU; ++u) {
-                if constexpr (!HASHED) break;  // (above)
+                if constexpr (!HASHED || DFP_HS_LK2) break;  // (above)
                 off[u] = kOob;
                 if (w0 + u * 64 >= R) continue;  // uniform: past the run
                 const uint32_t r = w0 + u * 64 + lane;
@@ -2487,43 +2579,186 @@ sl_lookup_kernel(TableView tv, uint32_t wlog, uint32_t nslices, int64_t ntiles, 
             DFP_PH(1);
             DFP_PH_WAIT();
             DFP_PH(2);
-            if constexpr (HASHED) {
-#pragma unroll
-                for (int u = 0; u < NU; ++u) {
-                    if (w0 + u * 64 >= R) continue;  // uniform: past the run
-                    const uint32_t o = off[u] & kOobMask;
-                    uint32_t v, c;  // ref and its row count (kCountUnknown: in its segment header)
-                    const unsigned long long sk = ev[u];
-                    if (o == kOob) {
-                        v = kMiss;  // no store, no correction
-                        c = 1;
-                    } else if (DFP_ABL(4)) {  // timing ablation: no bucket lookup (wrong pairs)
-                        v = (uint32_t)sk & 0xFFFFFFu;
-                        c = 1;
-                    } else if (sk == 0) {  // key 0: the side bucket (rare; loaded at the start)
-                        v = side_meta ? side_ref : kMiss;
-                        c = side_meta;
-                    } else {
-                        v = lds_bucket_ref(reinterpret_cast<const uint4*>(s_tab), tv.nb, sbase, cmask, sk, &c);
-                    }
-                    // counts not inline: read from the segment header in a wave-uniform branch
-                    // that waits there. Merged into the common path, that load's wait was an
-                    // s_waitcnt vmcnt(0) on every row — for the previous rows' ref stores (loads
-                    // and stores share vmcnt): one store round trip per 64 entries.
-                    if (__ballot(c == kCountUnknown) != 0) {
-                        if (c == kCountUnknown) c = tv.dup_rows[v & tv.off_mask];
-                        asm volatile("" : "+v"(c));
-                    }
-                    __builtin_amdgcn_raw_buffer_store_b32(v, rres, (int)(o * 4), 0, 0);
-                    uint32_t d = c - 1u;  // kOob: c = 1
-                    if (d != 0xFFFFFFFFu && d >= kBigCorr) {
-                        atomicAdd(&tcnt[tc + slane[off[u] >> 26]], (unsigned long long)d);
-                        d = 0;
-                    }
-                    corr_run += wave_incl_scan_dpp(d);
-                    if (off_end & (1u << u)) scst[off[u] >> 26] = corr_run;
-                    corr_run = (uint32_t)__builtin_amdgcn_readlane((int)corr_run, 63);
+            // one hashed row the general way (any count, key 0, probes past full buckets)
+            auto hashed_row = [&](const int u) __attribute__((always_inline)) {
+                if (w0 + u * 64 >= R) return;  // uniform: past the run
+                const uint32_t o = off[u] & kOobMask;
+                uint32_t v, c;  // ref and its row count (kCountUnknown: in its segment header)
+                const unsigned long long sk = ev[u];
+                if (o == kOob) {
+                    v = kMiss;  // no store, no correction
+                    c = 1;
+                } else if (DFP_ABL(4)) {  // timing ablation: no bucket lookup (wrong pairs)
+                    v = (uint32_t)sk & 0xFFFFFFu;
+                    c = 1;
+                } else if (sk == 0) {  // key 0: the side bucket (rare; loaded at the start)
+                    v = side_meta ? side_ref : kMiss;
+                    c = side_meta;
+                } else {
+                    v = lds_bucket_ref(reinterpret_cast<const uint4*>(s_tab), tv.nb, sbase, cmask, sk, &c);
                 }
+                // counts not inline: read from the segment header in a wave-uniform branch
+                // that waits there. Merged into the common path, that load's wait was an
+                // s_waitcnt vmcnt(0) on every row — for the previous rows' ref stores (loads
+                // and stores share vmcnt): one store round trip per 64 entries.
+                if (__ballot(c == kCountUnknown) != 0) {
+                    if (c == kCountUnknown) c = tv.dup_rows[v & tv.off_mask];
+                    asm volatile("" : "+v"(c));
+                }
+                __builtin_amdgcn_raw_buffer_store_b32(v, rres, (int)(o * 4), 0, 0);
+                uint32_t d = c - 1u;  // kOob: c = 1
+                if (d != 0xFFFFFFFFu && d >= kBigCorr) {
+                    atomicAdd(&tcnt[tc + slane[off[u] >> 26]], (unsigned long long)d);
+                    d = 0;
+                }
+                corr_run += wave_incl_scan_dpp(d);
+                if (off_end & (1u << u)) scst[off[u] >> 26] = corr_run;
+                corr_run = (uint32_t)__builtin_amdgcn_readlane((int)corr_run, 63);
+            };
+            // DFP_HS_DEFER: the queued entries, one per lane: probe on from the bucket after
+            // the home one; a hit stores its ref over the kMiss stored for it and adds its
+            // row count to its tile (the -1 of a miss was already in the running sum)
+            uint32_t dq_n = 0;  // uniform: queued entries of this wave
+            auto dq_flush = [&]() __attribute__((always_inline)) {
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront", "local");
+                __builtin_amdgcn_wave_barrier();
+                if ((uint32_t)lane < dq_n) {
+                    const unsigned long long sk = s_dqk[wave * 64 + lane];
+                    const uint32_t ofs = s_dqo[wave * 64 + lane];
+                    uint32_t b = stored_bucket(sk, tv.nb), c = 0;
+                    uint32_t ref = kMiss;
+                    bool more = true;
+                    for (uint32_t probes = 0; more && probes < cmask; ++probes) {
+                        b = (b & ~cmask) | ((b + 1) & cmask);
+                        uint4 q0, q1, q2, q3;
+                        lds_line(reinterpret_cast<const uint4*>(s_tab), b - sbase, q0, q1, q2, q3);
+                        ref = scan_line(q0, q1, q2, q3, sk, &more, &c);
+                    }
+                    if (ref != kMiss) {
+                        if (c == kCountUnknown) c = tv.dup_rows[ref & tv.off_mask];
+                        __builtin_amdgcn_raw_buffer_store_b32(ref, rres, (int)((ofs & kOobMask) * 4), 0, 0);
+                        atomicAdd(&tcnt[tc + slane[ofs >> 26]], (unsigned long long)c);
+                    }
+                }
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront", "local");
+                __builtin_amdgcn_wave_barrier();
+                dq_n = 0;
+            };
+            if constexpr (HASHED) {
+#if DFP_HS_LK2
+                // Rows in groups of kHsGroup2: the group's bucket lines are read together and
+                // each row costs five key compares and a select chain. Only a group with a
+                // lane on the rare path — key 0 (the side bucket), a probe past a bucket an
+                // insert passed full, or a duplicated key (its count) — takes the per-row
+                // path below. In the common group every valid entry is a single hit or a miss,
+                // so the correction running sum (count - 1 = -1 per miss) is the misses'
+                // ballot prefix (mbcnt) instead of a DPP scan. A bucket whose meta bit 0 is
+                // set is full (an insert sets it only after finding no free slot), so the
+                // empty-slot test of scan_line is not needed for `more`.
+#pragma unroll
+                for (int g0 = 0; g0 < NU; g0 += kHsGroup2) {
+                    if (w0 + g0 * 64 >= R) continue;  // uniform: past the run
+                    uint4 ln[kHsGroup2][4];
+                    uint32_t hb[kHsGroup2];  // home bucket (absolute; 0 for an unused lane)
+#pragma unroll
+                    for (int j = 0; j < kHsGroup2; ++j) {
+                        const uint32_t o = off[g0 + j] & kOobMask;
+                        const unsigned long long sk = ev[g0 + j];
+                        const bool use = o != kOob && sk != 0;
+                        hb[j] = use ? stored_bucket(sk, tv.nb) : sbase;
+                        lds_line(reinterpret_cast<const uint4*>(s_tab), hb[j] - sbase, ln[j][0], ln[j][1], ln[j][2],
+                                 ln[j][3]);
+                    }
+                    uint32_t vv[kHsGroup2];
+                    bool mo_[kHsGroup2];
+                    bool rare = false;
+#pragma unroll
+                    for (int j = 0; j < kHsGroup2; ++j) {
+                        const uint32_t o = off[g0 + j] & kOobMask;
+                        const unsigned long long sk = ev[g0 + j];
+                        const uint4 a0 = ln[j][0], a1 = ln[j][1], a2 = ln[j][2], a3 = ln[j][3];
+                        const unsigned long long k0 = ((unsigned long long)a0.y << 32) | a0.x;
+                        const unsigned long long k1 = ((unsigned long long)a0.w << 32) | a0.z;
+                        const unsigned long long k2 = ((unsigned long long)a1.y << 32) | a1.x;
+                        const unsigned long long k3 = ((unsigned long long)a1.w << 32) | a1.z;
+                        const unsigned long long k4 = ((unsigned long long)a2.y << 32) | a2.x;
+                        uint32_t ref = k4 == sk ? a3.z : kMiss;
+                        ref = k3 == sk ? a3.y : ref;
+                        ref = k2 == sk ? a3.x : ref;
+                        ref = k1 == sk ? a2.w : ref;
+                        ref = k0 == sk ? a2.z : ref;
+                        const bool valid = o != kOob;
+                        // a miss in a bucket some insert passed full (meta bit 0, so no free
+                        // slot): probe on inside the chunk, the lanes that need it only
+                        const bool mo = valid & (sk != 0) & (ref == kMiss) & ((a3.w & 1u) != 0);
+#if DFP_HS_DEFER
+                        mo_[j] = mo;  // queued in the common branch below
+#else
+                        if (!DFP_HS_NOPROBE && __ballot(mo) != 0) {  // uniform: most rows (one miss in twenty)
+                            if (mo) {
+                                // the next bucket straight (compares and selects only): almost
+                                // every probe on ends there; a lane that must go further loops
+                                uint32_t b = (hb[j] & ~cmask) | ((hb[j] + 1) & cmask), cdummy;
+                                uint4 q0, q1, q2, q3;
+                                lds_line(reinterpret_cast<const uint4*>(s_tab), b - sbase, q0, q1, q2, q3);
+                                ref = ((((unsigned long long)q2.y << 32) | q2.x) == sk) ? q3.z : kMiss;
+                                ref = ((((unsigned long long)q1.w << 32) | q1.z) == sk) ? q3.y : ref;
+                                ref = ((((unsigned long long)q1.y << 32) | q1.x) == sk) ? q3.x : ref;
+                                ref = ((((unsigned long long)q0.w << 32) | q0.z) == sk) ? q2.w : ref;
+                                ref = ((((unsigned long long)q0.y << 32) | q0.x) == sk) ? q2.z : ref;
+                                bool more = (ref == kMiss) & ((q3.w & 1u) != 0);
+                                for (uint32_t probes = 1; more && probes < cmask; ++probes) {
+                                    b = (b & ~cmask) | ((b + 1) & cmask);
+                                    uint4 q0, q1, q2, q3;
+                                    lds_line(reinterpret_cast<const uint4*>(s_tab), b - sbase, q0, q1, q2, q3);
+                                    ref = scan_line(q0, q1, q2, q3, sk, &more, &cdummy);
+                                }
+                            }
+                        }
+#endif
+                        vv[j] = valid ? ref : kMiss;
+                        // rare: key 0 (the side bucket) or a duplicated key (its count)
+                        rare |= valid & ((sk == 0) | ((ref >= kDupFlag) & (ref != kMiss)));
+                    }
+                    if (__ballot(rare) == 0) {
+#pragma unroll
+                        for (int j = 0; j < kHsGroup2; ++j) {
+                            const int u = g0 + j;
+                            const uint32_t o = off[u] & kOobMask;
+#if DFP_HS_DEFER
+                            {  // queued; counted as a miss here, the flush corrects a hit
+                                const unsigned long long mm = __ballot(mo_[j]);
+                                if (!DFP_HS_NOPROBE && mm != 0) {  // uniform: most rows (one miss in twenty)
+                                    const uint32_t nq = (uint32_t)__builtin_popcountll(mm);
+                                    if (dq_n + nq > 64) dq_flush();
+                                    if (mo_[j]) {
+                                        const uint32_t at = wave * 64 + dq_n +
+                                            __builtin_amdgcn_mbcnt_hi((uint32_t)(mm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mm, 0u));
+                                        s_dqk[at] = ev[u];
+                                        s_dqo[at] = off[u];
+                                    }
+                                    dq_n += nq;
+                                }
+                            }
+#endif
+                            __builtin_amdgcn_raw_buffer_store_b32(vv[j], rres, (int)(o * 4), 0, 0);
+                            const bool miss = o != kOob && vv[j] == kMiss;
+                            const unsigned long long mm = __ballot(miss);
+                            const uint32_t ex = __builtin_amdgcn_mbcnt_hi((uint32_t)(mm >> 32),
+                                                                          __builtin_amdgcn_mbcnt_lo((uint32_t)mm, 0u));
+                            if (off_end & (1u << u)) scst[off[u] >> 26] = corr_run - ex - (miss ? 1u : 0u);
+                            corr_run -= (uint32_t)__builtin_popcountll(mm);
+                        }
+                        continue;
+                    }
+#pragma unroll
+                    for (int j = 0; j < kHsGroup2; ++j) hashed_row(g0 + j);
+                }
+                if (DFP_HS_DEFER && dq_n != 0) dq_flush();
+#else
+#pragma unroll
+                for (int u = 0; u < NU; ++u) hashed_row(u);
+#endif
             } else {
 #pragma unroll
                 for (int g0 = 0; g0 < NU; g0 += kLkGroup) {

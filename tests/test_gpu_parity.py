@@ -359,6 +359,36 @@ def test_hashed_sliced_auto(dfp, oracle_mod, nb, np_, dup_frac, null_frac, key_t
         L.hj_set_build_mode(old_b)
 
 
+@pytest.mark.parametrize("lf,dup_frac", [(0.75, 0.0), (0.8, 0.25)])
+def test_hashed_sliced_high_load(dfp, oracle_mod, monkeypatch, lf, dup_frac):
+    """Hashed table at a high load factor: many home buckets were passed full, so many
+    probe rows continue past them — the sliced lookup queues those per wave and flushes the
+    queue mid-window when it fills (r05); displaced keys with duplicated rows (counts in the
+    bucket meta or the segment header) and key 0 among them. Same pairs as the oracle."""
+    monkeypatch.setenv("DFP_HJ_LOAD_FACTOR", str(lf))
+    L = dfp.load()
+    old_p = L.hj_set_probe_mode(4)  # the sliced probe
+    try:
+        rng = np.random.default_rng(int(lf * 100))
+        distinct = rng.integers(-(2**63), 2**63 - 1, 1_200_000, dtype=np.int64)
+        bk = distinct.copy()
+        nd = int(len(bk) * dup_frac)
+        if nd:
+            bk[:nd] = distinct[rng.integers(nd, len(bk), nd)]
+            bk[nd:nd + 90] = distinct[-1]  # one key with > 63 rows
+        bk[-1] = 0
+        pk = np.concatenate([bk[rng.integers(0, len(bk), 1_500_000)],
+                             rng.integers(-(2**63), 2**63 - 1, 1_500_000, dtype=np.int64)])
+        rng.shuffle(pk)
+        pk[:2] = [0, 0]
+        b, p, st = gpu_join(dfp, bk, pk)
+        assert st["buckets"] > 0
+        ob, op = oracle_mod.inner_join(bk, pk)
+        assert_same(b, p, ob, op)
+    finally:
+        L.hj_set_probe_mode(old_p)
+
+
 @pytest.mark.parametrize("layout", [0, 2])
 def test_hashed_build_every_key_twice(dfp, oracle_mod, layout):
     """Hashed table whose every key has two rows (plus a few with 3..40): each 1024-bucket
