@@ -2969,6 +2969,11 @@ hs_partition_kernel(uint32_t nb, uint32_t slog, uint32_t s0, uint32_t nslices, c
     }
 }
 
+// Measured (r05) and not kept: this partition in two workgroups per CU (one tile each, the
+// sorted keys staged in two 64 KB halves): its 16 (1024 threads) or 32 (512 threads) stored
+// keys per thread plus their ranks need more than the 64 / 128 VGPRs that two workgroups per
+// CU allow (50-130 spilled), so it was not timed.
+
 // row count behind a ref; packed dense refs carry counts <= 15 in bits 27-30. Other
 // duplicated keys read the count from their segment header, in a wave-uniform branch
 // that also waits for it there: merged into the common path, that load's wait would be
