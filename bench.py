@@ -523,8 +523,9 @@ def main():
     ap.add_argument("--native", default="auto", choices=["auto", "on", "off"],
                     help="multi-GPU sharded plan: its build side through the C entry point hj_dist_build_sharded "
                          "(RCCL inside the library; auto = on RCCL groups) or the torch.distributed steps (off)")
-    ap.add_argument("--comms", type=int, default=2,
-                    help="multi-GPU native plans: communicators used in turn (consecutive steps' host reads overlap)")
+    ap.add_argument("--comms", type=int, default=None,
+                    help="multi-GPU native plans: communicators used in turn (consecutive steps' host reads overlap; "
+                         "default 2 on one rank, 1 on more: DistributedHashJoin)")
     ap.add_argument("--build-priority", default="normal", choices=["normal", "high"],
                     help="multi-GPU plans: the build side's stream at high HIP priority (its kernels are the critical "
                          "path of the build side's host reads)")

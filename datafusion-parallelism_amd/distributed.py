@@ -664,18 +664,24 @@ class DistributedHashJoin:
 
     def __init__(self, group=None, partition_fn: Callable | None = None, local_join_fn: Callable | None = None,
                  chunks: int = 1, local_build_fn: Callable | None = None, compress_keys: bool = True,
-                 runtime_filter: bool = True, native: bool | None = None, comms: int = 2):
+                 runtime_filter: bool = True, native: bool | None = None, comms: int | None = None):
         """native: run the plans through the C entry points (hj_dist_build_sharded_async,
         hj_dist_join_radix: RCCL inside the library, one job per step on a communicator's
         worker thread) instead of the torch.distributed steps below; None = when the group's
         backend is nccl (RCCL) and the world is a power of two. comms: native communicators
         used in turn, one step each, so that consecutive steps' host reads overlap (each has
-        its own worker and streams)."""
+        its own worker and streams); None = 2 on one rank, 1 on more. Two communicators'
+        workers issue their collectives in an order that differs between ranks, and HIP
+        multiplexes the communicators' streams onto GPU_MAX_HW_QUEUES hardware queues that
+        run in submission order: a collective of one communicator queued behind the other's
+        on one rank, and the reverse on another, would wait for each other. With one
+        communicator every rank issues its collectives in job order on one stream."""
         self.group = group
         self.native = native
         self._comm: NativeComm | None = None
         self._comms: list[NativeComm] = []
-        self._ncomms = max(1, int(comms))
+        self.world = dist.get_world_size(group)
+        self._ncomms = max(1, int(comms)) if comms is not None else (2 if self.world == 1 else 1)
         self._turn = 0
         self.last_native = False  # the latest join / join_sharded ran the C entry point
         self.world = dist.get_world_size(group)
