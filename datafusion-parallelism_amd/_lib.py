@@ -94,6 +94,7 @@ SIGNATURES = [
     ("hj_pairs_free", None, [ctypes.POINTER(HjPairs)]),
     ("hj_probe_workspace_bytes", I64, [I64]),
     ("hj_set_probe_mode", I32, [I32]),
+    ("hj_set_probe_tile_log", I32, [I32]),
     ("hj_set_build_mode", I32, [I32]),
     ("hj_set_device_budget", I64, [I64]),
     ("hj_table_device_bytes", I32, [P, ctypes.POINTER(ctypes.c_int64)]),

@@ -1873,6 +1873,11 @@ int hj_set_probe_mode(int mode) {
     return old;
 }
 
+int hj_set_probe_tile_log(int tile_log) {
+    if (tile_log != 0 && tile_log != 14 && tile_log != 15) return -1;
+    return set_probe_tile_log(tile_log);
+}
+
 hj_status hj_probe_async(const hj_table* t, const void* keys, const uint8_t* validity, int64_t validity_offset,
                          int64_t n, uint64_t* out_build, uint32_t* out_probe, int64_t capacity, int64_t* d_total,
                          void* workspace, void* stream) {

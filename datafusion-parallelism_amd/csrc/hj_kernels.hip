@@ -1331,6 +1331,17 @@ constexpr int kSlOwnWinHashed = 1024;  // hashed slices: 16 per lane (u64 entrie
 // flag from the lookup) needs no count pass in the emission
 constexpr int kSlRanges = 8;
 constexpr int kSlRangeRows = kSlTile / kSlRanges;  // 2048
+// The probe's tiles: 2^14 rows (kSlTile, also the builds') or 2^15 (DFP_HJ_SL_TILE_LOG=15:
+// half the (tile, slice) fragments for the lookup to walk, each twice as long; the
+// partition and the emission then run one 1024-thread workgroup per CU with a 128 KB
+// image). Per tile log TL: rows, 4096-row partition groups, 2048-row emission ranges.
+template <int TL> struct SlT {
+    static_assert(TL == 14 || TL == 15, "probe tiles of 2^14 or 2^15 rows");
+    static constexpr int kRows = 1 << TL;
+    static constexpr int kGroups = kRows / (kSlThreads * 4);
+    static constexpr int kRanges = kRows / kSlRangeRows;
+    static constexpr int kEmitThreads = kRanges * 64;  // one emission wave per range
+};
 static_assert(kSlWidthLogMax + kSlTileLog <= 32, "entry = offset << tile bits | row");
 static_assert(kSlWidthLogMax <= 16 && kSlTileLog <= 16, "key offsets and rows leave as u16");
 
@@ -1345,8 +1356,12 @@ __device__ __forceinline__ void hist_excl_scan(uint32_t* s_hist, uint32_t* s_w, 
     __syncthreads();
 }
 
-template <typename K, bool HAS_VALID>
-__global__ void __launch_bounds__(kSlThreads, 8)  // 8 waves per SIMD = two workgroups per CU: <= 64 VGPRs
+#ifndef DFP_SL_PD
+#define DFP_SL_PD 3
+#endif
+template <typename K, bool HAS_VALID, int TL = kSlTileLog>
+// 2^14-row tiles: 8 waves per SIMD = two workgroups per CU, <= 64 VGPRs; 2^15: one (128 KB of LDS)
+__global__ void __launch_bounds__(kSlThreads, TL == 14 ? 8 : 4)
 sl_partition_kernel(int64_t dmin, uint64_t drange, uint32_t wlog, uint32_t nslices, const void* __restrict__ keys,
                     const uint8_t* __restrict__ valid, int64_t voff, int64_t n, bool vec,
                     uint16_t* __restrict__ ko, uint16_t* __restrict__ rl, uint16_t* __restrict__ toff, int nt,
@@ -1354,9 +1369,10 @@ sl_partition_kernel(int64_t dmin, uint64_t drange, uint32_t wlog, uint32_t nslic
                     unsigned long long* __restrict__ hdr,  // probe: workspace header (error word at [1]); build: null
                     unsigned long long* __restrict__ tcnt,      // probe: the tile's entry count; build: null
                     uint32_t* __restrict__ tent,  // probe: entries of the tile so far (earlier passes: append after them)
-                    uint16_t* __restrict__ wcnt,  // probe: entries per 2048-row range of the tile (kSlRanges u16)
+                    uint16_t* __restrict__ wcnt,  // probe: entries per 2048-row range of the tile (T::kRanges u16)
                     SpecGeo sg) {  // build with the key range on the device (mm null: dmin, drange, nslices given)
-    __shared__ __attribute__((aligned(16))) uint32_t s_ent[kSlTile];
+    using T = SlT<TL>;
+    __shared__ __attribute__((aligned(16))) uint32_t s_ent[T::kRows];
     if (sg.mm != nullptr) {  // (uniform) the geometry from the reduction's result; none: another layout
         const long long mn = sg.mm[0], mx = sg.mm[1];
         const uint32_t nb = spec_dense_blocks(mn, mx, sg.rows, sg.cap);
@@ -1372,13 +1388,13 @@ sl_partition_kernel(int64_t dmin, uint64_t drange, uint32_t wlog, uint32_t nslic
     uint32_t* s_wc = s_ent + kSlThreads / 64;
     const int64_t tile = blockIdx.x;          // tile of this key array
     const int64_t gtile = tile + tile_off;    // its output region (the build partitions several arrays)
-    const int64_t tile0 = tile * kSlTile;
+    const int64_t tile0 = tile * T::kRows;
     const uint32_t nbins = nslices + 1;  // bin nslices stays empty: its prefix is the total
     // multi-pass probe (tables beyond kSlMaxSlices slices): this pass's entries follow the
     // tile's entries of the earlier passes (hdr == null marks a later pass)
     const uint32_t ebase = (tent != nullptr && hdr == nullptr) ? tent[gtile] : 0u;
     for (uint32_t b = threadIdx.x; b < kSlHistBins; b += kSlThreads) s_hist[b] = 0;
-    if (threadIdx.x < kSlRanges) s_wc[threadIdx.x] = 0;
+    if (threadIdx.x < T::kRanges) s_wc[threadIdx.x] = 0;
     // probe: zero the workspace header incl. the error word (no memset launch)
     // (and the emission's tile counter after the tile counts: one tile per workgroup here)
     if (hdr != nullptr && blockIdx.x == 0 && threadIdx.x == 0) {
@@ -1387,14 +1403,13 @@ sl_partition_kernel(int64_t dmin, uint64_t drange, uint32_t wlog, uint32_t nslic
     }
     __syncthreads();
     // per row: entry (offset << 14 | row) and (slice << 14 | rank in slice), ~0 = no entry
-    uint32_t e[kSlGroups][4], sr[kSlGroups][4];
+    uint32_t e[T::kGroups][4], sr[T::kGroups][4];
     // the next group's keys load while this group's rows are ranked (one load round trip
     // per tile instead of one per group; two groups of keys fit the 64-register budget).
     // A whole aligned tile takes straight 16-byte loads with no branch between the groups
     // (a branch would make the next group's loads wait at its join).
     auto groups = [&](auto full_tag) {
         constexpr bool FULL = decltype(full_tag)::value;
-        int64_t kn[4];
         auto load_group = [&](int g, int64_t (&dst)[4]) {
             const int loc0 = g * (kSlThreads * 4) + threadIdx.x * 4;
             if constexpr (FULL && sizeof(K) == 8) {
@@ -1410,22 +1425,27 @@ sl_partition_kernel(int64_t dmin, uint64_t drange, uint32_t wlog, uint32_t nslic
                 load4<K>(keys, tile0 + loc0, n, vec, dst);
             }
         };
-        load_group(0, kn);
+        // groups in flight ahead of the one being ranked: 1 at 2^14-row tiles (32 waves per
+        // CU), DFP_SL_PD at 2^15 (16 waves per CU hold fewer loads in flight per CU)
+        constexpr int D = TL == 14 ? 1 : DFP_SL_PD;
+        int64_t kr[D + 1][4];  // ring of groups: group g in slot g % (D + 1)
 #pragma unroll
-        for (int g = 0; g < kSlGroups; ++g) {
+        for (int g = 0; g < D && g < T::kGroups; ++g) load_group(g, kr[g]);
+#pragma unroll
+        for (int g = 0; g < T::kGroups; ++g) {
             const int loc0 = g * (kSlThreads * 4) + threadIdx.x * 4;
             int64_t k[4];
 #pragma unroll
-            for (int q = 0; q < 4; ++q) k[q] = kn[q];
-            if (g + 1 < kSlGroups) load_group(g + 1, kn);
+            for (int q = 0; q < 4; ++q) k[q] = kr[g % (D + 1)][q];
+            if (g + D < T::kGroups) load_group(g + D, kr[(g + D) % (D + 1)]);
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 const int64_t row = tile0 + loc0 + q;
                 const uint64_t idx = (uint64_t)k[q] - (uint64_t)dmin;
                 const bool ok = row < n && (!HAS_VALID || bit_valid(valid, voff, row)) && idx < drange;
                 const uint32_t sl = (uint32_t)(idx >> wlog);
-                e[g][q] = ((uint32_t)(idx & ((1u << wlog) - 1)) << kSlTileLog) | (uint32_t)(loc0 + q);
-                sr[g][q] = ok ? (sl << kSlTileLog) | atomicAdd(&s_hist[sl], 1u) : 0xFFFFFFFFu;
+                e[g][q] = ((uint32_t)(idx & ((1u << wlog) - 1)) << TL) | (uint32_t)(loc0 + q);
+                sr[g][q] = ok ? (sl << TL) | atomicAdd(&s_hist[sl], 1u) : 0xFFFFFFFFu;
             }
             if (wcnt != nullptr) {  // probe: entries per emission range (a wave's rows of one group share a range)
                 uint32_t ws = 0;    // the wave's entries in group g: scalar popcounts of the entry ballots
@@ -1435,16 +1455,16 @@ sl_partition_kernel(int64_t dmin, uint64_t drange, uint32_t wlog, uint32_t nslic
             }
         }
     };
-    if (vec && tile0 + kSlTile <= n && !(nt & 1)) groups(std::true_type{});
+    if (vec && tile0 + T::kRows <= n && !(nt & 1)) groups(std::true_type{});
     else groups(std::false_type{});
     __syncthreads();
     // the range counts leave s_ent before the scan's barriers (its wave totals use s_ent[0, 16))
-    const uint32_t my_wc = (wcnt != nullptr && threadIdx.x < kSlRanges) ? s_wc[threadIdx.x] : 0u;
+    const uint32_t my_wc = (wcnt != nullptr && threadIdx.x < T::kRanges) ? s_wc[threadIdx.x] : 0u;
     // exclusive scan of the bins, four per thread
     uint32_t tot;
     hist_excl_scan(s_hist, s_w, &tot);
-    if (wcnt != nullptr && threadIdx.x < kSlRanges) {
-        uint16_t* wc = wcnt + gtile * kSlRanges + threadIdx.x;
+    if (wcnt != nullptr && threadIdx.x < T::kRanges) {
+        uint16_t* wc = wcnt + gtile * T::kRanges + threadIdx.x;
         *wc = (uint16_t)((ebase ? *wc : 0u) + my_wc);
     }
     uint16_t* to = toff + gtile * (int64_t)nbins;
@@ -1456,36 +1476,36 @@ sl_partition_kernel(int64_t dmin, uint64_t drange, uint32_t wlog, uint32_t nslic
     if (tcnt != nullptr && threadIdx.x == 0) tcnt[gtile] = (ebase ? tcnt[gtile] : 0ull) + tot;
     if (tent != nullptr && threadIdx.x == 0) tent[gtile] = ebase + tot;
 #pragma unroll
-    for (int g = 0; g < kSlGroups; ++g)
+    for (int g = 0; g < T::kGroups; ++g)
 #pragma unroll
         for (int q = 0; q < 4; ++q)
             if (sr[g][q] != 0xFFFFFFFFu)
-                s_ent[s_hist[sr[g][q] >> kSlTileLog] + (sr[g][q] & (kSlTile - 1))] = e[g][q];
+                s_ent[s_hist[sr[g][q] >> TL] + (sr[g][q] & (T::kRows - 1))] = e[g][q];
     __syncthreads();
     // entries leave split: the key offset in the slice (u16, read by S2) and the row in
     // the tile (u16, read by S3)
-    uint16_t* dst = ko + gtile * kSlTile;
-    uint16_t* dsr = rl + gtile * kSlTile;
+    uint16_t* dst = ko + gtile * T::kRows;
+    uint16_t* dsr = rl + gtile * T::kRows;
     if (ebase != 0) {  // a later pass: unaligned base, one entry per thread (2-byte stores)
         for (uint32_t i = threadIdx.x; i < tot; i += kSlThreads) {
             const uint32_t v = s_ent[i];
-            dst[ebase + i] = (uint16_t)(v >> kSlTileLog);
-            dsr[ebase + i] = (uint16_t)(v & (kSlTile - 1));
+            dst[ebase + i] = (uint16_t)(v >> TL);
+            dsr[ebase + i] = (uint16_t)(v & (T::kRows - 1));
         }
         return;
     }
     const uint32_t n4 = tot & ~3u;
     for (uint32_t i = threadIdx.x * 4; i < n4; i += kSlThreads * 4) {
         const uint4 v = *reinterpret_cast<const uint4*>(s_ent + i);
-        constexpr uint32_t m = kSlTile - 1;
-        *reinterpret_cast<uint2*>(dst + i) = make_uint2((v.x >> kSlTileLog) | ((v.y >> kSlTileLog) << 16),
-                                                        (v.z >> kSlTileLog) | ((v.w >> kSlTileLog) << 16));
+        constexpr uint32_t m = T::kRows - 1;
+        *reinterpret_cast<uint2*>(dst + i) = make_uint2((v.x >> TL) | ((v.y >> TL) << 16),
+                                                        (v.z >> TL) | ((v.w >> TL) << 16));
         *reinterpret_cast<uint2*>(dsr + i) = make_uint2((v.x & m) | ((v.y & m) << 16), (v.z & m) | ((v.w & m) << 16));
     }
     if (threadIdx.x < (tot & 3u)) {
         const uint32_t v = s_ent[n4 + threadIdx.x];
-        dst[n4 + threadIdx.x] = (uint16_t)(v >> kSlTileLog);
-        dsr[n4 + threadIdx.x] = (uint16_t)(v & (kSlTile - 1));
+        dst[n4 + threadIdx.x] = (uint16_t)(v >> TL);
+        dsr[n4 + threadIdx.x] = (uint16_t)(v & (T::kRows - 1));
     }
 }
 
@@ -2280,7 +2300,7 @@ __device__ unsigned long long g_dbg_lk_ph[8];
 #define DFP_PH_FLUSH() do { } while (0)
 #endif
 
-template <bool HASHED, int W>
+template <bool HASHED, int W, int TL = kSlTileLog>
 __global__ void __launch_bounds__(kSlThreads)
 sl_lookup_kernel(TableView tv, uint32_t wlog, uint32_t nslices, int64_t ntiles, uint32_t parts, uint32_t s1,
                  uint32_t parts2,  // slices [0, s1): `parts` items each; [s1, nslices): `parts2` smaller ones, last
@@ -2407,7 +2427,7 @@ sl_lookup_kernel(TableView tv, uint32_t wlog, uint32_t nslices, int64_t ntiles, 
             __builtin_amdgcn_mbcnt_hi((uint32_t)(ne >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)ne, 0u));
         const uint32_t nranks = (uint32_t)__builtin_popcountll(ne);
         if (len != 0) {
-            sbs[rank] = (uint32_t)lane * kSlTile + st - excl;  // >= 0: excl <= lane * kSlTile
+            sbs[rank] = (uint32_t)lane * SlT<TL>::kRows + st - excl;  // >= 0: excl <= lane * SlT<TL>::kRows
             slane[rank] = (uint32_t)lane;
             if constexpr (HASHED) send[rank] = excl + len;
         }
@@ -2428,9 +2448,9 @@ sl_lookup_kernel(TableView tv, uint32_t wlog, uint32_t nslices, int64_t ntiles, 
         const int64_t tcu = (int64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)tc) |
                             ((int64_t)__builtin_amdgcn_readfirstlane((int)(tc >> 32)) << 32);
         const __amdgpu_buffer_rsrc_t rko = __builtin_amdgcn_make_buffer_rsrc(
-            (void*)((const char*)ko + tcu * kSlTile * KB), 0, 64 * kSlTile * KB, 0x00020000);
+            (void*)((const char*)ko + tcu * SlT<TL>::kRows * KB), 0, 64 * SlT<TL>::kRows * KB, 0x00020000);
         const __amdgpu_buffer_rsrc_t rres =
-            __builtin_amdgcn_make_buffer_rsrc((void*)(res + tcu * kSlTile), 0, 64 * kSlTile * 4, 0x00020000);
+            __builtin_amdgcn_make_buffer_rsrc((void*)(res + tcu * SlT<TL>::kRows), 0, 64 * SlT<TL>::kRows * 4, 0x00020000);
         uint32_t kb = 0;  // segments started before the current row
         DFP_PH(0);
         for (uint32_t w0 = 0; w0 < R; w0 += W) {
@@ -2868,6 +2888,9 @@ sl_lookup_kernel(TableView tv, uint32_t wlog, uint32_t nslices, int64_t ntiles, 
 // tile (u16) leave in slice order, with the tile's slice bounds (u16). Persistent, one
 // workgroup per CU (128 KB of staged keys): the next tile's keys load into registers
 // once this tile's keys are staged, while they and the rows are written out.
+#ifndef DFP_HS_OPAQUE_TX
+#define DFP_HS_OPAQUE_TX 1
+#endif
 template <typename K, bool HAS_VALID>
 __global__ void __launch_bounds__(kSlThreads, 4)  // 16 waves per CU: <= 128 VGPRs
 hs_partition_kernel(uint32_t nb, uint32_t slog, uint32_t s0, uint32_t nslices, const void* __restrict__ keys,
@@ -2887,27 +2910,35 @@ hs_partition_kernel(uint32_t nb, uint32_t slog, uint32_t s0, uint32_t nslices, c
         tcnt[ntiles] = 0;     // the emission's tile counter
     }
     int64_t k[kSlGroups][4], nk[kSlGroups][4];
-    auto load = [&](int64_t t, int64_t (&dst)[kSlGroups][4]) {
+    auto load = [&](int64_t t, int64_t (&dst)[kSlGroups][4], uint32_t tx) {
 #pragma unroll
         for (int g = 0; g < kSlGroups; ++g)
-            load4<K>(keys, t * kSlTile + g * (kSlThreads * 4) + threadIdx.x * 4, n, vec, dst[g]);
+            load4<K>(keys, t * kSlTile + g * (kSlThreads * 4) + tx * 4, n, vec, dst[g]);
     };
     int64_t tile = blockIdx.x;
-    if (tile < ntiles) load(tile, nk);
+    if (tile < ntiles) load(tile, nk, threadIdx.x);
     for (; tile < ntiles; tile += gridDim.x) {
+#if DFP_HS_OPAQUE_TX
+        // the thread index made opaque per tile: otherwise the compiler hoists the rows'
+        // offsets and addresses out of the tile loop and spills them
+        uint32_t tx = threadIdx.x;
+        asm volatile("" : "+v"(tx));
+#else
+        const uint32_t tx = threadIdx.x;
+#endif
         const int64_t tile0 = tile * kSlTile;
         const int64_t gtile = tile + tile_off;  // its output region (the build partitions several segments)
 #pragma unroll
         for (int g = 0; g < kSlGroups; ++g)
 #pragma unroll
             for (int q = 0; q < 4; ++q) k[g][q] = nk[g][q];
-        for (uint32_t b = threadIdx.x; b < kSlHistBins; b += kSlThreads) s_hist[b] = 0;
+        for (uint32_t b = tx; b < kSlHistBins; b += kSlThreads) s_hist[b] = 0;
         const uint32_t ebase = later ? tent[tile] : 0u;
         __syncthreads();
         uint32_t sr[kSlGroups][4];  // slice << 14 | rank in slice, ~0 = no entry
 #pragma unroll
         for (int g = 0; g < kSlGroups; ++g) {
-            const int loc0 = g * (kSlThreads * 4) + threadIdx.x * 4;
+            const int loc0 = g * (kSlThreads * 4) + tx * 4;
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 const int64_t row = tile0 + loc0 + q;
@@ -2921,12 +2952,12 @@ hs_partition_kernel(uint32_t nb, uint32_t slog, uint32_t s0, uint32_t nslices, c
         uint32_t tot;
         hist_excl_scan(s_hist, s_w, &tot);
         uint16_t* to = toff + gtile * (int64_t)nbins;
-        for (uint32_t b = threadIdx.x; b < nbins; b += kSlThreads) to[b] = (uint16_t)(ebase + s_hist[b]);
-        if (threadIdx.x == 0 && probe) {
+        for (uint32_t b = tx; b < nbins; b += kSlThreads) to[b] = (uint16_t)(ebase + s_hist[b]);
+        if (tx == 0 && probe) {
             tcnt[tile] = (later ? tcnt[tile] : 0ull) + tot;  // S2 corrects it to the tile's pair count
             tent[tile] = ebase + tot;
         }
-        if (threadIdx.x == 0 && tile_base != nullptr) tile_base[gtile] = (uint32_t)(row_base + tile0);
+        if (tx == 0 && tile_base != nullptr) tile_base[gtile] = (uint32_t)(row_base + tile0);
         // pass 1: stored keys in slice order
 #pragma unroll
         for (int g = 0; g < kSlGroups; ++g)
@@ -2935,12 +2966,12 @@ hs_partition_kernel(uint32_t nb, uint32_t slog, uint32_t s0, uint32_t nslices, c
                 if (sr[g][q] != 0xFFFFFFFFu)
                     s_key[s_hist[sr[g][q] >> kSlTileLog] + (sr[g][q] & (kSlTile - 1))] = stored_key(k[g][q]);
         __syncthreads();
-        if (tile + (int64_t)gridDim.x < ntiles) load(tile + gridDim.x, nk);  // in flight during the write-out
+        if (tile + (int64_t)gridDim.x < ntiles) load(tile + gridDim.x, nk, tx);  // in flight during the write-out
         unsigned long long* dk = ko + gtile * kSlTile + ebase;
         if (ebase & 1) {  // a later pass at an odd base: 8-byte stores
-            for (uint32_t i = threadIdx.x; i < tot; i += kSlThreads) dk[i] = s_key[i];
+            for (uint32_t i = tx; i < tot; i += kSlThreads) dk[i] = s_key[i];
         } else {
-            for (uint32_t i = threadIdx.x * 2; i < tot; i += kSlThreads * 2) {
+            for (uint32_t i = tx * 2; i < tot; i += kSlThreads * 2) {
                 if (i + 2 <= tot) *reinterpret_cast<ulonglong2*>(dk + i) = *reinterpret_cast<const ulonglong2*>(s_key + i);
                 else dk[i] = s_key[i];
             }
@@ -2954,18 +2985,152 @@ hs_partition_kernel(uint32_t nb, uint32_t slog, uint32_t s0, uint32_t nslices, c
             for (int q = 0; q < 4; ++q)
                 if (sr[g][q] != 0xFFFFFFFFu)
                     s_row[s_hist[sr[g][q] >> kSlTileLog] + (sr[g][q] & (kSlTile - 1))] =
-                        (uint16_t)(g * (kSlThreads * 4) + threadIdx.x * 4 + q);
+                        (uint16_t)(g * (kSlThreads * 4) + tx * 4 + q);
         __syncthreads();
         uint16_t* dr = rl + gtile * kSlTile + ebase;
         if (ebase & 7) {  // a later pass at an unaligned base: 2-byte stores
-            for (uint32_t i = threadIdx.x; i < tot; i += kSlThreads) dr[i] = s_row[i];
+            for (uint32_t i = tx; i < tot; i += kSlThreads) dr[i] = s_row[i];
         } else {
-            for (uint32_t i = threadIdx.x * 8; i < tot; i += kSlThreads * 8) {
+            for (uint32_t i = tx * 8; i < tot; i += kSlThreads * 8) {
                 if (i + 8 <= tot) *reinterpret_cast<uint4*>(dr + i) = *reinterpret_cast<const uint4*>(s_row + i);
                 else for (uint32_t j = i; j < tot; ++j) dr[j] = s_row[j];
             }
         }
         __syncthreads();  // s_key / s_hist are rewritten for the next tile
+    }
+}
+
+// The same for 2^15-row tiles (probe only; DFP_HJ_SL_TILE_LOG=15). The tile's 32 stored
+// keys per thread stay in registers; the ranks, then the sorted positions, live in LDS
+// (u16 per row: holding them in registers beside the keys spills), and the sorted keys
+// leave through a 64 KB staging area in four quarters of 2^13 positions. Once the last
+// quarter is staged the key registers are free: the next tile's keys load into them
+// while that quarter and the rows are written out.
+template <typename K, bool HAS_VALID>
+__global__ void __launch_bounds__(kSlThreads, 4)  // 16 waves per CU: <= 128 VGPRs
+hs_partition32_kernel(uint32_t nb, uint32_t slog, uint32_t s0, uint32_t nslices, const void* __restrict__ keys,
+                      const uint8_t* __restrict__ valid, int64_t voff, int64_t n, int64_t ntiles, bool vec,
+                      unsigned long long* __restrict__ ko, uint16_t* __restrict__ rl, uint16_t* __restrict__ toff,
+                      unsigned long long* __restrict__ hdr, unsigned long long* __restrict__ tcnt,
+                      uint32_t* __restrict__ tent) {  // pass: slices [s0, s0 + nslices); hdr null = a later pass
+    using T = SlT<15>;
+    constexpr int kQ = T::kRows / 4;      // positions per staging quarter
+    constexpr uint16_t kNone = 0xFFFFu;   // no entry (positions and ranks are < 2^15)
+    __shared__ __attribute__((aligned(16))) unsigned long long s_key[kQ];  // also the rows (u16) pass
+    __shared__ __attribute__((aligned(16))) uint16_t s_pos[T::kRows];      // per row: rank, then position
+    __shared__ __attribute__((aligned(16))) uint32_t s_hist[kSlHistBins];
+    __shared__ uint32_t s_w[kSlThreads / 64];
+    const uint32_t nbins = nslices + 1;
+    const bool later = hdr == nullptr;
+    if (!later && blockIdx.x == 0 && threadIdx.x == 0) {
+        hdr[0] = hdr[1] = 0;  // workspace header (error word)
+        tcnt[ntiles] = 0;     // the emission's tile counter
+    }
+    int64_t k[T::kGroups][4];  // the keys, then their stored keys
+    auto load = [&](int64_t t, uint32_t tx) {
+#pragma unroll
+        for (int g = 0; g < T::kGroups; ++g)
+            load4<K>(keys, t * T::kRows + g * (kSlThreads * 4) + tx * 4, n, vec, k[g]);
+    };
+    auto slice_of = [&](unsigned long long sk) { return (stored_bucket(sk, nb) >> slog) - s0; };  // wraps past the pass
+    int64_t tile = blockIdx.x;
+    if (tile < ntiles) load(tile, threadIdx.x);
+    for (; tile < ntiles; tile += gridDim.x) {
+        // the thread index made opaque per tile: otherwise the compiler hoists every per-row
+        // offset and address of the 32 rows out of the tile loop and spills them
+        uint32_t tx = threadIdx.x;
+        asm volatile("" : "+v"(tx));
+        const int64_t tile0 = tile * T::kRows;
+        for (uint32_t b = tx; b < kSlHistBins; b += kSlThreads) s_hist[b] = 0;
+        const uint32_t ebase = later ? tent[tile] : 0u;
+        __syncthreads();
+        // ranks in slice: rows loc0 .. loc0 + 3 of group g are four adjacent u16 (one 8-byte LDS access)
+#pragma unroll
+        for (int g = 0; g < T::kGroups; ++g) {
+            const int loc0 = g * (kSlThreads * 4) + tx * 4;
+            uint32_t r[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int64_t row = tile0 + loc0 + q;
+                const unsigned long long sk = stored_key(k[g][q]);
+                k[g][q] = (int64_t)sk;
+                const uint32_t sl = slice_of(sk);
+                const bool ok = row < n && (!HAS_VALID || bit_valid(valid, voff, row)) && sl < nslices;
+                r[q] = ok ? atomicAdd(&s_hist[sl], 1u) : kNone;
+            }
+            *reinterpret_cast<uint2*>(s_pos + loc0) = make_uint2(r[0] | (r[1] << 16), r[2] | (r[3] << 16));
+        }
+        __syncthreads();
+        uint32_t tot;
+        hist_excl_scan(s_hist, s_w, &tot);
+        uint16_t* to = toff + tile * (int64_t)nbins;
+        for (uint32_t b = tx; b < nbins; b += kSlThreads) to[b] = (uint16_t)(ebase + s_hist[b]);
+        if (tx == 0) {
+            tcnt[tile] = (later ? tcnt[tile] : 0ull) + tot;  // S2 corrects it to the tile's pair count
+            tent[tile] = ebase + tot;
+        }
+        // ranks -> sorted positions (each thread rewrites only its own rows)
+#pragma unroll
+        for (int g = 0; g < T::kGroups; ++g) {
+            const int loc0 = g * (kSlThreads * 4) + tx * 4;
+            const uint2 v = *reinterpret_cast<const uint2*>(s_pos + loc0);
+            uint32_t r[4] = {v.x & 0xFFFFu, v.x >> 16, v.y & 0xFFFFu, v.y >> 16};
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                if (r[q] != kNone) r[q] += s_hist[slice_of((unsigned long long)k[g][q])];
+            *reinterpret_cast<uint2*>(s_pos + loc0) = make_uint2(r[0] | (r[1] << 16), r[2] | (r[3] << 16));
+        }
+        unsigned long long* dk = ko + tile * T::kRows + ebase;
+        // stored keys in slice order, a quarter of the positions at a time (every quarter is
+        // staged, so that the next tile's loads follow every use of k)
+#pragma unroll
+        for (int h = 0; h < 4; ++h) {
+            const uint32_t p0 = h * kQ;
+            const uint32_t p1 = min<uint32_t>(tot, p0 + kQ);
+#pragma unroll
+            for (int g = 0; g < T::kGroups; ++g) {
+                const int loc0 = g * (kSlThreads * 4) + tx * 4;
+                const uint2 v = *reinterpret_cast<const uint2*>(s_pos + loc0);
+                const uint32_t r[4] = {v.x & 0xFFFFu, v.x >> 16, v.y & 0xFFFFu, v.y >> 16};
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    if (r[q] - p0 < (uint32_t)kQ) s_key[r[q] - p0] = (unsigned long long)k[g][q];  // kNone: never
+            }
+            __syncthreads();
+            // the last quarter staged: the key registers are free, the next tile loads into them
+            if (h == 3 && tile + (int64_t)gridDim.x < ntiles) load(tile + gridDim.x, tx);
+            if (ebase & 1) {  // a later pass at an odd base: 8-byte stores
+                for (uint32_t i = p0 + tx; i < p1; i += kSlThreads) dk[i] = s_key[i - p0];
+            } else {
+                for (uint32_t i = p0 + tx * 2; i < p1; i += kSlThreads * 2) {
+                    if (i + 2 <= p1) *reinterpret_cast<ulonglong2*>(dk + i) = *reinterpret_cast<const ulonglong2*>(s_key + (i - p0));
+                    else dk[i] = s_key[i - p0];
+                }
+            }
+            __syncthreads();
+        }
+        // rows in the tile (u16), same order: 2^15 u16 in the staging area
+        uint16_t* s_row = reinterpret_cast<uint16_t*>(s_key);
+#pragma unroll
+        for (int g = 0; g < T::kGroups; ++g) {
+            const int loc0 = g * (kSlThreads * 4) + tx * 4;
+            const uint2 v = *reinterpret_cast<const uint2*>(s_pos + loc0);
+            const uint32_t r[4] = {v.x & 0xFFFFu, v.x >> 16, v.y & 0xFFFFu, v.y >> 16};
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                if (r[q] != kNone) s_row[r[q]] = (uint16_t)(loc0 + q);
+        }
+        __syncthreads();
+        uint16_t* dr = rl + tile * T::kRows + ebase;
+        if (ebase & 7) {  // a later pass at an unaligned base: 2-byte stores
+            for (uint32_t i = tx; i < tot; i += kSlThreads) dr[i] = s_row[i];
+        } else {
+            for (uint32_t i = tx * 8; i < tot; i += kSlThreads * 8) {
+                if (i + 8 <= tot) *reinterpret_cast<uint4*>(dr + i) = *reinterpret_cast<const uint4*>(s_row + i);
+                else for (uint32_t j = i; j < tot; ++j) dr[j] = s_row[j];
+            }
+        }
+        __syncthreads();  // s_key / s_pos / s_hist are rewritten for the next tile
     }
 }
 
@@ -3002,18 +3167,19 @@ constexpr int kSlWaveRows = kSlTile / (kSlEmitThreads / 64);  // 2048
 static_assert(kSlEmitThreads / 64 == kSlRanges && kSlWaveRows == kSlRangeRows,
               "emission waves and the partition's entry-count ranges must coincide");
 
-template <bool HAS_ROW_IDS, bool HAS_PROBE_IDS>
-__global__ void __launch_bounds__(kSlEmitThreads, 4)  // two workgroups per CU: <= 128 VGPRs
+template <bool HAS_ROW_IDS, bool HAS_PROBE_IDS, int TL = kSlTileLog>
+// 16 waves per CU (two 512-thread workgroups, or one of 1024 for 2^15-row tiles): <= 128 VGPRs
+__global__ void __launch_bounds__(SlT<TL>::kEmitThreads, 4)
 sl_emit_kernel(TableView tv, const uint32_t* __restrict__ tent, const uint16_t* __restrict__ rl,
                const uint32_t* __restrict__ res, const uint32_t* __restrict__ probe_ids, uint32_t pbase,
                const unsigned long long* __restrict__ tcnt, int64_t ntiles, uint64_t* __restrict__ out_b,
                uint32_t* __restrict__ out_p, int64_t cap, int64_t* __restrict__ d_total,
                const uint16_t* __restrict__ wcnt,  // entries per 2048-row range (null: always count)
                unsigned long long* __restrict__ dyn) {  // tile counter (zeroed by S1), null: static tiles
-    __shared__ __attribute__((aligned(16))) uint32_t s_ref[kSlTile];  // the tile's refs, kMiss = none
-    __shared__ unsigned long long s_w[kSlEmitThreads / 64];
-    __shared__ unsigned long long s_pre[kSlEmitThreads / 64];
-    __shared__ uint32_t s_own[kSlEmitThreads / 64][64];  // per wave: owner markers of one output window
+    __shared__ __attribute__((aligned(16))) uint32_t s_ref[SlT<TL>::kRows];  // the tile's refs, kMiss = none
+    __shared__ unsigned long long s_w[SlT<TL>::kEmitThreads / 64];
+    __shared__ unsigned long long s_pre[SlT<TL>::kEmitThreads / 64];
+    __shared__ uint32_t s_own[SlT<TL>::kEmitThreads / 64][64];  // per wave: owner markers of one output window
     __shared__ int64_t s_nxt;                              // dyn: the tile after the next one
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     // Measured (r04) and not kept: nontemporal pair stores (C2 162.4K -> 140.8K Mrows/s) and
@@ -3022,7 +3188,7 @@ sl_emit_kernel(TableView tv, const uint32_t* __restrict__ tent, const uint16_t* 
         out_b[o] = b;
         out_p[o] = p;
     };
-    constexpr int U = kSlTile / (kSlEmitThreads * 4);  // 8 x (4 rows + 4 refs) per thread
+    constexpr int U = SlT<TL>::kRows / (SlT<TL>::kEmitThreads * 4);  // 8 x (4 rows + 4 refs) per thread
     uint2 e4[U];
     uint4 r4[U];
     uint32_t cnt = 0;
@@ -3040,21 +3206,21 @@ sl_emit_kernel(TableView tv, const uint32_t* __restrict__ tent, const uint16_t* 
     // load per thread), so no scan launch runs between S2 and S3.
     auto count_sum = [&](int64_t lo, int64_t hi) -> unsigned long long {  // this thread's share
         unsigned long long v = 0;
-        for (int64_t j = lo + threadIdx.x; j < hi; j += kSlEmitThreads) v += tcnt[j] & kCountMask;
+        for (int64_t j = lo + threadIdx.x; j < hi; j += SlT<TL>::kEmitThreads) v += tcnt[j] & kCountMask;
         return v;
     };
     auto fetch = [&](int64_t t) {
         cnt = DFP_ABL(2) ? 0u : tent[t];  // the tile's entries over every pass
         if (wcnt != nullptr) {
             nflag = (uint32_t)(tcnt[t] >> kOddShift);  // the lookup's flag: some entry's count != 1
-            nwc = wcnt[t * kSlRanges + wave];
+            nwc = wcnt[t * SlT<TL>::kRanges + wave];
         }
-        const uint16_t* te = rl + t * kSlTile;
-        const uint32_t* tr = res + t * kSlTile;
+        const uint16_t* te = rl + t * SlT<TL>::kRows;
+        const uint32_t* tr = res + t * SlT<TL>::kRows;
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const uint32_t i = (u * kSlEmitThreads + threadIdx.x) * 4;
-            if (i < cnt) {  // whole uint4s: the region holds kSlTile entries, lanes past cnt are ignored
+            const uint32_t i = (u * SlT<TL>::kEmitThreads + threadIdx.x) * 4;
+            if (i < cnt) {  // whole uint4s: the region holds SlT<TL>::kRows entries, lanes past cnt are ignored
                 e4[u] = *reinterpret_cast<const uint2*>(te + i);
                 r4[u] = *reinterpret_cast<const uint4*>(tr + i);
             }
@@ -3070,7 +3236,7 @@ sl_emit_kernel(TableView tv, const uint32_t* __restrict__ tent, const uint16_t* 
         if (lane == 0) s_pre[wave] = v;
         if (dyn != nullptr && threadIdx.x == 0) s_nxt = (int64_t)gridDim.x + (int64_t)atomicAdd(dyn, 1ull);
         __syncthreads();
-        for (int w = 0; w < kSlEmitThreads / 64; ++w) base += s_pre[w];
+        for (int w = 0; w < SlT<TL>::kEmitThreads / 64; ++w) base += s_pre[w];
         next = dyn != nullptr ? s_nxt : tile + gridDim.x;
         __syncthreads();
     }
@@ -3080,13 +3246,13 @@ sl_emit_kernel(TableView tv, const uint32_t* __restrict__ tent, const uint16_t* 
         // of this tile, so the atomic's round trip hides behind the tile's work
         unsigned long long draw = 0;
         if (dyn != nullptr && threadIdx.x == 0 && next < ntiles) draw = atomicAdd(dyn, 1ull);
-        const int64_t tile0 = tile * kSlTile;
-        for (int i = threadIdx.x * 4; i < kSlTile; i += kSlEmitThreads * 4)
+        const int64_t tile0 = tile * SlT<TL>::kRows;
+        for (int i = threadIdx.x * 4; i < SlT<TL>::kRows; i += SlT<TL>::kEmitThreads * 4)
             *reinterpret_cast<uint4*>(s_ref + i) = make_uint4(kMiss, kMiss, kMiss, kMiss);
         __syncthreads();
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const uint32_t i = (u * kSlEmitThreads + threadIdx.x) * 4;
+            const uint32_t i = (u * SlT<TL>::kEmitThreads + threadIdx.x) * 4;
             if (i < cnt) s_ref[e4[u].x & 0xFFFF] = r4[u].x;
             if (i + 1 < cnt) s_ref[e4[u].x >> 16] = r4[u].y;
             if (i + 2 < cnt) s_ref[e4[u].y & 0xFFFF] = r4[u].z;
@@ -3111,7 +3277,7 @@ sl_emit_kernel(TableView tv, const uint32_t* __restrict__ tent, const uint16_t* 
         }
         __syncthreads();
         unsigned long long pos = base, tile_total = 0;
-        for (int w = 0; w < kSlEmitThreads / 64; ++w) {
+        for (int w = 0; w < SlT<TL>::kEmitThreads / 64; ++w) {
             if (w < wave) pos += s_w[w];
             tile_total += s_w[w];
         }
@@ -3209,7 +3375,7 @@ sl_emit_kernel(TableView tv, const uint32_t* __restrict__ tent, const uint16_t* 
         if (lane == 0) s_pre[wave] = pre;
         if (dyn != nullptr && threadIdx.x == 0) s_nxt = next < ntiles ? (int64_t)gridDim.x + (int64_t)draw : ntiles;
         __syncthreads();  // s_ref, s_w, s_pre and s_nxt are rewritten for the next tile
-        for (int w = 0; w < kSlEmitThreads / 64; ++w) base += s_pre[w];
+        for (int w = 0; w < SlT<TL>::kEmitThreads / 64; ++w) base += s_pre[w];
         tile = next;
         next = dyn != nullptr ? s_nxt : next + gridDim.x;
     }
@@ -4199,7 +4365,7 @@ ProbeWs probe_ws_layout(void* base, int64_t n) {
     return w;
 }
 
-// sliced probe workspace (16384-row tiles), after the 16-byte header (error word at
+// sliced probe workspace (2^tl-row tiles), after the 16-byte header (error word at
 // bytes 8..15): tcnt u64[nt + 2] (pair counts) | tent u32[nt + 2] (entries per tile over
 // the passes) | toff u16[nt][kSlMaxSlices + 1] (one pass's bounds) |
 // ko (entries: u16 key offsets in a dense slice, u64 stored keys in a hashed one; 8 B per
@@ -4214,17 +4380,18 @@ struct SlicedWs {
     uint16_t* wcnt;   // entries per 2048-row range of a tile (kSlRanges per tile)
     int64_t bytes;
 };
-SlicedWs sliced_ws_layout(void* base, int64_t n) {
-    const int64_t nt = (n + kSlTile - 1) / kSlTile;
+SlicedWs sliced_ws_layout(void* base, int64_t n, int tl) {
+    const int64_t tile = (int64_t)1 << tl;  // this probe's tiles
+    const int64_t nt = (n + tile - 1) / tile;
     SlicedWs w;
     uintptr_t p = (uintptr_t)base + 256;
     w.tcnt = (unsigned long long*)p;  p = al256(p + 8 * (nt + 2));
     w.tent = (uint32_t*)p;            p = al256(p + 4 * (nt + 2));
     w.toff = (uint16_t*)p;            p = al256(p + 2 * nt * (kSlMaxSlices + 1));  // one pass's bounds
-    w.ko = (void*)p;                  p = al256(p + 8 * nt * kSlTile);
-    w.rl = (uint16_t*)p;              p = al256(p + 2 * nt * kSlTile);
-    w.res = (uint32_t*)p;             p = al256(p + 4 * nt * kSlTile);
-    w.wcnt = (uint16_t*)p;            p = al256(p + 2 * kSlRanges * (nt + 2));
+    w.ko = (void*)p;                  p = al256(p + 8 * nt * tile);
+    w.rl = (uint16_t*)p;              p = al256(p + 2 * nt * tile);
+    w.res = (uint32_t*)p;             p = al256(p + 4 * nt * tile);
+    w.wcnt = (uint16_t*)p;            p = al256(p + 2 * (tile / kSlRangeRows) * (nt + 2));
     w.bytes = (int64_t)(p - (uintptr_t)base) + 256;
     return w;
 }
@@ -4253,7 +4420,8 @@ void set_probe_mode(int mode) {
 int get_probe_mode() { return probe_mode(); }
 
 int64_t probe_workspace(int64_t n) {
-    return std::max(probe_ws_layout(nullptr, n).bytes, sliced_ws_layout(nullptr, n).bytes);
+    return std::max(probe_ws_layout(nullptr, n).bytes,
+                    std::max(sliced_ws_layout(nullptr, n, 14).bytes, sliced_ws_layout(nullptr, n, 15).bytes));
 }
 
 namespace {
@@ -4323,15 +4491,17 @@ bool sl_auto(const TableView& tv, int64_t n) {
     return (int64_t)tv.drange >= min_range && 4 * n >= (int64_t)tv.drange;
 }
 
-hipError_t launch_probe_sliced(int key_bytes, const TableView& tv, const void* keys, const uint8_t* valid,
+template <int TL>
+hipError_t launch_probe_sliced_tl(int key_bytes, const TableView& tv, const void* keys, const uint8_t* valid,
                                int64_t voff, const uint32_t* probe_ids, uint32_t pbase, int64_t n, uint64_t* out_b,
                                uint32_t* out_p, int64_t cap, int64_t* d_total, void* workspace, hipEvent_t built,
                                hipStream_t s) {
     const bool hashed = tv.dense == nullptr;
-    const int64_t nt = (n + kSlTile - 1) / kSlTile;
+    constexpr int64_t kTile = SlT<TL>::kRows;
+    const int64_t nt = (n + kTile - 1) / kTile;
     const uint32_t nsl_all = sl_slices(tv), wlog = sl_wlog();
     const uint32_t npass = sl_passes(nsl_all);
-    SlicedWs w = sliced_ws_layout((void*)(((uintptr_t)workspace + 255) & ~(uintptr_t)255), n);
+    SlicedWs w = sliced_ws_layout((void*)(((uintptr_t)workspace + 255) & ~(uintptr_t)255), n, TL);
     const bool vec = (reinterpret_cast<uintptr_t>(keys) & 15) == 0;
     hipError_t e = hipSuccess;
     // workspace [0, 16): header with the caller's error word, zeroed by S1 (the layout
@@ -4355,9 +4525,9 @@ hipError_t launch_probe_sliced(int key_bytes, const TableView& tv, const void* k
     // dense lookup window: 2048 positions (32 per lane) or DFP_HJ_SL_DENSE_WIN=1024
     // (measured equal on C2 and C3, r04)
     static const bool dense_w1024 = sl_env_int("DFP_HJ_SL_DENSE_WIN", kSlOwnWin) == 1024;
-    const void* lk = hashed        ? (const void*)sl_lookup_kernel<true, kSlOwnWinHashed>
-                     : dense_w1024 ? (const void*)sl_lookup_kernel<false, 1024>
-                                   : (const void*)sl_lookup_kernel<false, kSlOwnWin>;
+    const void* lk = hashed        ? (const void*)sl_lookup_kernel<true, kSlOwnWinHashed, TL>
+                     : dense_w1024 ? (const void*)sl_lookup_kernel<false, 1024, TL>
+                                   : (const void*)sl_lookup_kernel<false, kSlOwnWin, TL>;
     e = hipFuncSetAttribute(lk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)tab_lds);
     if (e != hipSuccess) return e;
     // (slice, tile range) work items: about 768 of them, so that the resident workgroups
@@ -4372,7 +4542,19 @@ hipError_t launch_probe_sliced(int key_bytes, const TableView& tv, const void* k
         const uint32_t s0 = pass * (uint32_t)kSlMaxSlices;
         const uint32_t nsl = std::min<uint32_t>(nsl_all - s0, (uint32_t)kSlMaxSlices);
         unsigned long long* h = pass == 0 ? hdr : nullptr;  // a later pass appends to the tiles' entries
-        if (hashed) {
+        if (hashed && TL == 15) {
+            const unsigned pgrid = (unsigned)std::min<int64_t>(nt, sl_num_cus());
+#define DFP_HSP(KT, HV)                                                                                             \
+    hs_partition32_kernel<KT, HV><<<pgrid, kSlThreads, 0, s>>>(tv.nb, kHsSliceLog, s0, nsl, keys, valid, voff, n, nt, \
+                                                              vec, (unsigned long long*)w.ko, w.rl, w.toff, h, w.tcnt,   \
+                                                              w.tent)
+            if (key_bytes == 8) {
+                if (valid) DFP_HSP(int64_t, true); else DFP_HSP(int64_t, false);
+            } else {
+                if (valid) DFP_HSP(int32_t, true); else DFP_HSP(int32_t, false);
+            }
+#undef DFP_HSP
+        } else if (hashed) {
             const unsigned pgrid = (unsigned)std::min<int64_t>(nt, sl_num_cus());
 #define DFP_HSP(KT, HV)                                                                                           \
     hs_partition_kernel<KT, HV><<<pgrid, kSlThreads, 0, s>>>(tv.nb, kHsSliceLog, s0, nsl, keys, valid, voff, n, nt, \
@@ -4390,7 +4572,7 @@ hipError_t launch_probe_sliced(int key_bytes, const TableView& tv, const void* k
             const int64_t dmin_p = (int64_t)((uint64_t)tv.dmin + lo);
             const uint64_t drange_p = std::min<uint64_t>(tv.drange - lo, (uint64_t)nsl << wlog);
 #define DFP_SLP(KT, HV)                                                                                      \
-    sl_partition_kernel<KT, HV><<<(unsigned)nt, kSlThreads, 0, s>>>(dmin_p, drange_p, wlog, nsl, keys, valid, voff, n, \
+    sl_partition_kernel<KT, HV, TL><<<(unsigned)nt, kSlThreads, 0, s>>>(dmin_p, drange_p, wlog, nsl, keys, valid, voff, n, \
                                                                    vec, (uint16_t*)w.ko, w.rl, w.toff, sl_nt, 0, 0,   \
                                                                    nullptr, h, w.tcnt, w.tent, w.wcnt, SpecGeo{})
             if (key_bytes == 8) {
@@ -4405,7 +4587,7 @@ hipError_t launch_probe_sliced(int key_bytes, const TableView& tv, const void* k
         // at least ~1536 tiles per part: a smaller probe (a rank's share on N GPUs) loads each
         // slice image fewer times (profiles/r05_lookup_items_small.txt: 1.25*10^7 rows over C2's
         // table, one part per slice 24.4 us against 37.1 us at C2's three; C2 keeps three)
-        parts = std::max<uint32_t>(1, std::min<uint32_t>(parts, (uint32_t)(nt / kSlMinTilesPerPart)));
+        parts = std::max<uint32_t>(1, std::min<uint32_t>(parts, (uint32_t)(nt / ((kSlMinTilesPerPart << kSlTileLog) >> TL))));
         // the last round of small items: the slices beyond whole rounds of `parts` items
         // over the CUs split so that they fill about one round (DFP_HJ_SL_TAIL=0: even split)
         uint32_t s1 = nsl, parts2 = parts;
@@ -4442,13 +4624,13 @@ hipError_t launch_probe_sliced(int key_bytes, const TableView& tv, const void* k
             tp.drange = std::min<uint64_t>(tv.drange - lo, (uint64_t)nsl << wlog);
         }
         if (hashed)
-            sl_lookup_kernel<true, kSlOwnWinHashed><<<lgrid, kSlThreads, tab_lds, s>>>(
+            sl_lookup_kernel<true, kSlOwnWinHashed, TL><<<lgrid, kSlThreads, tab_lds, s>>>(
                 tp, wlog, nsl, nt, parts, s1, parts2, early, w.ko, w.res, w.toff, w.tcnt, s0);
         else if (dense_w1024)
-            sl_lookup_kernel<false, 1024><<<lgrid, kSlThreads, tab_lds, s>>>(tp, wlog, nsl, nt, parts, s1, parts2, early,
+            sl_lookup_kernel<false, 1024, TL><<<lgrid, kSlThreads, tab_lds, s>>>(tp, wlog, nsl, nt, parts, s1, parts2, early,
                                                                            w.ko, w.res, w.toff, w.tcnt, 0u);
         else
-            sl_lookup_kernel<false, kSlOwnWin><<<lgrid, kSlThreads, tab_lds, s>>>(tp, wlog, nsl, nt, parts, s1, parts2,
+            sl_lookup_kernel<false, kSlOwnWin, TL><<<lgrid, kSlThreads, tab_lds, s>>>(tp, wlog, nsl, nt, parts, s1, parts2,
                                                                                 early, w.ko, w.res, w.toff, w.tcnt, 0u);
     }
     const bool ri = tv.row_ids != nullptr, pi = probe_ids != nullptr;
@@ -4462,9 +4644,11 @@ hipError_t launch_probe_sliced(int key_bytes, const TableView& tv, const void* k
         const char* e = getenv("DFP_HJ_COUNT_FREE");
         return !(e != nullptr && e[0] == '0');
     }();
-    const unsigned egrid = (unsigned)std::min<int64_t>(nt, (int64_t)sl_emit_wgs_per_cu() * sl_num_cus());
+    // (2^15-row tiles: one 1024-thread workgroup per CU holds the 128 KB image; half the grid)
+    const int ewgs = TL == kSlTileLog ? sl_emit_wgs_per_cu() : std::max(1, sl_emit_wgs_per_cu() >> (TL - kSlTileLog));
+    const unsigned egrid = (unsigned)std::min<int64_t>(nt, (int64_t)ewgs * sl_num_cus());
 #define DFP_SLE(RI, PI)                                                                                           \
-    sl_emit_kernel<RI, PI><<<egrid, kSlEmitThreads, 0, s>>>(tv, w.tent, w.rl, w.res, probe_ids, pbase, w.tcnt, nt,   \
+    sl_emit_kernel<RI, PI, TL><<<egrid, SlT<TL>::kEmitThreads, 0, s>>>(tv, w.tent, w.rl, w.res, probe_ids, pbase, w.tcnt, nt,   \
                                                            out_b, out_p, cap, d_total,                      \
                                                            hashed || !count_free ? nullptr : w.wcnt,          \
                                                            emit_dyn ? w.tcnt + nt : nullptr)
@@ -4475,7 +4659,43 @@ hipError_t launch_probe_sliced(int key_bytes, const TableView& tv, const void* k
 #undef DFP_SLE
     return hipGetLastError();
 }
+// probe tiles (hj_set_probe_tile_log / DFP_HJ_SL_TILE_LOG): 0 auto = 2^14 rows for a
+// direct-addressed table, 2^15 for a hashed one (r05, profiles/r05_tile_log_ab.txt: C2h's
+// lookup walks half the (tile, slice) fragments, 687 -> 588 us, bench 61.4-62.2K ->
+// 65.7-65.8K Mrows/s; C2's partition in one 1024-thread workgroup per CU instead of two
+// loses more than its lookup gains, 214 -> 250 us against 117 -> 102 us)
+std::atomic<int> g_tile_log{-1};
+int sl_tile_log_setting() {
+    int v = g_tile_log.load(std::memory_order_relaxed);
+    if (v < 0) {
+        const char* e = getenv("DFP_HJ_SL_TILE_LOG");
+        const int x = e ? atoi(e) : 0;
+        v = x == 14 || x == 15 ? x : 0;
+        g_tile_log.store(v, std::memory_order_relaxed);
+    }
+    return v;
+}
+int sl_tile_log(bool hashed) {
+    const int v = sl_tile_log_setting();
+    return v ? v : hashed ? 15 : 14;
+}
+hipError_t launch_probe_sliced(int key_bytes, const TableView& tv, const void* keys, const uint8_t* valid,
+                               int64_t voff, const uint32_t* probe_ids, uint32_t pbase, int64_t n, uint64_t* out_b,
+                               uint32_t* out_p, int64_t cap, int64_t* d_total, void* workspace, hipEvent_t built,
+                               hipStream_t s) {
+    if (sl_tile_log(tv.dense == nullptr) == 15)
+        return launch_probe_sliced_tl<15>(key_bytes, tv, keys, valid, voff, probe_ids, pbase, n, out_b, out_p, cap,
+                                          d_total, workspace, built, s);
+    return launch_probe_sliced_tl<14>(key_bytes, tv, keys, valid, voff, probe_ids, pbase, n, out_b, out_p, cap, d_total,
+                                      workspace, built, s);
+}
 }  // namespace
+
+int set_probe_tile_log(int tl) {
+    const int old = sl_tile_log_setting();
+    g_tile_log.store(tl, std::memory_order_relaxed);
+    return old;
+}
 
 hipError_t launch_probe(int key_bytes, const TableView& tv, const void* keys, const uint8_t* valid, int64_t voff,
                         const uint32_t* probe_ids, uint32_t pbase, int64_t n, uint64_t* out_b, uint32_t* out_p, int64_t cap,

@@ -85,6 +85,8 @@ hipError_t launch_key_minmax_one(int key_bytes, const Segment* h_segs, Segment* 
 // 0 auto, 3 fused, 4 sliced
 void set_probe_mode(int mode);
 int get_probe_mode();
+// probe tile log of the sliced probe: 0 auto (14 dense, 15 hashed), 14 or 15; returns the previous setting
+int set_probe_tile_log(int tl);
 int64_t probe_tiles(int64_t n);
 int64_t probe_workspace(int64_t n);
 // workspace: [0,8) unused, [8,16) error word, then tile counts/offsets, then per-row refs

@@ -292,6 +292,14 @@ hj_status hj_probe_async_base(const hj_table* t, const void* keys, const uint8_t
  * and removed). Also settable with DFP_HJ_PROBE_MODE=fused|sliced. */
 int hj_set_probe_mode(int mode);
 
+/* Probe tiles of the sliced probe for later probes of this process: 0 auto (2^14 rows for
+ * a direct-addressed table, 2^15 for a hashed one), 14 or 15 (rows per tile = 2^tile_log).
+ * A longer tile halves the (tile, slice) fragments the lookups walk; results are identical.
+ * Returns the previous setting, -1 for a bad value. Also settable with
+ * DFP_HJ_SL_TILE_LOG=14|15. The tiles are the probe's own work units (no reference
+ * counterpart: the reference probes each RecordBatch row by row, lookup_implementation_3.rs). */
+int hj_set_probe_tile_log(int tile_log);
+
 /* Table layout for later builds of this process: 0 auto (a direct-addressed table - one
  * u32 ref per key value - when the build keys' range is at most 8x the build rows, the
  * "perfect hash" of dense integer keys; else 5-slot hashed buckets), 1 hashed buckets

@@ -112,6 +112,20 @@ def test_probe_mode_switch(dfp):
     assert L.hj_set_probe_mode(old) == 4
 
 
+def test_probe_tile_log_switch(dfp):
+    """hj_set_probe_tile_log: 0 auto (2^14-row tiles dense, 2^15 hashed), 14, 15; bad -> -1.
+    No device work."""
+    from datafusion_parallelism_amd import _lib
+
+    L = _lib.load()
+    for bad in (13, 16, -1, 1):
+        assert L.hj_set_probe_tile_log(bad) == -1
+    old = L.hj_set_probe_tile_log(15)
+    assert L.hj_set_probe_tile_log(14) == 15
+    assert L.hj_set_probe_tile_log(0) == 14
+    assert L.hj_set_probe_tile_log(old) == 0
+
+
 def test_join_type_names():
     """DataFusion JoinType names (probe_lookup_implementation.rs:32-43), host logic only."""
     from datafusion_parallelism_amd.operator import JoinType

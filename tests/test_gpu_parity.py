@@ -16,20 +16,25 @@ I64_MIN = np.iinfo(np.int64).min
 # (probe mode, table layout): hj_set_probe_mode 3 fused / 4 sliced; hj_set_build_mode 0
 # auto (direct-addressed for dense key ranges, built from the tile-local partition) /
 # 1 hashed / 2 auto with the histogram partition
-MODES = {"fused": (3, 0), "fused-hashed": (3, 1), "sliced": (4, 0), "sliced-hashed": (4, 1),
-         "sliced-histbuild": (4, 2)}
+# The sliced probe's tiles: 0 auto (2^14 rows dense, 2^15 hashed; hj_set_probe_tile_log),
+# "-t15" / "-t14" force the other size for the layout
+MODES = {"fused": (3, 0, 0), "fused-hashed": (3, 1, 0), "sliced": (4, 0, 0), "sliced-hashed": (4, 1, 0),
+         "sliced-histbuild": (4, 2, 0), "sliced-t15": (4, 0, 15), "sliced-hashed-t14": (4, 1, 14)}
 
 
 @pytest.fixture(params=list(MODES))
 def probe_mode(request, dfp):
-    """Run a test under every probe strategy and table layout (identical results required)."""
+    """Run a test under every probe strategy, table layout and probe tile size (identical
+    results required)."""
     L = dfp.load()
-    pm, bm = MODES[request.param]
+    pm, bm, tl = MODES[request.param]
     old_p = L.hj_set_probe_mode(pm)
     old_b = L.hj_set_build_mode(bm)
+    old_t = L.hj_set_probe_tile_log(tl)
     yield request.param
     L.hj_set_probe_mode(old_p)
     L.hj_set_build_mode(old_b)
+    L.hj_set_probe_tile_log(old_t)
 
 
 def gpu_join(dfp, bkeys, pkeys, bvalid=None, pvalid=None, key_type="int64", device_input=True, parts=None):
@@ -585,14 +590,17 @@ def _dense_build_levels(dfp, oracle_mod, nb, krange):
 
 # ---- sliced probe (LDS lookups, hj_set_probe_mode 4) --------------------------------
 
-@pytest.fixture
-def sliced_mode(dfp):
+@pytest.fixture(params=[14, 15], ids=["t14", "t15"])
+def sliced_mode(dfp, request):
+    """The sliced probe with 2^14- and 2^15-row probe tiles (hj_set_probe_tile_log)."""
     L = dfp.load()
     old_p = L.hj_set_probe_mode(4)
     old_b = L.hj_set_build_mode(0)
+    old_t = L.hj_set_probe_tile_log(request.param)
     yield
     L.hj_set_probe_mode(old_p)
     L.hj_set_build_mode(old_b)
+    L.hj_set_probe_tile_log(old_t)
 
 
 @pytest.mark.parametrize("nb,krange,np_,null_frac,key_type", [
