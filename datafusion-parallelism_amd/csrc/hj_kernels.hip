@@ -3134,6 +3134,10 @@ hs_partition32_kernel(uint32_t nb, uint32_t slog, uint32_t s0, uint32_t nslices,
     }
 }
 
+// Measured (r05) and not kept: the 2^15-row form with the sorted positions packed two per
+// register (u16 halves) instead of in LDS and the keys staged in two halves of 2^14
+// positions (so that the next tile's loads overlap more of the write-out): 62-72 VGPRs
+// spilled at the 128-register budget.
 // Measured (r05) and not kept: this partition in two workgroups per CU (one tile each, the
 // sorted keys staged in two 64 KB halves): its 16 (1024 threads) or 32 (512 threads) stored
 // keys per thread plus their ranks need more than the 64 / 128 VGPRs that two workgroups per
