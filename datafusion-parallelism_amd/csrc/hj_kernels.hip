@@ -3171,6 +3171,9 @@ constexpr int kSlWaveRows = kSlTile / (kSlEmitThreads / 64);  // 2048
 static_assert(kSlEmitThreads / 64 == kSlRanges && kSlWaveRows == kSlRangeRows,
               "emission waves and the partition's entry-count ranges must coincide");
 
+#ifndef DFP_EMIT_RESET
+#define DFP_EMIT_RESET 1
+#endif
 template <bool HAS_ROW_IDS, bool HAS_PROBE_IDS, int TL = kSlTileLog>
 // 16 waves per CU (two 512-thread workgroups, or one of 1024 for 2^15-row tiles): <= 128 VGPRs
 __global__ void __launch_bounds__(SlT<TL>::kEmitThreads, 4)
@@ -3245,15 +3248,23 @@ sl_emit_kernel(TableView tv, const uint32_t* __restrict__ tent, const uint16_t* 
         __syncthreads();
     }
     DFP_DBG_TS(g_dbg_em_ts, 1, wall_clock64());
+    // The image is cleared once; the write pass puts kMiss back into every row it reads, so
+    // no clear and no barrier for it stand between a tile and the next one's scatter
+    // (DFP_EMIT_RESET=0: the image cleared before every tile)
+    const bool reset_rows = DFP_EMIT_RESET && !DFP_ABL(1);
+    auto clear_image = [&]() {
+        for (int i = threadIdx.x * 4; i < SlT<TL>::kRows; i += SlT<TL>::kEmitThreads * 4)
+            *reinterpret_cast<uint4*>(s_ref + i) = make_uint4(kMiss, kMiss, kMiss, kMiss);
+        __syncthreads();
+    };
+    if (reset_rows) clear_image();
     while (tile < ntiles) {
         // dyn: draw the tile after the next one now; its value is needed only at the end
         // of this tile, so the atomic's round trip hides behind the tile's work
         unsigned long long draw = 0;
         if (dyn != nullptr && threadIdx.x == 0 && next < ntiles) draw = atomicAdd(dyn, 1ull);
         const int64_t tile0 = tile * SlT<TL>::kRows;
-        for (int i = threadIdx.x * 4; i < SlT<TL>::kRows; i += SlT<TL>::kEmitThreads * 4)
-            *reinterpret_cast<uint4*>(s_ref + i) = make_uint4(kMiss, kMiss, kMiss, kMiss);
-        __syncthreads();
+        if (!reset_rows) clear_image();
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const uint32_t i = (u * SlT<TL>::kEmitThreads + threadIdx.x) * 4;
@@ -3299,6 +3310,7 @@ sl_emit_kernel(TableView tv, const uint32_t* __restrict__ tent, const uint16_t* 
                 for (int k = 0; k < kSlWaveRows; k += 64) {
                     const int loc = row_w + k + lane;
                     const uint32_t r = s_ref[loc];
+                    if (reset_rows) s_ref[loc] = kMiss;
                     const unsigned long long hit = __ballot(r != kMiss);
                     if (r != kMiss) {
                         const uint32_t below = __builtin_amdgcn_mbcnt_hi(
@@ -3322,6 +3334,7 @@ sl_emit_kernel(TableView tv, const uint32_t* __restrict__ tent, const uint16_t* 
             for (int k = 0; !fast && k < kSlWaveRows; k += 64) {
                 const int loc = row_w + k + lane;
                 const uint32_t r = s_ref[loc];
+                if (reset_rows) s_ref[loc] = kMiss;
                 const uint32_t c = sl_count(tv, r);
                 const int64_t row = tile0 + loc;
                 uint32_t total;

@@ -21,7 +21,8 @@ import sys
 
 PROBE_KERNELS = ("probe_fused_kernel", "probe_lookup_kernel", "probe_emit_kernel", "scan_reduce_kernel<unsigned long long>",
                  "scan_down_kernel<unsigned long long>", "pp_partition_kernel", "pp_lookup_kernel",
-                 "pp_count_kernel", "sl_partition_kernel", "hs_partition_kernel", "sl_toff_transpose_kernel", "sl_lookup_kernel",
+                 "pp_count_kernel", "sl_partition_kernel", "hs_partition_kernel", "hs_partition32_kernel", "sl_toff_transpose_kernel",
+                 "sl_lookup_kernel",
                  "sl_count_kernel", "sl_emit_kernel")
 BUILD_KERNELS = ("key_minmax_kernel", "key_minmax_part_kernel", "minmax_final_kernel", "coarse_hist_kernel", "coarse_scatter", "fine_hist_kernel",
                  "fine_scatter", "chunk_starts_kernel", "scan_reduce_kernel<unsigned int>",
@@ -37,7 +38,8 @@ BUILD_KERNELS = ("key_minmax_kernel", "key_minmax_part_kernel", "minmax_final_ke
 # partitions once the speculative build launched a (no-op) dense frag build ahead of them
 # (round-4 verdict, "What's weak" 3).
 SHARED = ("sl_partition_kernel", "sl_toff_transpose_kernel", "hs_partition_kernel")
-PROBE_ONLY = ("sl_lookup_kernel", "sl_emit_kernel", "sl_count_kernel", "probe_fused_kernel", "probe_lookup_kernel",
+PROBE_ONLY = ("sl_lookup_kernel", "sl_emit_kernel", "sl_count_kernel", "hs_partition32_kernel", "probe_fused_kernel",
+              "probe_lookup_kernel",
               "probe_emit_kernel", "pp_")
 
 
