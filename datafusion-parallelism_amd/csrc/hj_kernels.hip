@@ -1326,6 +1326,13 @@ constexpr int kSlHistBins = 4096;                       // per-tile slice histog
 constexpr int kSlMaxSlices = kSlHistBins - 1;           // slices per pass: key ranges up to ~2^27 values
 constexpr int kSlOwnWin = 2048;        // flattened segment positions per owner window (32 per lane)
 constexpr int kSlOwnWinHashed = 1024;  // hashed slices: 16 per lane (u64 entries)
+#ifndef DFP_HS_W15
+#define DFP_HS_W15 1152
+#endif
+// hashed slices with 2^15-row tiles: a 64-tile block holds ~1075 positions at C2h (16.8 per
+// fragment), so 1152-position windows take most blocks in one window (r05: C2h lookup 597 ->
+// 566 us, bench 65.5-66.1K -> 66.1-66.5K Mrows/s against 1024, profiles/r05_hs_window_ab.txt)
+template <int TL> constexpr int hs_own_win() { return TL == 15 ? DFP_HS_W15 : kSlOwnWinHashed; }
 // the emission's waves own 2048-row ranges of a tile: the partition counts each range's
 // entries (wcnt) so that a tile whose entries all hit one unique row each (no correction
 // flag from the lookup) needs no count pass in the emission
@@ -1359,6 +1366,27 @@ __device__ __forceinline__ void hist_excl_scan(uint32_t* s_hist, uint32_t* s_w, 
 #ifndef DFP_SL_PD
 #define DFP_SL_PD 3
 #endif
+// hist_excl_scan without the per-wave loop over the wave totals (lane w < 16 holds wave w's
+// total; a DPP scan and two readlanes): the persistent 2^15-row partition, whose unrolled
+// loop there spilled
+__device__ __forceinline__ void hist_excl_scan_lanes(uint32_t* s_hist, uint32_t* s_w, uint32_t* tot) {
+    static_assert(kSlThreads / 64 <= 64, "wave totals in one wave's lanes");
+    const uint32_t b0 = threadIdx.x * 4;
+    const uint4 h = *reinterpret_cast<const uint4*>(s_hist + b0);
+    const uint32_t v = h.x + h.y + h.z + h.w;
+    const uint32_t incl = wave_incl_scan_dpp(v);
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    if (lane == 63) s_w[wave] = incl;
+    __syncthreads();
+    const uint32_t wt = wave_incl_scan_dpp(lane < kSlThreads / 64 ? s_w[lane] : 0u);
+    const uint32_t off = wave > 0 ? (uint32_t)__builtin_amdgcn_readlane((int)wt, wave - 1) : 0u;
+    *tot = (uint32_t)__builtin_amdgcn_readlane((int)wt, kSlThreads / 64 - 1);
+    const uint32_t ex = off + incl - v;
+    *reinterpret_cast<uint4*>(s_hist + b0) = make_uint4(ex, ex + h.x, ex + h.x + h.y, ex + h.x + h.y + h.z);
+    __syncthreads();
+}
+
 template <typename K, bool HAS_VALID, int TL = kSlTileLog>
 // 2^14-row tiles: 8 waves per SIMD = two workgroups per CU, <= 64 VGPRs; 2^15: one (128 KB of LDS)
 __global__ void __launch_bounds__(kSlThreads, TL == 14 ? 8 : 4)
@@ -3044,7 +3072,9 @@ hs_partition32_kernel(uint32_t nb, uint32_t slog, uint32_t s0, uint32_t nslices,
         for (uint32_t b = tx; b < kSlHistBins; b += kSlThreads) s_hist[b] = 0;
         const uint32_t ebase = later ? tent[tile] : 0u;
         __syncthreads();
-        // ranks in slice: rows loc0 .. loc0 + 3 of group g are four adjacent u16 (one 8-byte LDS access)
+        // ranks in slice: rows loc0 .. loc0 + 3 of group g are four adjacent u16 (one 8-byte LDS
+        // access). One group at a time (a scheduling barrier after each): interleaving the 32
+        // rows' key hashes for ILP spills
 #pragma unroll
         for (int g = 0; g < T::kGroups; ++g) {
             const int loc0 = g * (kSlThreads * 4) + tx * 4;
@@ -3059,10 +3089,13 @@ hs_partition32_kernel(uint32_t nb, uint32_t slog, uint32_t s0, uint32_t nslices,
                 r[q] = ok ? atomicAdd(&s_hist[sl], 1u) : kNone;
             }
             *reinterpret_cast<uint2*>(s_pos + loc0) = make_uint2(r[0] | (r[1] << 16), r[2] | (r[3] << 16));
+            __builtin_amdgcn_sched_barrier(0);
         }
         __syncthreads();
+        asm volatile("" : "+v"(tx));  // (again: the offsets of the phases below are recomputed, not kept live)
         uint32_t tot;
-        hist_excl_scan(s_hist, s_w, &tot);
+        hist_excl_scan_lanes(s_hist, s_w, &tot);
+        asm volatile("" : "+v"(tx));
         uint16_t* to = toff + tile * (int64_t)nbins;
         for (uint32_t b = tx; b < nbins; b += kSlThreads) to[b] = (uint16_t)(ebase + s_hist[b]);
         if (tx == 0) {
@@ -3085,6 +3118,7 @@ hs_partition32_kernel(uint32_t nb, uint32_t slog, uint32_t s0, uint32_t nslices,
         // staged, so that the next tile's loads follow every use of k)
 #pragma unroll
         for (int h = 0; h < 4; ++h) {
+            asm volatile("" : "+v"(tx));
             const uint32_t p0 = h * kQ;
             const uint32_t p1 = min<uint32_t>(tot, p0 + kQ);
 #pragma unroll
@@ -4542,7 +4576,7 @@ hipError_t launch_probe_sliced_tl(int key_bytes, const TableView& tv, const void
     // dense lookup window: 2048 positions (32 per lane) or DFP_HJ_SL_DENSE_WIN=1024
     // (measured equal on C2 and C3, r04)
     static const bool dense_w1024 = sl_env_int("DFP_HJ_SL_DENSE_WIN", kSlOwnWin) == 1024;
-    const void* lk = hashed        ? (const void*)sl_lookup_kernel<true, kSlOwnWinHashed, TL>
+    const void* lk = hashed        ? (const void*)sl_lookup_kernel<true, hs_own_win<TL>(), TL>
                      : dense_w1024 ? (const void*)sl_lookup_kernel<false, 1024, TL>
                                    : (const void*)sl_lookup_kernel<false, kSlOwnWin, TL>;
     e = hipFuncSetAttribute(lk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)tab_lds);
@@ -4641,7 +4675,7 @@ hipError_t launch_probe_sliced_tl(int key_bytes, const TableView& tv, const void
             tp.drange = std::min<uint64_t>(tv.drange - lo, (uint64_t)nsl << wlog);
         }
         if (hashed)
-            sl_lookup_kernel<true, kSlOwnWinHashed, TL><<<lgrid, kSlThreads, tab_lds, s>>>(
+            sl_lookup_kernel<true, hs_own_win<TL>(), TL><<<lgrid, kSlThreads, tab_lds, s>>>(
                 tp, wlog, nsl, nt, parts, s1, parts2, early, w.ko, w.res, w.toff, w.tcnt, s0);
         else if (dense_w1024)
             sl_lookup_kernel<false, 1024, TL><<<lgrid, kSlThreads, tab_lds, s>>>(tp, wlog, nsl, nt, parts, s1, parts2, early,
