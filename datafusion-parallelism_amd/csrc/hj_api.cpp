@@ -578,7 +578,9 @@ hj_status build_attempt(hj_table* t, const std::vector<Segment>& segs, double lf
     // dense builds that fit the tile-local partition skip the histogram/scan/scatter path
     const bool frag = dense && total > 0 && frag_build_mode() && frag_build_ok(g, ftiles);
     // hashed tables: the frag build unless mode 2 keeps the histogram path (DFP_HJ_FRAG_BUILD=0)
-    const bool hfrag = !dense && total > 0 && build_mode_raw() != 2 && hashed_frag_ok(g, ftiles);
+    // (the hashed frag build's tiles are 2^hashed_build_tile_log() rows, the dense one's 2^14)
+    const int64_t hftiles = frag_build_tiles(seg_n.data(), (int)segs.size(), hashed_build_tile_log());
+    const bool hfrag = !dense && total > 0 && build_mode_raw() != 2 && hashed_frag_ok(g, hftiles);
     hipDeviceProp_t* prop0 = device_props(t->device);
     const int64_t ntiles = build_tiles(total, prop0 ? prop0->multiProcessorCount : 256);
     const int64_t tile_rows = build_tile_rows(total, ntiles);
@@ -612,9 +614,10 @@ hj_status build_attempt(hj_table* t, const std::vector<Segment>& segs, double lf
         uint64_t* ids32 = nullptr;
         BigSeg* fbig;
         const int64_t fbytes =
-            frag ? frag_build_scratch_bytes(g, ftiles, total) : hashed_frag_scratch_bytes(g, ftiles, total);
+            frag ? frag_build_scratch_bytes(g, ftiles, total) : hashed_frag_scratch_bytes(g, hftiles, total);
         if ((st = dev_alloc(t, t->scratch, &fscr, (size_t)fbytes)) != HJ_OK) return st;
-        if ((st = dev_alloc(t, t->scratch, &p, sizeof(uint32_t) * (size_t)ftiles)) != HJ_OK) return st;
+        if ((st = dev_alloc(t, t->scratch, &p, sizeof(uint32_t) * (size_t)(frag ? ftiles : hftiles))) != HJ_OK)
+            return st;
         d_tb = (uint32_t*)p;
         if ((st = dev_alloc(t, t->scratch, &p, sizeof(BigSeg) * (size_t)(total / (kSmallSeg + 1) + 2))) != HJ_OK)
             return st;
@@ -646,7 +649,7 @@ hj_status build_attempt(hj_table* t, const std::vector<Segment>& segs, double lf
             if (spec) t->spec_pending.store(true, std::memory_order_release);
             return HJ_OK;
         }
-        HIP_TRY(launch_build_hashed_frag(t->key_bytes, segs.data(), (int)segs.size(), g, ftiles, fscr, d_tb, ids32,
+        HIP_TRY(launch_build_hashed_frag(t->key_bytes, segs.data(), (int)segs.size(), g, hftiles, fscr, d_tb, ids32,
                                          t->tbl, t->dup_rows, fbig, ctr, d_segs, total, ids_as_rows, cus, s));
         // a chunk can overflow (adversarial keys): read the error word back, rebuild at half load
         BuildCounters hc;

@@ -1871,7 +1871,7 @@ dense_frag_build_kernel(ChunkGeom g, uint32_t nblk, int64_t ntiles, const uint16
 constexpr int kHbSliceLog = 10;  // buckets per build slice: 1024 x 64 B = 64 KB of LDS
 constexpr uint32_t kHbSideSlot = (1u << kHbSliceLog) * kSlots;  // the side bucket's slot in the image
 
-template <int T, int RR>
+template <int T, int RR, int TL = kSlTileLog>
 __global__ void __launch_bounds__(T)
 hashed_frag_build_kernel(uint32_t nb, uint32_t clog2, uint32_t s0, uint32_t nsl, int64_t ntiles,
                          const uint16_t* __restrict__ toffT, const unsigned long long* __restrict__ ko,
@@ -1923,7 +1923,7 @@ hashed_frag_build_kernel(uint32_t nb, uint32_t clog2, uint32_t s0, uint32_t nsl,
         const uint32_t ex = block_excl_scan<uint32_t>(len, reinterpret_cast<uint32_t*>(s_w), &tot) + s_carry;
         if (t < ntiles) {
             s_to[t] = ex;
-            s_pb[t] = (uint32_t)t * kSlTile + st - ex;
+            s_pb[t] = (uint32_t)t * SlT<TL>::kRows + st - ex;
         }
         __syncthreads();
         if (threadIdx.x == 0) s_carry += tot;
@@ -1942,7 +1942,7 @@ hashed_frag_build_kernel(uint32_t nb, uint32_t clog2, uint32_t s0, uint32_t nsl,
             if (s_to[mid] <= r) lo = mid; else hi = mid - 1;
         }
         const uint32_t pos = s_pb[lo] + r;
-        if (pos >= (uint64_t)ntiles * kSlTile) {  // internal check (never expected)
+        if (pos >= (uint64_t)ntiles * SlT<TL>::kRows) {  // internal check (never expected)
             atomicOr(&ctr->err, 8ull);
             *sk = 0;
             *row = 0;
@@ -3028,7 +3028,7 @@ hs_partition_kernel(uint32_t nb, uint32_t slog, uint32_t s0, uint32_t nslices, c
     }
 }
 
-// The same for 2^15-row tiles (probe only; DFP_HJ_SL_TILE_LOG=15). The tile's 32 stored
+// The same for 2^15-row tiles (a hashed table's probe, and the hashed frag build). The tile's 32 stored
 // keys per thread stay in registers; the ranks, then the sorted positions, live in LDS
 // (u16 per row: holding them in registers beside the keys spills), and the sorted keys
 // leave through a 64 KB staging area in four quarters of 2^13 positions. Once the last
@@ -3040,7 +3040,8 @@ hs_partition32_kernel(uint32_t nb, uint32_t slog, uint32_t s0, uint32_t nslices,
                       const uint8_t* __restrict__ valid, int64_t voff, int64_t n, int64_t ntiles, bool vec,
                       unsigned long long* __restrict__ ko, uint16_t* __restrict__ rl, uint16_t* __restrict__ toff,
                       unsigned long long* __restrict__ hdr, unsigned long long* __restrict__ tcnt,
-                      uint32_t* __restrict__ tent) {  // pass: slices [s0, s0 + nslices); hdr null = a later pass
+                      uint32_t* __restrict__ tent,  // probe pass: slices [s0, s0 + nslices); hdr null = a later pass
+                      int64_t tile_off, int64_t row_base, uint32_t* __restrict__ tile_base) {  // build: tcnt null
     using T = SlT<15>;
     constexpr int kQ = T::kRows / 4;      // positions per staging quarter
     constexpr uint16_t kNone = 0xFFFFu;   // no entry (positions and ranks are < 2^15)
@@ -3049,8 +3050,9 @@ hs_partition32_kernel(uint32_t nb, uint32_t slog, uint32_t s0, uint32_t nslices,
     __shared__ __attribute__((aligned(16))) uint32_t s_hist[kSlHistBins];
     __shared__ uint32_t s_w[kSlThreads / 64];
     const uint32_t nbins = nslices + 1;
-    const bool later = hdr == nullptr;
-    if (!later && blockIdx.x == 0 && threadIdx.x == 0) {
+    const bool probe = tcnt != nullptr;  // else the hashed frag build's partition of one build segment
+    const bool later = probe && hdr == nullptr;
+    if (probe && !later && blockIdx.x == 0 && threadIdx.x == 0) {
         hdr[0] = hdr[1] = 0;  // workspace header (error word)
         tcnt[ntiles] = 0;     // the emission's tile counter
     }
@@ -3069,6 +3071,7 @@ hs_partition32_kernel(uint32_t nb, uint32_t slog, uint32_t s0, uint32_t nslices,
         uint32_t tx = threadIdx.x;
         asm volatile("" : "+v"(tx));
         const int64_t tile0 = tile * T::kRows;
+        const int64_t gtile = tile + tile_off;  // its output region (the build partitions several segments)
         for (uint32_t b = tx; b < kSlHistBins; b += kSlThreads) s_hist[b] = 0;
         const uint32_t ebase = later ? tent[tile] : 0u;
         __syncthreads();
@@ -3096,12 +3099,13 @@ hs_partition32_kernel(uint32_t nb, uint32_t slog, uint32_t s0, uint32_t nslices,
         uint32_t tot;
         hist_excl_scan_lanes(s_hist, s_w, &tot);
         asm volatile("" : "+v"(tx));
-        uint16_t* to = toff + tile * (int64_t)nbins;
+        uint16_t* to = toff + gtile * (int64_t)nbins;
         for (uint32_t b = tx; b < nbins; b += kSlThreads) to[b] = (uint16_t)(ebase + s_hist[b]);
-        if (tx == 0) {
+        if (tx == 0 && probe) {
             tcnt[tile] = (later ? tcnt[tile] : 0ull) + tot;  // S2 corrects it to the tile's pair count
             tent[tile] = ebase + tot;
         }
+        if (tx == 0 && tile_base != nullptr) tile_base[gtile] = (uint32_t)(row_base + tile0);
         // ranks -> sorted positions (each thread rewrites only its own rows)
 #pragma unroll
         for (int g = 0; g < T::kGroups; ++g) {
@@ -3113,7 +3117,7 @@ hs_partition32_kernel(uint32_t nb, uint32_t slog, uint32_t s0, uint32_t nslices,
                 if (r[q] != kNone) r[q] += s_hist[slice_of((unsigned long long)k[g][q])];
             *reinterpret_cast<uint2*>(s_pos + loc0) = make_uint2(r[0] | (r[1] << 16), r[2] | (r[3] << 16));
         }
-        unsigned long long* dk = ko + tile * T::kRows + ebase;
+        unsigned long long* dk = ko + gtile * T::kRows + ebase;
         // stored keys in slice order, a quarter of the positions at a time (every quarter is
         // staged, so that the next tile's loads follow every use of k)
 #pragma unroll
@@ -3155,7 +3159,7 @@ hs_partition32_kernel(uint32_t nb, uint32_t slog, uint32_t s0, uint32_t nslices,
                 if (r[q] != kNone) s_row[r[q]] = (uint16_t)(loc0 + q);
         }
         __syncthreads();
-        uint16_t* dr = rl + tile * T::kRows + ebase;
+        uint16_t* dr = rl + gtile * T::kRows + ebase;
         if (ebase & 7) {  // a later pass at an unaligned base: 2-byte stores
             for (uint32_t i = tx; i < tot; i += kSlThreads) dr[i] = s_row[i];
         } else {
@@ -4122,10 +4126,20 @@ hipError_t launch_key_minmax(int key_bytes, const Segment* h_segs, Segment* d_se
     return hipGetLastError();
 }
 
-int64_t frag_build_tiles(const int64_t* seg_n, int nseg) {
+int64_t frag_build_tiles(const int64_t* seg_n, int nseg, int tl) {
+    const int64_t tile = (int64_t)1 << tl;
     int64_t t = 0;
-    for (int i = 0; i < nseg; ++i) t += (seg_n[i] + kSlTile - 1) / kSlTile;
+    for (int i = 0; i < nseg; ++i) t += (seg_n[i] + tile - 1) / tile;
     return t;
+}
+// the hashed frag build's tiles: 2^15 rows (half the (tile, slice) fragments each slice's
+// workgroup gathers), DFP_HJ_HB_TILE_LOG=14 for the probe's 2^14
+int hashed_build_tile_log() {
+    static const int v = [] {
+        const char* e = getenv("DFP_HJ_HB_TILE_LOG");
+        return e && atoi(e) == 14 ? 14 : 15;
+    }();
+    return v;
 }
 bool frag_build_ok(const ChunkGeom& g, int64_t ftiles) {
     return g.dense && dense_one_level(g.nchunks) && dense_blocks(g.nchunks) <= (uint32_t)kSlMaxSlices &&
@@ -4219,14 +4233,17 @@ bool hashed_frag_ok(const ChunkGeom& g, int64_t ftiles) {
 uint32_t hashed_frag_slices(const ChunkGeom& g) { return (g.nb + (1u << kHbSliceLog) - 1) >> kHbSliceLog; }
 int64_t hashed_frag_scratch_bytes(const ChunkGeom& g, int64_t ftiles, int64_t total) {
     const int64_t nbins = std::min<uint32_t>(hashed_frag_slices(g), (uint32_t)kSlMaxSlices) + 1;
+    const int64_t kSlTile = (int64_t)1 << hashed_build_tile_log();  // ftiles: of this size
     return 8 * ftiles * kSlTile + 2 * ftiles * kSlTile + 2 * ftiles * nbins + 2 * ((ftiles + 63) & ~(int64_t)63) * nbins +
            32 * total + 6 * 256;  // spill pool: 16 B per row (rows) + up to 16 B per row (directories)
 }
-hipError_t launch_build_hashed_frag(int key_bytes, const Segment* h_segs, int nseg, const ChunkGeom& g, int64_t ftiles,
+template <int TL>
+hipError_t launch_build_hashed_frag_tl(int key_bytes, const Segment* h_segs, int nseg, const ChunkGeom& g, int64_t ftiles,
                                     void* scratch, uint32_t* tile_base, const uint64_t* ids32, Bucket* tbl,
                                     uint32_t* dup_rows, BigSeg* big, BuildCounters* ctr, const Segment* d_segs,
                                     int64_t total, bool ids_as_rows, int cus, hipStream_t s) {
     constexpr int T = 512, RR = 8;
+    constexpr int64_t kSlTile = SlT<TL>::kRows;  // this build's tiles (ftiles of them)
     const uint32_t nsl_all = hashed_frag_slices(g);
     const int64_t nbins_max = std::min<uint32_t>(nsl_all, (uint32_t)kSlMaxSlices) + 1;
     auto a256 = [](uintptr_t x) { return (x + 255) & ~(uintptr_t)255; };
@@ -4243,7 +4260,7 @@ hipError_t launch_build_hashed_frag(int key_bytes, const Segment* h_segs, int ns
     const size_t budget = 80 * 1024 - 256;
     const uint32_t dupcap = img < budget ? (uint32_t)((budget - img) / 12) : 0u;
     const size_t lds = img + (size_t)dupcap * 12;
-    const void* kfn = (const void*)hashed_frag_build_kernel<T, RR>;
+    const void* kfn = (const void*)hashed_frag_build_kernel<T, RR, TL>;
     hipError_t e = hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
     // DFP_HJ_DEBUG_SYNC=1: synchronise after every launch and report the failing one (stderr)
@@ -4263,10 +4280,15 @@ hipError_t launch_build_hashed_frag(int key_bytes, const Segment* h_segs, int ns
             if (nt == 0) continue;
             const bool vec = (reinterpret_cast<uintptr_t>(sg.keys) & 15) == 0;
             const unsigned pgrid = (unsigned)std::min<int64_t>(nt, cus);
-#define DFP_HBP(KT, HV)                                                                                           \
-    hs_partition_kernel<KT, HV><<<pgrid, kSlThreads, 0, s>>>(g.nb, kHbSliceLog, s0, nsl, sg.keys, sg.valid, sg.voff,  \
-                                                            sg.n, nt, vec, ko, rl, toff, nullptr, nullptr, nullptr,  \
-                                                            t0, sg.row_base, tile_base)
+#define DFP_HBP(KT, HV)                                                                                             \
+    if (TL == 15)                                                                                                   \
+        hs_partition32_kernel<KT, HV><<<pgrid, kSlThreads, 0, s>>>(g.nb, kHbSliceLog, s0, nsl, sg.keys, sg.valid,     \
+                                                                  sg.voff, sg.n, nt, vec, ko, rl, toff, nullptr,     \
+                                                                  nullptr, nullptr, t0, sg.row_base, tile_base);     \
+    else                                                                                                            \
+        hs_partition_kernel<KT, HV><<<pgrid, kSlThreads, 0, s>>>(g.nb, kHbSliceLog, s0, nsl, sg.keys, sg.valid,       \
+                                                                sg.voff, sg.n, nt, vec, ko, rl, toff, nullptr, nullptr, \
+                                                                nullptr, t0, sg.row_base, tile_base)
             if (key_bytes == 8) {
                 if (sg.valid) DFP_HBP(int64_t, true); else DFP_HBP(int64_t, false);
             } else {
@@ -4279,7 +4301,7 @@ hipError_t launch_build_hashed_frag(int key_bytes, const Segment* h_segs, int ns
         sl_toff_transpose_kernel<<<(unsigned)((ftiles + 63) / 64 * ((nbins + kSlTrChunk - 1) / kSlTrChunk)), 256, 0,
                                    s>>>(toff, nbins, ftiles, toffT, SpecGeo{});
         if ((e = chk("toff transpose")) != hipSuccess) return e;
-        hashed_frag_build_kernel<T, RR><<<nsl, T, lds, s>>>(g.nb, g.clog2, s0, nsl, ftiles, toffT, ko, rl, tile_base,
+        hashed_frag_build_kernel<T, RR, TL><<<nsl, T, lds, s>>>(g.nb, g.clog2, s0, nsl, ftiles, toffT, ko, rl, tile_base,
                                                            ids_as_rows ? ids32 : nullptr, tbl, dup_rows, big, ctr,
                                                            spill, dupcap, (uint64_t)(2 * total + 2),
                                                            (uint64_t)(4 * total));
@@ -4287,6 +4309,17 @@ hipError_t launch_build_hashed_frag(int key_bytes, const Segment* h_segs, int ns
     }
     dup_sort_big_kernel<<<cus, kBigThreads, 0, s>>>(dup_rows, big, ctr, d_segs, nseg, total, key_bytes, ids_as_rows);
     return hipGetLastError();
+}
+
+hipError_t launch_build_hashed_frag(int key_bytes, const Segment* h_segs, int nseg, const ChunkGeom& g, int64_t ftiles,
+                                    void* scratch, uint32_t* tile_base, const uint64_t* ids32, Bucket* tbl,
+                                    uint32_t* dup_rows, BigSeg* big, BuildCounters* ctr, const Segment* d_segs,
+                                    int64_t total, bool ids_as_rows, int cus, hipStream_t s) {
+    return hashed_build_tile_log() == 15
+               ? launch_build_hashed_frag_tl<15>(key_bytes, h_segs, nseg, g, ftiles, scratch, tile_base, ids32, tbl,
+                                                 dup_rows, big, ctr, d_segs, total, ids_as_rows, cus, s)
+               : launch_build_hashed_frag_tl<14>(key_bytes, h_segs, nseg, g, ftiles, scratch, tile_base, ids32, tbl,
+                                                 dup_rows, big, ctr, d_segs, total, ids_as_rows, cus, s);
 }
 
 hipError_t launch_build(int key_bytes, const Segment* d_segs, int nseg, int64_t total, const ChunkGeom& g,
@@ -4598,7 +4631,7 @@ hipError_t launch_probe_sliced_tl(int key_bytes, const TableView& tv, const void
 #define DFP_HSP(KT, HV)                                                                                             \
     hs_partition32_kernel<KT, HV><<<pgrid, kSlThreads, 0, s>>>(tv.nb, kHsSliceLog, s0, nsl, keys, valid, voff, n, nt, \
                                                               vec, (unsigned long long*)w.ko, w.rl, w.toff, h, w.tcnt,   \
-                                                              w.tent)
+                                                              w.tent, 0, 0, nullptr)
             if (key_bytes == 8) {
                 if (valid) DFP_HSP(int64_t, true); else DFP_HSP(int64_t, false);
             } else {

@@ -42,7 +42,9 @@ hipError_t launch_build(int key_bytes, const Segment* d_segs, int nseg, int64_t 
 // (written by the partition); ids32: the
 // explicit ids in row order (ids_as_rows) or NULL
 constexpr int64_t kFragTileRows = 16384;  // = the sliced probe's tile
-int64_t frag_build_tiles(const int64_t* seg_n, int nseg);
+int64_t frag_build_tiles(const int64_t* seg_n, int nseg, int tile_log = 14);
+// tile log of the hashed frag build's tiles (15 by default, DFP_HJ_HB_TILE_LOG=14)
+int hashed_build_tile_log();
 bool frag_build_ok(const ChunkGeom& g, int64_t ftiles);
 int64_t frag_build_scratch_bytes(const ChunkGeom& g, int64_t ftiles, int64_t total);
 hipError_t launch_build_frag(int key_bytes, const Segment* h_segs, int nseg, const ChunkGeom& g, int64_t ftiles,
