@@ -678,6 +678,10 @@ hj_status run_radix(hj_comm* c, const RadixArgs& a, hj_dist_job* j, int64_t jobn
     // the probe of the probe keys with ids probe_base + row — no partition, no host read.
     if (W == 1 && a.bbase == 0 && a.pkt == a.kt && w1_identity() && !injected(c, jobno, 0)) {
         HIP_OK(hipStreamWaitEvent(sb, j->ev_in, 0));
+        // the build span on the build stream itself: the exchange stream (sd) runs nothing on
+        // this path, and its start event could complete after a small build finished on sb
+        // (build_ms < 0; test_radix_one_rank_paths, r05)
+        HIP_OK(hipEventRecord(j->ev_t[0], sb));
         if (a.pbase < 0 || a.pbase + a.np > ((int64_t)1 << 32))
             return set_error(HJ_ERR_INVALID, "hj_dist_join_radix: probe ids (probe_base + row) must fit 32 bits");
         hj_table* t = nullptr;
