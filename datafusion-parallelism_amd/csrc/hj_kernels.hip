@@ -2281,8 +2281,9 @@ constexpr int kLkGroup = DFP_LK_GROUP;  // dense lookup: rows per branch-free gr
 constexpr int kHsGroup1 = DFP_HS_G1;  // hashed lookup: rows per group of owner searches and entry loads
 constexpr int kHsGroup2 = DFP_HS_G2;  // hashed lookup: rows per group of bucket-line reads
 // a tile's pair count (tcnt) is < 2^45 (16384 rows x < 2^31 build rows); the dense lookup
-// adds kOddFlag once per fragment with an entry of a missing or duplicated key (at most
-// 4095 slices x 3 passes of a direct-addressed range: the flag bits never wrap to 0)
+// adds kOddFlag once per fragment with an entry of a missing or duplicated key, the hashed
+// lookup once per fragment with a duplicated key (at most 4095 slices per pass and < 64
+// passes: the 18 flag bits never wrap to 0)
 constexpr int kOddShift = 46;
 constexpr unsigned long long kOddFlag = 1ull << kOddShift;
 constexpr unsigned long long kCountMask = kOddFlag - 1;
@@ -2336,7 +2337,9 @@ sl_lookup_kernel(TableView tv, uint32_t wlog, uint32_t nslices, int64_t ntiles, 
                  const void* __restrict__ ko, uint32_t* __restrict__ res, const uint16_t* __restrict__ toff,
                  unsigned long long* __restrict__ tcnt, uint32_t soff) {  // soff: first slice of this pass (hashed)
     extern __shared__ __attribute__((aligned(16))) uint32_t s_tab[];  // dense: 2^wlog refs; hashed: 2048 buckets
-    __shared__ uint8_t s_odd[HASHED ? 1 : kSlThreads];  // dense, per wave by rank: the fragment holds an entry of count != 1
+    // per wave by rank: the fragment holds an entry of count != 1 (dense: a missing or
+    // duplicated key; hashed: a duplicated key, misses being the common case there)
+    __shared__ uint8_t s_odd[kSlThreads];
     __shared__ uint32_t s_base[kSlThreads];
     __shared__ uint32_t s_lane[kSlThreads];  // per wave: tile lane of each non-empty segment, by rank
     // per wave, by rank: dense, the correction running sum at each fragment's start;
@@ -2468,8 +2471,8 @@ sl_lookup_kernel(TableView tv, uint32_t wlog, uint32_t nslices, int64_t ntiles, 
         // Hashed (half the entries of a uniform probe side miss): the running sum of every
         // row, recorded at each fragment's last position instead.
         scst[lane] = 0;
-        uint8_t* sodd = s_odd + (HASHED ? 0 : wave * 64);
-        if constexpr (!HASHED) sodd[lane] = 0;
+        uint8_t* sodd = s_odd + wave * 64;
+        sodd[lane] = 0;
         uint32_t corr_run = 0;
         // the 64 tiles' regions as buffers (wave-uniform bases): 32-bit offsets, and an
         // out-of-range offset turns a position past R into a dropped access
@@ -2654,6 +2657,7 @@ sl_lookup_kernel(TableView tv, uint32_t wlog, uint32_t nslices, int64_t ntiles, 
                     asm volatile("" : "+v"(c));
                 }
                 __builtin_amdgcn_raw_buffer_store_b32(v, rres, (int)(o * 4), 0, 0);
+                if (c > 1u) sodd[off[u] >> 26] = 1;  // kOob: c = 1 (the emission's 0/1 path is off for its tile)
                 uint32_t d = c - 1u;  // kOob: c = 1
                 if (d != 0xFFFFFFFFu && d >= kBigCorr) {
                     atomicAdd(&tcnt[tc + slane[off[u] >> 26]], (unsigned long long)d);
@@ -2684,6 +2688,7 @@ sl_lookup_kernel(TableView tv, uint32_t wlog, uint32_t nslices, int64_t ntiles, 
                     }
                     if (ref != kMiss) {
                         if (c == kCountUnknown) c = tv.dup_rows[ref & tv.off_mask];
+                        if (c > 1u) sodd[ofs >> 26] = 1;
                         __builtin_amdgcn_raw_buffer_store_b32(ref, rres, (int)((ofs & kOobMask) * 4), 0, 0);
                         atomicAdd(&tcnt[tc + slane[ofs >> 26]], (unsigned long long)c);
                     }
@@ -2884,10 +2889,10 @@ sl_lookup_kernel(TableView tv, uint32_t wlog, uint32_t nslices, int64_t ntiles, 
                 const uint32_t nxt = rank + 1 < nranks ? scst[rank + 1] : corr_run;
                 cr = (int)(nxt - scst[rank]);
             }
-            // dense: a fragment with a missing or duplicated key also turns off its tile's
-            // count-free emission (kOddFlag above the count bits, one atomic for both)
-            const unsigned long long add =
-                (unsigned long long)(long long)cr + (!HASHED && sodd[rank] ? kOddFlag : 0ull);
+            // a fragment with an entry of count != 1 (dense: missing or duplicated; hashed:
+            // duplicated) also turns off its tile's count-free (dense) or 0/1 (hashed)
+            // emission (kOddFlag above the count bits, one atomic for both)
+            const unsigned long long add = (unsigned long long)(long long)cr + (sodd[rank] ? kOddFlag : 0ull);
             if (add != 0) atomicAdd(&tcnt[tc + lane], add);
         }
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront", "local");  // LDS only: no wait for the ref stores
@@ -3220,7 +3225,9 @@ sl_emit_kernel(TableView tv, const uint32_t* __restrict__ tent, const uint16_t* 
                const unsigned long long* __restrict__ tcnt, int64_t ntiles, uint64_t* __restrict__ out_b,
                uint32_t* __restrict__ out_p, int64_t cap, int64_t* __restrict__ d_total,
                const uint16_t* __restrict__ wcnt,  // entries per 2048-row range (null: always count)
-               unsigned long long* __restrict__ dyn) {  // tile counter (zeroed by S1), null: static tiles
+               unsigned long long* __restrict__ dyn,  // tile counter (zeroed by S1), null: static tiles
+               bool flag01) {  // hashed: a tile without the lookup's flag has row counts 0 or 1
+    // (wcnt non-null: the dense count-free path; flag01: the hashed 0/1 path; at most one)
     __shared__ __attribute__((aligned(16))) uint32_t s_ref[SlT<TL>::kRows];  // the tile's refs, kMiss = none
     __shared__ unsigned long long s_w[SlT<TL>::kEmitThreads / 64];
     __shared__ unsigned long long s_pre[SlT<TL>::kEmitThreads / 64];
@@ -3256,10 +3263,8 @@ sl_emit_kernel(TableView tv, const uint32_t* __restrict__ tent, const uint16_t* 
     };
     auto fetch = [&](int64_t t) {
         cnt = DFP_ABL(2) ? 0u : tent[t];  // the tile's entries over every pass
-        if (wcnt != nullptr) {
-            nflag = (uint32_t)(tcnt[t] >> kOddShift);  // the lookup's flag: some entry's count != 1
-            nwc = wcnt[t * SlT<TL>::kRanges + wave];
-        }
+        if (wcnt != nullptr || flag01) nflag = (uint32_t)(tcnt[t] >> kOddShift);  // the lookup's flag: some count != 1
+        if (wcnt != nullptr) nwc = wcnt[t * SlT<TL>::kRanges + wave];
         const uint16_t* te = rl + t * SlT<TL>::kRows;
         const uint32_t* tr = res + t * SlT<TL>::kRows;
 #pragma unroll
@@ -3313,12 +3318,21 @@ sl_emit_kernel(TableView tv, const uint32_t* __restrict__ tent, const uint16_t* 
         }
         __syncthreads();
         const bool fast = wcnt != nullptr && nflag == 0;  // this tile's (read before the prefetch)
+        // hashed, no duplicated key in the tile: every row has 0 or 1 pairs (misses are the
+        // common case, so a wave's pairs are still counted, by its hits)
+        const bool b01 = flag01 && nflag == 0;
         const uint32_t fast_wc = nwc;
         if (next < ntiles) fetch(next);
         // pass 1: this wave's pair count (a count-free tile: its entries in the wave's range)
         const int row_w = wave * kSlWaveRows;
         if (fast) {
             if (lane == 0) s_w[wave] = fast_wc;
+        } else if (b01) {
+            uint32_t lsum = 0;  // <= 32
+#pragma unroll 8
+            for (int k = 0; k < kSlWaveRows; k += 64) lsum += s_ref[row_w + k + lane] != kMiss ? 1u : 0u;
+            const uint32_t wsum = wave_sum_dpp(lsum);
+            if (lane == 0) s_w[wave] = wsum;
         } else {
             uint32_t lsum = 0;  // < 32 rows x < 2^26 rows each
 #pragma unroll 8
@@ -3342,7 +3356,7 @@ sl_emit_kernel(TableView tv, const uint32_t* __restrict__ tent, const uint16_t* 
             // max-scan of start markers), so every store instruction writes one
             // contiguous run and the duplicate segments are read in parallel.
             uint32_t* own = s_own[wave];
-            if (fast) {
+            if (fast || b01) {
                 // count-free tile: one pair per hit row, the prefix a popcount of the hit mask
 #pragma unroll 4
                 for (int k = 0; k < kSlWaveRows; k += 64) {
@@ -3369,7 +3383,7 @@ sl_emit_kernel(TableView tv, const uint32_t* __restrict__ tent, const uint16_t* 
             // random line reads into dup_rows (30 MB, Infinity-Cache resident), not by one
             // round trip per window.
 #pragma unroll 2
-            for (int k = 0; !fast && k < kSlWaveRows; k += 64) {
+            for (int k = 0; !fast && !b01 && k < kSlWaveRows; k += 64) {
                 const int loc = row_w + k + lane;
                 const uint32_t r = s_ref[loc];
                 if (reset_rows) s_ref[loc] = kMiss;
@@ -4718,7 +4732,8 @@ hipError_t launch_probe_sliced_tl(int key_bytes, const TableView& tv, const void
                                                                                 early, w.ko, w.res, w.toff, w.tcnt, 0u);
     }
     const bool ri = tv.row_ids != nullptr, pi = probe_ids != nullptr;
-    // DFP_HJ_COUNT_FREE=0: every tile takes the emission's count pass (A/B of the count-free path)
+    // DFP_HJ_COUNT_FREE=0: every tile takes the emission's general count and write passes
+    // (A/B of the dense count-free path and of the hashed 0/1 path)
     // DFP_HJ_EMIT_DYN=0: the emission's static tile schedule (A/B of the tile counter)
     static const bool emit_dyn = [] {
         const char* e = getenv("DFP_HJ_EMIT_DYN");
@@ -4735,7 +4750,7 @@ hipError_t launch_probe_sliced_tl(int key_bytes, const TableView& tv, const void
     sl_emit_kernel<RI, PI, TL><<<egrid, SlT<TL>::kEmitThreads, 0, s>>>(tv, w.tent, w.rl, w.res, probe_ids, pbase, w.tcnt, nt,   \
                                                            out_b, out_p, cap, d_total,                      \
                                                            hashed || !count_free ? nullptr : w.wcnt,          \
-                                                           emit_dyn ? w.tcnt + nt : nullptr)
+                                                           emit_dyn ? w.tcnt + nt : nullptr, hashed && count_free)
     if (ri && pi) DFP_SLE(true, true);
     else if (ri) DFP_SLE(true, false);
     else if (pi) DFP_SLE(false, true);
