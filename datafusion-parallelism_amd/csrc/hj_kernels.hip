@@ -2881,8 +2881,9 @@ sl_lookup_kernel(TableView tv, uint32_t wlog, uint32_t nslices, int64_t ntiles, 
         // one atomic per tile that has a correction (64 contiguous counters)
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront", "local");  // LDS only: no wait for the ref stores
         __builtin_amdgcn_wave_barrier();
+        int cr = 0;
+        bool fodd = false;
         if (len != 0) {
-            int cr;
             if constexpr (HASHED) {  // end records: a fragment's minus its predecessor's
                 cr = (int)(scst[rank] - (rank > 0 ? scst[rank - 1] : 0u));
             } else {  // start records: the successor's minus its own
@@ -2892,9 +2893,14 @@ sl_lookup_kernel(TableView tv, uint32_t wlog, uint32_t nslices, int64_t ntiles, 
             // a fragment with an entry of count != 1 (dense: missing or duplicated; hashed:
             // duplicated) also turns off its tile's count-free (dense) or 0/1 (hashed)
             // emission (kOddFlag above the count bits, one atomic for both)
-            const unsigned long long add = (unsigned long long)(long long)cr + (sodd[rank] ? kOddFlag : 0ull);
-            if (add != 0) atomicAdd(&tcnt[tc + lane], add);
+            fodd = sodd[rank] != 0;
         }
+        // Measured (r05) and not kept: this atomic held back until the next block's first entry
+        // loads had issued (an atomic stays in vmcnt until the memory side has done it, and a
+        // wait for loads issued after it waits for it too): C2h lookup 542.6 -> 542.3 us, C3
+        // 261.5 -> 261.9, with 2 VGPRs spilled (profiles/r05_lookup_tail_ab.txt)
+        const unsigned long long add = (unsigned long long)(long long)cr + (fodd ? kOddFlag : 0ull);
+        if (add != 0) atomicAdd(&tcnt[tc + lane], add);
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront", "local");  // LDS only: no wait for the ref stores
         __builtin_amdgcn_wave_barrier();
         DFP_PH(4);
@@ -4698,8 +4704,17 @@ hipError_t launch_probe_sliced_tl(int key_bytes, const TableView& tv, const void
             const uint32_t rounds = nsl * parts / cus;
             const uint32_t a = rounds * cus / parts;  // slices in the whole rounds
             if (tail_on && rounds >= 1 && a < nsl && a > 0) {
-                const uint32_t p2 = std::min<uint32_t>(cus / (nsl - a), (uint32_t)std::min<int64_t>(8 * parts, (nt + 63) / 64));
-                if (p2 > parts) {
+                // the split whose tail rounds take the least time (in items of `parts` parts):
+                // ceil(r p / cus) rounds of 1/p items. C2: 50 slices over 256 CUs, p = 5 (one
+                // round of fifths); C2h (one part per slice): 162 slices, p = 3 (two rounds of
+                // thirds, 0.67 of an item instead of a whole round with 94 CUs idle)
+                const uint32_t r = nsl - a;
+                const uint32_t pmax = (uint32_t)std::min<int64_t>(8 * parts, (nt + 63) / 64);
+                auto tail = [&](uint32_t p) { return (double)((r * p + cus - 1) / cus) / p; };
+                uint32_t p2 = parts;
+                for (uint32_t p = parts + 1; p <= pmax; ++p)
+                    if (tail(p) < tail(p2) - 1e-9) p2 = p;
+                if (p2 > parts && tail(p2) <= tail(parts) - 0.15 / parts) {  // by >= 0.15 of an item
                     s1 = a;
                     parts2 = p2;
                 }
