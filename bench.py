@@ -547,19 +547,19 @@ def main():
         return dry_run(args, json_out)
     cfg = CONFIGS[args.config]
 
-    if args.force_dist and "RANK" not in os.environ:  # one rank without a launcher
-        import socket
-
-        with socket.socket() as so:
-            so.bind(("127.0.0.1", 0))
-            port = so.getsockname()[1]
-        os.environ.update(RANK="0", WORLD_SIZE="1", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    one_rank_store = None
+    if args.force_dist and "RANK" not in os.environ:  # one rank without a launcher: an in-memory store
+        # (a free TCP port found by binding port 0 can be taken again before the store listens)
+        os.environ.update(RANK="0", WORLD_SIZE="1", LOCAL_RANK="0")
+        one_rank_store = dist.HashStore()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     dev = torch.device("cuda", local_rank)
     torch.cuda.set_device(dev)
-    if world > 1 or args.force_dist:
+    if one_rank_store is not None:
+        dist.init_process_group("nccl", store=one_rank_store, rank=0, world_size=1, device_id=dev)
+    elif world > 1 or args.force_dist:
         dist.init_process_group("nccl", device_id=dev)
 
     use_dist = world > 1 or args.force_dist

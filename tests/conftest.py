@@ -32,3 +32,14 @@ def dfp():
 
     m.load()
     return m
+
+
+def init_one_rank_nccl():
+    """A one-rank RCCL process group on cuda:0 whose rendezvous is an in-memory store: a
+    free TCP port picked by binding port 0 and closing it can be taken again before the
+    store listens on it (EADDRINUSE seen on the GPU box, gpurun_out/r05y/tests.log)."""
+    import torch
+    import torch.distributed as dist
+
+    os.environ.update(RANK="0", WORLD_SIZE="1")
+    dist.init_process_group("nccl", store=dist.HashStore(), rank=0, world_size=1, device_id=torch.device("cuda", 0))

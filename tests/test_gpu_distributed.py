@@ -3,12 +3,12 @@ with global ids) run as one RCCL rank on the box's GPU, against the oracle; and 
 partition kernel against its host restatement. (N > 1 ranks: the driver's 8-GPU runs;
 the exchange logic at world_size 2 is covered on CPU by test_distributed_gloo.py.)"""
 import os
-import socket
 
 import numpy as np
 import pytest
 import torch
 import torch.distributed as dist
+from conftest import init_one_rank_nccl
 
 pytestmark = pytest.mark.gpu
 
@@ -77,12 +77,7 @@ def test_distributed_join_one_rank(dfp, oracle_mod, chunks):
     chunks > 1 the probe side is pipelined (one rank keeps the global order)."""
     from datafusion_parallelism_amd.distributed import DistributedHashJoin
 
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1")
-    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    init_one_rank_nccl()
     try:
         rng = np.random.default_rng(4)
         bk = rng.integers(0, 30000, 100000)
@@ -102,12 +97,7 @@ def test_broadcast_join_one_rank(dfp, oracle_mod, keys):
     (offsets from 2^62) too. Pairs equal the oracle's, probe ids = probe_base + row."""
     from datafusion_parallelism_amd.distributed import DistributedHashJoin, broadcast_key_plan
 
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1")
-    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    init_one_rank_nccl()
     try:
         rng = np.random.default_rng(7)
         off = 2**62 if keys == "dense_far" else 0
@@ -136,12 +126,7 @@ def test_large_exchange_one_rank(dfp):
     from datafusion_parallelism_amd import distributed
     from datafusion_parallelism_amd.distributed import all_to_all_rows, gpu_radix_partition
 
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1")
-    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    init_one_rank_nccl()
     try:
         n = 160_000_000
         dev = torch.device("cuda", 0)

@@ -12,13 +12,13 @@ one table, and each rank probes its own probe rows against it.
   canonical pairs of the whole join.
 """
 import os
-import socket
 import threading
 
 import numpy as np
 import pytest
 import torch
 import torch.distributed as dist
+from conftest import init_one_rank_nccl
 
 pytestmark = pytest.mark.gpu
 
@@ -45,12 +45,7 @@ def _keys(kind, rng, nb, np_):
 
 
 def _init_one_rank():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1")
-    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    init_one_rank_nccl()
 
 
 @pytest.mark.parametrize("native", [True, False])

@@ -5,6 +5,7 @@ import numpy as np
 import pytest
 
 from tpch_ref import q3_pandas, q9_pandas
+from conftest import init_one_rank_nccl
 
 pytestmark = pytest.mark.gpu
 
@@ -53,19 +54,13 @@ def test_distributed_plans_one_rank(dfp):
     self-copies; the GPU partition kernel and hash joins run for real): equal to the
     one-GPU plans and to pandas."""
     import os
-    import socket
 
     import torch
     import torch.distributed as dist
 
     from datafusion_parallelism_amd import tpch
 
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1")
-    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    init_one_rank_nccl()
     try:
         t = tpch.generate(0.05, "cuda:0", seed=11, q9=True)
         got3 = tpch.q3_dist(t, "BUILDING", "1995-03-15")
