@@ -3045,9 +3045,6 @@ hs_partition_kernel(uint32_t nb, uint32_t slog, uint32_t s0, uint32_t nslices, c
 // leave through a 64 KB staging area in four quarters of 2^13 positions. Once the last
 // quarter is staged the key registers are free: the next tile's keys load into them
 // while that quarter and the rows are written out.
-#ifndef DFP_HS32_RG
-#define DFP_HS32_RG 1  // rank groups per scheduling region
-#endif
 template <typename K, bool HAS_VALID>
 __global__ void __launch_bounds__(kSlThreads, 4)  // 16 waves per CU: <= 128 VGPRs
 hs_partition32_kernel(uint32_t nb, uint32_t slog, uint32_t s0, uint32_t nslices, const void* __restrict__ keys,
@@ -3106,7 +3103,10 @@ hs_partition32_kernel(uint32_t nb, uint32_t slog, uint32_t s0, uint32_t nslices,
                 r[q] = ok ? atomicAdd(&s_hist[sl], 1u) : kNone;
             }
             *reinterpret_cast<uint2*>(s_pos + loc0) = make_uint2(r[0] | (r[1] << 16), r[2] | (r[3] << 16));
-            if ((g + 1) % DFP_HS32_RG == 0) __builtin_amdgcn_sched_barrier(0);
+            // Measured (r05) and not kept: 2 or 8 groups per scheduling region (the rank
+            // atomics of several groups in flight; no spills either way): partition equal
+            // within noise, C2h 70.2-70.4K vs 70.3-70.6K Mrows/s (profiles/r05_hs32_rank_groups.txt)
+            __builtin_amdgcn_sched_barrier(0);
         }
         __syncthreads();
         asm volatile("" : "+v"(tx));  // (again: the offsets of the phases below are recomputed, not kept live)
