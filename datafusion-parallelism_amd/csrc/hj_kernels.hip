@@ -4637,13 +4637,16 @@ hipError_t launch_probe_sliced_tl(int key_bytes, const TableView& tv, const void
                                    : (const void*)sl_lookup_kernel<false, kSlOwnWin, TL>;
     e = hipFuncSetAttribute(lk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)tab_lds);
     if (e != hipSuccess) return e;
-    // (slice, tile range) work items: about 768 of them, so that the resident workgroups
+    // (slice, tile range) work items: about 512 of them (768 before r05), so that the resident workgroups
     // (one per CU at 128 KB slices) run several rounds and the tail stays short; more items
     // load each slice image more often (profiles/r03_lookup_items.txt: C2 768 vs 1024 items
     // +0.5 % in three alternating pairs, C3 +0.7 %, C2h the same one part per slice)
     static const uint32_t target = [] {
         const char* ev = getenv("DFP_HJ_SLICED_ITEMS");
-        return ev ? (uint32_t)std::max(1, atoi(ev)) : 768u;
+        // r05: 512 (C2 / C3: 2 parts per slice, the 50 slices past the whole rounds in fifths)
+        // against 768 (3 parts) and 1224 (4): lookup C2 116.5 -> 115.1 us, C3 262 -> 258, C3
+        // bench probe 1.153-1.159 -> 1.140-1.146 ms (profiles/r05_lookup_items2.txt)
+        return ev ? (uint32_t)std::max(1, atoi(ev)) : 512u;
     }();
     for (uint32_t pass = 0; pass < npass; ++pass) {
         const uint32_t s0 = pass * (uint32_t)kSlMaxSlices;

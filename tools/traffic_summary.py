@@ -27,7 +27,8 @@ PROBE_KERNELS = ("probe_fused_kernel", "probe_lookup_kernel", "probe_emit_kernel
 BUILD_KERNELS = ("key_minmax_kernel", "key_minmax_part_kernel", "minmax_final_kernel", "coarse_hist_kernel", "coarse_scatter", "fine_hist_kernel",
                  "fine_scatter", "chunk_starts_kernel", "scan_reduce_kernel<unsigned int>",
                  "scan_down_kernel<unsigned int>", "chunk_build_kernel", "dup_sort_big_kernel", "sl_partition_kernel",
-                 "sl_toff_transpose_kernel", "dense_frag_build_kernel", "hs_partition_kernel", "hashed_frag_build_kernel")
+                 "sl_toff_transpose_kernel", "dense_frag_build_kernel", "hs_partition_kernel", "hs_partition32_kernel",
+                 "hashed_frag_build_kernel")
 
 
 # kernels that run in both phases (the dense build reuses the sliced probe's partition, the
@@ -37,8 +38,10 @@ BUILD_KERNELS = ("key_minmax_kernel", "key_minmax_part_kernel", "minmax_final_ke
 # Keying the phase on the first build kernel instead mislabelled the hashed build's
 # partitions once the speculative build launched a (no-op) dense frag build ahead of them
 # (round-4 verdict, "What's weak" 3).
-SHARED = ("sl_partition_kernel", "sl_toff_transpose_kernel", "hs_partition_kernel")
-PROBE_ONLY = ("sl_lookup_kernel", "sl_emit_kernel", "sl_count_kernel", "hs_partition32_kernel", "probe_fused_kernel",
+# (r05: the hashed build's partition is hs_partition32 too since its frag build moved to
+# 2^15-row tiles; as a probe-only kernel its build launches were averaged into the probe's)
+SHARED = ("sl_partition_kernel", "sl_toff_transpose_kernel", "hs_partition_kernel", "hs_partition32_kernel")
+PROBE_ONLY = ("sl_lookup_kernel", "sl_emit_kernel", "sl_count_kernel", "probe_fused_kernel",
               "probe_lookup_kernel",
               "probe_emit_kernel", "pp_")
 
