@@ -377,17 +377,21 @@ def _spawn_ranks(n: int) -> int:
     touches a GPU, and never replaces this process: the children are new processes, this
     one waits for them and exits with the worst status. Rank 0's JSON line reaches stdout
     (inherited fd 1)."""
+    import datetime
     import signal
-    import socket
     import subprocess
 
-    with socket.socket() as so:
-        so.bind(("127.0.0.1", 0))
-        port = so.getsockname()[1]
+    # The rendezvous store lives in this (GPU-free) parent and keeps its listening socket
+    # for the children's whole life: the children join it as clients (DFP_BENCH_STORE), so no
+    # port is ever found by binding and closing a socket (another process could take it
+    # before a child listens: the EADDRINUSE of gpurun_out/r05y, DESIGN §7).
+    store = dist.TCPStore("127.0.0.1", 0, None, True, timeout=datetime.timedelta(seconds=600),
+                          wait_for_workers=False)
+    port = store.port
     procs = []
     for r in range(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
-                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), DFP_BENCH_STORE=f"127.0.0.1:{port}")
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
                                       stdout=None if r == 0 else subprocess.DEVNULL))
     rc = 0
@@ -402,7 +406,31 @@ def _spawn_ranks(n: int) -> int:
         for q in procs:
             if q.poll() is None:
                 q.kill()
+        del store  # the listening socket closes only after every rank has exited
     return rc
+
+
+def _spawned_store():
+    """A rank started by _spawn_ranks joins the parent's store as a client (None under a
+    launcher: torch.distributed.run's env:// rendezvous then applies)."""
+    spec = os.environ.get("DFP_BENCH_STORE")
+    if not spec:
+        return None
+    import datetime
+
+    host, port = spec.rsplit(":", 1)
+    return dist.TCPStore(host, int(port), None, False, timeout=datetime.timedelta(seconds=600))
+
+
+def init_group(backend: str, rank: int, world: int, **kw) -> str:
+    """init_process_group for a multi-rank run: through the spawning parent's store when this
+    rank was spawned by _spawn_ranks, else env:// (the launcher's MASTER_*). Returns which."""
+    store = _spawned_store()
+    if store is not None:
+        dist.init_process_group(backend, store=store, rank=rank, world_size=world, **kw)
+        return "parent-store"
+    dist.init_process_group(backend, rank=rank, world_size=world, **kw)
+    return "env"
 
 
 def _median(xs):
@@ -465,8 +493,9 @@ class DryRunJob:
 def dry_run(args, json_out):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
+    rendezvous = None
     if world > 1:
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+        rendezvous = init_group("gloo", rank, world)
     job = DryRunJob()
     for _ in range(args.warmup):
         job.step()
@@ -489,7 +518,8 @@ def dry_run(args, json_out):
                           "warmup": args.warmup, "ms_per_step": round(float(el.item()) / args.steps * 1e3, 4),
                           "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "int64",
                           "data": "dry-run (CPU, gloo: launcher and timing skeleton only, not a measurement)",
-                          "ranks_reporting": int(ranks.item()), "config": {"workload": "dry run"},
+                          "ranks_reporting": int(ranks.item()), "rendezvous": rendezvous,
+                          "config": {"workload": "dry run"},
                           **stage_fields(job)}),
               file=json_out, flush=True)
     if world > 1:
@@ -560,7 +590,7 @@ def main():
     if one_rank_store is not None:
         dist.init_process_group("nccl", store=one_rank_store, rank=0, world_size=1, device_id=dev)
     elif world > 1 or args.force_dist:
-        dist.init_process_group("nccl", device_id=dev)
+        init_group("nccl", rank, world, device_id=dev)
 
     use_dist = world > 1 or args.force_dist
     bk, pk, bbase, pbase = gen_inputs(cfg, rank, world, dev, strong=True)

@@ -23,6 +23,9 @@ def test_gpus_2_without_launcher_spawns_two_ranks():
     assert len(lines) == 1, r.stdout  # one JSON line (rank 0), nothing else on stdout
     d = json.loads(lines[0])
     assert d["n_gpus"] == 2 and d["ranks_reporting"] == 2
+    # the ranks joined the spawning parent's listening store, not a port picked by closing
+    # a socket
+    assert d["rendezvous"] == "parent-store"
     assert d["steps"] == 2 and d["warmup"] == 1
     assert "dry-run" in d["data"]
     # the stage fields the N > 1 lines carry: a measured build span (no literal 0.0) and
@@ -37,6 +40,21 @@ def test_no_literal_zero_build_ms():
     with open(os.path.join(ROOT, "bench.py")) as f:
         src = f.read()
     assert "build_ms.append(0.0)" not in src
+
+
+def test_no_port_picked_by_closing_a_socket():
+    """No launcher, test or tool finds a port by binding port 0 and closing the socket."""
+    import glob
+
+    files = [os.path.join(ROOT, "bench.py")] + glob.glob(os.path.join(ROOT, "tests", "*.py")) + \
+        glob.glob(os.path.join(ROOT, "tools", "*.py")) + \
+        glob.glob(os.path.join(ROOT, "datafusion-parallelism_amd", "*.py"))
+    for fn in files:
+        if os.path.abspath(fn) == os.path.abspath(__file__):
+            continue
+        with open(fn) as f:
+            src = f.read()
+        assert "socket.socket(" not in src and ".bind((" not in src, fn
 
 
 def test_world_size_mismatch_is_an_error():

@@ -4,7 +4,6 @@ global build/probe ids — joined per rank by the oracle (test-local stand-ins f
 HIP partition / local-join kernels, which need a GPU). Global pairs gathered from both
 ranks must equal the single-process oracle join after canonical ordering."""
 import os
-import socket
 import sys
 
 import numpy as np
@@ -12,6 +11,8 @@ import pytest
 import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
+
+import rendezvous
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
@@ -79,8 +80,7 @@ def _canonical(b, p):
 def _worker(rank, world, port, bks, pks, q, chunks=1, max_bytes=None, rfilter=True, plan="radix"):
     sys.path.insert(0, ROOT)
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    rendezvous.join(rank, world, port)
     from datafusion_parallelism_amd import distributed
     from datafusion_parallelism_amd.distributed import DistributedHashJoin
 
@@ -119,13 +119,6 @@ def _worker(rank, world, port, bks, pks, q, chunks=1, max_bytes=None, rfilter=Tr
     dist.destroy_process_group()
 
 
-def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
-    return port
-
 
 @pytest.mark.parametrize("world,chunks,wide,max_bytes,rfilter", [
     (2, 1, False, None, True), (2, 3, False, None, True), (2, 3, True, None, True), (2, 1, False, 5000, True),
@@ -147,7 +140,8 @@ def test_distributed_exchange_matches_single_join(oracle_mod, world, chunks, wid
     pks = [pk[pb[r]:pb[r + 1]] for r in range(world)]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = _free_port()
+    store = rendezvous.parent_store()  # held until the ranks exit
+    port = store.port
     procs = [ctx.Process(target=_worker, args=(r, world, port, bks, pks, q, chunks, max_bytes, rfilter)) for r in range(world)]
     for pr in procs:
         pr.start()
@@ -177,7 +171,8 @@ def test_broadcast_plan_is_canonical(oracle_mod, world):
     pks = [pk[pb[r]:pb[r + 1]] for r in range(world)]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = _free_port()
+    store = rendezvous.parent_store()  # held until the ranks exit
+    port = store.port
     procs = [ctx.Process(target=_worker, args=(r, world, port, bks, pks, q, 1, None, True, "broadcast"))
              for r in range(world)]
     for pr in procs:
@@ -241,8 +236,7 @@ def test_sharded_ok_boundaries():
 
 def _plan_worker(rank, world, port, shards, rows, q):
     sys.path.insert(0, ROOT)
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    rendezvous.join(rank, world, port)
     try:
         from datafusion_parallelism_amd.distributed import broadcast_key_plan
 
@@ -277,7 +271,8 @@ def test_broadcast_key_plan_world(case):
         want = None
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = _free_port()
+    store = rendezvous.parent_store()  # held until the ranks exit
+    port = store.port
     procs = [ctx.Process(target=_plan_worker, args=(r, world, port, shards, rows, q)) for r in range(world)]
     for pr in procs:
         pr.start()
@@ -291,8 +286,7 @@ def test_broadcast_key_plan_world(case):
 
 def _gather_worker(rank, world, port, lens, q):
     sys.path.insert(0, ROOT)
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    rendezvous.join(rank, world, port)
     try:
         from datafusion_parallelism_amd.distributed import DistributedHashJoin
 
@@ -319,7 +313,8 @@ def test_sharded_plan_gathers(lens):
     want = np.concatenate([np.arange(n, dtype=np.int32) + 1000 * r for r, n in enumerate(lens)])
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = _free_port()
+    store = rendezvous.parent_store()  # held until the ranks exit
+    port = store.port
     procs = [ctx.Process(target=_gather_worker, args=(r, world, port, lens, q)) for r in range(world)]
     for pr in procs:
         pr.start()

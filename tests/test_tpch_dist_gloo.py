@@ -4,7 +4,6 @@ merges) on rank-sharded generated tables, with the oracle as the per-rank local 
 numpy restatement of the partition (test-local stand-ins for the HIP kernels). Results
 must equal the pandas restatement over the whole (concatenated) tables."""
 import os
-import socket
 import sys
 
 import numpy as np
@@ -12,6 +11,8 @@ import pytest
 import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
+
+import rendezvous
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -26,8 +27,7 @@ def oracle_join(build, probe):
 
 def _worker(rank, world, port, sf, q, max_bytes=None):
     sys.path[:0] = [ROOT, HERE, os.path.join(ROOT, "oracle")]
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    rendezvous.join(rank, world, port)
     from test_distributed_gloo import cpu_partition
 
     from datafusion_parallelism_amd import distributed, tpch
@@ -45,13 +45,6 @@ def _worker(rank, world, port, sf, q, max_bytes=None):
         q.put(allres)
     dist.destroy_process_group()
 
-
-def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
-    return port
 
 
 def test_generator_shards_concatenate_to_the_whole_tables():
@@ -90,7 +83,8 @@ def test_q3_q9_distributed_match_pandas(oracle_mod, world, max_bytes):
     sf = 0.01
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = _free_port()
+    store = rendezvous.parent_store()  # held until the ranks exit
+    port = store.port
     procs = [ctx.Process(target=_worker, args=(r, world, port, sf, q, max_bytes)) for r in range(world)]
     for pr in procs:
         pr.start()

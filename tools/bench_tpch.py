@@ -15,7 +15,6 @@ Timed region: barrier + device synchronise on both sides, max over ranks."""
 import argparse
 import json
 import os
-import socket
 import sys
 import time
 
@@ -45,16 +44,15 @@ def main():
         set_device_budget(a.budget)
     rank, world = 0, 1
     if a.dist:
-        if "RANK" not in os.environ:  # one rank without a launcher
-            s = socket.socket()
-            s.bind(("127.0.0.1", 0))
-            os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(s.getsockname()[1]), RANK="0",
-                              WORLD_SIZE="1", LOCAL_RANK="0")
-            s.close()
+        store = None
+        if "RANK" not in os.environ:  # one rank without a launcher: an in-memory store, no port
+            os.environ.update(RANK="0", WORLD_SIZE="1", LOCAL_RANK="0")
+            store = dist.HashStore()
         rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
         local = int(os.environ.get("LOCAL_RANK", rank))
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local))
+        dist.init_process_group("nccl", store=store, rank=rank, world_size=world,
+                                device_id=torch.device("cuda", local))
     dev = f"cuda:{torch.cuda.current_device()}"
     for run in a.runs:
         q, sf = run.split(":")

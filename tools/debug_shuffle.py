@@ -3,7 +3,6 @@
 rank (radix partition with nparts 1 must be the identity; RCCL all_to_all_single self
 copies must be exact). Prints one line per check; no kernel indexes with the results."""
 import os
-import socket
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -14,11 +13,7 @@ from datafusion_parallelism_amd.distributed import gpu_radix_partition  # noqa: 
 
 
 def main():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(s.getsockname()[1]), RANK="0", WORLD_SIZE="1")
-    s.close()
-    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    dist.init_process_group("nccl", store=dist.HashStore(), rank=0, world_size=1, device_id=torch.device("cuda", 0))
     dev = torch.device("cuda", 0)
     for n in [int(x) for x in (sys.argv[1:] or ["100000000", "200000000", "320000000"])]:
         keys = torch.randint(0, 6 * 10**8, (n,), dtype=torch.int64, device=dev)
