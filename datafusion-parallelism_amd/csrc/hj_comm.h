@@ -92,6 +92,12 @@ struct hj_comm {
     int rank = 0, world = 1, device = 0;
     std::atomic<bool> aborted{false};
     int64_t* host = nullptr;  // pinned mailbox for the plan's small reads
+    // the plans' small device words (key range and status, minmax workspace, count and
+    // status vectors), allocated once with the communicator so that no plan can fail to get
+    // them between two collectives (a one-sided failure there would leave the peers blocked).
+    // Jobs run one at a time on the worker and every word is consumed by a host read of the
+    // job that wrote it, so consecutive jobs share them.
+    int64_t* words = nullptr;
     hipEvent_t ev = nullptr;  // marks a read's copy
     // the jobs' device work runs on the communicator's own streams (after the caller's
     // stream at submission): two communicators' jobs never share a stream, so their

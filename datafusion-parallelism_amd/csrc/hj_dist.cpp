@@ -355,6 +355,58 @@ bool counts_ok(const std::vector<int64_t>& m, int W, int me, int64_t cap) {
     return true;
 }
 
+// The communicator's persistent device words (hj_comm::words), carved per plan step:
+// [min | max, rows, failed] (8), two count vectors of W + 1 and their all-gathered
+// matrices, a [value, failed] status and its all-gather, the key-range workspace.
+struct Words {
+    int64_t *mm, *cnt, *allc, *cnt2, *allc2, *st, *allst;
+    void* mws;
+};
+size_t words_bytes(int W) {
+    const size_t w = 8 + 2 * ((size_t)W + 1) + 2 * (size_t)W * ((size_t)W + 1) + 2 + 2 * (size_t)W;
+    return w * 8 + (((size_t)hj_key_minmax_workspace_bytes() + 255) & ~(size_t)255);
+}
+Words words_of(hj_comm* c) {
+    const size_t W = (size_t)c->world;
+    Words w;
+    int64_t* p = c->words;
+    w.mm = p, p += 8;
+    w.cnt = p, p += W + 1;
+    w.allc = p, p += W * (W + 1);
+    w.cnt2 = p, p += W + 1;
+    w.allc2 = p, p += W * (W + 1);
+    w.st = p, p += 2;
+    w.allst = p, p += 2 * W;
+    w.mws = p;
+    return w;
+}
+
+// Receive buffers: sized before the count exchange that carries every rank's status, at a
+// bounded slack over the even share (2 x rows / W, never more than the global rows) instead
+// of the global rows (W x the expected peak at W ranks). A skewed plan whose received rows
+// pass the slack allocates the exact size after that exchange; a failure there is one-sided
+// and aborts the communicator (documented in hj.h).
+int64_t recv_slack(int64_t rows, int W) {
+    if (W == 1) return std::max<int64_t>(rows, 1);
+    const int64_t share = (rows + W - 1) / W;
+    return std::max<int64_t>(1, std::min<int64_t>(rows, 2 * share + 1024));
+}
+hj_status grow_recv(hj_comm* c, Scratch& scr, int64_t need, int64_t have, int okb, char** keys, uint64_t** ids,
+                    const char* what) {
+    if (need <= have) return HJ_OK;
+    char* k = (char*)scr.get((size_t)need * okb);
+    uint64_t* i = (uint64_t*)scr.get((size_t)need * 8);
+    if (!k || !i) {
+        c->tr->abort();
+        c->aborted = true;
+        return set_error(HJ_ERR_OOM, std::string("hj_dist: device allocation failed (") + what +
+                                         " past the even-share slack); the communicator was aborted");
+    }
+    *keys = k;
+    *ids = i;
+    return HJ_OK;
+}
+
 // ---- the sharded-build plan's build side -------------------------------------------------
 
 struct ShardedArgs {
@@ -414,9 +466,9 @@ hj_status run_sharded(hj_comm* c, const ShardedArgs& a, hj_dist_job* j, int64_t 
     }
 
     // 1. the global key range, build rows and status: [min | max, rows, failed]
-    int64_t* mm = (int64_t*)scr.get(8 * 8);
-    void* mws = scr.get((size_t)hj_key_minmax_workspace_bytes());
-    if (!mm || !mws) return set_error(HJ_ERR_OOM, "hj_dist: device allocation failed (plan words)");
+    const Words w = words_of(c);
+    int64_t* mm = w.mm;
+    void* mws = w.mws;
     if (injected(c, jobno, 0)) lf.note(set_error(HJ_ERR_INVALID, "injected failure (test hook) at the key range"));
     if (!lf.failed) lf.note(hj_key_minmax(a.kt, a.keys, a.valid, a.voff, a.n, mm, mws, s));
     {
@@ -467,13 +519,12 @@ hj_status run_sharded(hj_comm* c, const ShardedArgs& a, hj_dist_job* j, int64_t 
         const int64_t cap = std::max<int64_t>(a.n, 1);
         char* pk = (char*)get((size_t)cap * kb, "rows");
         uint64_t* pi = (uint64_t*)get((size_t)cap * 8, "ids");
-        int64_t* st2 = (int64_t*)get(16, "status");
-        int64_t* all2 = (int64_t*)get(16 * (size_t)W, "status");
+        int64_t* st2 = w.st;
+        int64_t* all2 = w.allst;
         void* pws = get((size_t)hj_partition_regions_workspace_bytes(a.n, 1), "workspace");
         // the gathered side: at most the global rows (sized before the status exchange)
         char* gk = (char*)get((size_t)std::max<int64_t>(rows, 1) * kb, "gathered keys");
         uint64_t* gi = (uint64_t*)get((size_t)std::max<int64_t>(rows, 1) * 8, "gathered ids");
-        if (!st2 || !all2) return set_error(HJ_ERR_OOM, "hj_dist: device allocation failed (status words)");
         if (injected(c, jobno, 1)) lf.note(set_error(HJ_ERR_INVALID, "injected failure (test hook) at the partition"));
         if (!lf.failed)
             lf.note(hj_partition_regions(a.kt, a.keys, a.valid, a.voff, nullptr, (uint64_t)a.base, a.n, 1, nullptr, pk,
@@ -529,13 +580,12 @@ hj_status run_sharded(hj_comm* c, const ShardedArgs& a, hj_dist_job* j, int64_t 
     }
     const int64_t nvalues = offs[W - 1] + lens[W - 1];
     if ((uint64_t)nvalues != rng_m1 + 1) return set_error(HJ_ERR_INVALID, "hj_dist: range shares do not tile the domain");
-    const int64_t rcap = W == 1 ? cap : std::max<int64_t>(rows, 1);
+    const int64_t rcap = W == 1 ? cap : recv_slack(rows, W);
     const int64_t dcap = 2 * rows + 2 * (int64_t)W + 4;
-    int64_t* cnt = (int64_t*)get(8 * ((size_t)W + 1), "counts");
-    int64_t* allc = (int64_t*)get(8 * (size_t)W * ((size_t)W + 1), "count matrix");
-    int64_t* used = (int64_t*)get(16, "segment words");
-    int64_t* allu = (int64_t*)get(16 * (size_t)W, "segment words");
-    if (!cnt || !allc || !used || !allu) return set_error(HJ_ERR_OOM, "hj_dist: device allocation failed (counts)");
+    int64_t* cnt = w.cnt;
+    int64_t* allc = w.allc;
+    int64_t* used = w.st;
+    int64_t* allu = w.allst;
     char* rk = (char*)get((size_t)cap * W * okb, "regions");
     uint64_t* ri = (uint64_t*)get((size_t)cap * W * 8, "regions");
     void* pws = get((size_t)hj_partition_regions_workspace_bytes(a.n, W), "workspace");
@@ -566,7 +616,8 @@ hj_status run_sharded(hj_comm* c, const ShardedArgs& a, hj_dist_job* j, int64_t 
         return set_error(HJ_ERR_HIP, "hj_dist: partition count out of range (device look-back failure)");
     int64_t R = 0;
     for (int src = 0; src < W; ++src) R += m[(size_t)src * W + me];
-    if (R > rcap) return set_error(HJ_ERR_HIP, "hj_dist: received rows exceed the global rows");
+    if (R > std::max<int64_t>(rows, 1)) return set_error(HJ_ERR_HIP, "hj_dist: received rows exceed the global rows");
+    if (W > 1) ST_OK(grow_recv(c, scr, R, rcap, okb, &bk, &bi, "received build rows"));
     if (W > 1) {  // per peer: keys then ids, in pieces; both sides issue the same sequence
         ST_OK(c->tr->group_start());
         ST_OK(exchange_regions(c, m, rk, cap, okb, bk, s));
@@ -722,10 +773,16 @@ hj_status run_radix(hj_comm* c, const RadixArgs& a, hj_dist_job* j, int64_t jobn
         return scr.defer();
     }
 
-    // 1. the plan: [min | max, rows, failed] of the build side
-    int64_t* mm = (int64_t*)scr.get(8 * 8);
-    void* mws = scr.get((size_t)hj_key_minmax_workspace_bytes());
-    if (!mm || !mws) return set_error(HJ_ERR_OOM, "hj_dist: device allocation failed (plan words)");
+    // 1. the plan: [min | max, rows, failed] of the build side. A rank's own argument
+    // errors are noted before the status word is written, so every rank returns them
+    // together (a rank returning alone would leave its peers in the next collective).
+    const Words w = words_of(c);
+    int64_t* mm = w.mm;
+    void* mws = w.mws;
+    if (a.pbase < 0 || a.pbase + a.np > ((int64_t)1 << 32))
+        lf.note(set_error(HJ_ERR_INVALID, "hj_dist_join_radix: probe ids (probe_base + row) must fit 32 bits"));
+    if (a.pkt == HJ_INT32 && a.kt == HJ_INT64)
+        lf.note(set_error(HJ_ERR_INVALID, "hj_dist_join_radix: int32 probe keys need int32 build keys"));
     if (injected(c, jobno, 0)) lf.note(set_error(HJ_ERR_INVALID, "injected failure (test hook) at the key range"));
     if (!lf.failed) lf.note(hj_key_minmax(a.kt, a.bkeys, a.bvalid, a.bvoff, a.nb, mm, mws, sd));
     {
@@ -763,12 +820,8 @@ hj_status run_radix(hj_comm* c, const RadixArgs& a, hj_dist_job* j, int64_t jobn
     const int64_t koff = narrow ? (int64_t)((uint64_t)gmin + (1ull << 31)) : 0;
     const int okb = narrow ? 4 : kb;
     const hj_key_type lkt = okb == 8 ? HJ_INT64 : HJ_INT32;
-    if (a.pkt == HJ_INT32 && a.kt == HJ_INT64)
-        return set_error(HJ_ERR_INVALID, "hj_dist_join_radix: int32 probe keys need int32 build keys");
     const int64_t pkoff = a.pkt == HJ_INT64 && okb == 4 ? koff : 0;
     const bool u31 = rows < ((int64_t)1 << 31);
-    if (a.pbase < 0 || a.pbase + a.np > ((int64_t)1 << 32))
-        return set_error(HJ_ERR_INVALID, "hj_dist_join_radix: probe ids (probe_base + row) must fit 32 bits");
     hj_part_spec spec{dense && W > 1 ? 1 : 0, gmin, gmax};
     int64_t llo = gmin, lhi = gmax;  // this rank's build key range (the whole range under the hash map)
     bool lempty = false;
@@ -778,18 +831,17 @@ hj_status run_radix(hj_comm* c, const RadixArgs& a, hj_dist_job* j, int64_t jobn
     // 2. both sides into per-destination regions; the build side's receive buffers sized
     // by the global rows before the count exchange carries the statuses
     const int64_t bcap = std::max<int64_t>(a.nb, 1), pcap = std::max<int64_t>(a.np, 1);
-    int64_t* bcnt = (int64_t*)get(8 * ((size_t)W + 1), "counts");
-    int64_t* ballc = (int64_t*)get(8 * (size_t)W * ((size_t)W + 1), "count matrix");
-    int64_t* pcnt = (int64_t*)get(8 * ((size_t)W + 1), "counts");
-    int64_t* pallc = (int64_t*)get(8 * (size_t)W * ((size_t)W + 1), "count matrix");
-    if (!bcnt || !ballc || !pcnt || !pallc) return set_error(HJ_ERR_OOM, "hj_dist: device allocation failed (counts)");
+    int64_t* bcnt = w.cnt;
+    int64_t* ballc = w.allc;
+    int64_t* pcnt = w.cnt2;
+    int64_t* pallc = w.allc2;
     char* brk = (char*)get((size_t)bcap * W * okb, "build regions");
     uint64_t* bri = (uint64_t*)get((size_t)bcap * W * 8, "build regions");
     void* bws = get((size_t)hj_partition_regions_workspace_bytes(a.nb, W), "workspace");
     char* prk = (char*)get((size_t)pcap * W * okb, "probe regions");
     uint32_t* pri = (uint32_t*)get((size_t)pcap * W * 4, "probe regions");
     void* pws = get((size_t)hj_partition_regions_workspace_bytes(a.np, W), "workspace");
-    const int64_t rcap = W == 1 ? bcap : std::max<int64_t>(rows, 1);
+    const int64_t rcap = W == 1 ? bcap : recv_slack(rows, W);
     char* bk = W == 1 ? brk : (char*)get((size_t)rcap * okb, "received build keys");
     uint64_t* bi = W == 1 ? bri : (uint64_t*)get((size_t)rcap * 8, "received build ids");
     if (injected(c, jobno, 1)) lf.note(set_error(HJ_ERR_INVALID, "injected failure (test hook) at the partition"));
@@ -818,7 +870,8 @@ hj_status run_radix(hj_comm* c, const RadixArgs& a, hj_dist_job* j, int64_t jobn
         return set_error(HJ_ERR_HIP, "hj_dist: partition count out of range (device look-back failure)");
     int64_t Rb = 0;
     for (int src = 0; src < W; ++src) Rb += mb[(size_t)src * W + me];
-    if (Rb > rcap) return set_error(HJ_ERR_HIP, "hj_dist: received rows exceed the global rows");
+    if (Rb > std::max<int64_t>(rows, 1)) return set_error(HJ_ERR_HIP, "hj_dist: received rows exceed the global rows");
+    if (W > 1) ST_OK(grow_recv(c, scr, Rb, rcap, okb, &bk, &bi, "received build rows"));
     HIP_OK(hipEventRecord(j->ev_t[1], sd));  // exchange start
     if (W > 1) {
         ST_OK(c->tr->group_start());
@@ -1007,6 +1060,10 @@ hj_status start(hj_comm* c) {
         hipStreamCreateWithPriority(&c->build, hipStreamNonBlocking, prio) != hipSuccess ||
         hipStreamCreateWithPriority(&c->probe, hipStreamNonBlocking, prio) != hipSuccess)
         return set_error(HJ_ERR_HIP, "hj_comm: pinned mailbox / event / streams");
+    if (hipMalloc((void**)&c->words, words_bytes(c->world)) != hipSuccess) {
+        c->words = nullptr;
+        return set_error(HJ_ERR_OOM, "hj_comm: the plans' device words");
+    }
     c->evs.assign(kEvents, nullptr);
     for (auto& e : c->evs)
         if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess)
@@ -1084,6 +1141,7 @@ void hj_comm_free(hj_comm* c) {
     if (c->probe) (void)hipStreamDestroy(c->probe);
     if (c->ev) (void)hipEventDestroy(c->ev);
     if (c->host) (void)hipHostFree(c->host);
+    if (c->words) (void)hipFree(c->words);
     delete c;
 }
 

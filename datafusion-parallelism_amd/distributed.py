@@ -481,6 +481,7 @@ class NativeJob:
 
     def __init__(self, L, handle: ctypes.c_void_p, device: torch.device, keep=(), key_type: int = HJ_INT64):
         self._L, self._h, self.device, self._keep, self.key_type = L, handle, device, list(keep), key_type
+        self._consumers = []  # torch streams current when pairs() handed out the job's buffers
 
     def wait(self):
         info = _lib.HjDistInfo()
@@ -500,6 +501,9 @@ class NativeJob:
         values]) as device tensors over the job's buffers (no copy)."""
         b, p, n = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_int64()
         check_l(self._L, self._L.hj_dist_job_pairs(self._h, ctypes.byref(b), ctypes.byref(p), ctypes.byref(n)))
+        cur = torch.cuda.current_stream(self.device)
+        if all(c != cur for c in self._consumers):
+            self._consumers.append(cur)
         return (_tensor_of(b.value, n.value, torch.int64, self.device, self),
                 _tensor_of(p.value, n.value, torch.int32, self.device, self))
 
@@ -511,6 +515,20 @@ class NativeJob:
 
     def close(self):
         if getattr(self, "_h", None):
+            # hj_dist_job_free returns the pairs' blocks to the library's cache, which is not
+            # stream-ordered (the next job may reuse them at once): first wait for what the
+            # consumers queued on the streams that held the tensors (the stream current at
+            # pairs() and the one current now; a consumer on another stream must hold the
+            # tensors, i.e. this job, until its work is done)
+            streams = list(self._consumers)
+            if torch.cuda.is_available():
+                cur = torch.cuda.current_stream(self.device)
+                if all(c != cur for c in streams):
+                    streams.append(cur)
+            for st in streams:
+                ev = torch.cuda.Event()
+                ev.record(st)
+                ev.synchronize()
             self._L.hj_dist_job_free(self._h)
             self._h = None
 

@@ -362,3 +362,99 @@ def test_rank_failure_is_collective(ctl, oracle_mod, plan, step):
     else:
         b, p = _merge([o[1] for o in out])
     assert np.array_equal(b, ob) and np.array_equal(p, op)
+
+
+def test_radix_probe_ids_past_32_bits_fail_collectively(ctl, oracle_mod):
+    """a rank whose probe ids (probe_base + row) pass 2^32 notes the
+    error before the plan's first status exchange, so every rank's job returns it (the others
+    'a peer rank failed') instead of that rank returning alone while its peers block in the
+    next collective; the next job on the same communicators is correct."""
+    from datafusion_parallelism_amd._lib import HJ_ERR_INVALID, HJ_ERR_RCCL, HjError
+
+    world = 4
+    rng = np.random.default_rng(11)
+    bk, pk = _keys("dense", rng, 20_000, 60_000)
+    ranks = Ranks(ctl, world, timeout_s=30)
+
+    def body(r, comm):
+        b0, b1 = _split(bk.size, world, r)
+        p0, p1 = _split(pk.size, world, r)
+        keys = torch.from_numpy(bk[b0:b1]).cuda()
+        probe = torch.from_numpy(pk[p0:p1]).cuda()
+        s = torch.cuda.Stream()
+        torch.cuda.synchronize()
+        bad = (1 << 32) - 10 if r == world - 1 else p0
+        j0 = comm.join_radix(keys, b0, probe, bad, s.cuda_stream)
+        j1 = comm.join_radix(keys, b0, probe, p0, s.cuda_stream)
+        status = None
+        try:
+            j0.wait()
+        except HjError as e:
+            status = (e.status, str(e))
+        b, p = j1.pairs()
+        res = (b.cpu().numpy().astype(np.uint64), p.cpu().numpy().astype(np.uint32))
+        del b, p
+        j0.close()
+        j1.close()
+        return status, res
+
+    try:
+        out, errs = ranks.run(body)
+    finally:
+        ranks.close()
+    assert all(e is None for e in errs), errs
+    for r, (status, _) in enumerate(out):
+        assert status is not None, f"rank {r}'s job 0 did not fail"
+        if r == world - 1:
+            assert status[0] == HJ_ERR_INVALID and "32 bits" in status[1]
+        else:
+            assert status[0] == HJ_ERR_RCCL and "peer rank failed" in status[1]
+    b, p = _merge([o[1] for o in out])
+    ob, op = oracle_mod.inner_join(bk, pk)
+    assert np.array_equal(b, ob) and np.array_equal(p, op)
+
+
+def test_radix_pairs_outlive_consumer_after_job_free(ctl, oracle_mod):
+    """the pairs' tensors sit on job-owned blocks that return to the
+    library's (not stream-ordered) cache when the job is freed. A consumer queued on the
+    caller's stream behind a long kernel, then the tensors dropped and the job freed, then a
+    new join started at once: the consumer still reads the first join's pairs."""
+    if not hasattr(torch.cuda, "_sleep"):
+        pytest.skip("torch.cuda._sleep unavailable")
+    rng = np.random.default_rng(5)
+    bk, pk = _keys("dense", rng, 200_000, 400_000)
+    pk2 = (pk + 7) % max(int(bk.max()), 1)
+    ranks = Ranks(ctl, 1)
+
+    def body(r, comm):
+        keys = torch.from_numpy(bk).cuda()
+        probe = torch.from_numpy(pk).cuda()
+        probe2 = torch.from_numpy(pk2).cuda()
+        s = torch.cuda.Stream()
+        torch.cuda.synchronize()
+        with torch.cuda.stream(s):
+            j0 = comm.join_radix(keys, 0, probe, 0, s.cuda_stream)
+            b, p = j0.pairs()
+            torch.cuda._sleep(200_000_000)  # the consumer waits behind a long kernel
+            cb, cp = b.clone(), p.clone()
+            del b, p
+            j0.close()
+            j1 = comm.join_radix(keys, 0, probe2, 0, s.cuda_stream)
+            b1, p1 = j1.pairs()
+            torch.cuda.synchronize()
+            res = (cb.cpu().numpy().astype(np.uint64), cp.cpu().numpy().astype(np.uint32),
+                   b1.cpu().numpy().astype(np.uint64), p1.cpu().numpy().astype(np.uint32))
+            del b1, p1
+            j1.close()
+        return res
+
+    try:
+        out, errs = ranks.run(body)
+    finally:
+        ranks.close()
+    assert all(e is None for e in errs), errs
+    cb, cp, b1, p1 = out[0]
+    ob, op = oracle_mod.inner_join(bk, pk)
+    assert np.array_equal(cb, ob) and np.array_equal(cp, op)
+    ob2, op2 = oracle_mod.inner_join(bk, pk2)
+    assert np.array_equal(b1, ob2) and np.array_equal(p1, op2)

@@ -217,3 +217,42 @@ def test_generators(oracle_mod):
     c = np.empty(1000, np.int64)
     oracle_mod.lib().ora_gen_uniform(c.ctypes.data, 1000, 0xC0FFEE, 2 * 10**7)
     assert np.array_equal(u, c)
+
+
+def _exp_digests():
+    import hashlib
+
+    with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "exponential_digests.json")) as f:
+        return json.load(f)["sizes"], hashlib
+
+
+def _check_exp_digests(gen):
+    sizes, hashlib = _exp_digests()
+    for r in sizes:
+        a = np.ascontiguousarray(gen(r["lo"], r["hi"]).astype("<i4"))
+        assert hashlib.sha256(a.tobytes()).hexdigest() == r["libm"]["sha256"], (r["lo"], r["hi"])
+        assert np.unique(a).size == r["libm"]["distinct"]
+
+
+def test_exponential_generator_digests(oracle_mod):
+    """the C3 generator pinned at six sizes (up to C3's 10^7) against
+    committed digests (tests/golden/make_exponential_digests.py), for the oracle and the
+    product generator, so a libm change cannot silently move C3's key multiset. At 10^7
+    the libm (f32::powf) keys have 6,603,254 distinct values; numpy's float32 power gives
+    SURVEY.md §8(d)'s 6,602,610 (recorded beside it)."""
+    from datafusion_parallelism_amd.api_utils import make_exponential_int_array
+
+    _check_exp_digests(oracle_mod.make_exponential_int_array)
+    _check_exp_digests(make_exponential_int_array)
+    sizes, _ = _exp_digests()
+    big = [r for r in sizes if r["hi"] - r["lo"] == 10**7][0]
+    assert big["libm"]["distinct"] == 6603254 and big["numpy"]["distinct"] == 6602610
+
+
+@pytest.mark.gpu
+def test_exponential_generator_digests_on_gpu_box():
+    """The same digests on the GPU box's libm (GPUTEST): bench.py's C3 keys there are the
+    committed multiset."""
+    from datafusion_parallelism_amd.api_utils import make_exponential_int_array
+
+    _check_exp_digests(make_exponential_int_array)
