@@ -128,6 +128,36 @@ struct TableView {
 constexpr uint32_t kFullMask = 0x7FFFFFFFu;
 constexpr uint32_t kPackedMask = 0x07FFFFFFu;
 
+// Run refs (packed dense tables, r06). A duplicated key whose rows, in the canonical
+// descending order, are consecutive integers top, top - 1, ..., top - c + 1 - a build side
+// clustered by key (sorted input, a fact table stored in foreign-key order; C3's exponential
+// keys) - keeps them in the ref itself: kDupFlag | 1 << 27 | (c - 2) << 24 | top, for
+// 2 <= c <= kRunMaxRows and top < 2^24. A packed count of 1 occurs in no other ref (a
+// duplicated key has >= 2 rows), so bits 27-31 = 0x11 mark a run. Readers then need no
+// dup_rows segment read (the emission's random segment reads were its cost at C3: 683 ->
+// 453 us without them, profiles/r06_emit_ablations.txt). The key's dup_rows segment is
+// still written (the build allocates it before it knows), but no reader uses it.
+constexpr uint32_t kRunMaxRows = 9;
+__host__ __device__ inline bool run_ref(uint32_t r, uint32_t off_mask) {
+    return off_mask == kPackedMask && (r >> 27) == 0x11u;
+}
+__host__ __device__ inline uint32_t run_ref_count(uint32_t r) { return ((r >> 24) & 7u) + 2u; }
+__host__ __device__ inline uint32_t make_run_ref(uint32_t top, uint32_t c) {
+    return kDupFlag | (1u << 27) | ((c - 2u) << 24) | top;
+}
+// the count of a ref when it is in the ref (0 kMiss, 1 a single row, a packed or run count),
+// else kCountUnknown (in the segment header)
+__host__ __device__ inline uint32_t ref_count_inline(uint32_t r, uint32_t off_mask) {
+    if (r == kMiss) return 0u;
+    if (!(r & kDupFlag)) return 1u;
+    const uint32_t c4 = off_mask == kPackedMask ? ((r >> 27) & 15u) : 0u;
+    return c4 == 1u ? run_ref_count(r) : c4 ? c4 : kCountUnknown;
+}
+// row j (0-based, descending) of a duplicated key's ref
+__host__ __device__ inline uint32_t dup_ref_row(const uint32_t* dup_rows, uint32_t r, uint32_t off_mask, uint32_t j) {
+    return run_ref(r, off_mask) ? (r & 0xFFFFFFu) - j : dup_rows[(r & off_mask) + 1 + j];
+}
+
 // Build partition geometry: hashed chunks of 2^clog2 buckets (chunk nchunks = the side
 // bucket of INT64_MIN) or, dense, chunks of 2^kDenseShift consecutive key values from dmin.
 constexpr uint32_t kDenseShift = 11;

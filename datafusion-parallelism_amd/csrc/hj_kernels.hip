@@ -827,6 +827,7 @@ dense_chunk_build_kernel(ChunkGeom g, const uint32_t* __restrict__ starts, const
         __syncthreads();
         for (unsigned li = threadIdx.x; li < ndup; li += T) {
             const unsigned n = d_cnt[li], off = d_off[li];
+            d_cur[li] = 0;  // (the placement cursor is done): a run ref, or 0
             if (n <= (unsigned)kSmallSeg) {
                 uint32_t v[16];
 #pragma unroll
@@ -835,8 +836,14 @@ dense_chunk_build_kernel(ChunkGeom g, const uint32_t* __restrict__ starts, const
 #pragma unroll
                 for (int i = 0; i < 16; ++i)
                     if (i < (int)n) dup_rows[off + 1 + i] = v[i];
+                // consecutive rows: the ref holds them (run ref, hj_device.h)
+                bool run = g.packed && n <= kRunMaxRows && v[0] < (1u << 24);
+#pragma unroll
+                for (int i = 1; i < (int)kRunMaxRows; ++i) run &= i >= (int)n || v[i] == v[0] - (uint32_t)i;
+                if (run) d_cur[li] = make_run_ref(v[0], n);
             }
         }
+        __syncthreads();
         for (uint32_t i = threadIdx.x; i < kDenseSub; i += T) {
             const uint32_t rv = img[i];
             if (rv != kMiss && (rv & kDupFlag)) {
@@ -846,7 +853,7 @@ dense_chunk_build_kernel(ChunkGeom g, const uint32_t* __restrict__ starts, const
                     big[bi] = BigSeg{(unsigned long long)((uint64_t)g.dmin + cbase + lo + i), d_off[li], 0u};
                 }
                 const uint32_t c4 = (g.packed && d_cnt[li] <= 15u) ? d_cnt[li] : 0u;
-                img[i] = kDupFlag | (c4 << 27) | d_off[li];
+                img[i] = d_cur[li] ? d_cur[li] : kDupFlag | (c4 << 27) | d_off[li];
             }
         }
         __syncthreads();
@@ -967,8 +974,8 @@ __device__ __forceinline__ void load4(const void* keys, int64_t row0, int64_t n,
 
 // count of build rows behind a match ref
 __device__ __forceinline__ uint32_t ref_count(const uint32_t* dup_rows, uint32_t ref, uint32_t off_mask) {
-    if (ref == kMiss) return 0;
-    return (ref & kDupFlag) ? dup_rows[ref & off_mask] : 1u;
+    const uint32_t c = ref_count_inline(ref, off_mask);
+    return c == kCountUnknown ? dup_rows[ref & off_mask] : c;
 }
 
 // One bucket line: ref of `sk` if present, else kMiss; *more = the line is full, does
@@ -1021,9 +1028,8 @@ __device__ __forceinline__ void lookup4(const TableView& tv, const void* __restr
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             ref[q] = r[q];
-            // packed dense refs carry counts <= 15 in bits 27-30 (kPackedMask tables)
-            const uint32_t c4 = tv.off_mask == kPackedMask ? ((r[q] >> 27) & 15u) : 0u;
-            cnt[q] = r[q] == kMiss ? 0u : (!(r[q] & kDupFlag) ? 1u : (c4 ? c4 : kCountUnknown));
+            // packed dense refs carry counts <= 15 (or a run) in bits 24-30 (kPackedMask tables)
+            cnt[q] = ref_count_inline(r[q], tv.off_mask);
         }
         return;
     }
@@ -1091,15 +1097,14 @@ __device__ __forceinline__ void emit4(const TableView& tv, const uint32_t* __res
         const uint32_t r = ref[q];
         if (c == 1) {
             if (pos < (unsigned long long)cap) {
-                const uint32_t br = (r & kDupFlag) ? tv.dup_rows[(r & tv.off_mask) + 1] : r;
+                const uint32_t br = (r & kDupFlag) ? dup_ref_row(tv.dup_rows, r, tv.off_mask, 0) : r;
                 out_b[pos] = HAS_ROW_IDS ? tv.row_ids[br] : (uint64_t)br;
                 out_p[pos] = pidx;
             }
         } else {
-            const uint32_t* seg = tv.dup_rows + (r & tv.off_mask) + 1;
             for (uint32_t t = 0; t < c; ++t) {
                 if (pos + t < (unsigned long long)cap) {
-                    const uint32_t br = seg[t];
+                    const uint32_t br = dup_ref_row(tv.dup_rows, r, tv.off_mask, t);
                     out_b[pos + t] = HAS_ROW_IDS ? tv.row_ids[br] : (uint64_t)br;
                     out_p[pos + t] = pidx;
                 }
@@ -1255,9 +1260,9 @@ probe_fused_kernel(TableView tv, const void* __restrict__ keys, const uint8_t* _
                     if (a < b) {
                         const uint32_t r = ref[g][q];
                         const uint32_t pidx = HAS_PROBE_IDS ? probe_ids[row0 + q] : (uint32_t)(row0 + q) + pbase;
-                        const uint32_t* seg = (r & kDupFlag) ? tv.dup_rows + (r & tv.off_mask) + 1 : nullptr;
+                        const bool dup = (r & kDupFlag) != 0;
                         for (unsigned long long t = a; t < b; ++t) {
-                            const uint32_t br = seg ? seg[t - p] : r;
+                            const uint32_t br = dup ? dup_ref_row(tv.dup_rows, r, tv.off_mask, (uint32_t)(t - p)) : r;
                             s_b[t - w0] = HAS_ROW_IDS ? tv.row_ids[br] : (uint64_t)br;
                             s_p[t - w0] = pidx;
                         }
@@ -1829,6 +1834,7 @@ dense_frag_build_kernel(ChunkGeom g, uint32_t nblk, int64_t ntiles, const uint16
         __syncthreads();
         for (unsigned li = threadIdx.x; li < ndup; li += T) {
             const unsigned n = d_cnt[li], off = d_off[li];
+            d_cur[li] = 0;  // (the placement cursor is done): a run ref, or 0
             if (n <= (unsigned)kSmallSeg) {
                 uint32_t v[16];
 #pragma unroll
@@ -1837,8 +1843,14 @@ dense_frag_build_kernel(ChunkGeom g, uint32_t nblk, int64_t ntiles, const uint16
 #pragma unroll
                 for (int i = 0; i < 16; ++i)
                     if (i < (int)n) dup_rows[off + 1 + i] = v[i];
+                // consecutive rows: the ref holds them (run ref, hj_device.h)
+                bool run = g.packed && n <= kRunMaxRows && v[0] < (1u << 24);
+#pragma unroll
+                for (int i = 1; i < (int)kRunMaxRows; ++i) run &= i >= (int)n || v[i] == v[0] - (uint32_t)i;
+                if (run) d_cur[li] = make_run_ref(v[0], n);
             }
         }
+        __syncthreads();
         for (uint32_t i = threadIdx.x; i < kDenseSub; i += T) {
             const uint32_t rv = img[i];
             if (rv != kMiss && (rv & kDupFlag)) {
@@ -1848,7 +1860,7 @@ dense_frag_build_kernel(ChunkGeom g, uint32_t nblk, int64_t ntiles, const uint16
                     big[bi] = BigSeg{(unsigned long long)((uint64_t)g.dmin + cbase + lo + i), d_off[li], 0u};
                 }
                 const uint32_t c4 = (g.packed && d_cnt[li] <= 15u) ? d_cnt[li] : 0u;
-                img[i] = kDupFlag | (c4 << 27) | d_off[li];
+                img[i] = d_cur[li] ? d_cur[li] : kDupFlag | (c4 << 27) | d_off[li];
             }
         }
         __syncthreads();
@@ -2847,10 +2859,7 @@ sl_lookup_kernel(TableView tv, uint32_t wlog, uint32_t nslices, int64_t ntiles, 
                     const bool special = o != kOob && v >= kDupFlag;
                     if (__ballot(special) != 0) {
                         uint32_t c = 1;  // row count (kCountUnknown: in its segment header)
-                        if (special) {
-                            const uint32_t c4 = tv.off_mask == kPackedMask ? ((v >> 27) & 15u) : 0u;
-                            c = v == kMiss ? 0u : c4 ? c4 : kCountUnknown;
-                        }
+                        if (special) c = ref_count_inline(v, tv.off_mask);
                         // counts not inline: read from the segment header in a wave-uniform branch
                         // that waits there. Merged into the common path, that load's wait was an
                         // s_waitcnt vmcnt(0) on every row — for the previous rows' ref stores (loads
@@ -3202,8 +3211,7 @@ hs_partition32_kernel(uint32_t nb, uint32_t slog, uint32_t s0, uint32_t nslices,
 // waiting for the next tile's prefetch in the emission's count pass and for the
 // previous step's stores in its write pass (C2 emit 222 -> ? us).
 __device__ __forceinline__ uint32_t sl_count(const TableView& tv, uint32_t r) {
-    const uint32_t c4 = tv.off_mask == kPackedMask ? ((r >> 27) & 15u) : 0u;
-    uint32_t c = r == kMiss ? 0u : !(r & kDupFlag) ? 1u : c4 ? c4 : kCountUnknown;
+    uint32_t c = ref_count_inline(r, tv.off_mask);
     if (__ballot(c == kCountUnknown) != 0) {
         if (c == kCountUnknown) c = tv.dup_rows[r & tv.off_mask];
         asm volatile("" : "+v"(c));  // the wait stays in this branch
@@ -3436,7 +3444,7 @@ sl_emit_kernel(TableView tv, const uint32_t* __restrict__ tent, const uint16_t* 
                         if (p < total && o < (unsigned long long)cap) {
                             const uint32_t br = !(rj & kDupFlag) ? rj
                                                 : DFP_ABL(8) ? (rj & tv.off_mask) + (p - xj)  // ablation: no segment reads
-                                                            : tv.dup_rows[(rj & tv.off_mask) + 1 + (p - xj)];
+                                                            : dup_ref_row(tv.dup_rows, rj, tv.off_mask, p - xj);
                             const int64_t rowj = tile0 + row_w + k + j;
                             put(o, HAS_ROW_IDS ? tv.row_ids[br] : (uint64_t)br,
                                 HAS_PROBE_IDS ? probe_ids[rowj] : (uint32_t)rowj + pbase);
@@ -3538,9 +3546,9 @@ __global__ void chain_links_kernel(TableView tv, int64_t* prev) {
             ref = tv.tbl[s / kSlots].ref[s % kSlots];
         }
         if (!(ref & kDupFlag)) continue;
-        const uint32_t* seg = tv.dup_rows + (ref & tv.off_mask);
-        const uint32_t c = seg[0];
-        for (uint32_t t = 0; t + 1 < c; ++t) prev[seg[1 + t]] = seg[2 + t];
+        const uint32_t c = ref_count(tv.dup_rows, ref, tv.off_mask);
+        for (uint32_t t = 0; t + 1 < c; ++t)
+            prev[dup_ref_row(tv.dup_rows, ref, tv.off_mask, t)] = dup_ref_row(tv.dup_rows, ref, tv.off_mask, t + 1);
     }
 }
 
@@ -4876,7 +4884,8 @@ __global__ void __launch_bounds__(256) dense_rebase_kernel(uint32_t* __restrict_
                                                            uint32_t mask) {
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
         const uint32_t r = refs[i];
-        if (r != kMiss && (r & kDupFlag)) refs[i] = (r & ~mask) | ((r & mask) + base);
+        // (a run ref holds its rows, not a segment offset: unchanged)
+        if (r != kMiss && (r & kDupFlag) && !run_ref(r, mask)) refs[i] = (r & ~mask) | ((r & mask) + base);
     }
 }
 

@@ -38,6 +38,9 @@ def _keys(kind, rng, nb, np_):
         bk = np.concatenate([rng.integers(0, nb // 8, nb - 400), np.full(400, nb // 16)])
         rng.shuffle(bk)
         pk = rng.integers(-50, nb // 8 + 50, np_)
+    elif kind == "runs":  # sorted build keys: duplicated keys on consecutive (global) rows, run refs
+        bk = np.repeat(np.arange(nb // 4, dtype=np.int64) * 2, 4)[:nb]
+        pk = rng.integers(-20, nb // 2 + 20, np_)
     elif kind == "clustered":  # build keys at both ends of the range: middle pieces empty
         bk = np.concatenate([rng.integers(0, 1000, nb // 2), rng.integers(7 * nb, 7 * nb + 1000, nb - nb // 2)])
         pk = rng.integers(-10, 7 * nb + 1010, np_)
@@ -148,7 +151,7 @@ def _sharded_rank(r, comm, world, bk, pk, valid, key_dtype, probe_dtype, base0, 
 
 
 @pytest.mark.parametrize("world", [2, 4, 8])
-@pytest.mark.parametrize("kind", ["dense", "dups", "clustered", "sparse_piece", "sparse", "dense_far"])
+@pytest.mark.parametrize("kind", ["dense", "dups", "runs", "clustered", "sparse_piece", "sparse", "dense_far"])
 def test_sharded_threads(ctl, oracle_mod, world, kind):
     rng = np.random.default_rng(world * 100 + len(kind))
     bk, pk = _keys(kind, rng, 60_000, 200_000)
@@ -235,7 +238,7 @@ def _merge(parts):
 
 
 @pytest.mark.parametrize("world", [1, 2, 4, 8])
-@pytest.mark.parametrize("kind", ["dense", "dups", "clustered", "sparse"])
+@pytest.mark.parametrize("kind", ["dense", "dups", "runs", "clustered", "sparse"])
 def test_radix_threads(ctl, oracle_mod, world, kind):
     rng = np.random.default_rng(world * 31 + len(kind))
     bk, pk = _keys(kind, rng, 60_000, 200_000)

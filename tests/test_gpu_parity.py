@@ -213,6 +213,73 @@ def test_exponential_keys_parity(dfp, oracle_mod, probe_mode):
     assert st["dup_keys"] > 0
 
 
+def _run_keys(rng, nkeys=3000, maxrun=12):
+    """Sorted build keys in runs of 1..maxrun rows (consecutive rows per key: run refs for
+    2..9 rows, dup_rows segments beyond), a few keys whose rows are not consecutive, and
+    probe keys over and beyond the build range."""
+    lens = rng.integers(1, maxrun + 1, nkeys)
+    bk = np.repeat(np.arange(nkeys, dtype=np.int64) * 3, lens)
+    # keys whose rows are split (not a run): the same key again further on
+    bk = np.concatenate([bk, bk[:: max(1, len(bk) // 50)]])
+    pk = rng.integers(-5, nkeys * 3 + 5, 40000).astype(np.int64)
+    return bk, pk
+
+
+def test_run_refs_parity(dfp, oracle_mod, probe_mode):
+    """Run refs (hj_device.h): keys with consecutive rows keep them in the ref (2..9 rows),
+    longer or split ones keep their dup_rows segment; nulls break runs; two partitions
+    number rows across the partition boundary. Bit-exact against the oracle under every
+    probe strategy, table layout and tile size."""
+    rng = np.random.default_rng(61)
+    bk, pk = _run_keys(rng)
+    b, p, st = gpu_join(dfp, bk, pk)
+    ob, op = oracle_mod.inner_join(bk, pk)
+    assert_same(b, p, ob, op)
+    assert st["max_key_rows"] >= 12
+    bv = rng.random(len(bk)) > 0.05
+    n = len(bk)
+    b, p, _ = gpu_join(dfp, bk, pk, bvalid=bv, parts=[0, n // 3, n])
+    ob, op = oracle_mod.inner_join(bk, pk, bv, None)
+    assert_same(b, p, ob, op)
+
+
+def test_run_refs_chain_links_and_stats(dfp):
+    """hj_table_chain_links and hj_table_stats decode run refs: sorted keys in runs."""
+    rng = np.random.default_rng(62)
+    bk, _ = _run_keys(rng, nkeys=2000)
+    with dfp.HashTable(1, "int64", 0) as t:
+        t.build(torch.from_numpy(bk).cuda())
+        prev = t.chain_links(len(bk))
+        st = t.stats()
+    last = {}
+    want = np.full(len(bk), -1, np.int64)
+    for i, k in enumerate(bk.tolist()):
+        want[i] = last.get(k, -1)
+        last[k] = i
+    assert np.array_equal(prev, want)
+    vals, cnt = np.unique(bk, return_counts=True)
+    assert st["distinct_keys"] == len(vals) and st["dup_keys"] == int((cnt > 1).sum())
+    assert st["dup_rows"] == int(cnt[cnt > 1].sum()) and st["max_key_rows"] == int(cnt.max())
+
+
+@pytest.mark.parametrize("pmode", [4, 3])
+def test_run_refs_rows_past_2_24(dfp, oracle_mod, pmode):
+    """Runs whose top row is >= 2^24 keep their dup_rows segment (the run ref holds 24
+    bits): a 17.5 M-row sorted build with keys in pairs, probed across the 2^24 boundary."""
+    L = dfp.load()
+    old = L.hj_set_probe_mode(pmode)
+    try:
+        nb = 17_500_000
+        bk = np.arange(nb, dtype=np.int64) // 2
+        pk = np.concatenate([np.arange(8_300_000, 8_450_000, dtype=np.int64),
+                             np.arange(0, 10_000, dtype=np.int64), np.array([nb // 2 - 1, nb // 2 + 3])])
+        b, p, st = gpu_join(dfp, bk, pk)
+    finally:
+        L.hj_set_probe_mode(old)
+    ob, op = oracle_mod.inner_join(bk, pk)
+    assert_same(b, p, ob, op)
+
+
 @pytest.mark.parametrize("frag_t", ["512", "1024"])
 def test_frag_build_workgroup_sizes(dfp, oracle_mod, monkeypatch, frag_t):
     """Both forms of the dense frag build (DFP_HJ_FRAG_T: 512 threads x 16 rows, the

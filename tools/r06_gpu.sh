@@ -53,6 +53,22 @@ pmc)
     python3 tools/traffic_summary.py $O/pmc_$cfg $cfg > $O/traffic_$cfg.txt
     head -30 $O/traffic_$cfg.txt
   done ;;
+sq)
+  # SQ counters of the sliced kernels (tools/probe_one.py), one rocprofv3 pass per counter set
+  # and RUNS entry; CTRS1 / CTRS2 (<= 8 SQ counters each)
+  C1=${CTRS1:-"SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM SQ_INSTS_VALU"}
+  C2=${CTRS2:-"SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_INST_LDS SQ_ACTIVE_INST_SCA SQ_INSTS_BRANCH SQ_WAVES"}
+  for cfg in ${CFGS:-c3}; do
+    for r in ${RUNS:-prod:}; do
+      n=${r%%:*}; ev=${r#*:}; i=0
+      for C in "$C1" "$C2"; do
+        i=$((i+1))
+        env ${ev//,/ } timeout -s KILL 120 rocprofv3 --pmc $C -d $O/sq_${cfg}_${n}_$i -o pmc --output-format csv -- \
+            python3 tools/probe_one.py --config=$cfg > $O/sq_${cfg}_${n}_$i.log 2>&1 || { echo "FAILED sq $cfg $n"; exit 1; }
+        python3 tools/pmc_kernels.py $O/sq_${cfg}_${n}_$i "sl_lookup|hs_part|sl_emit|sl_partition" | sed "s/^/$cfg $n /"
+      done
+    done
+  done ;;
 kt)
   step 300 rocprofv3 --kernel-trace --stats -d $O/kt_c2 -o kt --output-format csv -- python3 bench.py --no-cpu-baseline > $O/kt_c2.json 2> $O/kt_c2.err
   python3 tools/kstats.py $O/kt_c2 > $O/kt_c2.txt; head -8 $O/kt_c2.txt ;;
