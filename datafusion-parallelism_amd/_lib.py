@@ -131,6 +131,9 @@ SIGNATURES = [
     ("hj_dist_job_times", I32, [P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
                                 ctypes.POINTER(ctypes.c_double)]),
     ("hj_dist_job_free", None, [P]),
+    ("hj_dist_shuffle", I32, [P, I32, P, I64, I32, P, P, P, PP]),
+    ("hj_dist_gather", I32, [P, I64, I32, P, P, P, PP]),
+    ("hj_dist_job_columns", I32, [P, P, PP, P, I32, ctypes.POINTER(ctypes.c_int64)]),
     ("hj_gen_perm_keys", I32, [P, I64, I64, I64, P]),
     ("hj_gen_uniform_keys", I32, [P, I64, U64, I64, P]),
     ("hj_gen_exponential_keys", I32, [P, I32, I32]),

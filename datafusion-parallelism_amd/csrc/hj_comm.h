@@ -82,6 +82,10 @@ struct hj_dist_job {
     int64_t rvoff = 0, pbase = 0;
     void* ws = nullptr;
     hipStream_t stream = nullptr;
+    // exchange jobs (hj_dist_shuffle / hj_dist_gather): the received rows, job-owned blocks
+    const void* out_keys = nullptr;
+    std::vector<const void*> out_cols;
+    int64_t out_rows = -1;
     std::vector<std::pair<void*, size_t>> blocks;  // job-owned device blocks
     struct hj_comm* comm = nullptr;  // valid until hj_comm_free (the job's free needs only `device`)
     int device = 0;

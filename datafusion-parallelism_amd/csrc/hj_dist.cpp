@@ -964,6 +964,174 @@ hj_status run_radix(hj_comm* c, const RadixArgs& a, hj_dist_job* j, int64_t jobn
     return scr.defer();
 }
 
+// ---- relational exchanges (TPC-H plans: tpch.q3_dist / q9_dist) --------
+
+// grouped exchange: this rank's rows grouped by destination (m[me][d] rows for peer d, in
+// destination order) to their owners; rank src's rows for this rank land at the rows of the
+// ranks before src (stable: source rank, then source row order); the own group by a device copy
+hj_status exchange_grouped(hj_comm* c, const std::vector<int64_t>& m, const char* grouped, int esz, char* out,
+                           hipStream_t s) {
+    const int W = c->world, me = c->rank;
+    std::vector<int64_t> soff(W, 0), roff(W, 0);
+    for (int d = 1; d < W; ++d) soff[d] = soff[d - 1] + m[(size_t)me * W + d - 1];
+    for (int src = 1; src < W; ++src) roff[src] = roff[src - 1] + m[(size_t)(src - 1) * W + me];
+    const int64_t self = m[(size_t)me * W + me];
+    if (self > 0)
+        HIP_OK(hipMemcpyAsync(out + roff[me] * esz, grouped + soff[me] * esz, (size_t)self * esz,
+                              hipMemcpyDeviceToDevice, s));
+    const int64_t per = std::max<int64_t>(1, (int64_t)(kMaxMsgBytes / (size_t)esz));
+    for (int p = 0; p < W; ++p) {
+        if (p == me) continue;
+        const int64_t ns = m[(size_t)me * W + p], nr = m[(size_t)p * W + me];
+        for (int64_t a = 0; a < ns; a += per)
+            ST_OK(c->tr->send(grouped + (soff[p] + a) * esz, (size_t)std::min(per, ns - a) * esz, p, s));
+        for (int64_t a = 0; a < nr; a += per)
+            ST_OK(c->tr->recv(out + (roff[p] + a) * esz, (size_t)std::min(per, nr - a) * esz, p, s));
+    }
+    return HJ_OK;
+}
+
+struct ExchangeArgs {
+    hj_key_type kt;  // shuffle: the key column's type
+    const void* keys;  // shuffle: the key column; gather: null
+    int64_t n;
+    std::vector<const void*> cols;
+    std::vector<int> widths;
+};
+
+bool width_ok(int w) { return w == 1 || w == 2 || w == 4 || w == 8 || w == 16; }
+
+// the received buffers: after the last status exchange, so a failure is one-sided and aborts
+// the communicator (its peers' transfers would otherwise wait for it forever)
+hj_status recv_buffers(hj_comm* c, Scratch& scr, hj_dist_job* j, int64_t R, int kb, const ExchangeArgs& a,
+                       char** rk, std::vector<char*>* rc) {
+    bool ok = true;
+    if (kb) ok = (*rk = (char*)scr.get((size_t)std::max<int64_t>(R, 1) * kb)) != nullptr;
+    rc->assign(a.cols.size(), nullptr);
+    for (size_t i = 0; ok && i < a.cols.size(); ++i)
+        ok = ((*rc)[i] = (char*)scr.get((size_t)std::max<int64_t>(R, 1) * a.widths[i])) != nullptr;
+    if (!ok) {
+        if (c->tr) c->tr->abort();
+        c->aborted = true;
+        return set_error(HJ_ERR_OOM, "hj_dist: device allocation failed (received rows); the communicator was aborted");
+    }
+    if (kb) scr.give(j, *rk);
+    for (char* p : *rc) scr.give(j, p);
+    j->out_keys = kb ? *rk : nullptr;
+    j->out_cols.assign(rc->begin(), rc->end());
+    j->out_rows = R;
+    return HJ_OK;
+}
+
+// Hash repartition of a key column with fixed-width payload columns (DataFusion's
+// RepartitionExec Hash over the links): row i goes to rank (mix64 hash bits of its key, the
+// hj_partition_rows map) with its payload; received rows in (source rank, source row)
+// order. One rank: the rows as they are (copied into the job's buffers).
+hj_status run_shuffle(hj_comm* c, const ExchangeArgs& a, hj_dist_job* j, int64_t jobno) {
+    const int W = c->world, me = c->rank;
+    const int kb = a.kt == HJ_INT64 ? 8 : 4;
+    hipStream_t s = c->side;
+    HIP_OK(hipStreamWaitEvent(s, j->ev_in, 0));
+    Scratch scr(c, {s});
+    LocalFail lf;
+    auto get = [&](size_t bytes, const char* what) -> void* {
+        void* p = scr.get(bytes);
+        if (!p) lf.note_oom(what);
+        return p;
+    };
+    const int64_t n = a.n, cap = std::max<int64_t>(n, 1);
+    if (W == 1) {
+        char* rk = nullptr;
+        std::vector<char*> rc;
+        ST_OK(recv_buffers(c, scr, j, n, kb, a, &rk, &rc));
+        if (n > 0) {
+            HIP_OK(hipMemcpyAsync(rk, a.keys, (size_t)n * kb, hipMemcpyDeviceToDevice, s));
+            for (size_t i = 0; i < a.cols.size(); ++i)
+                HIP_OK(hipMemcpyAsync(rc[i], a.cols[i], (size_t)n * a.widths[i], hipMemcpyDeviceToDevice, s));
+        }
+        HIP_OK(hipEventRecord(j->ev_total, s));
+        return scr.defer();
+    }
+    // 1. keys grouped by destination, ids = source rows (the stable permutation), each
+    // payload column gathered by it; the counts with this rank's status, all-gathered
+    const Words w = words_of(c);
+    const int ib = n < ((int64_t)1 << 32) ? 4 : 8;
+    char* gk = (char*)get((size_t)cap * kb, "grouped keys");
+    void* perm = get((size_t)cap * ib, "permutation");
+    void* pws = get((size_t)std::max<int64_t>(hj_partition_workspace_bytes(n, W), 8), "workspace");
+    std::vector<char*> gc(a.cols.size(), nullptr);
+    for (size_t i = 0; i < a.cols.size(); ++i) gc[i] = (char*)get((size_t)cap * a.widths[i], "grouped payload");
+    if (injected(c, jobno, 1)) lf.note(set_error(HJ_ERR_INVALID, "injected failure (test hook) at the partition"));
+    if (!lf.failed && n > 0)
+        lf.note(hj_partition_rows(a.kt, a.keys, nullptr, 0, nullptr, 0, n, W, nullptr, gk, kb, 0, perm, ib, w.cnt,
+                                  pws, s));
+    for (size_t i = 0; i < a.cols.size() && !lf.failed; ++i)
+        if (n > 0) lf.note(hj_gather_fixed(a.cols[i], nullptr, 0, a.widths[i], perm, ib, n, gc[i], nullptr, s));
+    if (lf.failed || n == 0) HIP_OK(hipMemsetAsync(w.cnt, 0, 8 * (size_t)W, s));
+    {
+        int64_t f = lf.failed ? 1 : 0;
+        ST_OK(write_dev(c, w.cnt + W, &f, 1, s));
+    }
+    ST_OK(allgather_read(c, w.cnt, w.allc, W + 1, s));
+    std::vector<int64_t> m((size_t)W * W);
+    bool anyfail = false;
+    for (int src = 0; src < W; ++src) {
+        for (int d = 0; d < W; ++d) m[(size_t)src * W + d] = c->host[(size_t)src * (W + 1) + d];
+        anyfail |= c->host[(size_t)src * (W + 1) + W] != 0;
+    }
+    if (anyfail) return lf.raise("the shuffle's partition");
+    if (!counts_ok(m, W, me, n)) return set_error(HJ_ERR_HIP, "hj_dist_shuffle: partition count out of range");
+    int64_t R = 0;
+    for (int src = 0; src < W; ++src) R += m[(size_t)src * W + me];
+    // 2. the received rows: keys, then every payload column, per peer in one group
+    char* rk = nullptr;
+    std::vector<char*> rc;
+    ST_OK(recv_buffers(c, scr, j, R, kb, a, &rk, &rc));
+    ST_OK(c->tr->group_start());
+    ST_OK(exchange_grouped(c, m, gk, kb, rk, s));
+    for (size_t i = 0; i < a.cols.size(); ++i) ST_OK(exchange_grouped(c, m, gc[i], a.widths[i], rc[i], s));
+    ST_OK(c->tr->group_end(s));
+    HIP_OK(hipEventRecord(j->ev_total, s));
+    return scr.defer();
+}
+
+// Broadcast exchange: every rank receives the concatenation, in rank order, of all ranks'
+// rows of the columns (the small filtered dimension sides of a plan, per-rank partial
+// results); one all-gather of the row counts, then the columns (an even split in one
+// all-gather, else point to point).
+hj_status run_gather(hj_comm* c, const ExchangeArgs& a, hj_dist_job* j, int64_t jobno) {
+    const int W = c->world;
+    hipStream_t s = c->side;
+    HIP_OK(hipStreamWaitEvent(s, j->ev_in, 0));
+    Scratch scr(c, {s});
+    const Words w = words_of(c);
+    {
+        int64_t v[2] = {a.n, injected(c, jobno, 0) ? 1 : 0};
+        ST_OK(write_dev(c, w.st, v, 2, s));
+    }
+    ST_OK(allgather_read(c, w.st, w.allst, 2, s));
+    std::vector<int64_t> lens(W), offs(W, 0);
+    bool anyfail = false;
+    for (int d = 0; d < W; ++d) {
+        lens[d] = c->host[2 * d];
+        anyfail |= c->host[2 * d + 1] != 0 || lens[d] < 0;
+    }
+    if (anyfail) {
+        LocalFail lf;
+        if (injected(c, jobno, 0)) lf.note(set_error(HJ_ERR_INVALID, "injected failure (test hook) at the gather"));
+        return lf.raise("the gather's row counts");
+    }
+    for (int d = 1; d < W; ++d) offs[d] = offs[d - 1] + lens[d - 1];
+    const int64_t R = offs[W - 1] + lens[W - 1];
+    char* rk = nullptr;
+    std::vector<char*> rc;
+    ST_OK(recv_buffers(c, scr, j, R, 0, a, &rk, &rc));
+    for (size_t i = 0; i < a.cols.size(); ++i)
+        ST_OK(allgather_var(c, rc[i], offs, lens, (const char*)a.cols[i], a.widths[i], s));
+    HIP_OK(hipEventRecord(j->ev_total, s));
+    return scr.defer();
+}
+
 // ---- the worker ----------------------------------------------------------------------------
 
 void worker_loop(hj_comm* c) {
@@ -1207,6 +1375,78 @@ hj_status hj_dist_join_radix(hj_comm* c, hj_key_type build_key_type, const void*
         return st;
     }
     *out = j;
+    return HJ_OK;
+}
+
+hj_status hj_dist_shuffle(hj_comm* c, hj_key_type key_type, const void* keys, int64_t n, int ncols,
+                          const void* const* cols, const int* col_bytes, void* stream, hj_dist_job** out) {
+    if (out == nullptr) return set_error(HJ_ERR_INVALID, "null out");
+    *out = nullptr;
+    ST_OK(check_comm(c));
+    if (key_type != HJ_INT32 && key_type != HJ_INT64) return set_error(HJ_ERR_INVALID, "unsupported key type");
+    if (n < 0 || ncols < 0 || (ncols > 0 && (cols == nullptr || col_bytes == nullptr)))
+        return set_error(HJ_ERR_INVALID, "negative n/ncols or null columns");
+    if (n > 0 && keys == nullptr) return set_error(HJ_ERR_INVALID, "null keys");
+    if ((c->world & (c->world - 1)) != 0 || c->world > 64)
+        return set_error(HJ_ERR_INVALID, "hj_dist_shuffle: the hash map needs a power-of-two world <= 64");
+    ExchangeArgs a{key_type, keys, n, {}, {}};
+    for (int i = 0; i < ncols; ++i) {
+        if (!width_ok(col_bytes[i])) return set_error(HJ_ERR_INVALID, "payload column width must be 1/2/4/8/16 bytes");
+        if (n > 0 && cols[i] == nullptr) return set_error(HJ_ERR_INVALID, "null payload column");
+        a.cols.push_back(cols[i]);
+        a.widths.push_back(col_bytes[i]);
+    }
+    hj_dist_job* j = nullptr;
+    ST_OK(new_job(c, true, stream, &j));
+    const int64_t no = c->jobs++;
+    j->fn = [c, a, no](hj_dist_job* jj) { return run_shuffle(c, a, jj, no); };
+    hj_status st = submit(c, j);
+    if (st != HJ_OK) {
+        hj_dist_job_free(j);
+        return st;
+    }
+    *out = j;
+    return HJ_OK;
+}
+
+hj_status hj_dist_gather(hj_comm* c, int64_t n, int ncols, const void* const* cols, const int* col_bytes,
+                         void* stream, hj_dist_job** out) {
+    if (out == nullptr) return set_error(HJ_ERR_INVALID, "null out");
+    *out = nullptr;
+    ST_OK(check_comm(c));
+    if (n < 0 || ncols < 1 || cols == nullptr || col_bytes == nullptr)
+        return set_error(HJ_ERR_INVALID, "negative n or no columns");
+    ExchangeArgs a{HJ_INT64, nullptr, n, {}, {}};
+    for (int i = 0; i < ncols; ++i) {
+        if (!width_ok(col_bytes[i])) return set_error(HJ_ERR_INVALID, "column width must be 1/2/4/8/16 bytes");
+        if (n > 0 && cols[i] == nullptr) return set_error(HJ_ERR_INVALID, "null column");
+        a.cols.push_back(cols[i]);
+        a.widths.push_back(col_bytes[i]);
+    }
+    hj_dist_job* j = nullptr;
+    ST_OK(new_job(c, true, stream, &j));
+    const int64_t no = c->jobs++;
+    j->fn = [c, a, no](hj_dist_job* jj) { return run_gather(c, a, jj, no); };
+    hj_status st = submit(c, j);
+    if (st != HJ_OK) {
+        hj_dist_job_free(j);
+        return st;
+    }
+    *out = j;
+    return HJ_OK;
+}
+
+hj_status hj_dist_job_columns(hj_dist_job* j, void* stream, const void** keys, const void** cols, int ncols,
+                              int64_t* rows) {
+    if (j == nullptr || rows == nullptr || (ncols > 0 && cols == nullptr)) return set_error(HJ_ERR_INVALID, "null args");
+    ST_OK(wait_job(j));
+    if (j->out_rows < 0) return set_error(HJ_ERR_INVALID, "hj_dist_job_columns: not an exchange job");
+    if ((size_t)ncols != j->out_cols.size()) return set_error(HJ_ERR_INVALID, "hj_dist_job_columns: column count");
+    HIP_OK(hipSetDevice(j->device));
+    HIP_OK(hipStreamWaitEvent((hipStream_t)stream, j->ev_total, 0));  // consumers on `stream` follow the exchange
+    if (keys) *keys = j->out_keys;
+    for (int i = 0; i < ncols; ++i) cols[i] = j->out_cols[(size_t)i];
+    *rows = j->out_rows;
     return HJ_OK;
 }
 

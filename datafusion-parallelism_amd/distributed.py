@@ -468,6 +468,17 @@ class _DevArray:
                                          "version": 2}
 
 
+_TYPESTR = {torch.int64: "<i8", torch.int32: "<i4", torch.int16: "<i2", torch.int8: "|i1", torch.uint8: "|u1",
+            torch.bool: "|b1", torch.float64: "<f8", torch.float32: "<f4"}
+
+
+def _tensor_any(ptr: int | None, n: int, dtype: torch.dtype, device: torch.device, owner) -> torch.Tensor:
+    """A device tensor of `dtype` over a job-owned buffer (the owner lives as long as it)."""
+    if n == 0 or not ptr:
+        return torch.empty(0, dtype=dtype, device=device)
+    return torch.as_tensor(_DevArray(ptr, n, _TYPESTR[dtype], owner), device=device)
+
+
 def _tensor_of(ptr: int, n: int, dtype: torch.dtype, device: torch.device, owner) -> torch.Tensor:
     if n == 0 or not ptr:
         return torch.empty(0, dtype=dtype, device=device)
@@ -482,6 +493,7 @@ class NativeJob:
     def __init__(self, L, handle: ctypes.c_void_p, device: torch.device, keep=(), key_type: int = HJ_INT64):
         self._L, self._h, self.device, self._keep, self.key_type = L, handle, device, list(keep), key_type
         self._consumers = []  # torch streams current when pairs() handed out the job's buffers
+        self.key_dtype, self.col_dtypes = None, []  # exchange jobs: the received columns' dtypes
 
     def wait(self):
         info = _lib.HjDistInfo()
@@ -506,6 +518,22 @@ class NativeJob:
             self._consumers.append(cur)
         return (_tensor_of(b.value, n.value, torch.int64, self.device, self),
                 _tensor_of(p.value, n.value, torch.int32, self.device, self))
+
+    def columns(self):
+        """An exchange job's received rows (hj_dist_job_columns; torch's current stream waits
+        for the exchange) -> (keys or None, [columns]) as device tensors over the job's
+        buffers (no copy), in the dtypes of the submitted columns."""
+        n = len(self.col_dtypes)
+        k = ctypes.c_void_p()
+        cols = (ctypes.c_void_p * max(n, 1))()
+        rows = ctypes.c_int64()
+        stream = torch.cuda.current_stream(self.device)
+        check_l(self._L, self._L.hj_dist_job_columns(self._h, stream.cuda_stream or None, ctypes.byref(k), cols, n,
+                                                     ctypes.byref(rows)))
+        if all(c != stream for c in self._consumers):
+            self._consumers.append(stream)
+        keys = None if self.key_dtype is None else _tensor_any(k.value, rows.value, self.key_dtype, self.device, self)
+        return keys, [_tensor_any(cols[i], rows.value, dt, self.device, self) for i, dt in enumerate(self.col_dtypes)]
 
     def times(self) -> tuple[float, float, float]:
         """(build_ms, exchange_ms, probe_ms) of the finished job's device stages."""
@@ -617,6 +645,41 @@ class NativeComm:
             None if probe_valid is None else probe_valid.data_ptr(), probe_valid_offset, probe_keys.numel(), probe_base,
             stream or None, ctypes.byref(h)))
         return NativeJob(self._L, h, probe_keys.device, keep=[build_keys, probe_keys, build_valid, probe_valid])
+
+    def shuffle(self, keys: torch.Tensor, payload: list[torch.Tensor], stream: int | None = None) -> NativeJob:
+        """hj_dist_shuffle: hash repartition of `keys` (int32 / int64) with fixed-width payload
+        columns -> a NativeJob whose columns() are the received (keys, payload), ordered by
+        (source rank, source row)."""
+        keys = keys.contiguous()
+        payload = [p.contiguous() for p in payload]
+        for p in payload:
+            assert p.numel() == keys.numel(), "shuffle: payload columns of the keys' length"
+        n = len(payload)
+        ptrs = (ctypes.c_void_p * max(n, 1))(*[p.data_ptr() if p.numel() else None for p in payload])
+        widths = (ctypes.c_int * max(n, 1))(*[p.element_size() for p in payload])
+        s = stream if stream is not None else torch.cuda.current_stream(keys.device).cuda_stream
+        h = ctypes.c_void_p()
+        check_l(self._L, self._L.hj_dist_shuffle(self._h, self._kt(keys), keys.data_ptr() if keys.numel() else None,
+                                                 keys.numel(), n, ptrs, widths, s or None, ctypes.byref(h)))
+        job = NativeJob(self._L, h, keys.device, keep=[keys] + payload)
+        job.key_dtype, job.col_dtypes = keys.dtype, [p.dtype for p in payload]
+        return job
+
+    def gather(self, cols: list[torch.Tensor], stream: int | None = None) -> NativeJob:
+        """hj_dist_gather: every rank receives all ranks' rows of `cols` in rank order ->
+        a NativeJob whose columns() are (None, the gathered columns)."""
+        cols = [c.contiguous() for c in cols]
+        n = cols[0].numel()
+        for c in cols:
+            assert c.numel() == n, "gather: columns of one length"
+        ptrs = (ctypes.c_void_p * len(cols))(*[c.data_ptr() if c.numel() else None for c in cols])
+        widths = (ctypes.c_int * len(cols))(*[c.element_size() for c in cols])
+        s = stream if stream is not None else torch.cuda.current_stream(cols[0].device).cuda_stream
+        h = ctypes.c_void_p()
+        check_l(self._L, self._L.hj_dist_gather(self._h, n, len(cols), ptrs, widths, s or None, ctypes.byref(h)))
+        job = NativeJob(self._L, h, cols[0].device, keep=cols)
+        job.col_dtypes = [c.dtype for c in cols]
+        return job
 
     def close(self):
         if getattr(self, "_h", None):
@@ -1264,6 +1327,67 @@ class DistributedHashJoin:
 
 
 # ---- relational exchanges for multi-GPU query plans (TPC-H C4/C5, tpch.py) -------------
+
+class TorchExchange:
+    """A query plan's exchanges over torch.distributed (gloo on the CPU tests, or RCCL):
+    `shuffle` (hash repartition with payload), `gather` (rows of every rank in rank order)
+    and `sum` (an element-wise sum over the ranks)."""
+
+    def __init__(self, group=None, partition_fn: Callable | None = None):
+        self.group, self.partition_fn = group, partition_fn
+
+    def shuffle(self, keys: torch.Tensor, payload: list[torch.Tensor]):
+        return shuffle(keys, payload, self.group, self.partition_fn)
+
+    def gather(self, cols: list[torch.Tensor]) -> list[torch.Tensor]:
+        return all_gather_rows(cols, self.group)
+
+    def sum(self, t: torch.Tensor) -> torch.Tensor:
+        t = t.clone()
+        dist.all_reduce(t, group=self.group)
+        return t
+
+
+class NativeExchange:
+    """The same exchanges as jobs of an hj_comm behind the C ABI (hj_dist_shuffle /
+    hj_dist_gather, RCCL inside the library, or the test library's thread transport): the
+    whole query's data movement goes through include/hj.h, as a Rust host would drive it
+    (INTEGRATION.md §8). `sum` gathers one row per rank and adds them on the device."""
+
+    def __init__(self, comm: "NativeComm", world: int):
+        self.comm, self.world = comm, world
+
+    def shuffle(self, keys: torch.Tensor, payload: list[torch.Tensor]):
+        job = self.comm.shuffle(keys, payload)
+        k, cols = job.columns()
+        return k, cols
+
+    def gather(self, cols: list[torch.Tensor]) -> list[torch.Tensor]:
+        _, out = self.comm.gather(cols).columns()
+        return out
+
+    def sum(self, t: torch.Tensor) -> torch.Tensor:
+        (g,) = self.gather([t.reshape(-1)])
+        return g.reshape(self.world, -1).sum(0).reshape(t.shape)
+
+
+_NATIVE_COMMS: dict = {}
+
+
+def default_exchange(group=None, partition_fn: Callable | None = None):
+    """The plans' exchange for `group`: jobs of a (cached) hj_comm on an RCCL group with a
+    power-of-two world and no stand-in partition function; torch.distributed otherwise."""
+    if partition_fn is not None or dist.get_backend(group) != "nccl":
+        return TorchExchange(group, partition_fn)
+    world = dist.get_world_size(group)
+    if world & (world - 1):
+        return TorchExchange(group, partition_fn)
+    dev = torch.device("cuda", torch.cuda.current_device())
+    key = (id(group), dev.index)
+    if key not in _NATIVE_COMMS:
+        _NATIVE_COMMS[key] = NativeComm(dev, group)
+    return NativeExchange(_NATIVE_COMMS[key], world)
+
 
 def all_gather_rows(cols: list[torch.Tensor], group=None, sizes: list[int] | None = None) -> list[torch.Tensor]:
     """Broadcast exchange: every rank receives the concatenation, in rank order, of all

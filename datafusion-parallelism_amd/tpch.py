@@ -377,29 +377,30 @@ def _order_q3(okey: torch.Tensor, rev: torch.Tensor, odate: torch.Tensor) -> tor
 
 
 def q3_dist(t: Tables, segment: str = "BUILDING", date: str = "1995-03-15", limit: int = 10, group=None,
-            join_fn=None, partition_fn=None) -> Q3Result:
+            join_fn=None, partition_fn=None, exchange=None) -> Q3Result:
     """Q3 over rank-sharded tables (generate(..., rank, world)); the result on every rank.
 
     customer (filtered) is broadcast; the qualifying orders and the ship-date-filtered
     lines are hash-repartitioned on orderkey with their payload, so each order's group
     lives on exactly one rank; the per-rank top-`limit` candidates are gathered and
-    merged. `join_fn(build, probe) -> (build rows, probe rows)` defaults to the GPU hash
-    join (the stand-in hook exists only for the CPU gloo tests)."""
-    import torch.distributed as dist
+    merged. `exchange` moves the data (distributed.default_exchange: on an RCCL group the
+    hj_dist_shuffle / hj_dist_gather jobs of the C ABI, else torch.distributed);
+    `join_fn(build, probe) -> (build rows, probe rows)` defaults to the GPU hash join (the
+    stand-in hooks exist only for the CPU gloo tests)."""
+    from .distributed import check_ids, default_exchange
 
-    from .distributed import all_gather_rows, check_ids, shuffle
-
+    ex = exchange or default_exchange(group, partition_fn)
     join = join_fn or _join
     seg = SEGMENTS.index(segment)
     d = day(date)
-    (cust,) = all_gather_rows([t.c_custkey[t.c_mktsegment == seg]], group)
+    (cust,) = ex.gather([t.c_custkey[t.c_mktsegment == seg]])
     o_rows = torch.nonzero(t.o_orderdate < d).squeeze(1)
     _, po = join(cust, t.o_custkey[o_rows])
     sel = o_rows[po]
-    ok, (od, osp) = shuffle(t.o_orderkey[sel], [t.o_orderdate[sel], t.o_shippriority[sel]], group, partition_fn)
+    ok, (od, osp) = ex.shuffle(t.o_orderkey[sel], [t.o_orderdate[sel], t.o_shippriority[sel]])
     l_rows = torch.nonzero(t.l_shipdate > d).squeeze(1)
     rev = t.l_extendedprice[l_rows] * (100 - t.l_discount[l_rows].to(torch.int64))
-    lk, (lrev,) = shuffle(t.l_orderkey[l_rows], [rev], group, partition_fn)
+    lk, (lrev,) = ex.shuffle(t.l_orderkey[l_rows], [rev])
     bo, pl = join(ok, lk)
     check_ids(bo, ok.numel(), "q3_dist order rows")
     sums = torch.zeros(ok.numel(), dtype=torch.int64, device=ok.device).index_add_(0, bo, lrev[pl])
@@ -408,49 +409,47 @@ def q3_dist(t: Tables, segment: str = "BUILDING", date: str = "1995-03-15", limi
     g = torch.nonzero(has).squeeze(1)
     okey, r, dt, sp = ok[g], sums[g], od[g], osp[g]
     top = _order_q3(okey, r, dt)[:limit]
-    ngroups = torch.tensor([g.numel()], dtype=torch.int64, device=ok.device)
-    dist.all_reduce(ngroups, group=group)
-    okey, r, dt, sp = all_gather_rows([okey[top], r[top], dt[top], sp[top]], group)
+    ngroups = ex.sum(torch.tensor([g.numel()], dtype=torch.int64, device=ok.device))
+    okey, r, dt, sp = ex.gather([okey[top], r[top], dt[top], sp[top]])
     top = _order_q3(okey, r, dt)[:limit]
     return Q3Result(okey[top].tolist(), r[top].tolist(), dt[top].tolist(), sp[top].tolist(), int(ngroups.item()))
 
 
-def q9_dist(t: Tables, group=None, join_fn=None, partition_fn=None) -> list[tuple[str, int, int]]:
+def q9_dist(t: Tables, group=None, join_fn=None, partition_fn=None, exchange=None) -> list[tuple[str, int, int]]:
     """Q9 over rank-sharded tables; the result on every rank.
 
     green part keys and supplier are broadcast; lineitem (green parts only) and partsupp
     are repartitioned on (partkey, suppkey), then the joined lines and orders on
-    orderkey; the (nation, year) sums merge with one int64 all-reduce."""
-    import torch.distributed as dist
-
-    from .distributed import all_gather_rows, check_ids, shuffle
+    orderkey; the (nation, year) sums merge with one sum over the ranks. `exchange`: as
+    q3_dist's."""
+    from .distributed import check_ids, default_exchange
 
     if t.l_partkey is None:
         raise ValueError("generate(..., q9=True) tables are needed")
+    ex = exchange or default_exchange(group, partition_fn)
     join = join_fn or _join
     dev = t.device
-    (green,) = all_gather_rows([t.p_partkey[t.p_green]], group)
+    (green,) = ex.gather([t.p_partkey[t.p_green]])
     _, li = join(green, t.l_partkey)
     gross = t.l_extendedprice[li] * (100 - t.l_discount[li].to(torch.int64))
     psk = (t.l_partkey[li] << 32) | t.l_suppkey[li]
-    lk, (ls, lok, gross, qty) = shuffle(psk, [t.l_suppkey[li], t.l_orderkey[li], gross, t.l_quantity[li]], group,
-                                        partition_fn)
-    pk, (cost,) = shuffle((t.ps_partkey << 32) | t.ps_suppkey, [t.ps_supplycost], group, partition_fn)
+    lk, (ls, lok, gross, qty) = ex.shuffle(psk, [t.l_suppkey[li], t.l_orderkey[li], gross, t.l_quantity[li]])
+    pk, (cost,) = ex.shuffle((t.ps_partkey << 32) | t.ps_suppkey, [t.ps_supplycost])
     b_ps, p_l = join(pk, lk)
     amount = gross[p_l] - cost[b_ps] * qty[p_l] * 100
     ls, lok = ls[p_l], lok[p_l]
-    s_key, s_nat = all_gather_rows([t.s_suppkey, t.s_nationkey], group)
+    s_key, s_nat = ex.gather([t.s_suppkey, t.s_nationkey])
     b_s, p_l = join(s_key, ls)
     nation, amount, lok = s_nat[b_s], amount[p_l], lok[p_l]
-    ok, (year,) = shuffle(t.o_orderkey, [year_of(t.o_orderdate)], group, partition_fn)
-    lk2, (nat2, amt2) = shuffle(lok, [nation, amount], group, partition_fn)
+    ok, (year,) = ex.shuffle(t.o_orderkey, [year_of(t.o_orderdate)])
+    lk2, (nat2, amt2) = ex.shuffle(lok, [nation, amount])
     b_o, p_l = join(ok, lk2)
     gid = nat2[p_l] * 8 + (year[b_o] - 1992)
     check_ids(gid, 25 * 8, "q9_dist (nation, year) group ids")  # exchanged payload indexes the sums
     sums = torch.zeros(25 * 8, dtype=torch.int64, device=dev).index_add_(0, gid, amt2[p_l])
     cnt = torch.zeros(25 * 8, dtype=torch.int64, device=dev).index_add_(0, gid, torch.ones_like(gid))
-    dist.all_reduce(sums, group=group)
-    dist.all_reduce(cnt, group=group)
+    sums = ex.sum(sums)
+    cnt = ex.sum(cnt)
     out = [(NATIONS[g // 8], 1992 + g % 8, int(sums[g])) for g in torch.nonzero(cnt).squeeze(1).tolist()]
     out.sort(key=lambda r: (r[0], -r[1]))
     return out

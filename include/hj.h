@@ -584,6 +584,34 @@ hj_status hj_dist_join_radix(hj_comm* c, hj_key_type build_key_type, const void*
                              int64_t probe_validity_offset, int64_t np, int64_t probe_base,
                              void* stream, hj_dist_job** job);
 
+/* Relational exchanges for multi-GPU query plans (C4/C5: TPC-H Q3 / Q9 over 8 ranks; the
+ * reference's TPC-H runner drives whole queries, tpc/src/main.rs:290-384, and its output
+ * step is take_multiple_record_batch, src/shared/shared.rs:83-92). Jobs like the plans
+ * above (same ordering, failure and lifetime rules); every rank submits the same sequence.
+ *
+ * hj_dist_shuffle: hash repartition (DataFusion's RepartitionExec Hash over the links) of a
+ * key column with `ncols` fixed-width payload columns (col_bytes 1/2/4/8/16): row i goes to
+ * rank (mix64 hash bits of keys[i], the hj_partition_rows map; a power-of-two world) with
+ * its payload - two sides shuffled on the same key meet on one rank. Steps: the keys grouped
+ * by destination (stable), each payload column gathered by that permutation, the count
+ * matrix all-gathered with every rank's status (one host read), then keys and columns per
+ * peer (ncclSend / ncclRecv in one group, messages above 256 MiB in pieces). The received
+ * rows are ordered by (source rank, source row). One rank: the rows as they are.
+ * hj_dist_gather: broadcast exchange - every rank receives the concatenation, in rank
+ * order, of all ranks' rows of `ncols` columns (n rows on this rank): the small filtered
+ * dimension sides of a plan and per-rank partial results (a sum over ranks = a gather of
+ * one row per rank). The received buffers are allocated after the last status exchange: a
+ * failed allocation aborts the communicator (as the radix plan's received probe rows). */
+hj_status hj_dist_shuffle(hj_comm* c, hj_key_type key_type, const void* keys, int64_t n, int ncols,
+                          const void* const* cols, const int* col_bytes, void* stream, hj_dist_job** job);
+hj_status hj_dist_gather(hj_comm* c, int64_t n, int ncols, const void* const* cols, const int* col_bytes,
+                         void* stream, hj_dist_job** job);
+/* An exchange job's received rows: waits for the job's host steps and makes `stream` wait
+ * for its device work; device pointers owned by the job (valid until hj_dist_job_free):
+ * *keys (shuffle; NULL for a gather), cols[0 .. ncols) in the submitted order, *rows. */
+hj_status hj_dist_job_columns(hj_dist_job* job, void* stream, const void** keys, const void** cols, int ncols,
+                              int64_t* rows);
+
 /* Wait for the job's host steps (not for its device work); its status and info. */
 hj_status hj_dist_job_wait(hj_dist_job* job, hj_dist_info* info);
 /* Wait and take the job's table (the sharded build side; the radix plan's local shard,

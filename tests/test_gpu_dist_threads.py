@@ -461,3 +461,159 @@ def test_radix_pairs_outlive_consumer_after_job_free(ctl, oracle_mod):
     assert np.array_equal(cb, ob) and np.array_equal(cp, op)
     ob2, op2 = oracle_mod.inner_join(bk, pk2)
     assert np.array_equal(b1, ob2) and np.array_equal(p1, op2)
+
+
+# ---- relational exchanges behind the C ABI (hj_dist_shuffle / hj_dist_gather) -----------
+
+def _dest(keys, world):
+    """hj_partition_rows' hash map restated on the host (mix64 low bits)."""
+    from test_distributed_gloo import _mix64
+
+    return (_mix64(np.asarray(keys, np.int64)) & np.uint64(world - 1)).astype(np.int64)
+
+
+@pytest.mark.parametrize("world", [1, 2, 4, 8])
+@pytest.mark.parametrize("key_dtype", [np.int64, np.int32])
+def test_shuffle_threads(ctl, world, key_dtype):
+    """Every rank's received (keys, payload) = the rows of every source rank whose key hashes
+    to it, ordered by (source rank, source row); payload columns of 8, 4, 2 and 1 bytes; an
+    empty rank; two jobs back to back."""
+    rng = np.random.default_rng(world * 7 + (key_dtype == np.int32))
+    sizes = [int(x) for x in rng.integers(1000, 30000, world)]
+    if world > 1:
+        sizes[1] = 0
+    keys = [rng.integers(-(2**31), 2**31 - 1, n).astype(key_dtype) for n in sizes]
+    pay = [(rng.integers(-(2**62), 2**62, n), rng.integers(0, 2**31, n).astype(np.int32),
+            rng.integers(-(2**15), 2**15, n).astype(np.int16), rng.integers(-128, 128, n).astype(np.int8))
+           for n in sizes]
+    ranks = Ranks(ctl, world)
+
+    def body(r, comm):
+        k = torch.from_numpy(keys[r]).cuda()
+        cols = [torch.from_numpy(c).cuda() for c in pay[r]]
+        torch.cuda.synchronize()
+        jobs = [comm.shuffle(k, cols) for _ in range(2)]
+        out = []
+        for j in jobs:
+            rk, rc = j.columns()
+            out.append((rk.cpu().numpy(), [c.cpu().numpy() for c in rc]))
+            del rk, rc
+            j.close()
+        return out
+
+    try:
+        out, errs = ranks.run(body)
+    finally:
+        ranks.close()
+    assert all(e is None for e in errs), errs
+    for me in range(world):
+        sel = [_dest(keys[s], world) == me if world > 1 else np.ones(len(keys[s]), bool) for s in range(world)]
+        want_k = np.concatenate([keys[s][sel[s]] for s in range(world)])
+        want_c = [np.concatenate([pay[s][i][sel[s]] for s in range(world)]) for i in range(4)]
+        for step in range(2):
+            got_k, got_c = out[me][step]
+            assert np.array_equal(got_k, want_k), (me, step)
+            for i in range(4):
+                assert got_c[i].dtype == want_c[i].dtype and np.array_equal(got_c[i], want_c[i]), (me, step, i)
+
+
+@pytest.mark.parametrize("world", [1, 2, 4, 8])
+def test_gather_threads(ctl, world):
+    """Every rank receives all ranks' rows in rank order (uneven, one empty rank)."""
+    rng = np.random.default_rng(world)
+    sizes = [int(x) for x in rng.integers(0, 5000, world)]
+    sizes[0] = 0
+    a = [rng.integers(-(2**62), 2**62, n) for n in sizes]
+    b = [rng.integers(0, 100, n).astype(np.int8) for n in sizes]
+    ranks = Ranks(ctl, world)
+
+    def body(r, comm):
+        cols = [torch.from_numpy(a[r]).cuda(), torch.from_numpy(b[r]).cuda()]
+        torch.cuda.synchronize()
+        j = comm.gather(cols)
+        _, (ga, gb) = j.columns()
+        res = (ga.cpu().numpy(), gb.cpu().numpy())
+        del ga, gb
+        j.close()
+        return res
+
+    try:
+        out, errs = ranks.run(body)
+    finally:
+        ranks.close()
+    assert all(e is None for e in errs), errs
+    for r in range(world):
+        assert np.array_equal(out[r][0], np.concatenate(a)) and np.array_equal(out[r][1], np.concatenate(b))
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_tpch_plans_over_exchange_jobs(ctl, world):
+    """C4/C5's plans with every exchange a job of the C ABI (tpch.q3_dist / q9_dist with a
+    NativeExchange over the thread transport): each rank generates its block of the tables,
+    and every rank's answer equals the one-GPU plan's on the whole tables."""
+    from datafusion_parallelism_amd import tpch
+    from datafusion_parallelism_amd.distributed import NativeExchange
+
+    sf = 0.05
+    whole = tpch.generate(sf, "cuda", seed=11, q9=True)
+    want3 = tpch.q3(whole)
+    want9 = tpch.q9(whole)
+    del whole
+    ranks = Ranks(ctl, world)
+
+    def body(r, comm):
+        t = tpch.generate(sf, "cuda", seed=11, q9=True, rank=r, world=world)
+        ex = NativeExchange(comm, world)
+        return tpch.q3_dist(t, exchange=ex), tpch.q9_dist(t, exchange=ex)
+
+    try:
+        out, errs = ranks.run(body)
+    finally:
+        ranks.close()
+    assert all(e is None for e in errs), errs
+    for r in range(world):
+        q3r, q9r = out[r]
+        assert q3r == want3, (r, q3r, want3)
+        assert q9r == want9, r
+
+
+def test_exchange_failure_is_collective(ctl):
+    """A rank whose shuffle fails locally (test hook at the partition) makes every rank's job
+    fail, none hangs, and the next exchange on the same communicators is correct."""
+    from datafusion_parallelism_amd._lib import HJ_ERR_INVALID, HJ_ERR_RCCL, HjError
+
+    world = 4
+    rng = np.random.default_rng(3)
+    keys = [rng.integers(0, 10**6, 5000) for _ in range(world)]
+    ranks = Ranks(ctl, world, timeout_s=30, fail_at=(2, 0, 1))
+
+    def body(r, comm):
+        k = torch.from_numpy(keys[r]).cuda()
+        torch.cuda.synchronize()
+        j0 = comm.shuffle(k, [k])
+        j1 = comm.shuffle(k, [k])
+        status = None
+        try:
+            j0.columns()
+        except HjError as e:
+            status = (e.status, str(e))
+        rk, (rc,) = j1.columns()
+        res = (rk.cpu().numpy(), rc.cpu().numpy())
+        del rk, rc
+        j0.close()
+        j1.close()
+        return status, res
+
+    try:
+        out, errs = ranks.run(body)
+    finally:
+        ranks.close()
+    assert all(e is None for e in errs), errs
+    for r, (status, (rk, rc)) in enumerate(out):
+        assert status is not None
+        if r == 2:
+            assert status[0] == HJ_ERR_INVALID and "injected" in status[1]
+        else:
+            assert status[0] == HJ_ERR_RCCL and "peer rank failed" in status[1]
+        want = np.concatenate([keys[s][_dest(keys[s], world) == r] for s in range(world)])
+        assert np.array_equal(rk, want) and np.array_equal(rc, want)
