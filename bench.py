@@ -362,6 +362,121 @@ def cpu_baseline(cfg):
     }
 
 
+class _TimedJoin:
+    """tpch's join_fn with HIP events on the current stream around every join (build +
+    probe): the per-join device spans and sizes of a query run (B, P, M)."""
+
+    def __init__(self):
+        from datafusion_parallelism_amd import tpch
+
+        self._join = tpch._join
+        self.record = False
+        self.joins = []
+
+    def __call__(self, build, probe):
+        if not self.record:
+            return self._join(build, probe)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        b, p = self._join(build, probe)
+        e1.record()
+        self.joins.append((int(build.numel()), int(probe.numel()), int(b.numel()), e0, e1))
+        return b, p
+
+
+def bench_c4(args, json_out):
+    """--config c4: TPC-H Q3 at SF100 (BASELINE.json configs[3], quoted on 8 GPUs; one
+    MI355X holds SF100, so this line is the one-GPU plan tpch.q3 with the tables resident in
+    HBM). A step = one whole query (filters, both hash joins, the group-by sum, the top 10);
+    value = lineitem rows / s. roofline: the two joins (customer ⋈ orders, orders ⋈
+    lineitem) with 8P + 16B + 12M algorithmic bytes each over their device spans (HIP events
+    around build + probe). cpu_baseline: the same plan on the host at SF1 with the oracle's C
+    join (kind "port")."""
+    from datafusion_parallelism_amd import tpch
+
+    if int(os.environ.get("WORLD_SIZE", "1")) != 1:
+        raise SystemExit("--config c4 is a one-GPU line (tools/bench_tpch.py --dist runs the 8-rank plans)")
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    sf = float(os.environ.get("DFP_BENCH_C4_SF", "100"))
+    t = tpch.generate(sf, dev, seed=1)
+    nl = int(t.l_orderkey.numel())
+    tj = _TimedJoin()
+    for _ in range(args.warmup):
+        tpch.q3(t, join_fn=tj)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        res = tpch.q3(t, join_fn=tj)
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    # per-join spans from instrumented runs after the timed loop (median of 3)
+    spans = []
+    for _ in range(3):
+        tj.joins, tj.record = [], True
+        tpch.q3(t, join_fn=tj)
+        torch.cuda.synchronize(dev)
+        tj.record = False
+        spans.append([(B, P, M, e0.elapsed_time(e1)) for B, P, M, e0, e1 in tj.joins])
+    joins = []
+    for i in range(len(spans[0])):
+        B, P, M = spans[0][i][:3]
+        ms = float(np.median([s[i][3] for s in spans]))
+        joins.append({"build_rows": B, "probe_rows": P, "matches": M, "ms": round(ms, 4),
+                      "alg_bytes": 8 * P + 16 * B + 12 * M})
+    alg = sum(j["alg_bytes"] for j in joins)
+    jms = sum(j["ms"] for j in joins)
+    achieved = alg / (jms / 1e3) / 1e9
+    value = nl / (elapsed / args.steps) / 1e6
+    cpu = None if args.no_cpu_baseline else cpu_baseline_c4()
+    line = {
+        "metric": "probe Mrows/s + build ms, 10^8-row int64 inner join; 1/2/4/8 GPUs",
+        "value": round(value, 3), "unit": "Mrows/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True, "scaling": "strong",
+        "vs_baseline": None, "dtype": "int64",
+        "data": "synthetic TPC-H-shaped tables generated on the device (tpch.generate: spec key structure and value "
+                "domains, not dbgen's streams)",
+        "config": {"workload": f"C4: TPC-H Q3 SF{sf:g} (lineitem ⋈ orders ⋈ customer), one MI355X, tables in HBM",
+                   "lineitem_rows": nl, "groups": res.groups, "parallelism": "single-gpu"},
+        "value_unit_note": "lineitem rows per second of whole queries",
+        "query_ms": round(elapsed / args.steps * 1e3, 4),
+        "joins": joins,
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                     "kernel": "Q3's two hash joins (build + probe each; HIP events around each join)",
+                     "alg_bytes_per_launch": alg, "alg_bytes_formula": "sum over the joins of 8*P + 16*B + 12*M"},
+        "cpu_baseline": cpu,
+    }
+    print(json.dumps(line), file=json_out, flush=True)
+
+
+def cpu_baseline_c4():
+    """tpch.q3 on the host (torch CPU tensors) at SF1 with the oracle's C inner join
+    (oracle/hj_oracle.c, one thread): lineitem rows / s, 3 runs (median, range)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+
+    from datafusion_parallelism_amd import tpch
+
+    def join(build, probe):
+        b, p = oracle.inner_join(build.numpy(), probe.numpy())
+        return torch.from_numpy(b.astype(np.int64)), torch.from_numpy(p.astype(np.int64))
+
+    t = tpch.generate(1, "cpu", seed=1)
+    nl = int(t.l_orderkey.numel())
+    vals = []
+    for _ in range(3):
+        t0 = time.perf_counter()
+        tpch.q3(t, join_fn=join)
+        vals.append(nl / (time.perf_counter() - t0) / 1e6)
+    vals.sort()
+    return {"value": round(vals[1], 3), "unit": "Mrows/s", "cores": 1, "kind": "port",
+            "sample": f"tpch.q3 at SF1 ({nl} lineitem rows) on the host: torch CPU ops for the filters, group-by and "
+                      f"top-k, the oracle's C inner join (oracle/hj_oracle.c, single thread) for both joins; 3 runs, "
+                      f"median (range beside it); on {_cpu_model()}",
+            "runs": [round(v, 3) for v in vals], "range": [round(vals[0], 3), round(vals[-1], 3)]}
+
+
 def load_traffic(config_name):
     p = os.path.join(ROOT, "profiles", f"traffic_{config_name}.json")
     if os.path.exists(p):
@@ -531,7 +646,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS) + ["c4"],
+                    help="c2 (the headline), c2h, c3: joins of SURVEY.md §8d; c4: TPC-H Q3 SF100 on one GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--stream-priority", default="none", choices=["none", "probe-high", "build-low"],
                     help="single GPU: HIP stream priorities of the probe / build streams")
@@ -575,6 +691,8 @@ def main():
     os.dup2(2, 1)
     if args.dry_run:
         return dry_run(args, json_out)
+    if args.config == "c4":
+        return bench_c4(args, json_out)
     cfg = CONFIGS[args.config]
 
     one_rank_store = None

@@ -105,6 +105,7 @@ def main():
             "lineitem_rows": nl,
             "query_ms_min": round(best * 1e3, 3), "query_ms_median": round(sorted(times)[len(times) // 2] * 1e3, 3),
             "lineitem_mrows_s": round(nl / best / 1e6, 1),
+            "times_ms": [round(x * 1e3, 3) for x in times],
         }
         if q == "q3":
             line.update(groups=r.groups, top1=[r.l_orderkey[0], r.revenue[0], r.o_orderdate[0]] if r.l_orderkey else None)
