@@ -191,18 +191,74 @@ void* cache_alloc(int dev, size_t bytes, hipError_t* err) {
         }
     }
     void* p = nullptr;
+    // DFP_HJ_ALLOC_LOG=1: every cache miss (a hipMalloc) and every release of the cache to stderr
+    static const bool alog = [] {
+        const char* e = getenv("DFP_HJ_ALLOC_LOG");
+        return e != nullptr && e[0] == '1';
+    }();
+    if (alog) fprintf(stderr, "[dfp alloc] miss dev %d bytes %zu class %zu cached %zu\n", dev, bytes, c, g_cache.cached_bytes);
     *err = hipMalloc(&p, c);
     if (*err != hipSuccess) {
         (void)hipGetLastError();
-        // release every cached block of this device and retry once
+        // Cached blocks of this device are released until the allocation fits - not the whole
+        // cache: the 8-shard SF300 Q9 on one GPU (torch holding 156 GB beside this cache's up to
+        // 129 GB) released everything on such a miss and re-allocated it in the next join, 1.5-3.9
+        // s per query against 0.29 s (profiles/r06_q9_sf300_alloc.txt)
         std::lock_guard<std::mutex> g(g_cache.mu);
-        for (auto& kv : g_cache.bins) {
-            if ((int)(kv.first >> 48) != dev) continue;
-            for (void* q : kv.second) (void)hipFree(q);
-            g_cache.cached_bytes -= (kv.first & ((1ull << 48) - 1)) * kv.second.size();
-            kv.second.clear();
+        if (alog) fprintf(stderr, "[dfp alloc] hipMalloc %zu failed with %zu cached bytes\n", c, g_cache.cached_bytes);
+        // first the smallest cached block of at least this size is released (one hipFree of about
+        // the request: the big blocks other joins reuse stay cached), then, if that is not enough,
+        // blocks from the largest down. (Handing a larger cached block out instead, with no free,
+        // left the HSA runtime no device memory for its own resources: the process aborted with
+        // HSA_STATUS_ERROR_OUT_OF_RESOURCES, gpurun_out/r06m.)
+        for (auto it = g_cache.bins.lower_bound(key); it != g_cache.bins.end() && (it->first >> 48) == (uint64_t)dev;
+             ++it) {
+            if (it->second.empty()) continue;
+            void* q = it->second.back();
+            it->second.pop_back();
+            (void)hipFree(q);
+            g_cache.cached_bytes -= (size_t)(it->first & ((1ull << 48) - 1));
+            *err = hipMalloc(&p, c);
+            if (*err == hipSuccess) {
+                if (alog) fprintf(stderr, "[dfp alloc] released one cached block of %zu bytes: ok\n",
+                                  (size_t)(it->first & ((1ull << 48) - 1)));
+                g_cache.cls[p] = c;
+                return p;
+            }
+            (void)hipGetLastError();
+            break;
         }
-        *err = hipMalloc(&p, c);
+        size_t freed = 0;
+        for (;;) {
+            auto lo = g_cache.bins.lower_bound((uint64_t)dev << 48);
+            auto hi = g_cache.bins.lower_bound((uint64_t)(dev + 1) << 48);
+            auto big = g_cache.bins.end();
+            for (auto it = hi; it != lo;) {  // the largest class with a cached block
+                --it;
+                if (!it->second.empty()) {
+                    big = it;
+                    break;
+                }
+            }
+            if (big == g_cache.bins.end()) break;
+            void* q = big->second.back();
+            big->second.pop_back();
+            (void)hipFree(q);
+            const size_t qc = (size_t)(big->first & ((1ull << 48) - 1));
+            g_cache.cached_bytes -= qc;
+            freed += qc;
+            if (freed >= c) {
+                *err = hipMalloc(&p, c);
+                if (*err == hipSuccess) break;
+                (void)hipGetLastError();
+            }
+        }
+        if (*err != hipSuccess) *err = hipMalloc(&p, c);
+        if (alog) fprintf(stderr, "[dfp alloc] released %zu bytes: %s\n", freed, *err == hipSuccess ? "ok" : "failed");
+        if (*err == hipSuccess) {
+            g_cache.cls[p] = c;
+            return p;
+        }
     }
     if (*err != hipSuccess) return nullptr;
     std::lock_guard<std::mutex> g(g_cache.mu);

@@ -90,6 +90,8 @@ def main():
             if a.dist:
                 dist.all_reduce(dt, op=dist.ReduceOp.MAX)
             times.append(float(dt.item()))
+            print(f"[rep] {q} sf {sf} {times[-1] * 1e3:.1f} ms torch reserved {torch.cuda.memory_reserved() >> 20} MiB "
+                  f"allocated {torch.cuda.memory_allocated() >> 20} MiB", file=sys.stderr, flush=True)
         nl = torch.tensor([t.l_orderkey.numel()], dtype=torch.int64, device=dev)
         if a.dist:
             dist.all_reduce(nl)
