@@ -1331,13 +1331,11 @@ constexpr int kSlHistBins = 4096;                       // per-tile slice histog
 constexpr int kSlMaxSlices = kSlHistBins - 1;           // slices per pass: key ranges up to ~2^27 values
 constexpr int kSlOwnWin = 2048;        // flattened segment positions per owner window (32 per lane)
 constexpr int kSlOwnWinHashed = 1024;  // hashed slices: 16 per lane (u64 entries)
-#ifndef DFP_HS_W15
-#define DFP_HS_W15 1152
-#endif
 // hashed slices with 2^15-row tiles: a 64-tile block holds ~1075 positions at C2h (16.8 per
 // fragment), so 1152-position windows take most blocks in one window (r05: C2h lookup 597 ->
 // 566 us, bench 65.5-66.1K -> 66.1-66.5K Mrows/s against 1024, profiles/r05_hs_window_ab.txt)
-template <int TL> constexpr int hs_own_win() { return TL == 15 ? DFP_HS_W15 : kSlOwnWinHashed; }
+constexpr int kSlOwnWinHashed15 = 1152;
+template <int TL> constexpr int hs_own_win() { return TL == 15 ? kSlOwnWinHashed15 : kSlOwnWinHashed; }
 // the emission's waves own 2048-row ranges of a tile: the partition counts each range's
 // entries (wcnt) so that a tile whose entries all hit one unique row each (no correction
 // flag from the lookup) needs no count pass in the emission
@@ -1368,9 +1366,7 @@ __device__ __forceinline__ void hist_excl_scan(uint32_t* s_hist, uint32_t* s_w, 
     __syncthreads();
 }
 
-#ifndef DFP_SL_PD
-#define DFP_SL_PD 3
-#endif
+constexpr int kSlPrefetch15 = 3;  // 2^15-row partition tiles: groups of keys in flight ahead of the ranked one
 // hist_excl_scan without the per-wave loop over the wave totals (lane w < 16 holds wave w's
 // total; a DPP scan and two readlanes): the persistent 2^15-row partition, whose unrolled
 // loop there spilled
@@ -1459,8 +1455,8 @@ sl_partition_kernel(int64_t dmin, uint64_t drange, uint32_t wlog, uint32_t nslic
             }
         };
         // groups in flight ahead of the one being ranked: 1 at 2^14-row tiles (32 waves per
-        // CU), DFP_SL_PD at 2^15 (16 waves per CU hold fewer loads in flight per CU)
-        constexpr int D = TL == 14 ? 1 : DFP_SL_PD;
+        // CU), kSlPrefetch15 at 2^15 (16 waves per CU hold fewer loads in flight per CU)
+        constexpr int D = TL == 14 ? 1 : kSlPrefetch15;
         int64_t kr[D + 1][4];  // ring of groups: group g in slot g % (D + 1)
 #pragma unroll
         for (int g = 0; g < D && g < T::kGroups; ++g) load_group(g, kr[g]);
@@ -2224,10 +2220,7 @@ constexpr int kHsSliceLog = 11;  // buckets per hashed slice: 2^11 x 64 B = 128 
 // with every line in plain order, 16 lanes reading the same quad of random buckets meet on
 // 4 slots (about 6-way); the XOR by the next two bucket bits spreads them over all 16.
 // (r03 rotated by the bucket's low bits, which leaves the 4 slots as they were.)
-#ifndef DFP_HS_ROT
-#define DFP_HS_ROT 1
-#endif
-__device__ __forceinline__ uint32_t hs_quad_rot(uint32_t bl) { return DFP_HS_ROT ? (bl >> 2) & 3u : 0u; }
+__device__ __forceinline__ uint32_t hs_quad_rot(uint32_t bl) { return (bl >> 2) & 3u; }
 __device__ __forceinline__ void lds_line(const uint4* __restrict__ img, uint32_t bl, uint4& a0, uint4& a1, uint4& a2,
                                          uint4& a3) {
     const uint4* p = img + (size_t)bl * 4;
@@ -2271,27 +2264,11 @@ __device__ __forceinline__ uint32_t lds_bucket_ref(const uint4* __restrict__ img
 // by LDS bank conflicts, and the extra dependent read lengthens every chain.
 
 constexpr uint32_t kBigCorr = 1u << 16;  // counts - 1 from here on correct the tile count directly
-#ifndef DFP_LK_GROUP
-#define DFP_LK_GROUP 4
-#endif
-constexpr int kLkGroup = DFP_LK_GROUP;  // dense lookup: rows per branch-free group (divides the window's rows)
-#ifndef DFP_HS_LK2  // hashed lookup: the common-path rows (r05); 0 restores the per-row path
-#define DFP_HS_LK2 1
-#endif
-#ifndef DFP_HS_DEFER  // hashed lookup: probes past a full home bucket queued per wave (r05)
-#define DFP_HS_DEFER 1
-#endif
-#ifndef DFP_HS_NOPROBE  // timing ablation (wrong pairs): no probe past a full bucket
-#define DFP_HS_NOPROBE 0
-#endif
-#ifndef DFP_HS_G1
-#define DFP_HS_G1 1
-#endif
-#ifndef DFP_HS_G2
-#define DFP_HS_G2 1
-#endif
-constexpr int kHsGroup1 = DFP_HS_G1;  // hashed lookup: rows per group of owner searches and entry loads
-constexpr int kHsGroup2 = DFP_HS_G2;  // hashed lookup: rows per group of bucket-line reads
+constexpr int kLkGroup = 4;  // dense lookup: rows per branch-free group (divides the window's rows)
+// hashed lookup: rows per group of owner searches and entry loads, of bucket-line reads
+// (r05: groups of 2-4 rows were slower in every form, 784-1,303 us against 751)
+constexpr int kHsGroup1 = 1;
+constexpr int kHsGroup2 = 1;
 // a tile's pair count (tcnt) is < 2^45 (16384 rows x < 2^31 build rows); the dense lookup
 // adds kOddFlag once per fragment with an entry of a missing or duplicated key, the hashed
 // lookup once per fragment with a duplicated key (at most 4095 slices per pass and < 64
@@ -2359,10 +2336,10 @@ sl_lookup_kernel(TableView tv, uint32_t wlog, uint32_t nslices, int64_t ntiles, 
     __shared__ uint32_t s_cst[kSlThreads];
     __shared__ uint32_t s_end[HASHED ? kSlThreads : 1];  // hashed, per wave: end position of each fragment, by rank
     __shared__ unsigned long long s_mask[kSlThreads / 64][W / 64];
-    // hashed (DFP_HS_DEFER): per wave, the window's entries that must probe past a full home
+    // hashed: per wave, the window's entries that must probe past a full home
     // bucket, queued (stored key, entry index | owner rank << 26) and looked up 64 at a time
-    __shared__ unsigned long long s_dqk[HASHED && DFP_HS_DEFER ? kSlThreads : 1];
-    __shared__ uint32_t s_dqo[HASHED && DFP_HS_DEFER ? kSlThreads : 1];
+    __shared__ unsigned long long s_dqk[HASHED ? kSlThreads : 1];
+    __shared__ uint32_t s_dqo[HASHED ? kSlThreads : 1];
     DFP_DBG_TS(g_dbg_lk_ts, 0, wall_clock64());
     // Items: the first s1 slices in `parts` parts each, then the rest in `parts2` smaller
     // ones; every XCD runs its share of the first stage before its share of the second
@@ -2560,7 +2537,6 @@ sl_lookup_kernel(TableView tv, uint32_t wlog, uint32_t nslices, int64_t ntiles, 
                     }
                 }
             }
-#if DFP_HS_LK2
             if constexpr (HASHED) {
                 // hashed: the dense path's row groups (mask reads, then owner bases and
                 // fragment ends, then the entry loads of kHsGroup1 rows issue together)
@@ -2606,38 +2582,6 @@ sl_lookup_kernel(TableView tv, uint32_t wlog, uint32_t nslices, int64_t ntiles, 
                     }
                 }
             }
-#endif
-#pragma unroll
-            for (int u = 0; u < NU; ++u) {
-                if constexpr (!HASHED || DFP_HS_LK2) break;  // (above)
-                off[u] = kOob;
-                if (w0 + u * 64 >= R) continue;  // uniform: past the run
-                const uint32_t r = w0 + u * 64 + lane;
-                const unsigned long long m = smask[u];  // the same word for every lane
-                const uint32_t mlo = __builtin_amdgcn_readfirstlane((uint32_t)m);
-                const uint32_t mhi = __builtin_amdgcn_readfirstlane((uint32_t)(m >> 32));
-                const unsigned long long mu = ((unsigned long long)mhi << 32) | mlo;
-                // owner rank: segments started at or before this position, minus one
-                const unsigned long long m1 = mu >> 1;
-                const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m1 >> 32),
-                                                                  __builtin_amdgcn_mbcnt_lo((uint32_t)m1, 0u));
-                const uint32_t k = kb + (uint32_t)(mu & 1) + below - 1;
-                kb += (uint32_t)__builtin_popcountll(mu);
-                const uint32_t ps = sbs[k & 63] + r;
-                const uint32_t o = r < R ? ps : kOob;
-                if constexpr (HASHED) {
-                    if (r + 1 == send[k & 63]) off_end |= 1u << u;  // last position of its fragment
-                }
-                if constexpr (HASHED) {
-                    const uint2 v = __builtin_bit_cast(
-                        uint2, __builtin_amdgcn_raw_buffer_load_b64(rko, (int)(o * 8), 0, 0));
-                    ev[u] = ((unsigned long long)v.y << 32) | v.x;
-                } else {
-                    // ablation 1024: no entry loads (wrong pairs)
-                    ev[u] = DFP_ABL(1024) ? (r & 0x7FFF) : __builtin_amdgcn_raw_buffer_load_b16(rko, (int)(o * 2), 0, 0);
-                }
-                off[u] = o | ((k & 63) << 26);  // the owner's rank (its tile lane: slane, read only for a correction)
-            }
             wait_image();
             DFP_PH(1);
             DFP_PH_WAIT();
@@ -2679,7 +2623,7 @@ sl_lookup_kernel(TableView tv, uint32_t wlog, uint32_t nslices, int64_t ntiles, 
                 if (off_end & (1u << u)) scst[off[u] >> 26] = corr_run;
                 corr_run = (uint32_t)__builtin_amdgcn_readlane((int)corr_run, 63);
             };
-            // DFP_HS_DEFER: the queued entries, one per lane: probe on from the bucket after
+            // the queued entries, one per lane: probe on from the bucket after
             // the home one; a hit stores its ref over the kMiss stored for it and adds its
             // row count to its tile (the -1 of a miss was already in the running sum)
             uint32_t dq_n = 0;  // uniform: queued entries of this wave
@@ -2710,7 +2654,6 @@ sl_lookup_kernel(TableView tv, uint32_t wlog, uint32_t nslices, int64_t ntiles, 
                 dq_n = 0;
             };
             if constexpr (HASHED) {
-#if DFP_HS_LK2
                 // Rows in groups of kHsGroup2: the group's bucket lines are read together and
                 // each row costs five key compares and a select chain. Only a group with a
                 // lane on the rare path — key 0 (the side bucket), a probe past a bucket an
@@ -2756,31 +2699,7 @@ sl_lookup_kernel(TableView tv, uint32_t wlog, uint32_t nslices, int64_t ntiles, 
                         // a miss in a bucket some insert passed full (meta bit 0, so no free
                         // slot): probe on inside the chunk, the lanes that need it only
                         const bool mo = valid & (sk != 0) & (ref == kMiss) & ((a3.w & 1u) != 0);
-#if DFP_HS_DEFER
                         mo_[j] = mo;  // queued in the common branch below
-#else
-                        if (!DFP_HS_NOPROBE && __ballot(mo) != 0) {  // uniform: most rows (one miss in twenty)
-                            if (mo) {
-                                // the next bucket straight (compares and selects only): almost
-                                // every probe on ends there; a lane that must go further loops
-                                uint32_t b = (hb[j] & ~cmask) | ((hb[j] + 1) & cmask), cdummy;
-                                uint4 q0, q1, q2, q3;
-                                lds_line(reinterpret_cast<const uint4*>(s_tab), b - sbase, q0, q1, q2, q3);
-                                ref = ((((unsigned long long)q2.y << 32) | q2.x) == sk) ? q3.z : kMiss;
-                                ref = ((((unsigned long long)q1.w << 32) | q1.z) == sk) ? q3.y : ref;
-                                ref = ((((unsigned long long)q1.y << 32) | q1.x) == sk) ? q3.x : ref;
-                                ref = ((((unsigned long long)q0.w << 32) | q0.z) == sk) ? q2.w : ref;
-                                ref = ((((unsigned long long)q0.y << 32) | q0.x) == sk) ? q2.z : ref;
-                                bool more = (ref == kMiss) & ((q3.w & 1u) != 0);
-                                for (uint32_t probes = 1; more && probes < cmask; ++probes) {
-                                    b = (b & ~cmask) | ((b + 1) & cmask);
-                                    uint4 q0, q1, q2, q3;
-                                    lds_line(reinterpret_cast<const uint4*>(s_tab), b - sbase, q0, q1, q2, q3);
-                                    ref = scan_line(q0, q1, q2, q3, sk, &more, &cdummy);
-                                }
-                            }
-                        }
-#endif
                         vv[j] = valid ? ref : kMiss;
                         // rare: key 0 (the side bucket) or a duplicated key (its count)
                         rare |= valid & ((sk == 0) | ((ref >= kDupFlag) & (ref != kMiss)));
@@ -2790,10 +2709,9 @@ sl_lookup_kernel(TableView tv, uint32_t wlog, uint32_t nslices, int64_t ntiles, 
                         for (int j = 0; j < kHsGroup2; ++j) {
                             const int u = g0 + j;
                             const uint32_t o = off[u] & kOobMask;
-#if DFP_HS_DEFER
                             {  // queued; counted as a miss here, the flush corrects a hit
                                 const unsigned long long mm = __ballot(mo_[j]);
-                                if (!DFP_HS_NOPROBE && mm != 0) {  // uniform: most rows (one miss in twenty)
+                                if (mm != 0) {  // uniform: most rows (one miss in twenty)
                                     const uint32_t nq = (uint32_t)__builtin_popcountll(mm);
                                     if (dq_n + nq > 64) dq_flush();
                                     if (mo_[j]) {
@@ -2805,7 +2723,6 @@ sl_lookup_kernel(TableView tv, uint32_t wlog, uint32_t nslices, int64_t ntiles, 
                                     dq_n += nq;
                                 }
                             }
-#endif
                             __builtin_amdgcn_raw_buffer_store_b32(vv[j], rres, (int)(o * 4), 0, 0);
                             const bool miss = o != kOob && vv[j] == kMiss;
                             const unsigned long long mm = __ballot(miss);
@@ -2819,11 +2736,7 @@ sl_lookup_kernel(TableView tv, uint32_t wlog, uint32_t nslices, int64_t ntiles, 
 #pragma unroll
                     for (int j = 0; j < kHsGroup2; ++j) hashed_row(g0 + j);
                 }
-                if (DFP_HS_DEFER && dq_n != 0) dq_flush();
-#else
-#pragma unroll
-                for (int u = 0; u < NU; ++u) hashed_row(u);
-#endif
+                if (dq_n != 0) dq_flush();
             } else {
 #pragma unroll
                 for (int g0 = 0; g0 < NU; g0 += kLkGroup) {
@@ -2936,9 +2849,6 @@ sl_lookup_kernel(TableView tv, uint32_t wlog, uint32_t nslices, int64_t ntiles, 
 // tile (u16) leave in slice order, with the tile's slice bounds (u16). Persistent, one
 // workgroup per CU (128 KB of staged keys): the next tile's keys load into registers
 // once this tile's keys are staged, while they and the rows are written out.
-#ifndef DFP_HS_OPAQUE_TX
-#define DFP_HS_OPAQUE_TX 1
-#endif
 template <typename K, bool HAS_VALID>
 __global__ void __launch_bounds__(kSlThreads, 4)  // 16 waves per CU: <= 128 VGPRs
 hs_partition_kernel(uint32_t nb, uint32_t slog, uint32_t s0, uint32_t nslices, const void* __restrict__ keys,
@@ -2966,14 +2876,10 @@ hs_partition_kernel(uint32_t nb, uint32_t slog, uint32_t s0, uint32_t nslices, c
     int64_t tile = blockIdx.x;
     if (tile < ntiles) load(tile, nk, threadIdx.x);
     for (; tile < ntiles; tile += gridDim.x) {
-#if DFP_HS_OPAQUE_TX
         // the thread index made opaque per tile: otherwise the compiler hoists the rows'
         // offsets and addresses out of the tile loop and spills them
         uint32_t tx = threadIdx.x;
         asm volatile("" : "+v"(tx));
-#else
-        const uint32_t tx = threadIdx.x;
-#endif
         const int64_t tile0 = tile * kSlTile;
         const int64_t gtile = tile + tile_off;  // its output region (the build partitions several segments)
 #pragma unroll
@@ -3231,9 +3137,6 @@ constexpr int kSlWaveRows = kSlTile / (kSlEmitThreads / 64);  // 2048
 static_assert(kSlEmitThreads / 64 == kSlRanges && kSlWaveRows == kSlRangeRows,
               "emission waves and the partition's entry-count ranges must coincide");
 
-#ifndef DFP_EMIT_RESET
-#define DFP_EMIT_RESET 1
-#endif
 template <bool HAS_ROW_IDS, bool HAS_PROBE_IDS, int TL = kSlTileLog>
 // 16 waves per CU (two 512-thread workgroups, or one of 1024 for 2^15-row tiles): <= 128 VGPRs
 __global__ void __launch_bounds__(SlT<TL>::kEmitThreads, 4)
@@ -3310,8 +3213,8 @@ sl_emit_kernel(TableView tv, const uint32_t* __restrict__ tent, const uint16_t* 
     DFP_DBG_TS(g_dbg_em_ts, 1, wall_clock64());
     // The image is cleared once; the write pass puts kMiss back into every row it reads, so
     // no clear and no barrier for it stand between a tile and the next one's scatter
-    // (DFP_EMIT_RESET=0: the image cleared before every tile)
-    const bool reset_rows = DFP_EMIT_RESET && !DFP_ABL(1);
+    // (the diagnostic ablation without a write pass clears it before every tile)
+    const bool reset_rows = !DFP_ABL(1);
     auto clear_image = [&]() {
         for (int i = threadIdx.x * 4; i < SlT<TL>::kRows; i += SlT<TL>::kEmitThreads * 4)
             *reinterpret_cast<uint4*>(s_ref + i) = make_uint4(kMiss, kMiss, kMiss, kMiss);
