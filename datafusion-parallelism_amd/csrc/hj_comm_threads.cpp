@@ -52,6 +52,9 @@ struct hj_test_hub {
     int64_t gen = 0;
     bool broken = false;
     std::vector<const std::vector<Op>*> slots;
+    // each rank's posted group, owned by the hub (not the posting call's stack): a peer that is
+    // still staging from it when the rank's second barrier times out reads valid memory
+    std::vector<std::vector<Op>> posted;
 };
 
 namespace {
@@ -114,14 +117,19 @@ struct ThreadTransport final : dfp::comm::Transport {
     }
 
     hj_status flush(hipStream_t s) {
-        std::vector<Op> ops;
-        ops.swap(pending);
         if (hipStreamSynchronize(s) != hipSuccess) return set_error(HJ_ERR_HIP, "thread transport: stream sync");
         const int W = hub->world;
         {
             std::lock_guard<std::mutex> g(hub->mu);
-            hub->slots[(size_t)rank] = &ops;
+            if (hub->broken) {
+                pending.clear();
+                return set_error(HJ_ERR_RCCL, "thread transport: the hub broke at an earlier timeout");
+            }
+            hub->posted[(size_t)rank].swap(pending);
+            pending.clear();
+            hub->slots[(size_t)rank] = &hub->posted[(size_t)rank];
         }
+        const std::vector<Op>& ops = hub->posted[(size_t)rank];
         if (!barrier(hub)) return set_error(HJ_ERR_RCCL, "thread transport: barrier timeout (a rank did not reach the collective)");
         // validate: the same collectives everywhere; every receive meets a send of its size
         std::string bad;
@@ -168,7 +176,12 @@ struct ThreadTransport final : dfp::comm::Transport {
             if (hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToHost, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess)
                 st = set_error(HJ_ERR_HIP, "thread transport: staging copy failed");
         };
-        if (bad.empty()) {
+        bool broken_now;
+        {
+            std::lock_guard<std::mutex> g(hub->mu);
+            broken_now = hub->broken;  // a broken hub stages nothing more
+        }
+        if (bad.empty() && !broken_now) {
             size_t ci = 0;
             std::vector<size_t> ri(W, 0);
             for (size_t i = 0; i < ops.size(); ++i) {
@@ -233,6 +246,7 @@ hj_test_hub* hj_test_hub_create(int world, double timeout_s) {
     h->world = world;
     h->timeout_s = timeout_s > 0 ? timeout_s : 60;
     h->slots.assign((size_t)world, nullptr);
+    h->posted.assign((size_t)world, {});
     return h;
 }
 
