@@ -3327,6 +3327,11 @@ sl_emit_kernel(TableView tv, const uint32_t* __restrict__ tent, const uint16_t* 
                     const uint32_t incl = wave_incl_scan_dpp(c);  // < 2^32: 64 rows of < 2^26 rows each
                     total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
                     const uint32_t excl = incl - c;
+                    // a step whose duplicated keys are all run refs (or single rows): the build row
+                    // of output position p is (top + excl) - p of its owner row - one cross-lane
+                    // read per window instead of two, no segment read (r06)
+                    const bool runs_only = __ballot(c > 1u && !run_ref(r, tv.off_mask)) == 0;
+                    const uint32_t vsum = ((r & kDupFlag) ? (r & 0xFFFFFFu) : r) + excl;
                     uint32_t carry = 0;
                     // Measured (r04) and not kept: each window's pairs stored one window later
                     // (the next window's segment read issued first, two register sets): C3
@@ -3340,14 +3345,19 @@ sl_emit_kernel(TableView tv, const uint32_t* __restrict__ tent, const uint16_t* 
                         const uint32_t ol = max(wave_incl_max_dpp(own[lane]), carry);
                         carry = (uint32_t)__builtin_amdgcn_readlane((int)ol, 63);
                         const int j = (int)((ol - 1) & 63);
-                        const uint32_t xj = (uint32_t)__shfl((int)excl, j, 64);
-                        const uint32_t rj = (uint32_t)__shfl((int)r, j, 64);
                         const uint32_t p = w0 + lane;
+                        uint32_t br;
+                        if (runs_only) {
+                            br = (uint32_t)__shfl((int)vsum, j, 64) - p;
+                        } else {
+                            const uint32_t xj = (uint32_t)__shfl((int)excl, j, 64);
+                            const uint32_t rj = (uint32_t)__shfl((int)r, j, 64);
+                            br = !(rj & kDupFlag) ? rj
+                                 : DFP_ABL(8) ? (rj & tv.off_mask) + (p - xj)  // ablation: no segment reads
+                                              : (p < total ? dup_ref_row(tv.dup_rows, rj, tv.off_mask, p - xj) : 0u);
+                        }
                         const unsigned long long o = pos + p;
                         if (p < total && o < (unsigned long long)cap) {
-                            const uint32_t br = !(rj & kDupFlag) ? rj
-                                                : DFP_ABL(8) ? (rj & tv.off_mask) + (p - xj)  // ablation: no segment reads
-                                                            : dup_ref_row(tv.dup_rows, rj, tv.off_mask, p - xj);
                             const int64_t rowj = tile0 + row_w + k + j;
                             put(o, HAS_ROW_IDS ? tv.row_ids[br] : (uint64_t)br,
                                 HAS_PROBE_IDS ? probe_ids[rowj] : (uint32_t)rowj + pbase);
