@@ -2764,37 +2764,47 @@ sl_lookup_kernel(TableView tv, uint32_t wlog, uint32_t nslices, int64_t ntiles, 
                       }
                       continue;
                   }
+                  {
+                      // the group's counts, then its rows' correction scans issued together
+                      // (independent until the carry) and its start masks in one LDS round
+                      // trip: a build with many missing or duplicated keys (C3) has a special
+                      // row in nearly every group (r06)
+                      uint32_t dd[kLkGroup];
+                      unsigned long long sm[kLkGroup];
+                      bool unk = false;
 #pragma unroll
-                  for (int j = 0; j < kLkGroup; ++j) {
-                    const int u = g0 + j;
-                    const uint32_t o = off[u] & kOobMask;
-                    const uint32_t v = vv[j];
-                    const bool special = o != kOob && v >= kDupFlag;
-                    if (__ballot(special) != 0) {
-                        uint32_t c = 1;  // row count (kCountUnknown: in its segment header)
-                        if (special) c = ref_count_inline(v, tv.off_mask);
-                        // counts not inline: read from the segment header in a wave-uniform branch
-                        // that waits there. Merged into the common path, that load's wait was an
-                        // s_waitcnt vmcnt(0) on every row — for the previous rows' ref stores (loads
-                        // and stores share vmcnt): one store round trip per 64 entries.
-                        if (__ballot(c == kCountUnknown) != 0) {
-                            if (c == kCountUnknown) c = tv.dup_rows[v & tv.off_mask];
-                            asm volatile("" : "+v"(c));
-                        }
-                        // a fragment start (start mask bit) records the running sum before it
-                        const bool odd = special && c != 1;
-                        if (odd) sodd[off[u] >> 26] = 1;  // the emission's count-free path is off for its tile
-                        uint32_t d = odd ? c - 1u : 0u;
-                        if (d != 0xFFFFFFFFu && d >= kBigCorr) {  // a huge duplicate: straight to its tile
-                            atomicAdd(&tcnt[tc + slane[off[u] >> 26]], (unsigned long long)d);
-                            d = 0;
-                        }
-                        const uint32_t ci = wave_incl_scan_dpp(d) + corr_run;
-                        if ((smask[u] >> lane) & 1ull) scst[off[u] >> 26] = ci - d;
-                        corr_run = (uint32_t)__builtin_amdgcn_readlane((int)ci, 63);
-                    } else if (corr_run != 0) {  // uniform
-                        if ((smask[u] >> lane) & 1ull) scst[off[u] >> 26] = corr_run;
-                    }
+                      for (int j = 0; j < kLkGroup; ++j) {
+                          sm[j] = smask[g0 + j];
+                          const bool special = (off[g0 + j] & kOobMask) != kOob && vv[j] >= kDupFlag;
+                          dd[j] = special ? ref_count_inline(vv[j], tv.off_mask) : 1u;
+                          unk |= dd[j] == kCountUnknown;
+                      }
+                      if (__ballot(unk) != 0) {
+#pragma unroll
+                          for (int j = 0; j < kLkGroup; ++j)
+                              if (dd[j] == kCountUnknown) dd[j] = tv.dup_rows[vv[j] & tv.off_mask];
+#pragma unroll
+                          for (int j = 0; j < kLkGroup; ++j) asm volatile("" : "+v"(dd[j]));
+                      }
+#pragma unroll
+                      for (int j = 0; j < kLkGroup; ++j) {
+                          const bool odd = dd[j] != 1u;  // non-special rows hold 1
+                          if (odd) sodd[off[g0 + j] >> 26] = 1;
+                          uint32_t d = dd[j] - 1u;
+                          if (odd && d != 0xFFFFFFFFu && d >= kBigCorr) {
+                              atomicAdd(&tcnt[tc + slane[off[g0 + j] >> 26]], (unsigned long long)d);
+                              d = 0;
+                          }
+                          dd[j] = d;
+                      }
+                      uint32_t sc[kLkGroup];
+#pragma unroll
+                      for (int j = 0; j < kLkGroup; ++j) sc[j] = wave_incl_scan_dpp(dd[j]);
+#pragma unroll
+                      for (int j = 0; j < kLkGroup; ++j) {
+                          if ((sm[j] >> lane) & 1ull) scst[off[g0 + j] >> 26] = sc[j] + corr_run - dd[j];
+                          corr_run += (uint32_t)__builtin_amdgcn_readlane((int)sc[j], 63);
+                      }
                   }
                 }
             }
