@@ -873,6 +873,38 @@ def test_probe_base(dfp, oracle_mod, probe_mode, base):
             _probe_async_base(dfp, t, pk, 2**32 - 10)
 
 
+def test_probe_capacity_truncates(dfp, oracle_mod, probe_mode):
+    """include/hj.h hj_probe_async: min(total, capacity) pairs are written - the first ones
+    of the canonical order - and the total still comes back; nothing past the capacity is
+    touched. Build keys with single rows, runs (sorted duplicates) and scattered
+    duplicates, so count-free steps, run windows and segment windows all meet the bound."""
+    rng = np.random.default_rng(7)
+    runs = np.repeat(np.arange(0, 40_000, dtype=np.int64), rng.integers(1, 6, 40_000))
+    scattered = rng.integers(40_000, 120_000, 150_000).astype(np.int64)
+    bk = np.concatenate([runs, scattered])
+    pk = rng.integers(-100, 125_000, 400_001).astype(np.int64)
+    ob, op = oracle_mod.inner_join(bk, pk)
+    m = len(ob)
+    n = len(pk)
+    keys = torch.from_numpy(pk).cuda()
+    ws = torch.empty(dfp.HashTable.workspace_bytes(n), dtype=torch.uint8, device="cuda")
+    s = torch.cuda.current_stream().cuda_stream
+    with dfp.HashTable(1, "int64", 0) as t:
+        t.append(0, torch.from_numpy(bk).cuda())
+        t.finish(0)
+        for cap in (1, 63, 64, 65, 12_345, m // 2, m - 1, m):
+            ob_d = torch.full((m + 64,), -7, dtype=torch.int64, device="cuda")
+            op_d = torch.full((m + 64,), -7, dtype=torch.int32, device="cuda")
+            dt = torch.zeros(1, dtype=torch.int64, device="cuda")
+            t.probe_async(keys.data_ptr(), n, ob_d.data_ptr(), op_d.data_ptr(), cap, dt.data_ptr(), ws.data_ptr(), s)
+            assert int(dt.item()) == m, cap
+            b = ob_d.cpu().numpy()
+            p = op_d.cpu().numpy()
+            assert np.array_equal(b[:cap].astype(np.uint64), ob[:cap]), cap
+            assert np.array_equal(p[:cap].view(np.uint32), op[:cap]), cap
+            assert (b[cap:] == -7).all() and (p[cap:] == -7).all(), cap
+
+
 # ---- the range-free dense build (the partition learns the key range) -------------
 
 @pytest.mark.parametrize("case", ["aligned", "straddle", "negative", "near_min", "max_blocks", "past_blocks",
