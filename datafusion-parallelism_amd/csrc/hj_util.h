@@ -35,6 +35,10 @@ __device__ __forceinline__ uint32_t wave_incl_scan_dpp(uint32_t v) {
     x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, false);  // row_shr:8
     x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xa, 0xf, false);  // row_bcast:15 -> rows 1, 3
     x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xc, 0xf, false);  // row_bcast:31 -> rows 2, 3
+    // opaque result: otherwise the compiler rewrites a caller's `incl - v` as the sum of the
+    // six shifted partials, which keeps every DPP move apart from its add (18 VALU + 3
+    // instead of 6 fused v_add_u32_dpp + 1 per scan; r06: C3 emission 494.5 -> 475.7 us)
+    asm volatile("" : "+v"(x));
     return (uint32_t)x;
 }
 
